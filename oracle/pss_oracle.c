@@ -1,0 +1,419 @@
+/*
+ * pss_oracle.c -- TEST INFRASTRUCTURE ONLY.  CPU restatement of the reference sampler's
+ * index-generation path, used as the *checker* by tests/, __graft_entry__.smoke() and the
+ * cpu_baseline leg of bench.py.  Nothing in the product links, loads or calls this file.
+ *
+ * Two families live here:
+ *
+ *  (1) "exact": a plain-C restatement of the reference algorithm, bit-for-bit, including the
+ *      CPython 3.10 `random` module (MT19937) it depends on.  The MT code follows the
+ *      published CPython 3.10.12 `_randommodule.c` algorithm (init_genrand, init_by_array,
+ *      genrand_uint32, random_seed) and `/usr/lib/python3.10/random.py:239-249`
+ *      (_randbelow_with_getrandbits), `:375-378` (choice), `:380-396` (shuffle).
+ *      Pinned by tests/golden/mt_kats.json and the v1_xxx / v2_xxx fixtures, which were generated
+ *      by running the reference itself (tools/gen_golden.py).
+ *
+ *  (2) "philox": the C twin of the counter-based schedule the HIP kernels implement
+ *      (DESIGN.md §3).  The GPU must match it bit-for-bit; it shares the reference's
+ *      multiset/assignment semantics (checked against (1)) but not its within-pool order.
+ *
+ * Build: see oracle/Makefile (gcc -O2 -shared -fPIC).
+ */
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#include <math.h>
+
+/* ------------------------------------------------------------------------------------ */
+/* (1a) CPython MT19937                                                                  */
+/* ------------------------------------------------------------------------------------ */
+#define MT_N 624
+#define MT_M 397
+
+typedef struct { uint32_t mt[MT_N]; int mti; } orc_mt;
+
+static void mt_init_genrand(orc_mt *s, uint32_t seed) {
+    s->mt[0] = seed;
+    for (int i = 1; i < MT_N; i++)
+        s->mt[i] = 1812433253U * (s->mt[i - 1] ^ (s->mt[i - 1] >> 30)) + (uint32_t)i;
+    s->mti = MT_N;
+}
+
+static void mt_init_by_array(orc_mt *s, const uint32_t *key, size_t klen) {
+    mt_init_genrand(s, 19650218U);
+    size_t i = 1, j = 0;
+    size_t k = (MT_N > klen ? MT_N : klen);
+    for (; k; k--) {
+        s->mt[i] = (s->mt[i] ^ ((s->mt[i - 1] ^ (s->mt[i - 1] >> 30)) * 1664525U)) + key[j] +
+                   (uint32_t)j;
+        i++; j++;
+        if (i >= MT_N) { s->mt[0] = s->mt[MT_N - 1]; i = 1; }
+        if (j >= klen) j = 0;
+    }
+    for (k = MT_N - 1; k; k--) {
+        s->mt[i] = (s->mt[i] ^ ((s->mt[i - 1] ^ (s->mt[i - 1] >> 30)) * 1566083941U)) -
+                   (uint32_t)i;
+        i++;
+        if (i >= MT_N) { s->mt[0] = s->mt[MT_N - 1]; i = 1; }
+    }
+    s->mt[0] = 0x80000000U;
+    s->mti = MT_N;
+}
+
+uint32_t orc_mt_u32(orc_mt *s) {
+    static const uint32_t mag01[2] = {0x0U, 0x9908b0dfU};
+    uint32_t y;
+    if (s->mti >= MT_N) {
+        int kk;
+        for (kk = 0; kk < MT_N - MT_M; kk++) {
+            y = (s->mt[kk] & 0x80000000U) | (s->mt[kk + 1] & 0x7fffffffU);
+            s->mt[kk] = s->mt[kk + MT_M] ^ (y >> 1) ^ mag01[y & 0x1U];
+        }
+        for (; kk < MT_N - 1; kk++) {
+            y = (s->mt[kk] & 0x80000000U) | (s->mt[kk + 1] & 0x7fffffffU);
+            s->mt[kk] = s->mt[kk + (MT_M - MT_N)] ^ (y >> 1) ^ mag01[y & 0x1U];
+        }
+        y = (s->mt[MT_N - 1] & 0x80000000U) | (s->mt[0] & 0x7fffffffU);
+        s->mt[MT_N - 1] = s->mt[MT_M - 1] ^ (y >> 1) ^ mag01[y & 0x1U];
+        s->mti = 0;
+    }
+    y = s->mt[s->mti++];
+    y ^= (y >> 11);
+    y ^= (y << 7) & 0x9d2c5680U;
+    y ^= (y << 15) & 0xefc60000U;
+    y ^= (y >> 18);
+    return y;
+}
+
+/* random.seed(a) for an int a: key = 32-bit little-endian words of abs(a) (CPython
+ * random_seed; keyused = max(1, ceil(bits/32))).  Words are passed in by the caller so
+ * arbitrarily large Python ints work; orc_mt_seed_i64 covers the int64 seeds the
+ * reference actually produces (epoch + k, epoch + buffers*10000). */
+void orc_mt_seed_words(orc_mt *s, const uint32_t *words, int64_t nwords) {
+    uint32_t zero = 0;
+    while (nwords > 1 && words[nwords - 1] == 0) nwords--;
+    if (nwords <= 0) { words = &zero; nwords = 1; }
+    mt_init_by_array(s, words, (size_t)nwords);
+}
+
+void orc_mt_seed_i64(orc_mt *s, int64_t a) {
+    uint64_t m = a < 0 ? (uint64_t)(-(a + 1)) + 1u : (uint64_t)a;
+    uint32_t w[2] = {(uint32_t)m, (uint32_t)(m >> 32)};
+    orc_mt_seed_words(s, w, w[1] ? 2 : 1);
+}
+
+static int bit_length_u64(uint64_t n) { int k = 0; while (n) { k++; n >>= 1; } return k; }
+
+/* random.py:239-249, restricted to n < 2**32 (every list the reference shuffles). */
+uint64_t orc_mt_randbelow(orc_mt *s, uint64_t n) {
+    if (!n) return 0;
+    int k = bit_length_u64(n);
+    uint64_t r;
+    if (k <= 32) {
+        do { r = orc_mt_u32(s) >> (32 - k); } while (r >= n);
+    } else { /* getrandbits(k>32): words little-endian, top word masked (CPython) */
+        do {
+            uint64_t lo = orc_mt_u32(s);
+            uint64_t hi = orc_mt_u32(s) >> (64 - k);
+            r = lo | (hi << 32);
+        } while (r >= n);
+    }
+    return r;
+}
+
+/* random.py:380-396 */
+void orc_mt_shuffle_i64(orc_mt *s, int64_t *x, int64_t n) {
+    for (int64_t i = n - 1; i >= 1; i--) {
+        int64_t j = (int64_t)orc_mt_randbelow(s, (uint64_t)(i + 1));
+        int64_t t = x[i]; x[i] = x[j]; x[j] = t;
+    }
+}
+void orc_mt_shuffle_i32(orc_mt *s, int32_t *x, int64_t n) {
+    for (int64_t i = n - 1; i >= 1; i--) {
+        int64_t j = (int64_t)orc_mt_randbelow(s, (uint64_t)(i + 1));
+        int32_t t = x[i]; x[i] = x[j]; x[j] = t;
+    }
+}
+
+orc_mt *orc_mt_new(void) { orc_mt *s = (orc_mt *)calloc(1, sizeof(orc_mt)); orc_mt_seed_i64(s, 0); return s; }
+void orc_mt_free(orc_mt *s) { free(s); }
+
+/* seed(a); shuffle(x) -- the idiom of V1:114-119 and V2:143-146 */
+void orc_seeded_shuffle_i32(int64_t seed, int32_t *x, int64_t n) {
+    orc_mt s; orc_mt_seed_i64(&s, seed); orc_mt_shuffle_i32(&s, x, n);
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* (1b) partition math -- V1:42 `int(math.ceil(N * 1.0 / R))` evaluated in IEEE doubles   */
+/* ------------------------------------------------------------------------------------ */
+int64_t orc_num_samples(int64_t N, int64_t R) {
+    double q = (double)N / (double)R;
+    return (int64_t)ceil(q);
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* (1c) exact reference streams                                                          */
+/* ------------------------------------------------------------------------------------ */
+static inline int64_t wrap_id(int64_t id, int64_t N) { return id >= N ? id - N : id; }
+
+/* V1 stream of one rank: V1:102,114-115 (window 0, seed(epoch)) and V1:157-172 (windows
+ * b>=1, seed(epoch + b*10000)).  `resume_pos` >= 0 reproduces find_ckpt_position
+ * (V1:134-140): the window holding resume_pos is left UNshuffled (the reference's lossy
+ * resume) and generation starts at resume_pos.  Returns the number of ids written, or -1
+ * where the reference itself would raise IndexError. */
+int64_t orc_v1_exact_stream(int64_t epoch, int64_t start, int64_t ns, int64_t B, int64_t N,
+                            int shuffle, int64_t resume_pos, int64_t *out) {
+    orc_mt s;
+    int64_t *ids = (int64_t *)malloc(sizeof(int64_t) * (size_t)(B > 0 ? B : 1));
+    int64_t buffers = 0, pos = 0, len, n_out = 0;
+    if (resume_pos < 0) {
+        len = B < ns ? B : ns;
+        for (int64_t i = 0; i < len; i++) ids[i] = i;
+        if (shuffle) { orc_mt_seed_i64(&s, epoch); orc_mt_shuffle_i64(&s, ids, len); }
+    } else {
+        buffers = resume_pos / B;
+        len = ns - buffers * B; if (len > B) len = B; if (len < 0) len = 0;
+        for (int64_t i = 0; i < len; i++) ids[i] = i;
+        pos = resume_pos - buffers * B;
+        if (len > 0 && pos >= len) { free(ids); return -1; }
+    }
+    while (len > 0) {
+        out[n_out++] = wrap_id(ids[pos] + B * buffers + start, N);
+        pos++;
+        if (pos >= len) {
+            buffers++;
+            len = ns - buffers * B; if (len > B) len = B; if (len < 0) len = 0;
+            for (int64_t i = 0; i < len; i++) ids[i] = i;
+            if (shuffle) { orc_mt_seed_i64(&s, epoch + buffers * 10000); orc_mt_shuffle_i64(&s, ids, len); }
+            pos = 0;
+        }
+    }
+    free(ids);
+    return n_out;
+}
+
+/* V2 stream of one rank: pools seeded from the OLD start (V2:135-138), MT reseeded with
+ * seed(epoch+2) at the end of init_iter (V2:147), then get_index (V2:96-116): choice +
+ * list.remove from pool1, choice + remove from pool2 appended to pool1, reseed
+ * seed(epoch + buffers*10000) and refill pool2 from the NEW start whenever it empties.
+ * `skip` ids are drawn and discarded first (find_ckpt_position replay, V2:118-122). */
+int64_t orc_v2_exact_stream(int64_t epoch, int64_t old_start, int64_t new_start, int64_t ns,
+                            int64_t B, int64_t N, int64_t skip, int64_t *out) {
+    orc_mt s;
+    int64_t cap = B > 0 ? B : 1;
+    int64_t *p1 = (int64_t *)malloc(sizeof(int64_t) * (size_t)(cap + 1));
+    int64_t *p2 = (int64_t *)malloc(sizeof(int64_t) * (size_t)cap);
+    int64_t n1 = 0, n2 = 0, buffers = 0, n_out = 0, drawn = 0;
+    int64_t e1 = old_start + (B < ns ? B : ns);
+    for (int64_t v = old_start; v < e1; v++) p1[n1++] = v;
+    int64_t e2 = old_start + 2 * B; if (e2 > old_start + ns) e2 = old_start + ns;
+    for (int64_t v = old_start + B; v < e2; v++) p2[n2++] = v;
+    orc_mt_seed_i64(&s, epoch + 2);
+    while (n1 > 0 || n2 > 0) {
+        int64_t k = (int64_t)orc_mt_randbelow(&s, (uint64_t)n1);
+        if (n1 == 0) break; /* choice([]) raises IndexError in the reference */
+        int64_t index = p1[k];
+        memmove(p1 + k, p1 + k + 1, sizeof(int64_t) * (size_t)(n1 - k - 1));
+        n1--;
+        if (n2 != 0) {
+            int64_t k2 = (int64_t)orc_mt_randbelow(&s, (uint64_t)n2);
+            int64_t index2 = p2[k2];
+            memmove(p2 + k2, p2 + k2 + 1, sizeof(int64_t) * (size_t)(n2 - k2 - 1));
+            n2--;
+            p1[n1++] = index2;
+        }
+        if (n2 == 0) {
+            orc_mt_seed_i64(&s, epoch + buffers * 10000);
+            buffers++;
+            int64_t lo = new_start + (buffers + 1) * B;
+            int64_t hi = new_start + (buffers + 2) * B;
+            if (hi > new_start + ns) hi = new_start + ns;
+            for (int64_t v = lo; v < hi; v++) p2[n2++] = v;
+        }
+        if (drawn++ >= skip) out[n_out++] = wrap_id(index, N);
+    }
+    free(p1); free(p2);
+    return n_out;
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* (2) Philox schedule -- C twin of the HIP kernels                        */
+/* ------------------------------------------------------------------------------------ */
+#define PHILOX_M0 0xD2511F53U
+#define PHILOX_M1 0xCD9E8D57U
+#define PHILOX_W0 0x9E3779B9U
+#define PHILOX_W1 0xBB67AE85U
+enum { DOM_V1_WIN = 1, DOM_V2_SLOT = 2, DOM_V2_INS = 3, DOM_V2_TAIL = 4 };
+
+void orc_philox4x32(const uint32_t ctr_in[4], uint64_t key64, uint32_t out[4]) {
+    uint32_t c0 = ctr_in[0], c1 = ctr_in[1], c2 = ctr_in[2], c3 = ctr_in[3];
+    uint32_t k0 = (uint32_t)key64, k1 = (uint32_t)(key64 >> 32);
+    for (int r = 0; r < 10; r++) {
+        uint64_t p0 = (uint64_t)PHILOX_M0 * c0;
+        uint64_t p1 = (uint64_t)PHILOX_M1 * c2;
+        uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
+        uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+        c0 = n0; c1 = (uint32_t)p1; c2 = n2; c3 = (uint32_t)p0;
+        k0 += PHILOX_W0; k1 += PHILOX_W1;
+    }
+    out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+
+uint64_t orc_mix64(uint64_t z) {
+    z += 0x9E3779B97F4A7C15ULL;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+
+uint64_t orc_epoch_key(uint64_t seed, int64_t epoch) {
+    return orc_mix64(orc_mix64(seed) ^ (uint64_t)epoch);
+}
+
+static inline uint32_t lowbias32(uint32_t x) {
+    x ^= x >> 16; x *= 0x7feb352dU; x ^= x >> 15; x *= 0x846ca68bU; x ^= x >> 16;
+    return x;
+}
+
+/* keyed bijection of [0,n): 4-round balanced Feistel on 2h bits + cycle walking */
+uint32_t orc_feistel(uint32_t x, uint32_t n, const uint32_t rk[4]) {
+    if (n <= 1) return 0;
+    int bits = 0; while ((1ull << bits) < (uint64_t)n) bits++;
+    int h = (bits + 1) >> 1;
+    uint32_t mask = (1u << h) - 1u;
+    do {
+        uint32_t L = x >> h, R = x & mask;
+        for (int i = 0; i < 4; i++) {
+            uint32_t t = L ^ (lowbias32(R ^ rk[i]) & mask);
+            L = R; R = t;
+        }
+        x = (L << h) | R;
+    } while (x >= n);
+    return x;
+}
+
+typedef struct { uint32_t key; uint32_t idx; } kv_t;
+static int kv_cmp(const void *a, const void *b) {
+    const kv_t *x = (const kv_t *)a, *y = (const kv_t *)b;
+    if (x->key != y->key) return x->key < y->key ? -1 : 1;
+    return x->idx < y->idx ? -1 : (x->idx > y->idx);
+}
+
+/* perm = stable argsort of Philox keys ctr=(i>>2, c1, rank, dom)[i&3], i<n */
+void orc_sort_perm(uint64_t key64, uint32_t c1, uint32_t rank, uint32_t dom, int64_t n,
+                   uint32_t *perm) {
+    kv_t *a = (kv_t *)malloc(sizeof(kv_t) * (size_t)(n > 0 ? n : 1));
+    for (int64_t q = 0; q * 4 < n; q++) {
+        uint32_t ctr[4] = {(uint32_t)q, c1, rank, dom}, o[4];
+        orc_philox4x32(ctr, key64, o);
+        for (int w = 0; w < 4 && q * 4 + w < n; w++) {
+            a[q * 4 + w].key = o[w];
+            a[q * 4 + w].idx = (uint32_t)(q * 4 + w);
+        }
+    }
+    qsort(a, (size_t)n, sizeof(kv_t), kv_cmp);
+    for (int64_t i = 0; i < n; i++) perm[i] = a[i].idx;
+    free(a);
+}
+
+/* V1 under the Philox schedule: window w of the rank block is ordered by perm_w = stable
+ * argsort of Philox keys (i>>2, w, rank, DOM_V1_WIN); id = start + w*B + perm_w[p] (wrap at
+ * N, V1:161-163).  Same multiset as orc_v1_exact_stream.  Positions [pos_lo, pos_lo+count). */
+int64_t orc_v1_philox_stream(uint64_t key64, uint32_t rank, int64_t start, int64_t ns,
+                             int64_t B, int64_t N, int shuffle, int64_t pos_lo, int64_t count,
+                             int64_t *out) {
+    int64_t pos_hi = pos_lo + count; if (pos_hi > ns) pos_hi = ns;
+    if (pos_lo >= pos_hi) return 0;
+    uint32_t *perm = (uint32_t *)malloc(sizeof(uint32_t) * (size_t)B);
+    int64_t n_out = 0;
+    for (int64_t w = pos_lo / B; w * B < pos_hi; w++) {
+        int64_t len = ns - w * B; if (len > B) len = B;
+        if (shuffle) orc_sort_perm(key64, (uint32_t)w, rank, DOM_V1_WIN, len, perm);
+        else for (int64_t i = 0; i < len; i++) perm[i] = (uint32_t)i;
+        int64_t p0 = pos_lo > w * B ? pos_lo - w * B : 0;
+        int64_t p1 = pos_hi - w * B < len ? pos_hi - w * B : len;
+        for (int64_t p = p0; p < p1; p++) out[n_out++] = wrap_id(start + w * B + perm[p], N);
+    }
+    free(perm);
+    return n_out;
+}
+
+static inline uint32_t v2_slot(uint64_t key64, uint32_t rank, int64_t t, uint32_t P1) {
+    uint64_t c = (uint64_t)(t >> 8) * 64u + (uint64_t)(t & 63);
+    uint32_t ctr[4] = {(uint32_t)c, (uint32_t)(c >> 32), rank, DOM_V2_SLOT}, o[4];
+    orc_philox4x32(ctr, key64, o);
+    uint32_t u = o[(t >> 6) & 3];
+    return (uint32_t)(((uint64_t)u * P1) >> 32);
+}
+
+/* virtual index v in [0,ns) of one rank -> global id: the first two windows come from the
+ * OLD start (V2:135-138), the rest from the NEW one (V2:110-112). */
+static inline int64_t v2_vid_to_id(int64_t v, int64_t old_start, int64_t new_start, int64_t B,
+                                   int64_t N) {
+    return wrap_id((v < 2 * B ? old_start : new_start) + v, N);
+}
+
+/* V2 under the Philox schedule (slot-replacement form of V2:96-116):
+ *   P1 = min(B, ns) slots initialised with window 0 (v = s); T = ns - P1 steps;
+ *   step t draws slot k_t (Philox DOM_V2_SLOT), emits buf[k_t] and stores the t-th inserted
+ *   element there: window w = 1 + t/B, inserted in the order of the Feistel bijection keyed
+ *   by Philox (w, 0, rank, DOM_V2_INS);  then the final buffer is emitted in the order of a
+ *   stable argsort of Philox keys (j>>2, 0, rank, DOM_V2_TAIL).
+ * Writes all ns ids (rank order) to out; returns ns. */
+int64_t orc_v2_philox_stream(uint64_t key64, uint32_t rank, int64_t old_start,
+                             int64_t new_start, int64_t ns, int64_t B, int64_t N, int64_t *out) {
+    int64_t P1 = B < ns ? B : ns;
+    int64_t T = ns - P1;
+    uint32_t *buf = (uint32_t *)malloc(sizeof(uint32_t) * (size_t)P1);
+    for (int64_t s = 0; s < P1; s++) buf[s] = (uint32_t)s;
+    int64_t cur_w = -1;
+    uint32_t rk[4] = {0, 0, 0, 0};
+    for (int64_t t = 0; t < T; t++) {
+        uint32_t k = v2_slot(key64, rank, t, (uint32_t)P1);
+        out[t] = v2_vid_to_id(buf[k], old_start, new_start, B, N);
+        int64_t w = 1 + t / B, p = t % B;
+        if (w != cur_w) {
+            uint32_t ctr[4] = {(uint32_t)w, 0, rank, DOM_V2_INS};
+            orc_philox4x32(ctr, key64, rk);
+            cur_w = w;
+        }
+        int64_t len = ns - w * B; if (len > B) len = B;
+        buf[k] = (uint32_t)(w * B + orc_feistel((uint32_t)p, (uint32_t)len, rk));
+    }
+    uint32_t *perm = (uint32_t *)malloc(sizeof(uint32_t) * (size_t)P1);
+    orc_sort_perm(key64, 0, rank, DOM_V2_TAIL, P1, perm);
+    for (int64_t j = 0; j < P1; j++)
+        out[T + j] = v2_vid_to_id(buf[perm[j]], old_start, new_start, B, N);
+    free(perm); free(buf);
+    return ns;
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* id -> (file position, offset) over an exclusive prefix of the shuffled file order      */
+/* (V1:181-221 for ids below the scanned total; reflection is host-side semantics).       */
+/* ------------------------------------------------------------------------------------ */
+void orc_map(const int64_t *prefix, int64_t F, const int64_t *ids, int64_t n, int32_t *fpos,
+             int64_t *off) {
+    for (int64_t i = 0; i < n; i++) {
+        int64_t lo = 0, hi = F; /* largest f with prefix[f] <= id, skipping empty files */
+        int64_t id = ids[i];
+        while (hi - lo > 1) {
+            int64_t mid = (lo + hi) >> 1;
+            if (prefix[mid] <= id) lo = mid; else hi = mid;
+        }
+        fpos[i] = (int32_t)lo;
+        off[i] = id - prefix[lo];
+    }
+}
+
+uint64_t orc_digest(const int64_t *ids, int64_t n) {
+    uint64_t d = 0;
+    for (int64_t i = 0; i < n; i++) d += orc_mix64((uint64_t)ids[i]);
+    return d;
+}
+
+uint64_t orc_digest_range(int64_t lo, int64_t hi) {
+    uint64_t d = 0;
+    for (int64_t i = lo; i < hi; i++) d += orc_mix64((uint64_t)i);
+    return d;
+}
