@@ -1,0 +1,102 @@
+/*
+ * pss.h -- C-ABI of the MI355X partial-shuffle sampler (libpss.so).
+ *
+ * The reference (microsoft/PartiallyShuffleDistributedSampler) is pure Python; its index
+ * generation lives inside two `torch.utils.data.Sampler` subclasses:
+ *   V1 = DistributedSamplerViaLocallyShuffle.py, V2 = DistributedSamplerViaLocallyShuffleV2.py.
+ * Each entry point below replaces the reference code cited next to it; the Python facade in
+ * partiallyshuffledistributedsampler_amd/ binds them with ctypes.
+ *
+ * Conventions
+ *   - every function returns PSS_OK (0) or a PSS_E* code; pss_last_error() has the text
+ *     (thread-local).  No C++ exception crosses this boundary.
+ *   - `*_dev` arguments are device pointers on the sampler's device; `stream` is a
+ *     hipStream_t (NULL = default stream).  Device work is stream-ordered and asynchronous;
+ *     nothing on the per-epoch path allocates once workspaces have grown to their size.
+ *   - a handle is not thread-safe; distinct handles share no state.
+ */
+#ifndef PSS_H
+#define PSS_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct pss_sampler pss_sampler;
+
+#define PSS_OK 0
+#define PSS_EINVAL 1    /* bad argument */
+#define PSS_EHIP 2      /* HIP runtime error (text has hipGetErrorString) */
+#define PSS_ENOTSUP 3   /* configuration outside what the kernels implement */
+#define PSS_ESTATE 4    /* call out of order (e.g. generate before init_iter) */
+#define PSS_EDEVICE 5   /* a kernel reported a device-side error flag */
+
+const char *pss_last_error(void);
+int pss_abi_version(void);
+
+/* Constructor math of __init__ (V1:16-56, V2:16-52):
+ *   files_len[F]  -- per-file sample counts in dataset.files order (files_len dict, or the
+ *                    reader(path, get_data=False) probe, V1:186-189)
+ *   total_size    -- ori_total_size: sum over ALL files_len keys (V1:29-31), else total_size
+ *   num_samples   =  int(math.ceil(total_size * 1.0 / num_replicas)) (V1:42)
+ *   version       -- 1 (one pool) or 2 (two pools, TF-like); shuffle is ignored by V2.
+ *   seed          -- Philox key of the pool permutations (extension; the reference has none)
+ *   device        -- HIP device ordinal used for every device call of this handle.
+ * No device memory is touched until the first device call. */
+int pss_create(const int64_t *files_len, int64_t num_files, int64_t total_size,
+               int32_t num_replicas, int64_t shuffle_buffer, int32_t version, int32_t shuffle,
+               uint64_t seed, int32_t device, pss_sampler **out);
+int pss_destroy(pss_sampler *h);
+int pss_num_samples(const pss_sampler *h, int64_t *num_samples);   /* __len__ (V1:261-262) */
+
+/* One init_iter() for `epoch` (V1:100-132, V2:124-159): the cumulative file-order shuffle
+ * (seed(e+1) in V1 / seed(e) in V2, CPython MT19937, exact), V1's cumulative block shuffle
+ * (seed(e+2)) or V2's reset+shuffle (seed(e+1)), old/new start_num per rank.  Host-side,
+ * O(F + R).  Every later device call works on this epoch. */
+int pss_init_iter(pss_sampler *h, int64_t epoch);
+int pss_file_order(const pss_sampler *h, int32_t *order /* [F] dataset positions */);
+int pss_blocks(const pss_sampler *h, int32_t *blocks /* [R] */);
+int pss_rank_starts(const pss_sampler *h, int64_t *old_start /* [R] */, int64_t *new_start /* [R] */);
+
+/* Upload the epoch descriptors and run the device prefix scan over the shuffled files_len
+ * (replaces the lazy past_files_samples scan, V1:181-190).  Implied by the calls below. */
+int pss_prepare(pss_sampler *h, void *stream);
+
+/* Index generation (V1:151-172 / V2:96-116,170-176): positions [pos_lo, pos_lo+count) of
+ * the per-epoch streams of logical ranks [rank_lo, rank_hi), written rank-major to
+ * out_dev[(r - rank_lo) * count + (pos - pos_lo)] as int64 global sample ids.
+ * Positions past num_samples are left untouched.  pos_lo = step*batch_size gives an O(1)
+ * resume (find_ckpt_position, V1:134-140 / V2:118-122). */
+int pss_generate(pss_sampler *h, int32_t rank_lo, int32_t rank_hi, int64_t pos_lo,
+                 int64_t count, int64_t *out_dev, void *stream);
+
+/* id -> (position in the shuffled file order, offset in that file) (V1:181-221).  Ids at or
+ * past the scanned total are reflected as V1:191-196 does and flagged by
+ * file_pos = -1 - f (the host moves them to the end of their batch). */
+int pss_map(pss_sampler *h, const int64_t *ids_dev, int64_t n, int32_t *file_pos_dev,
+            int64_t *offset_dev, void *stream);
+
+/* File -> rank partition: for ranks [rank_lo, rank_hi), the (file position, lo, hi) segments
+ * their epoch reads, in stream order of the id ranges.  seg_off_dev[0..n] is always written
+ * (exclusive offsets); segments only when seg_cap >= seg_off_dev[n]. */
+int pss_partition(pss_sampler *h, int32_t rank_lo, int32_t rank_hi, int64_t *seg_off_dev,
+                  int32_t *seg_file_dev, int64_t *seg_lo_dev, int64_t *seg_hi_dev,
+                  int64_t seg_cap, void *stream);
+
+/* Coverage digest: *acc_dev += sum(splitmix64(id)) mod 2^64 (commutative, duplicate-
+ * sensitive).  pss_digest_range digests the ids lo..hi-1. */
+int pss_digest(const int64_t *ids_dev, int64_t n, uint64_t *acc_dev, void *stream);
+int pss_digest_range(int64_t lo, int64_t hi, uint64_t *acc_dev, void *stream);
+
+/* Synchronise `stream` and report any device-side error flag of the handle. */
+int pss_check(pss_sampler *h, void *stream);
+
+/* Self-test of the wave64 DPP scan primitive: out_dev[2i] = 64-bit inclusive wave scan,
+ * out_dev[2i+1] = 32-bit one (low words), for n inputs. */
+int pss_debug_wave_scan(const uint64_t *in_dev, uint64_t *out_dev, int64_t n, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PSS_H */

@@ -1,0 +1,80 @@
+// pss_common.h -- counter-based schedule primitives shared by the gfx950 kernels and the
+// host runtime (the Philox schedule of DESIGN.md §3).  oracle/pss_oracle.c restates the same
+// functions independently in C as the test checker; the two must agree bit-for-bit.
+#pragma once
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define PSS_HD __host__ __device__ __forceinline__
+#else
+#define PSS_HD static inline
+#endif
+
+namespace pss {
+
+enum : uint32_t { DOM_V1_WIN = 1, DOM_V2_SLOT = 2, DOM_V2_INS = 3, DOM_V2_TAIL = 4 };
+
+// Philox4x32-10 (Salmon et al., SC'11).  Each 64-bit product is one v_mad_u64_u32 on gfx950.
+PSS_HD void philox4x32_10(uint32_t &c0, uint32_t &c1, uint32_t &c2, uint32_t &c3,
+                          uint32_t k0, uint32_t k1) {
+#pragma unroll
+    for (int r = 0; r < 10; r++) {
+        const uint64_t p0 = (uint64_t)0xD2511F53u * c0;
+        const uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
+        const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
+        const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+        c0 = n0; c1 = (uint32_t)p1; c2 = n2; c3 = (uint32_t)p0;
+        k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+    }
+}
+
+PSS_HD uint64_t mix64(uint64_t z) {
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+PSS_HD uint64_t epoch_key(uint64_t seed, int64_t epoch) {
+    return mix64(mix64(seed) ^ (uint64_t)epoch);
+}
+
+PSS_HD uint32_t lowbias32(uint32_t x) {
+    x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
+    return x;
+}
+
+PSS_HD int ceil_log2_u64(uint64_t n) {  // smallest b with 2^b >= n (n >= 1)
+    int b = 0;
+    while ((1ull << b) < n) b++;
+    return b;
+}
+
+// Keyed bijection of [0, n): 4-round balanced Feistel over 2h bits + cycle walking.
+PSS_HD uint32_t feistel(uint32_t x, uint32_t n, uint32_t h, uint32_t rk0, uint32_t rk1,
+                        uint32_t rk2, uint32_t rk3) {
+    if (n <= 1) return 0;
+    const uint32_t mask = (1u << h) - 1u;
+    do {
+        uint32_t L = x >> h, R = x & mask, t;
+        t = L ^ (lowbias32(R ^ rk0) & mask); L = R; R = t;
+        t = L ^ (lowbias32(R ^ rk1) & mask); L = R; R = t;
+        t = L ^ (lowbias32(R ^ rk2) & mask); L = R; R = t;
+        t = L ^ (lowbias32(R ^ rk3) & mask); L = R; R = t;
+        x = (L << h) | R;
+    } while (x >= n);
+    return x;
+}
+
+PSS_HD uint32_t feistel_half_bits(uint32_t n) {
+    const int bits = ceil_log2_u64(n);
+    return (uint32_t)((bits + 1) >> 1);
+}
+
+// Lemire multiply-shift: uniform-ish slot in [0, n) from one 32-bit word (bias <= n/2^32).
+PSS_HD uint32_t scale32(uint32_t u, uint32_t n) {
+    return (uint32_t)(((uint64_t)u * n) >> 32);
+}
+
+}  // namespace pss

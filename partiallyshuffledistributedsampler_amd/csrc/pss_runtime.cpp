@@ -1,0 +1,434 @@
+// pss_runtime.cpp -- native runtime behind include/pss.h.
+//
+// Owns a sampler handle: the reference's constructor math (V1:16-56), its stateful epoch
+// history (init_iter, V1:100-132 / V2:124-159) evaluated on the host with a CPython-exact
+// MT19937, the device buffers of the current epoch, and the kernel launches.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/pss.h"
+#include "pss_common.h"
+#include "pss_kernels.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string &msg) {
+    g_err = msg;
+    return code;
+}
+
+#define PSS_HIP(call)                                                                     \
+    do {                                                                                  \
+        hipError_t e_ = (call);                                                           \
+        if (e_ != hipSuccess)                                                             \
+            return fail(e_ == hipErrorNotSupported ? PSS_ENOTSUP : PSS_EHIP,              \
+                        std::string(#call) + ": " + hipGetErrorString(e_));               \
+    } while (0)
+
+// ------------------------------------------------------------------------------------------
+// CPython 3.10 `random` (MT19937): seed(int) = init_by_array over the 32-bit words of
+// abs(seed); shuffle = Fisher-Yates with _randbelow_with_getrandbits (random.py:239-249,
+// 380-396).  The file-order and block permutations pin the file->rank assignment, so they
+// must match the reference exactly.
+// ------------------------------------------------------------------------------------------
+class CPythonMT {
+  public:
+    void seed(int64_t a) {
+        uint64_t m = a < 0 ? (uint64_t)(-(a + 1)) + 1u : (uint64_t)a;
+        uint32_t key[2] = {(uint32_t)m, (uint32_t)(m >> 32)};
+        init_by_array(key, key[1] ? 2 : 1);
+    }
+    uint32_t next() {
+        if (mti_ >= kN) twist();
+        uint32_t y = mt_[mti_++];
+        y ^= y >> 11;
+        y ^= (y << 7) & 0x9d2c5680u;
+        y ^= (y << 15) & 0xefc60000u;
+        y ^= y >> 18;
+        return y;
+    }
+    uint32_t randbelow(uint32_t n) {  // n < 2^32
+        if (n == 0) return 0;
+        int k = 0;
+        for (uint64_t v = n; v; v >>= 1) k++;
+        uint32_t r;
+        do { r = next() >> (32 - k); } while (r >= n);
+        return r;
+    }
+    template <typename T>
+    void shuffle(T *x, int64_t n) {
+        for (int64_t i = n - 1; i >= 1; i--) {
+            const int64_t j = randbelow((uint32_t)(i + 1));
+            const T t = x[i]; x[i] = x[j]; x[j] = t;
+        }
+    }
+
+  private:
+    static constexpr int kN = 624, kM = 397;
+    uint32_t mt_[kN];
+    int mti_ = kN + 1;
+
+    void init_genrand(uint32_t s) {
+        mt_[0] = s;
+        for (int i = 1; i < kN; i++) mt_[i] = 1812433253u * (mt_[i - 1] ^ (mt_[i - 1] >> 30)) + (uint32_t)i;
+        mti_ = kN;
+    }
+    void init_by_array(const uint32_t *key, int klen) {
+        init_genrand(19650218u);
+        int i = 1, j = 0;
+        for (int k = kN > klen ? kN : klen; k; k--) {
+            mt_[i] = (mt_[i] ^ ((mt_[i - 1] ^ (mt_[i - 1] >> 30)) * 1664525u)) + key[j] + (uint32_t)j;
+            i++; j++;
+            if (i >= kN) { mt_[0] = mt_[kN - 1]; i = 1; }
+            if (j >= klen) j = 0;
+        }
+        for (int k = kN - 1; k; k--) {
+            mt_[i] = (mt_[i] ^ ((mt_[i - 1] ^ (mt_[i - 1] >> 30)) * 1566083941u)) - (uint32_t)i;
+            i++;
+            if (i >= kN) { mt_[0] = mt_[kN - 1]; i = 1; }
+        }
+        mt_[0] = 0x80000000u;
+        mti_ = kN;
+    }
+    void twist() {
+        static const uint32_t mag01[2] = {0u, 0x9908b0dfu};
+        int kk = 0;
+        uint32_t y;
+        for (; kk < kN - kM; kk++) {
+            y = (mt_[kk] & 0x80000000u) | (mt_[kk + 1] & 0x7fffffffu);
+            mt_[kk] = mt_[kk + kM] ^ (y >> 1) ^ mag01[y & 1u];
+        }
+        for (; kk < kN - 1; kk++) {
+            y = (mt_[kk] & 0x80000000u) | (mt_[kk + 1] & 0x7fffffffu);
+            mt_[kk] = mt_[kk + (kM - kN)] ^ (y >> 1) ^ mag01[y & 1u];
+        }
+        y = (mt_[kN - 1] & 0x80000000u) | (mt_[0] & 0x7fffffffu);
+        mt_[kN - 1] = mt_[kM - 1] ^ (y >> 1) ^ mag01[y & 1u];
+        mti_ = 0;
+    }
+};
+
+class DeviceGuard {  // run on the handle's device, restore the caller's afterwards
+  public:
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev_) != hipSuccess) prev_ = -1;
+        if (prev_ != dev) (void)hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        int cur = -1;
+        if (prev_ >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev_) (void)hipSetDevice(prev_);
+    }
+
+  private:
+    int prev_ = -1;
+};
+
+template <typename T>
+struct DevBuf {
+    T *p = nullptr;
+    size_t n = 0;  // elements
+    hipError_t ensure(size_t want) {
+        if (want <= n && p) return hipSuccess;
+        if (p) { (void)hipFree(p); p = nullptr; n = 0; }
+        hipError_t e = hipMalloc((void **)&p, (want ? want : 1) * sizeof(T));
+        if (e == hipSuccess) n = want;
+        return e;
+    }
+    void release() { if (p) (void)hipFree(p); p = nullptr; n = 0; }
+};
+
+}  // namespace
+
+struct pss_sampler {
+    // constructor state (V1:27-56)
+    std::vector<int64_t> files_len;
+    int64_t F = 0, N = 0, ns = 0, B = 0;
+    int32_t R = 0, version = 1, shuffle = 1, device = 0;
+    uint64_t seed = 0;
+    // history state
+    std::vector<int32_t> order;   // self.files as dataset positions
+    std::vector<int32_t> blocks;  // self.blocks
+    std::vector<pss::RankDesc> ranks;
+    int64_t epoch = 0;
+    bool iterated = false;
+    // device state
+    bool dev_init = false;
+    bool dirty = true;
+    DevBuf<int64_t> d_lens, d_prefix;
+    DevBuf<int32_t> d_order, d_err;
+    DevBuf<pss::RankDesc> d_ranks;
+    DevBuf<uint32_t> d_val, d_buf, d_sort;
+    int32_t *h_stage_order = nullptr;      // pinned staging of the epoch upload
+    pss::RankDesc *h_stage_ranks = nullptr;
+    hipEvent_t upload_done = nullptr;
+    bool upload_pending = false;
+
+    pss::Geometry geometry() const {
+        pss::Geometry g{};
+        g.N = N; g.ns = ns; g.B = B; g.R = R; g.version = version;
+        g.shuffle = version == 1 ? shuffle : 1;
+        const uint64_t k = pss::epoch_key(seed, epoch);
+        g.key0 = (uint32_t)k; g.key1 = (uint32_t)(k >> 32);
+        return g;
+    }
+};
+
+namespace {
+
+int ensure_device(pss_sampler *h) {
+    if (h->dev_init) return PSS_OK;
+    PSS_HIP(pss::init_kernel_attributes());
+    PSS_HIP(h->d_lens.ensure((size_t)h->F));
+    PSS_HIP(h->d_order.ensure((size_t)h->F));
+    PSS_HIP(h->d_prefix.ensure((size_t)h->F + 1));
+    PSS_HIP(h->d_ranks.ensure((size_t)h->R));
+    PSS_HIP(h->d_err.ensure(1));
+    PSS_HIP(hipMemset(h->d_err.p, 0, sizeof(int32_t)));
+    if (h->F) PSS_HIP(hipMemcpy(h->d_lens.p, h->files_len.data(), sizeof(int64_t) * h->F, hipMemcpyHostToDevice));
+    PSS_HIP(hipHostMalloc((void **)&h->h_stage_order, sizeof(int32_t) * (h->F ? h->F : 1)));
+    PSS_HIP(hipHostMalloc((void **)&h->h_stage_ranks, sizeof(pss::RankDesc) * h->R));
+    PSS_HIP(hipEventCreateWithFlags(&h->upload_done, hipEventDisableTiming));
+    h->dev_init = true;
+    return PSS_OK;
+}
+
+int prepare(pss_sampler *h, hipStream_t s) {
+    if (!h->iterated) return fail(PSS_ESTATE, "pss_init_iter must be called before device work");
+    int rc = ensure_device(h);
+    if (rc) return rc;
+    if (!h->dirty) return PSS_OK;
+    if (h->upload_pending) PSS_HIP(hipEventSynchronize(h->upload_done));
+    std::memcpy(h->h_stage_order, h->order.data(), sizeof(int32_t) * h->F);
+    std::memcpy(h->h_stage_ranks, h->ranks.data(), sizeof(pss::RankDesc) * h->R);
+    if (h->F) PSS_HIP(hipMemcpyAsync(h->d_order.p, h->h_stage_order, sizeof(int32_t) * h->F, hipMemcpyHostToDevice, s));
+    PSS_HIP(hipMemcpyAsync(h->d_ranks.p, h->h_stage_ranks, sizeof(pss::RankDesc) * h->R, hipMemcpyHostToDevice, s));
+    PSS_HIP(hipEventRecord(h->upload_done, s));
+    h->upload_pending = true;
+    PSS_HIP(pss::launch_scan_prefix(h->d_lens.p, h->d_order.p, h->F, h->d_prefix.p, s));
+    h->dirty = false;
+    return PSS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char *pss_last_error(void) { return g_err.c_str(); }
+int pss_abi_version(void) { return 1; }
+
+int pss_create(const int64_t *files_len, int64_t num_files, int64_t total_size,
+               int32_t num_replicas, int64_t shuffle_buffer, int32_t version, int32_t shuffle,
+               uint64_t seed, int32_t device, pss_sampler **out) {
+    if (!out) return fail(PSS_EINVAL, "out is NULL");
+    *out = nullptr;
+    if (num_files < 0 || (num_files > 0 && !files_len)) return fail(PSS_EINVAL, "bad files_len");
+    if (num_files >= (int64_t)INT32_MAX) return fail(PSS_ENOTSUP, "more than 2^31-1 files");
+    if (num_replicas <= 0) return fail(PSS_EINVAL, "num_replicas must be positive");
+    if (shuffle_buffer <= 0) return fail(PSS_EINVAL, "shuffle_buffer must be positive");
+    if (version != 1 && version != 2) return fail(PSS_EINVAL, "version must be 1 or 2");
+    if (total_size <= 0) return fail(PSS_EINVAL, "total_size must be positive");
+    pss_sampler *h = new pss_sampler();
+    h->files_len.assign(files_len, files_len + num_files);
+    for (int64_t v : h->files_len)
+        if (v < 0) { delete h; return fail(PSS_EINVAL, "negative file length"); }
+    h->F = num_files;
+    h->N = total_size;
+    h->R = num_replicas;
+    h->B = shuffle_buffer;
+    h->version = version;
+    h->shuffle = shuffle ? 1 : 0;
+    h->seed = seed;
+    h->device = device;
+    h->ns = (int64_t)std::ceil((double)total_size / (double)num_replicas);  // V1:42 (float ceil)
+    if (h->ns >= (int64_t)UINT32_MAX) { delete h; return fail(PSS_ENOTSUP, "num_samples >= 2^32 per rank"); }
+    h->order.resize(num_files);
+    for (int64_t i = 0; i < num_files; i++) h->order[i] = (int32_t)i;
+    h->blocks.resize(num_replicas);
+    for (int32_t r = 0; r < num_replicas; r++) h->blocks[r] = r;
+    h->ranks.resize(num_replicas);
+    for (int32_t r = 0; r < num_replicas; r++) {   // V1:52-53: start_num = ns * blocks[rank]
+        h->ranks[r].old_start = h->ns * r;
+        h->ranks[r].new_start = h->ns * r;
+    }
+    *out = h;
+    return PSS_OK;
+}
+
+int pss_destroy(pss_sampler *h) {
+    if (!h) return PSS_OK;
+    if (h->dev_init) {
+        DeviceGuard dg(h->device);
+        if (h->upload_pending) (void)hipEventSynchronize(h->upload_done);
+        h->d_lens.release(); h->d_prefix.release(); h->d_order.release(); h->d_err.release();
+        h->d_ranks.release(); h->d_val.release(); h->d_buf.release(); h->d_sort.release();
+        if (h->h_stage_order) (void)hipHostFree(h->h_stage_order);
+        if (h->h_stage_ranks) (void)hipHostFree(h->h_stage_ranks);
+        if (h->upload_done) (void)hipEventDestroy(h->upload_done);
+    }
+    delete h;
+    return PSS_OK;
+}
+
+int pss_num_samples(const pss_sampler *h, int64_t *ns) {
+    if (!h || !ns) return fail(PSS_EINVAL, "NULL argument");
+    *ns = h->ns;
+    return PSS_OK;
+}
+
+int pss_init_iter(pss_sampler *h, int64_t epoch) {
+    if (!h) return fail(PSS_EINVAL, "NULL handle");
+    CPythonMT mt;
+    std::vector<int32_t> fid(h->F);
+    for (int64_t i = 0; i < h->F; i++) fid[i] = (int32_t)i;
+    for (int32_t r = 0; r < h->R; r++) h->ranks[r].old_start = h->ranks[r].new_start;
+    if (h->version == 1) {
+        if (h->shuffle) {                              // V1:113-125
+            mt.seed(epoch + 1);
+            mt.shuffle(fid.data(), h->F);
+            mt.seed(epoch + 2);
+            mt.shuffle(h->blocks.data(), h->R);        // cumulative: self.blocks is kept
+            std::vector<int32_t> o(h->F);
+            for (int64_t i = 0; i < h->F; i++) o[i] = h->order[fid[i]];
+            h->order.swap(o);
+        }
+    } else {                                           // V2:142-152
+        mt.seed(epoch);
+        mt.shuffle(fid.data(), h->F);
+        for (int32_t r = 0; r < h->R; r++) h->blocks[r] = r;
+        mt.seed(epoch + 1);
+        mt.shuffle(h->blocks.data(), h->R);
+        std::vector<int32_t> o(h->F);
+        for (int64_t i = 0; i < h->F; i++) o[i] = h->order[fid[i]];
+        h->order.swap(o);
+    }
+    for (int32_t r = 0; r < h->R; r++) h->ranks[r].new_start = h->ns * (int64_t)h->blocks[r];
+    h->epoch = epoch;
+    h->iterated = true;
+    h->dirty = true;
+    return PSS_OK;
+}
+
+int pss_file_order(const pss_sampler *h, int32_t *order) {
+    if (!h || (!order && h->F)) return fail(PSS_EINVAL, "NULL argument");
+    std::memcpy(order, h->order.data(), sizeof(int32_t) * h->F);
+    return PSS_OK;
+}
+
+int pss_blocks(const pss_sampler *h, int32_t *blocks) {
+    if (!h || !blocks) return fail(PSS_EINVAL, "NULL argument");
+    std::memcpy(blocks, h->blocks.data(), sizeof(int32_t) * h->R);
+    return PSS_OK;
+}
+
+int pss_rank_starts(const pss_sampler *h, int64_t *old_start, int64_t *new_start) {
+    if (!h) return fail(PSS_EINVAL, "NULL handle");
+    for (int32_t r = 0; r < h->R; r++) {
+        if (old_start) old_start[r] = h->ranks[r].old_start;
+        if (new_start) new_start[r] = h->ranks[r].new_start;
+    }
+    return PSS_OK;
+}
+
+int pss_prepare(pss_sampler *h, void *stream) {
+    if (!h) return fail(PSS_EINVAL, "NULL handle");
+    DeviceGuard dg(h->device);
+    return prepare(h, (hipStream_t)stream);
+}
+
+int pss_generate(pss_sampler *h, int32_t rank_lo, int32_t rank_hi, int64_t pos_lo,
+                 int64_t count, int64_t *out_dev, void *stream) {
+    if (!h) return fail(PSS_EINVAL, "NULL handle");
+    if (rank_lo < 0 || rank_hi > h->R || rank_lo > rank_hi) return fail(PSS_EINVAL, "bad rank range");
+    if (pos_lo < 0 || count < 0) return fail(PSS_EINVAL, "bad position range");
+    if (count > 0 && rank_hi > rank_lo && !out_dev) return fail(PSS_EINVAL, "out_dev is NULL");
+    DeviceGuard dg(h->device);
+    hipStream_t s = (hipStream_t)stream;
+    int rc = prepare(h, s);
+    if (rc) return rc;
+    const int32_t nr = rank_hi - rank_lo;
+    if (nr == 0 || count == 0 || pos_lo >= h->ns) return PSS_OK;
+    const pss::Geometry g = h->geometry();
+    if (h->version == 1) {
+        PSS_HIP(pss::launch_v1(g, h->d_ranks.p, rank_lo, nr, pos_lo, count, out_dev, h->d_sort.p, h->d_err.p, s));
+    } else {
+        const size_t vb = pss::v2_val_bytes(g, nr) / sizeof(uint32_t);
+        PSS_HIP(h->d_val.ensure(vb));
+        PSS_HIP(pss::launch_v2(g, h->d_ranks.p, rank_lo, nr, pos_lo, count, out_dev, h->d_val.p,
+                               h->d_buf.p, h->d_sort.p, h->d_err.p, s));
+    }
+    return PSS_OK;
+}
+
+int pss_map(pss_sampler *h, const int64_t *ids_dev, int64_t n, int32_t *file_pos_dev,
+            int64_t *offset_dev, void *stream) {
+    if (!h) return fail(PSS_EINVAL, "NULL handle");
+    if (n < 0 || (n > 0 && (!ids_dev || !file_pos_dev || !offset_dev))) return fail(PSS_EINVAL, "bad arguments");
+    if (h->F == 0) return fail(PSS_ESTATE, "no files to map into");
+    DeviceGuard dg(h->device);
+    hipStream_t s = (hipStream_t)stream;
+    int rc = prepare(h, s);
+    if (rc) return rc;
+    PSS_HIP(pss::launch_map(h->d_prefix.p, h->F, ids_dev, n, file_pos_dev, offset_dev, s));
+    return PSS_OK;
+}
+
+int pss_partition(pss_sampler *h, int32_t rank_lo, int32_t rank_hi, int64_t *seg_off_dev,
+                  int32_t *seg_file_dev, int64_t *seg_lo_dev, int64_t *seg_hi_dev,
+                  int64_t seg_cap, void *stream) {
+    if (!h) return fail(PSS_EINVAL, "NULL handle");
+    if (rank_lo < 0 || rank_hi > h->R || rank_lo > rank_hi) return fail(PSS_EINVAL, "bad rank range");
+    if (!seg_off_dev) return fail(PSS_EINVAL, "seg_off_dev is NULL");
+    if (seg_cap > 0 && (!seg_file_dev || !seg_lo_dev || !seg_hi_dev)) return fail(PSS_EINVAL, "NULL segment arrays");
+    if (h->F == 0) return fail(PSS_ESTATE, "no files to partition");
+    DeviceGuard dg(h->device);
+    hipStream_t s = (hipStream_t)stream;
+    int rc = prepare(h, s);
+    if (rc) return rc;
+    PSS_HIP(pss::launch_partition(h->geometry(), h->d_ranks.p, rank_lo, rank_hi - rank_lo,
+                                  h->d_prefix.p, h->F, seg_off_dev, seg_file_dev, seg_lo_dev,
+                                  seg_hi_dev, seg_cap, h->d_err.p, s));
+    return PSS_OK;
+}
+
+int pss_digest(const int64_t *ids_dev, int64_t n, uint64_t *acc_dev, void *stream) {
+    if (n < 0 || (n > 0 && (!ids_dev || !acc_dev))) return fail(PSS_EINVAL, "bad arguments");
+    PSS_HIP(pss::launch_digest(ids_dev, n, acc_dev, (hipStream_t)stream));
+    return PSS_OK;
+}
+
+int pss_digest_range(int64_t lo, int64_t hi, uint64_t *acc_dev, void *stream) {
+    if (!acc_dev) return fail(PSS_EINVAL, "acc_dev is NULL");
+    PSS_HIP(pss::launch_digest_range(lo, hi, acc_dev, (hipStream_t)stream));
+    return PSS_OK;
+}
+
+int pss_check(pss_sampler *h, void *stream) {
+    if (!h) return fail(PSS_EINVAL, "NULL handle");
+    DeviceGuard dg(h->device);
+    PSS_HIP(hipStreamSynchronize((hipStream_t)stream));
+    PSS_HIP(hipGetLastError());
+    if (!h->dev_init) return PSS_OK;
+    int32_t err = 0;
+    PSS_HIP(hipMemcpy(&err, h->d_err.p, sizeof(int32_t), hipMemcpyDeviceToHost));
+    if (err) {
+        PSS_HIP(hipMemset(h->d_err.p, 0, sizeof(int32_t)));
+        return fail(PSS_EDEVICE, "device error flag " + std::to_string(err) +
+                                     " (1: partition capacity exceeded, 2: sort bucket overflow)");
+    }
+    return PSS_OK;
+}
+
+int pss_debug_wave_scan(const uint64_t *in_dev, uint64_t *out_dev, int64_t n, void *stream) {
+    if (n <= 0 || !in_dev || !out_dev) return fail(PSS_EINVAL, "bad arguments");
+    PSS_HIP(pss::launch_debug_wave_scan(in_dev, out_dev, n, (hipStream_t)stream));
+    return PSS_OK;
+}
+
+}  // extern "C"

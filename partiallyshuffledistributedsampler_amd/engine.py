@@ -1,0 +1,171 @@
+"""IndexEngine: one libpss sampler handle plus the torch plumbing around it.
+
+torch is used only for device memory and streams; every index is produced by the HIP
+kernels behind include/pss.h.  Construction needs no GPU (the handle's host-side history,
+pss_init_iter, is pure host code); every device method requires a ROCm GPU and raises
+otherwise -- there is no CPU fallback.
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+
+_i64p = ctypes.POINTER(ctypes.c_int64)
+_i32p = ctypes.POINTER(ctypes.c_int32)
+
+
+def _stream_ptr(stream, device):
+    if stream is None:
+        stream = torch.cuda.current_stream(device)
+    return ctypes.c_void_p(stream.cuda_stream)
+
+
+def require_gpu():
+    if not torch.cuda.is_available():
+        raise RuntimeError("partiallyshuffledistributedsampler_amd needs a ROCm GPU for index "
+                           "generation (no CPU fallback)")
+
+
+class IndexEngine:
+    """Device index generator of one sampler configuration (all R logical ranks)."""
+
+    def __init__(self, files_len, total_size, num_replicas, shuffle_buffer, version,
+                 shuffle=True, seed=0, device=0):
+        lib = _lib.load()
+        fl = np.ascontiguousarray(files_len, dtype=np.int64)
+        self.num_files = len(fl)
+        self.total_size = int(total_size)
+        self.num_replicas = int(num_replicas)
+        self.shuffle_buffer = int(shuffle_buffer)
+        self.version = int(version)
+        self.device = int(device)
+        h = ctypes.c_void_p()
+        _lib.check(lib.pss_create(fl.ctypes.data_as(_i64p), len(fl), self.total_size,
+                                  self.num_replicas, self.shuffle_buffer, self.version,
+                                  int(bool(shuffle)), int(seed) & 0xFFFFFFFFFFFFFFFF,
+                                  self.device, ctypes.byref(h)), "pss_create")
+        self._h = h
+        ns = ctypes.c_int64()
+        _lib.check(lib.pss_num_samples(h, ctypes.byref(ns)), "pss_num_samples")
+        self.num_samples = ns.value
+        self.epoch = None
+
+    def close(self):
+        if getattr(self, "_h", None):
+            _lib.load().pss_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- host-side epoch history ---------------------------------------------------------
+    def init_iter(self, epoch):
+        _lib.call("pss_init_iter", self._h, int(epoch))
+        self.epoch = int(epoch)
+
+    def file_order(self):
+        o = np.empty(self.num_files, dtype=np.int32)
+        _lib.call("pss_file_order", self._h, o.ctypes.data_as(_i32p))
+        return o
+
+    def blocks(self):
+        b = np.empty(self.num_replicas, dtype=np.int32)
+        _lib.call("pss_blocks", self._h, b.ctypes.data_as(_i32p))
+        return b
+
+    def rank_starts(self):
+        o = np.empty(self.num_replicas, dtype=np.int64)
+        n = np.empty(self.num_replicas, dtype=np.int64)
+        _lib.call("pss_rank_starts", self._h, o.ctypes.data_as(_i64p), n.ctypes.data_as(_i64p))
+        return o, n
+
+    # ---- device --------------------------------------------------------------------------
+    def _dev(self):
+        require_gpu()
+        return torch.device("cuda", self.device)
+
+    def prepare(self, stream=None):
+        d = self._dev()
+        _lib.call("pss_prepare", self._h, _stream_ptr(stream, d))
+
+    def generate(self, rank_lo, rank_hi, pos_lo=0, count=None, out=None, stream=None):
+        """int64 ids of positions [pos_lo, pos_lo+count) for ranks [rank_lo, rank_hi)."""
+        d = self._dev()
+        if count is None:
+            count = self.num_samples - pos_lo
+        count = max(0, int(count))
+        nr = rank_hi - rank_lo
+        if out is None:
+            out = torch.empty((nr, count), dtype=torch.int64, device=d)
+        assert out.is_contiguous() and out.dtype == torch.int64 and out.numel() >= nr * count
+        _lib.call("pss_generate", self._h, int(rank_lo), int(rank_hi), int(pos_lo), count,
+                  ctypes.c_void_p(out.data_ptr()), _stream_ptr(stream, d))
+        return out
+
+    def map(self, ids, fpos=None, off=None, stream=None):
+        d = self._dev()
+        ids = ids.contiguous()
+        n = ids.numel()
+        if fpos is None:
+            fpos = torch.empty(n, dtype=torch.int32, device=d)
+        if off is None:
+            off = torch.empty(n, dtype=torch.int64, device=d)
+        _lib.call("pss_map", self._h, ctypes.c_void_p(ids.data_ptr()), n,
+                  ctypes.c_void_p(fpos.data_ptr()), ctypes.c_void_p(off.data_ptr()),
+                  _stream_ptr(stream, d))
+        return fpos, off
+
+    def partition(self, rank_lo, rank_hi, stream=None):
+        """Host arrays (seg_off[n+1], seg_file, seg_lo, seg_hi) of the ranks' file segments."""
+        d = self._dev()
+        nr = rank_hi - rank_lo
+        sp = _stream_ptr(stream, d)
+        seg_off = torch.zeros(nr + 1, dtype=torch.int64, device=d)
+        null = ctypes.c_void_p(0)
+        _lib.call("pss_partition", self._h, rank_lo, rank_hi, ctypes.c_void_p(seg_off.data_ptr()),
+                  null, null, null, 0, sp)
+        total = int(seg_off[-1].item())
+        sf = torch.empty(max(total, 1), dtype=torch.int32, device=d)
+        sl = torch.empty(max(total, 1), dtype=torch.int64, device=d)
+        sh = torch.empty(max(total, 1), dtype=torch.int64, device=d)
+        _lib.call("pss_partition", self._h, rank_lo, rank_hi, ctypes.c_void_p(seg_off.data_ptr()),
+                  ctypes.c_void_p(sf.data_ptr()), ctypes.c_void_p(sl.data_ptr()),
+                  ctypes.c_void_p(sh.data_ptr()), max(total, 1), sp)
+        self.check(stream)
+        return (seg_off.cpu().numpy(), sf[:total].cpu().numpy(), sl[:total].cpu().numpy(),
+                sh[:total].cpu().numpy())
+
+    def check(self, stream=None):
+        d = self._dev()
+        _lib.call("pss_check", self._h, _stream_ptr(stream, d))
+
+
+def digest(ids, acc=None, stream=None):
+    """acc (int64 device tensor holding a uint64 bit pattern) += sum(splitmix64(ids))."""
+    require_gpu()
+    d = ids.device
+    if acc is None:
+        acc = torch.zeros(1, dtype=torch.int64, device=d)
+    _lib.call("pss_digest", ctypes.c_void_p(ids.data_ptr()), ids.numel(),
+              ctypes.c_void_p(acc.data_ptr()), _stream_ptr(stream, d))
+    return acc
+
+
+def digest_range(lo, hi, device, acc=None, stream=None):
+    require_gpu()
+    d = torch.device("cuda", device) if isinstance(device, int) else device
+    if acc is None:
+        acc = torch.zeros(1, dtype=torch.int64, device=d)
+    _lib.call("pss_digest_range", int(lo), int(hi), ctypes.c_void_p(acc.data_ptr()),
+              _stream_ptr(stream, d))
+    return acc
+
+
+def as_u64(t):
+    """Read a 1-element int64 tensor as the uint64 digest it stores."""
+    return int(t.item()) & 0xFFFFFFFFFFFFFFFF
