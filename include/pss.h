@@ -89,6 +89,13 @@ int pss_partition(pss_sampler *h, int32_t rank_lo, int32_t rank_hi, int64_t *seg
 int pss_digest(const int64_t *ids_dev, int64_t n, uint64_t *acc_dev, void *stream);
 int pss_digest_range(int64_t lo, int64_t hi, uint64_t *acc_dev, void *stream);
 
+/* Kernel timing: while enabled, every launch of this handle is bracketed by HIP events on
+ * its stream.  pss_profile_read synchronises on them and returns, per kernel kind
+ * (0 scan, 1 v1_window, 2 v2_lastocc, 3 v2_emit, 4 v2_tail, 5 map, 6 partition, 7 digest),
+ * the summed milliseconds and launch counts since the last read; it then clears them. */
+int pss_profile(pss_sampler *h, int32_t enable);
+int pss_profile_read(pss_sampler *h, double *total_ms, int64_t *launches, int32_t nkinds);
+
 /* Synchronise `stream` and report any device-side error flag of the handle. */
 int pss_check(pss_sampler *h, void *stream);
 

@@ -54,6 +54,8 @@ def lib():
         L.orc_v1_exact_stream.restype = ctypes.c_int64
         L.orc_v2_exact_stream.argtypes = [ctypes.c_int64] * 7 + [I64P]
         L.orc_v2_exact_stream.restype = ctypes.c_int64
+        L.orc_v2_exact_prefix.argtypes = [ctypes.c_int64] * 7 + [I64P]
+        L.orc_v2_exact_prefix.restype = ctypes.c_int64
         L.orc_philox4x32.argtypes = [U32P, ctypes.c_uint64, U32P]
         L.orc_mix64.argtypes = [ctypes.c_uint64]
         L.orc_mix64.restype = ctypes.c_uint64
@@ -181,6 +183,12 @@ def v1_exact_stream(epoch, start, ns, B, N, shuffle=True, resume_pos=-1):
 def v2_exact_stream(epoch, old_start, new_start, ns, B, N, skip=0):
     out = np.empty(ns, dtype=np.int64)
     n = lib().orc_v2_exact_stream(epoch, old_start, new_start, ns, B, N, skip, _p64(out))
+    return out[:n]
+
+
+def v2_exact_prefix(epoch, old_start, new_start, ns, B, N, limit):
+    out = np.empty(limit, dtype=np.int64)
+    n = lib().orc_v2_exact_prefix(epoch, old_start, new_start, ns, B, N, limit, _p64(out))
     return out[:n]
 
 

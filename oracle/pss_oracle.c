@@ -197,8 +197,8 @@ int64_t orc_v1_exact_stream(int64_t epoch, int64_t start, int64_t ns, int64_t B,
  * list.remove from pool1, choice + remove from pool2 appended to pool1, reseed
  * seed(epoch + buffers*10000) and refill pool2 from the NEW start whenever it empties.
  * `skip` ids are drawn and discarded first (find_ckpt_position replay, V2:118-122). */
-int64_t orc_v2_exact_stream(int64_t epoch, int64_t old_start, int64_t new_start, int64_t ns,
-                            int64_t B, int64_t N, int64_t skip, int64_t *out) {
+static int64_t v2_exact(int64_t epoch, int64_t old_start, int64_t new_start, int64_t ns,
+                        int64_t B, int64_t N, int64_t skip, int64_t limit, int64_t *out) {
     orc_mt s;
     int64_t cap = B > 0 ? B : 1;
     int64_t *p1 = (int64_t *)malloc(sizeof(int64_t) * (size_t)(cap + 1));
@@ -231,9 +231,21 @@ int64_t orc_v2_exact_stream(int64_t epoch, int64_t old_start, int64_t new_start,
             for (int64_t v = lo; v < hi; v++) p2[n2++] = v;
         }
         if (drawn++ >= skip) out[n_out++] = wrap_id(index, N);
+        if (limit >= 0 && n_out >= limit) break;
     }
     free(p1); free(p2);
     return n_out;
+}
+
+int64_t orc_v2_exact_stream(int64_t epoch, int64_t old_start, int64_t new_start, int64_t ns,
+                            int64_t B, int64_t N, int64_t skip, int64_t *out) {
+    return v2_exact(epoch, old_start, new_start, ns, B, N, skip, -1, out);
+}
+
+/* the first `limit` ids only (bench.py's bounded cpu_baseline sample) */
+int64_t orc_v2_exact_prefix(int64_t epoch, int64_t old_start, int64_t new_start, int64_t ns,
+                            int64_t B, int64_t N, int64_t limit, int64_t *out) {
+    return v2_exact(epoch, old_start, new_start, ns, B, N, 0, limit, out);
 }
 
 /* ------------------------------------------------------------------------------------ */

@@ -30,6 +30,16 @@ struct V2Plan {         // slot-machine tiling of one V2 stream (DESIGN.md §3.3
     int32_t global_buf; // 1: slot table lives in HBM scratch (P1 beyond the LDS budget)
 };
 
+// optional per-kernel timing: `mark(ctx, kind, stream)` is called right before each launch
+// and once more (kind = -1) after the last one; the runtime records HIP events there.
+enum KernelKind { K_SCAN = 0, K_V1 = 1, K_V2_LASTOCC = 2, K_V2_EMIT = 3, K_V2_TAIL = 4,
+                  K_MAP = 5, K_PARTITION = 6, K_DIGEST = 7, K_NUM_KINDS = 8 };
+struct Marker {
+    void (*mark)(void *ctx, int kind, hipStream_t s) = nullptr;
+    void *ctx = nullptr;
+    void operator()(int kind, hipStream_t s) const { if (mark) mark(ctx, kind, s); }
+};
+
 constexpr int kLdsSortMax = 16384;  // largest pool sorted entirely in LDS
 constexpr int kLdsSlotMax = 16384;  // largest V2 slot table kept in LDS
 constexpr uint32_t kNone = 0xFFFFFFFFu;
@@ -55,13 +65,14 @@ hipError_t launch_digest_range(int64_t lo, int64_t hi, uint64_t *acc, hipStream_
 // V1: ids of positions [pos_lo, pos_lo+count) of ranks [rank_lo, rank_lo+nr) -> out[r][count]
 hipError_t launch_v1(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, int32_t nr,
                      int64_t pos_lo, int64_t count, int64_t *out, uint32_t *sort_ws,
-                     int32_t *err, hipStream_t s);
+                     int32_t *err, hipStream_t s, const Marker &mk = Marker());
 size_t v1_workspace_bytes(const Geometry &g, int32_t nr, int64_t pos_lo, int64_t count);
 
 // V2: same contract; val_ws holds the per-tile slot tables
 hipError_t launch_v2(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, int32_t nr,
                      int64_t pos_lo, int64_t count, int64_t *out, uint32_t *val_ws,
-                     uint32_t *buf_ws, uint32_t *sort_ws, int32_t *err, hipStream_t s);
+                     uint32_t *buf_ws, uint32_t *sort_ws, int32_t *err, hipStream_t s,
+                     const Marker &mk = Marker());
 size_t v2_val_bytes(const Geometry &g, int32_t nr);
 size_t v2_buf_bytes(const Geometry &g, int32_t nr);
 size_t v2_sort_bytes(const Geometry &g, int32_t nr);
@@ -70,5 +81,7 @@ size_t v2_sort_bytes(const Geometry &g, int32_t nr);
 hipError_t launch_debug_wave_scan(const uint64_t *in, uint64_t *out, int64_t n, hipStream_t s);
 
 hipError_t init_kernel_attributes();
+
+
 
 }  // namespace pss

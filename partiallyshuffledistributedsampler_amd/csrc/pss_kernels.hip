@@ -610,17 +610,19 @@ size_t v1_workspace_bytes(const Geometry &, int32_t, int64_t, int64_t) { return 
 
 hipError_t launch_v1(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, int32_t nr,
                      int64_t pos_lo, int64_t count, int64_t *out, uint32_t *, int32_t *,
-                     hipStream_t s) {
+                     hipStream_t s, const Marker &mk) {
     int64_t pos_hi = pos_lo + count < g.ns ? pos_lo + count : g.ns;
     if (nr <= 0 || pos_hi <= pos_lo) return hipSuccess;
     const int64_t w_lo = pos_lo / g.B, w_hi = (pos_hi - 1) / g.B;
     const int64_t nw = w_hi - w_lo + 1;
     const int64_t nmax = g.B < g.ns ? g.B : g.ns;
     if (nmax > kLdsSortMax) return hipErrorNotSupported;   // HBM multi-pass: see launch_v1_big
+    mk(K_V1, s);
     if (nmax <= 1024) launch_v1_ept<4>(g, ranks, rank_lo, nr, w_lo, nw, pos_lo, count, out, s);
     else if (nmax <= 4096) launch_v1_ept<16>(g, ranks, rank_lo, nr, w_lo, nw, pos_lo, count, out, s);
     else if (nmax <= 8192) launch_v1_ept<32>(g, ranks, rank_lo, nr, w_lo, nw, pos_lo, count, out, s);
     else launch_v1_ept<64>(g, ranks, rank_lo, nr, w_lo, nw, pos_lo, count, out, s);
+    mk(-1, s);
     return hipGetLastError();
 }
 
@@ -641,7 +643,7 @@ static void launch_tail_ept(const Geometry &g, const V2Plan &pl, const RankDesc 
 
 hipError_t launch_v2(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, int32_t nr,
                      int64_t pos_lo, int64_t count, int64_t *out, uint32_t *VAL, uint32_t *,
-                     uint32_t *, int32_t *, hipStream_t s) {
+                     uint32_t *, int32_t *, hipStream_t s, const Marker &mk) {
     const V2Plan pl = v2_plan(g);
     int64_t pos_hi = pos_lo + count < g.ns ? pos_lo + count : g.ns;
     if (nr <= 0 || pos_hi <= pos_lo) return hipSuccess;
@@ -653,24 +655,29 @@ hipError_t launch_v2(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, 
     if (pl.G > 0) {
         const int64_t last_emit = pos_lo < pl.T ? ((pos_hi < pl.T ? pos_hi : pl.T) - 1) / pl.L : -1;
         const int64_t g_need = need_tail ? pl.G : last_emit + 1;
-        if (g_need > 0)
+        if (g_need > 0) {
+            mk(K_V2_LASTOCC, s);
             hipLaunchKernelGGL(k_v2_lastocc, dim3((uint32_t)(nr * g_need)), dim3(256), lds_slot, s,
                                g, pl, rank_lo, g_need, VAL);
+        }
         // k_v2_lastocc indexes VAL by (rl*G + tile) with tile < g_need: consistent layout
         if (last_emit >= 0) {
             const int64_t g_lo = pos_lo / pl.L;
             const int64_t ng = last_emit - g_lo + 1;
+            mk(K_V2_EMIT, s);
             hipLaunchKernelGGL(k_v2_emit, dim3((uint32_t)(nr * ng)), dim3(64), lds_slot, s,
                                g, pl, ranks, rank_lo, g_lo, ng, (const uint32_t *)VAL, pos_lo, count, out);
         }
     }
     if (need_tail) {
+        mk(K_V2_TAIL, s);
         const int64_t P1 = pl.P1;
         if (P1 <= 1024) launch_tail_ept<4>(g, pl, ranks, rank_lo, nr, VAL, pos_lo, count, out, s);
         else if (P1 <= 4096) launch_tail_ept<16>(g, pl, ranks, rank_lo, nr, VAL, pos_lo, count, out, s);
         else if (P1 <= 8192) launch_tail_ept<32>(g, pl, ranks, rank_lo, nr, VAL, pos_lo, count, out, s);
         else launch_tail_ept<64>(g, pl, ranks, rank_lo, nr, VAL, pos_lo, count, out, s);
     }
+    mk(-1, s);
     return hipGetLastError();
 }
 

@@ -169,6 +169,14 @@ struct pss_sampler {
     pss::RankDesc *h_stage_ranks = nullptr;
     hipEvent_t upload_done = nullptr;
     bool upload_pending = false;
+    // optional per-kernel timing (pss_profile): events recorded around every launch
+    bool profiling = false;
+    std::vector<hipEvent_t> ev_pool;
+    size_t ev_used = 0;
+    struct Span { int kind; size_t a, b; };
+    std::vector<Span> spans;
+    int open_kind = -1;
+    size_t open_ev = 0;
 
     pss::Geometry geometry() const {
         pss::Geometry g{};
@@ -181,6 +189,27 @@ struct pss_sampler {
 };
 
 namespace {
+
+// Marker callback: close the open span (if any) and open one for `kind` (kind < 0: close).
+void prof_mark(void *ctx, int kind, hipStream_t s) {
+    pss_sampler *h = (pss_sampler *)ctx;
+    if (h->ev_used == h->ev_pool.size()) {
+        hipEvent_t e;
+        if (hipEventCreate(&e) != hipSuccess) return;
+        h->ev_pool.push_back(e);
+    }
+    const size_t e = h->ev_used++;
+    (void)hipEventRecord(h->ev_pool[e], s);
+    if (h->open_kind >= 0) h->spans.push_back({h->open_kind, h->open_ev, e});
+    h->open_kind = kind;
+    h->open_ev = e;
+}
+
+pss::Marker marker_of(pss_sampler *h) {
+    pss::Marker m;
+    if (h->profiling) { m.mark = prof_mark; m.ctx = h; }
+    return m;
+}
 
 int ensure_device(pss_sampler *h) {
     if (h->dev_init) return PSS_OK;
@@ -211,7 +240,10 @@ int prepare(pss_sampler *h, hipStream_t s) {
     PSS_HIP(hipMemcpyAsync(h->d_ranks.p, h->h_stage_ranks, sizeof(pss::RankDesc) * h->R, hipMemcpyHostToDevice, s));
     PSS_HIP(hipEventRecord(h->upload_done, s));
     h->upload_pending = true;
+    const pss::Marker mk = marker_of(h);
+    mk(pss::K_SCAN, s);
     PSS_HIP(pss::launch_scan_prefix(h->d_lens.p, h->d_order.p, h->F, h->d_prefix.p, s));
+    mk(-1, s);
     h->dirty = false;
     return PSS_OK;
 }
@@ -271,6 +303,7 @@ int pss_destroy(pss_sampler *h) {
         if (h->h_stage_order) (void)hipHostFree(h->h_stage_order);
         if (h->h_stage_ranks) (void)hipHostFree(h->h_stage_ranks);
         if (h->upload_done) (void)hipEventDestroy(h->upload_done);
+        for (hipEvent_t e : h->ev_pool) (void)hipEventDestroy(e);
     }
     delete h;
     return PSS_OK;
@@ -355,14 +388,40 @@ int pss_generate(pss_sampler *h, int32_t rank_lo, int32_t rank_hi, int64_t pos_l
     const int32_t nr = rank_hi - rank_lo;
     if (nr == 0 || count == 0 || pos_lo >= h->ns) return PSS_OK;
     const pss::Geometry g = h->geometry();
+    const pss::Marker mk = marker_of(h);
     if (h->version == 1) {
-        PSS_HIP(pss::launch_v1(g, h->d_ranks.p, rank_lo, nr, pos_lo, count, out_dev, h->d_sort.p, h->d_err.p, s));
+        PSS_HIP(pss::launch_v1(g, h->d_ranks.p, rank_lo, nr, pos_lo, count, out_dev, h->d_sort.p, h->d_err.p, s, mk));
     } else {
         const size_t vb = pss::v2_val_bytes(g, nr) / sizeof(uint32_t);
         PSS_HIP(h->d_val.ensure(vb));
         PSS_HIP(pss::launch_v2(g, h->d_ranks.p, rank_lo, nr, pos_lo, count, out_dev, h->d_val.p,
-                               h->d_buf.p, h->d_sort.p, h->d_err.p, s));
+                               h->d_buf.p, h->d_sort.p, h->d_err.p, s, mk));
     }
+    return PSS_OK;
+}
+
+int pss_profile(pss_sampler *h, int32_t enable) {
+    if (!h) return fail(PSS_EINVAL, "NULL handle");
+    h->profiling = enable != 0;
+    h->spans.clear();
+    h->ev_used = 0;
+    h->open_kind = -1;
+    return PSS_OK;
+}
+
+int pss_profile_read(pss_sampler *h, double *total_ms, int64_t *launches, int32_t nkinds) {
+    if (!h || !total_ms || !launches) return fail(PSS_EINVAL, "NULL argument");
+    DeviceGuard dg(h->device);
+    for (int32_t k = 0; k < nkinds; k++) { total_ms[k] = 0; launches[k] = 0; }
+    for (const auto &sp : h->spans) {
+        PSS_HIP(hipEventSynchronize(h->ev_pool[sp.b]));
+        float ms = 0.f;
+        PSS_HIP(hipEventElapsedTime(&ms, h->ev_pool[sp.a], h->ev_pool[sp.b]));
+        if (sp.kind >= 0 && sp.kind < nkinds) { total_ms[sp.kind] += ms; launches[sp.kind] += 1; }
+    }
+    h->spans.clear();
+    h->ev_used = 0;
+    h->open_kind = -1;
     return PSS_OK;
 }
 

@@ -144,6 +144,21 @@ class IndexEngine:
         d = self._dev()
         _lib.call("pss_check", self._h, _stream_ptr(stream, d))
 
+    KERNEL_KINDS = ("scan", "v1_window", "v2_lastocc", "v2_emit", "v2_tail", "map",
+                    "partition", "digest")
+
+    def profile(self, enable=True):
+        """Bracket every launch of this handle with HIP events on its stream."""
+        _lib.call("pss_profile", self._h, int(bool(enable)))
+
+    def profile_read(self):
+        """{kind: (total_ms, launches)} since the last read (synchronises on the events)."""
+        n = len(self.KERNEL_KINDS)
+        ms = (ctypes.c_double * n)()
+        cnt = (ctypes.c_int64 * n)()
+        _lib.call("pss_profile_read", self._h, ms, cnt, n)
+        return {k: (ms[i], cnt[i]) for i, k in enumerate(self.KERNEL_KINDS) if cnt[i]}
+
 
 def digest(ids, acc=None, stream=None):
     """acc (int64 device tensor holding a uint64 bit pattern) += sum(splitmix64(ids))."""
