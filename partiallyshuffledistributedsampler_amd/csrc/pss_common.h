@@ -46,9 +46,7 @@ PSS_HD uint32_t lowbias32(uint32_t x) {
 }
 
 PSS_HD int ceil_log2_u64(uint64_t n) {  // smallest b with 2^b >= n (n >= 1)
-    int b = 0;
-    while ((1ull << b) < n) b++;
-    return b;
+    return n <= 1 ? 0 : 64 - __builtin_clzll(n - 1);
 }
 
 // Keyed bijection of [0, n): 4-round balanced Feistel over 2h bits + cycle walking.

@@ -19,6 +19,8 @@
 #include "pss_common.h"
 #include "pss_kernels.h"
 
+#include <cstdlib>
+
 namespace pss {
 
 // ------------------------------------------------------------------------------------------
@@ -457,7 +459,13 @@ __global__ __launch_bounds__(64) void k_v2_emit(Geometry g, V2Plan pl,
                                                 int64_t *__restrict__ out) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     const int P1 = (int)pl.P1;
-    uint32_t *buf = smem, *rk = smem + P1;
+    uint32_t *buf = smem;                                   // slot table: P1 virtual ids
+    uint32_t *rk = smem + P1;                               // Feistel keys of the tile's windows
+    const int64_t nwin_max = pl.L / g.B + 2;
+    // collision probe, P1 bytes; volatile so the read-back is never forwarded from the store,
+    // and explicitly in LDS (a generic volatile pointer would lower to flat sc0 sc1 accesses)
+    typedef __attribute__((address_space(3))) volatile uint8_t lds_vu8;
+    lds_vu8 *mark = (lds_vu8 *)(rk + 4 * nwin_max);
     const int lane = threadIdx.x;
     const int32_t rl = (int32_t)(blockIdx.x / ng);
     const int64_t tile = g_lo + (int64_t)(blockIdx.x % ng);
@@ -471,36 +479,87 @@ __global__ __launch_bounds__(64) void k_v2_emit(Geometry g, V2Plan pl,
     for (int s = lane; s < P1; s += 64) buf[s] = slot_value_after(VALr, pl, tile - 1, s);
     stage_round_keys(g, rank, w_lo, nwin, rk);
     __syncthreads();
-    const InsCtx ic{rk, w_lo};
-    const int kbits = ceil_log2_u64((uint64_t)P1);
     const uint64_t lt_mask = (1ull << lane) - 1ull;
     const uint64_t gt_mask = ~lt_mask << 1;
     const int64_t sb_lo = tlo >> 8, sb_hi = (thi - 1) >> 8;
+    // tile-local 32-bit step index tl = t - tlo; the tile emits tl in [e_lo, e_hi)
     const int64_t pos_hi = pos_lo + count;
-    int64_t *o = out + (int64_t)rl * count - pos_lo;
-    for (int64_t sb = sb_lo; sb <= sb_hi; sb++) {
+    const uint32_t nvalid = (uint32_t)(thi - tlo);
+    const uint32_t e_lo = (uint32_t)(pos_lo > tlo ? (pos_lo - tlo < nvalid ? pos_lo - tlo : nvalid) : 0);
+    const uint32_t e_hi = (uint32_t)(pos_hi < thi ? (pos_hi > tlo ? pos_hi - tlo : 0) : nvalid);
+    int64_t *o = out + (int64_t)rl * count + (tlo - pos_lo);
+    // ids: v < 2B came from the OLD start, the rest from the NEW one; 32-bit when N allows
+    const bool narrow = g.N + g.ns < (int64_t)UINT32_MAX;
+    const uint32_t twoB = (uint32_t)(2 * g.B < g.ns ? 2 * g.B : g.ns);
+    const uint32_t old32 = (uint32_t)rd.old_start, new32 = (uint32_t)rd.new_start;
+    const uint32_t N32 = (uint32_t)g.N;
+    // pool2 window bookkeeping without per-step division: (w0, p0) = window and insertion
+    // index of the sub-batch's first step t0, advanced by 64 per sub-batch.
+    const uint32_t B = (uint32_t)g.B;
+    const uint32_t hB = feistel_half_bits(B);
+    const uint32_t w_last = (uint32_t)(1 + (pl.T - 1) / g.B);     // last pool2 window (may be short)
+    const uint32_t len_last = (uint32_t)(g.ns - (int64_t)w_last * g.B);
+    const uint32_t h_last = feistel_half_bits(len_last);
+    const uint32_t w_lo32 = (uint32_t)w_lo;
+    const int64_t t_first = sb_lo * 256;
+    uint32_t w0 = (uint32_t)(1 + t_first / g.B);
+    uint32_t p0 = (uint32_t)(t_first - (int64_t)(w0 - 1) * g.B);
+    int32_t tl0 = (int32_t)(t_first - tlo);   // negative while the super-batch starts before the tile
+    for (int64_t sb = sb_lo; sb <= sb_hi; sb++, tl0 += 256) {
         uint32_t u[4];
         slot_words(g, rank, sb, lane, u);
 #pragma unroll
         for (int j = 0; j < 4; j++) {
-            const int64_t t = sb * 256 + j * 64 + lane;
-            const bool valid = t >= tlo && t < thi;
+            const int32_t tl = tl0 + j * 64 + lane;
+            const bool valid = (uint32_t)tl < nvalid;
             const uint32_t k = scale32(u[j], (uint32_t)P1);
-            uint64_t peers = __ballot(valid);
-            for (int b = 0; b < kbits; b++) {
-                const bool bit = (k >> b) & 1u;
-                const uint64_t m = __ballot(bit);
-                peers &= bit ? m : ~m;
+            // insertion of step t: window w, index p (p0 + lane crosses at most one window
+            // boundary when B >= 64; smaller pools loop)
+            uint32_t p = p0 + (uint32_t)lane;
+            uint32_t w = w0;
+            if (p >= B) {
+                p -= B; w++;
+                while (p >= B) { p -= B; w++; }
             }
-            const uint64_t lower = peers & lt_mask;
-            const bool last = (peers & gt_mask) == 0;
-            const uint32_t ins = valid ? ins_value(g, ic, t) : 0u;
+            uint32_t ins = 0;
+            if (valid) {
+                const bool lastw = w == w_last;
+                const uint32_t *kk = rk + 4 * (w - w_lo32);
+                ins = w * B + feistel(p, lastw ? len_last : B, lastw ? h_last : hB,
+                                      kk[0], kk[1], kk[2], kk[3]);
+            }
+            // collision probe: every valid lane writes its lane id to mark[k]; a lane that
+            // reads back another id shares its slot with a lane of this sub-batch
+            if (valid) mark[k] = (uint8_t)lane;
+            const bool clash = valid && mark[k] != (uint8_t)lane;
+            // peers of each clashing slot: one compare + ballot per distinct slot
+            uint64_t cm = __ballot(clash);
+            uint64_t lower = 0;
+            bool last = true;
+            while (cm) {
+                const int c = __ffsll((long long)cm) - 1;
+                const uint32_t sc = (uint32_t)__builtin_amdgcn_readlane((int)k, c);
+                const bool same = valid && k == sc;
+                const uint64_t m = __ballot(same);
+                if (same) { lower = m & lt_mask; last = (m & gt_mask) == 0; }
+                cm &= ~m;
+            }
             const int src = lower ? 63 - __clzll((long long)lower) : lane;
             const uint32_t from_peer = (uint32_t)__shfl((int)ins, src);
             const uint32_t from_buf = buf[k];
             const uint32_t v = lower ? from_peer : from_buf;
             if (valid && last) buf[k] = ins;
-            if (valid && t >= pos_lo && t < pos_hi) o[t] = v2_id(v, rd, g);
+            if ((uint32_t)tl >= e_lo && (uint32_t)tl < e_hi) {
+                if (narrow) {
+                    uint32_t id = (v < twoB ? old32 : new32) + v;
+                    id = id >= N32 ? id - N32 : id;
+                    o[tl] = (int64_t)id;
+                } else {
+                    o[tl] = v2_id(v, rd, g);
+                }
+            }
+            p0 += 64;
+            while (p0 >= B) { p0 -= B; w0++; }
         }
     }
 }
@@ -541,7 +600,11 @@ V2Plan v2_plan(const Geometry &g) {
     p.P1 = g.B < g.ns ? g.B : g.ns;
     p.T = g.ns - p.P1;
     p.global_buf = p.P1 > kLdsSlotMax;
-    const int64_t mult = 16;
+    static const int64_t mult = [] {
+        const char *e = getenv("PSS_V2_TILE_MULT");   // tuning knob: tile = mult * P1 steps
+        const long v = e ? atol(e) : 0;
+        return (int64_t)(v > 0 ? v : 16);
+    }();
     p.L = cdiv(mult * p.P1, 256) * 256;
     p.G = p.T > 0 ? cdiv(p.T, p.L) : 0;
     return p;
@@ -649,7 +712,8 @@ hipError_t launch_v2(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, 
     if (nr <= 0 || pos_hi <= pos_lo) return hipSuccess;
     if (pl.P1 > kLdsSlotMax || pl.P1 > kLdsSortMax) return hipErrorNotSupported;
     const int64_t nwin_max = pl.L / g.B + 2;
-    const size_t lds_slot = (size_t)(pl.P1 + 4 * nwin_max) * sizeof(uint32_t);
+    const size_t lds_slot = (size_t)(pl.P1 + 4 * nwin_max) * sizeof(uint32_t) +
+                            (size_t)((pl.P1 + 15) / 16 * 16);   // + collision-probe bytes
     const bool need_tail = pos_hi > pl.T;
     // tiles needed: pass A over [0, g_need), pass B over the tiles overlapping the range
     if (pl.G > 0) {
