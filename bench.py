@@ -26,7 +26,9 @@ import torch.distributed as dist
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-from partiallyshuffledistributedsampler_amd.engine import IndexEngine, as_u64, digest, digest_range  # noqa: E402
+from partiallyshuffledistributedsampler_amd.distributed import (  # noqa: E402
+    coverage_ok, expected_digest_gpu, gather_pairs, shard)
+from partiallyshuffledistributedsampler_amd.engine import IndexEngine, as_u64, digest  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 BYTES_PER_ID = 8               # one int64 id written per emitted index
@@ -137,7 +139,7 @@ def main():
     lengths = np.full(F, L, dtype=np.int64)
     eng = IndexEngine(lengths, N, R, B, ver, shuffle=True, seed=0, device=local)
     ns = eng.num_samples
-    r_lo, r_hi = rank * RG, (rank + 1) * RG
+    r_lo, r_hi = shard(R, world, rank)
     out = torch.empty((RG, ns), dtype=torch.int64, device=dev)
     stream = torch.cuda.current_stream(dev)
 
@@ -166,21 +168,10 @@ def main():
     eng.profile(False)
 
     # coverage of the last epoch across all GPUs: (count, digest) all-gather over RCCL
-    acc = digest(out.view(-1))
-    cnt = torch.tensor([out.numel()], dtype=torch.int64, device=dev)
-    pair = torch.stack([cnt.view(()), acc.view(())]).view(1, 2)
-    if world > 1:
-        gathered = [torch.empty_like(pair) for _ in range(world)]
-        dist.all_gather(gathered, pair)
-        pairs = torch.cat(gathered).cpu().numpy()
-    else:
-        pairs = pair.cpu().numpy()
-    coverage_ok = None
+    pairs = gather_pairs(out.numel(), as_u64(digest(out.view(-1))), device=dev)
+    coverage = None
     if rank == 0:
-        pad = ns * R - N
-        expect = (as_u64(digest_range(0, N, dev)) + as_u64(digest_range(0, pad, dev))) & (2 ** 64 - 1)
-        got = int(sum(int(x) & (2 ** 64 - 1) for x in pairs[:, 1])) & (2 ** 64 - 1)
-        coverage_ok = bool(int(pairs[:, 0].sum()) == ns * R and got == expect)
+        coverage = coverage_ok(pairs, ns, R, expected_digest_gpu(N, ns, R, dev))
 
     ids_total = RG * ns * world * args.steps
     value = ids_total / dt / 1e9
@@ -218,7 +209,7 @@ def main():
                      "traffic": traffic, "launch_ms": per_launch_ms,
                      "algorithmic_bytes_per_launch": units * BYTES_PER_ID},
         "kernels_ms_per_step": {k: v[0] / max(1, args.steps) for k, v in prof.items()},
-        "coverage_ok": coverage_ok,
+        "coverage_ok": coverage,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline()

@@ -1,0 +1,184 @@
+// pss_device.h -- wave64 / workgroup primitives shared by the gfx950 kernels.
+#pragma once
+#include "pss_common.h"
+#include "pss_kernels.h"
+
+namespace pss {
+
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t x) {
+    // old = 0: lanes whose source is outside the row (or whose row is masked) read 0
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, ROWMASK, 0xF, false);
+}
+
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ uint64_t dpp_u64(uint64_t x) {
+    const uint32_t lo = dpp_u32<CTRL, ROWMASK>((uint32_t)x);
+    const uint32_t hi = dpp_u32<CTRL, ROWMASK>((uint32_t)(x >> 32));
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// Inclusive wave64 scan: row_shr 1/2/4/8 inside each 16-lane row, then row_bcast15 and
+// row_bcast31 carry the row totals across rows (gfx9 DPP; no LDS traffic).
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
+    x += dpp_u32<0x111, 0xF>(x);
+    x += dpp_u32<0x112, 0xF>(x);
+    x += dpp_u32<0x114, 0xF>(x);
+    x += dpp_u32<0x118, 0xF>(x);
+    x += dpp_u32<0x142, 0xA>(x);
+    x += dpp_u32<0x143, 0xC>(x);
+    return x;
+}
+
+__device__ __forceinline__ uint64_t wave_incl_scan(uint64_t x) {
+    x += dpp_u64<0x111, 0xF>(x);
+    x += dpp_u64<0x112, 0xF>(x);
+    x += dpp_u64<0x114, 0xF>(x);
+    x += dpp_u64<0x118, 0xF>(x);
+    x += dpp_u64<0x142, 0xA>(x);
+    x += dpp_u64<0x143, 0xC>(x);
+    return x;
+}
+
+__device__ __forceinline__ uint64_t wave_sum(uint64_t x) {
+    x = wave_incl_scan(x);
+    return __shfl(x, 63);
+}
+
+// Exclusive scan over a workgroup of NT threads; `tot` is NT/64 words of LDS.
+template <int NT, typename T>
+__device__ __forceinline__ T block_excl_scan(T x, T *tot, T &total) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const T inc = wave_incl_scan(x);
+    if (lane == 63) tot[wid] = inc;
+    __syncthreads();
+    T pre = 0, all = 0;
+#pragma unroll
+    for (int i = 0; i < NT / 64; i++) {
+        const T v = tot[i];
+        if (i < wid) pre += v;
+        all += v;
+    }
+    __syncthreads();
+    total = all;
+    return pre + inc - x;
+}
+
+__device__ __forceinline__ int64_t wrap_id(int64_t id, int64_t N) { return id >= N ? id - N : id; }
+
+// ------------------------------------------------------------------------------------------
+// LDS pool permutation: perm = stable argsort of Philox keys (i>>2, c1, rank, dom)[i&3].
+// One 256-thread workgroup, n <= 256*EPT.  Keys stay in registers; LDS holds a 2^hb-bucket
+// histogram (hb = ceil(log2 n), i.e. the keys' top hb bits) and the n packed slots
+// (low 32-hb key bits << hb | i).  A bucket averages one element, so the in-bucket fix-up is
+// a short insertion sort.  Result: S[p] & (2^hb - 1) = index of the p-th smallest key.
+// ------------------------------------------------------------------------------------------
+template <int EPT>
+__device__ __forceinline__ int block_sort_keys(uint32_t k0, uint32_t k1, uint32_t c1,
+                                               uint32_t rank, uint32_t dom, int n,
+                                               uint32_t *S, uint32_t *hist, uint32_t *tot) {
+    constexpr int NQ = EPT / 4;
+    const int tid = threadIdx.x;
+    const int hb = n > 1 ? ceil_log2_u64((uint64_t)n) : 0;
+    const int nb = 1 << hb;
+    uint32_t key[NQ][4];
+#pragma unroll
+    for (int j = 0; j < NQ; j++) {
+        uint32_t c0 = (uint32_t)(tid + 256 * j), cc1 = c1, c2 = rank, c3 = dom;
+        philox4x32_10(c0, cc1, c2, c3, k0, k1);
+        key[j][0] = c0; key[j][1] = cc1; key[j][2] = c2; key[j][3] = c3;
+    }
+    for (int i = tid; i < nb; i += 256) hist[i] = 0;
+    __syncthreads();
+    const int sh = 32 - hb;
+#pragma unroll
+    for (int j = 0; j < NQ; j++)
+#pragma unroll
+        for (int w = 0; w < 4; w++) {
+            const int i = 4 * (tid + 256 * j) + w;
+            if (i < n) atomicAdd(&hist[hb ? key[j][w] >> sh : 0], 1u);
+        }
+    __syncthreads();
+    const int per = nb >= 256 ? nb / 256 : 1;
+    const int blo = tid * per < nb ? tid * per : nb;
+    const int bhi = blo + per < nb ? blo + per : nb;
+    uint32_t s = 0;
+    for (int b = blo; b < bhi; b++) s += hist[b];
+    uint32_t total;
+    uint32_t run = block_excl_scan<256>(s, tot, total);
+    for (int b = blo; b < bhi; b++) { const uint32_t c = hist[b]; hist[b] = run; run += c; }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < NQ; j++)
+#pragma unroll
+        for (int w = 0; w < 4; w++) {
+            const int i = 4 * (tid + 256 * j) + w;
+            if (i < n) {
+                const uint32_t k = key[j][w];
+                const uint32_t pos = atomicAdd(&hist[hb ? k >> sh : 0], 1u);
+                S[pos] = hb ? ((k << hb) | (uint32_t)i) : 0u;
+            }
+        }
+    __syncthreads();
+    for (int b = blo; b < bhi; b++) {  // hist[b] is now the END of bucket b
+        const int e = (int)hist[b];
+        const int st = b ? (int)hist[b - 1] : 0;
+        for (int x = st + 1; x < e; x++) {
+            const uint32_t v = S[x];
+            int y = x - 1;
+            while (y >= st && S[y] > v) { S[y + 1] = S[y]; y--; }
+            S[y + 1] = v;
+        }
+    }
+    __syncthreads();
+    return hb;
+}
+
+template <int EPT>
+constexpr size_t sort_lds_bytes() { return (size_t)(2 * 256 * EPT + 16) * sizeof(uint32_t); }
+
+// ------------------------------------------------------------------------------------------
+// V2 helpers
+// ------------------------------------------------------------------------------------------
+// slot draw of step t: super-batch sb = t>>8 holds 256 steps; lane l of a wave draws the
+// Philox block (sb*64 + l) and its word j is the slot of step sb*256 + j*64 + l.
+__device__ __forceinline__ void slot_words(const Geometry &g, uint32_t rank, int64_t sb, int lane,
+                                           uint32_t u[4]) {
+    const uint64_t c = (uint64_t)sb * 64u + (uint64_t)lane;
+    uint32_t c0 = (uint32_t)c, c1 = (uint32_t)(c >> 32), c2 = rank, c3 = DOM_V2_SLOT;
+    philox4x32_10(c0, c1, c2, c3, g.key0, g.key1);
+    u[0] = c0; u[1] = c1; u[2] = c2; u[3] = c3;
+}
+
+__device__ __forceinline__ void window_round_keys(const Geometry &g, uint32_t rank, int64_t w,
+                                                  uint32_t k[4]) {
+    uint32_t c0 = (uint32_t)w, c1 = 0, c2 = rank, c3 = DOM_V2_INS;
+    philox4x32_10(c0, c1, c2, c3, g.key0, g.key1);
+    k[0] = c0; k[1] = c1; k[2] = c2; k[3] = c3;
+}
+
+// virtual index inserted at step t (pool2 window w = 1 + t/B in Feistel order), given the
+// window's round keys
+__device__ __forceinline__ uint32_t ins_value_k(const Geometry &g, int64_t t, const uint32_t *k) {
+    const int64_t w = 1 + t / g.B;
+    const int64_t p = t - (w - 1) * g.B;
+    const int64_t rem = g.ns - w * g.B;
+    const uint32_t len = (uint32_t)(rem < g.B ? rem : g.B);
+    return (uint32_t)(w * g.B) + feistel((uint32_t)p, len, feistel_half_bits(len), k[0], k[1], k[2], k[3]);
+}
+
+__device__ __forceinline__ int64_t v2_id(uint32_t v, const RankDesc &rd, const Geometry &g) {
+    return wrap_id(((int64_t)v < 2 * g.B ? rd.old_start : rd.new_start) + (int64_t)v, g.N);
+}
+
+// value held by slot s after tile `tile` (walk back over tiles that never drew s)
+__device__ __forceinline__ uint32_t slot_value_after(const uint32_t *VALr, int64_t P1,
+                                                     int64_t tile, int64_t s) {
+    for (int64_t gg = tile; gg >= 0; gg--) {
+        const uint32_t v = VALr[gg * P1 + s];
+        if (v != kNone) return v;
+    }
+    return (uint32_t)s;  // initial pool1 = window 0 in slot order
+}
+
+}  // namespace pss

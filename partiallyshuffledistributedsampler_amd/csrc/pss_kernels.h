@@ -43,6 +43,51 @@ struct Marker {
 constexpr int kLdsSortMax = 16384;  // largest pool sorted entirely in LDS
 constexpr int kLdsSlotMax = 16384;  // largest V2 slot table kept in LDS
 constexpr uint32_t kNone = 0xFFFFFFFFu;
+constexpr int kMarkBytes = 4096;    // V2 collision-probe bytes in LDS (slot & 4095)
+constexpr int kBucketCap = 8192;    // largest bucket the HBM multi-pass sort finishes in LDS
+
+// Pools too large for LDS (pss_bigsort.hip): a batch of independent permutation jobs.
+// Job j of the batch -> (rank, counter word c1, length n); all share the Philox domain.
+struct SortJobs {
+    int32_t kind;        // 0: V1 windows, j = rl*nw + (w - w_lo);  1: V2 tails, j = rl
+    int32_t rank_lo;
+    int64_t nw, w_lo;    // V1
+    int64_t B, ns, P1;
+    int64_t nmax;        // longest job
+    uint32_t dom;
+};
+
+__host__ __device__ inline void sort_job(const SortJobs &J, int64_t j, uint32_t &rank,
+                                         uint32_t &c1, int64_t &n) {
+    if (J.kind == 0) {
+        const int64_t rl = j / J.nw, w = J.w_lo + j % J.nw;
+        rank = (uint32_t)(J.rank_lo + rl);
+        c1 = (uint32_t)w;
+        const int64_t rem = J.ns - w * J.B;
+        n = rem < J.B ? rem : J.B;
+    } else {
+        rank = (uint32_t)(J.rank_lo + j);
+        c1 = 0;
+        n = J.P1;
+    }
+}
+
+struct BigSortWS {       // per batch of nj jobs, stride nmax (see big_sort_bytes)
+    uint32_t *start;     // [nj][nb + 1] bucket starts (exclusive scan), start[nb] = n
+    uint32_t *cur;       // [nj][nb]     scatter cursors
+    uint64_t *tmp;       // [nj][nmax]   (key << 32 | index) in bucket order
+    uint32_t *perm;      // [nj][nmax]   sorted indices
+    int64_t nb, nmax;
+    int32_t hb;          // bucket bits
+};
+size_t big_sort_bytes(int64_t nmax, int64_t nj);
+BigSortWS big_sort_ws(void *base, int64_t nmax, int64_t nj);
+// sorts jobs [job_lo, job_lo + nj) into ws.perm
+hipError_t launch_big_sort(const Geometry &g, const SortJobs &J, int64_t job_lo, int64_t nj,
+                           const BigSortWS &ws, int32_t *err, hipStream_t s);
+// jobs per batch so that one batch's workspace stays within `budget` bytes
+int64_t big_sort_batch(int64_t nmax, int64_t njobs, size_t budget);
+constexpr size_t kBigSortBudget = (size_t)2 << 30;
 
 V2Plan v2_plan(const Geometry &g);
 
@@ -81,6 +126,8 @@ size_t v2_sort_bytes(const Geometry &g, int32_t nr);
 hipError_t launch_debug_wave_scan(const uint64_t *in, uint64_t *out, int64_t n, hipStream_t s);
 
 hipError_t init_kernel_attributes();
+hipError_t init_kernel_attributes_v2();
+hipError_t init_kernel_attributes_bigsort();
 
 
 

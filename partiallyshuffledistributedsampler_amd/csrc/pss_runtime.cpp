@@ -389,11 +389,16 @@ int pss_generate(pss_sampler *h, int32_t rank_lo, int32_t rank_hi, int64_t pos_l
     if (nr == 0 || count == 0 || pos_lo >= h->ns) return PSS_OK;
     const pss::Geometry g = h->geometry();
     const pss::Marker mk = marker_of(h);
+    auto words = [](size_t bytes) { return (bytes + sizeof(uint32_t) - 1) / sizeof(uint32_t); };
     if (h->version == 1) {
+        const size_t sb = pss::v1_workspace_bytes(g, nr, pos_lo, count);
+        if (sb) PSS_HIP(h->d_sort.ensure(words(sb)));
         PSS_HIP(pss::launch_v1(g, h->d_ranks.p, rank_lo, nr, pos_lo, count, out_dev, h->d_sort.p, h->d_err.p, s, mk));
     } else {
-        const size_t vb = pss::v2_val_bytes(g, nr) / sizeof(uint32_t);
-        PSS_HIP(h->d_val.ensure(vb));
+        PSS_HIP(h->d_val.ensure(words(pss::v2_val_bytes(g, nr))));
+        const size_t bb = pss::v2_buf_bytes(g, nr), sb = pss::v2_sort_bytes(g, nr);
+        if (bb) PSS_HIP(h->d_buf.ensure(words(bb)));
+        if (sb) PSS_HIP(h->d_sort.ensure(words(sb)));
         PSS_HIP(pss::launch_v2(g, h->d_ranks.p, rank_lo, nr, pos_lo, count, out_dev, h->d_val.p,
                                h->d_buf.p, h->d_sort.p, h->d_err.p, s, mk));
     }

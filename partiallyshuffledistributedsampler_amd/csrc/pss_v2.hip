@@ -1,0 +1,472 @@
+// pss_v2.hip -- the V2 two-pool shuffle buffer (V2:96-116) in slot-replacement form
+// (DESIGN.md §3.3):
+//
+//   k_v2_lastocc     pass A, slot table in LDS: per tile the last step that drew each slot
+//                    (order-independent ds_max) -> VAL[tile][s] = value inserted there
+//   k_v2_lastocc_g   pass A, slot table in HBM (pools > 16384): global atomicMax ...
+//   k_v2_convert_g   ... then last step -> inserted value, in place
+//   k_v2_init_g      HBM variant: slot table of each tile = state after the previous tile
+//   k_v2_emit<GBUF>  pass B: one wave replays a tile in step order, 64 steps per iteration;
+//                    each step exchanges its insertion into the drawn slot (ds_wrxchg_rtn /
+//                    global_atomic_swap) and emits what it held; lanes of one iteration that
+//                    drew the same slot are chained through ds_bpermute instead
+//   k_v2_tail<EPT>   the final pool1 drained in Philox-sorted order (LDS sort)
+//   k_v2_tail_big    ... or from the HBM multi-pass sort (pss_bigsort.hip)
+#include <cstdlib>
+
+#include "pss_device.h"
+
+namespace pss {
+
+
+static inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+__device__ __forceinline__ void tile_bounds(const V2Plan &pl, int64_t tile, int64_t &tlo,
+                                            int64_t &thi) {
+    tlo = tile * pl.L;
+    thi = tlo + pl.L < pl.T ? tlo + pl.L : pl.T;
+}
+
+__device__ __forceinline__ void stage_round_keys(const Geometry &g, uint32_t rank, int64_t w_lo,
+                                                 int nwin, uint32_t *rk) {
+    for (int j = threadIdx.x; j < nwin; j += blockDim.x) window_round_keys(g, rank, w_lo + j, rk + 4 * j);
+}
+
+// ---- pass A, LDS --------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_v2_lastocc(Geometry g, V2Plan pl, int32_t rank_lo,
+                                                    int64_t ng, uint32_t *__restrict__ VAL) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+    const int P1 = (int)pl.P1;
+    uint32_t *lastT = smem, *rk = smem + P1;
+    const int32_t rl = (int32_t)(blockIdx.x / ng);
+    const int64_t tile = (int64_t)(blockIdx.x % ng);
+    const uint32_t rank = (uint32_t)(rank_lo + rl);
+    int64_t tlo, thi;
+    tile_bounds(pl, tile, tlo, thi);
+    const int64_t w_lo = 1 + tlo / g.B;
+    const int nwin = (int)(1 + (thi - 1) / g.B - w_lo + 1);
+    for (int s = threadIdx.x; s < P1; s += 256) lastT[s] = 0;
+    stage_round_keys(g, rank, w_lo, nwin, rk);
+    __syncthreads();
+    const int64_t sb_lo = tlo >> 8, sb_hi = (thi - 1) >> 8;
+    const int64_t ncnt = (sb_hi - sb_lo + 1) * 64;
+    for (int64_t ci = threadIdx.x; ci < ncnt; ci += 256) {
+        const int64_t sb = sb_lo + (ci >> 6);
+        const int lane = (int)(ci & 63);
+        uint32_t u[4];
+        slot_words(g, rank, sb, lane, u);
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int64_t t = sb * 256 + j * 64 + lane;
+            if (t >= tlo && t < thi) atomicMax(&lastT[scale32(u[j], (uint32_t)P1)], (uint32_t)(t - tlo + 1));
+        }
+    }
+    __syncthreads();
+    uint32_t *V = VAL + ((int64_t)rl * pl.G + tile) * P1;
+    for (int s = threadIdx.x; s < P1; s += 256) {
+        const uint32_t lt = lastT[s];
+        if (!lt) { V[s] = kNone; continue; }
+        const int64_t t = tlo + (int64_t)lt - 1;
+        V[s] = ins_value_k(g, t, rk + 4 * (1 + t / g.B - w_lo));
+    }
+}
+
+// ---- pass A, HBM ----------------------------------------------------------------------------
+constexpr int64_t kLastoccChunk = 65536;   // steps per workgroup
+
+__global__ __launch_bounds__(256) void k_v2_lastocc_g(Geometry g, V2Plan pl, int32_t rank_lo,
+                                                      int64_t ng, uint32_t *__restrict__ VAL) {
+    const int64_t tiles = blockIdx.y;
+    const int32_t rl = (int32_t)(tiles / ng);
+    const int64_t tile = tiles % ng;
+    const uint32_t rank = (uint32_t)(rank_lo + rl);
+    int64_t tlo, thi;
+    tile_bounds(pl, tile, tlo, thi);
+    const int64_t clo = tlo + (int64_t)blockIdx.x * kLastoccChunk;
+    if (clo >= thi) return;
+    const int64_t chi = clo + kLastoccChunk < thi ? clo + kLastoccChunk : thi;
+    uint32_t *V = VAL + ((int64_t)rl * pl.G + tile) * pl.P1;
+    const int64_t sb_lo = clo >> 8, sb_hi = (chi - 1) >> 8;
+    const int64_t ncnt = (sb_hi - sb_lo + 1) * 64;
+    for (int64_t ci = threadIdx.x; ci < ncnt; ci += 256) {
+        const int64_t sb = sb_lo + (ci >> 6);
+        const int lane = (int)(ci & 63);
+        uint32_t u[4];
+        slot_words(g, rank, sb, lane, u);
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int64_t t = sb * 256 + j * 64 + lane;
+            if (t >= clo && t < chi) atomicMax(&V[scale32(u[j], (uint32_t)pl.P1)], (uint32_t)(t - tlo + 1));
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void k_v2_convert_g(Geometry g, V2Plan pl, int32_t rank_lo,
+                                                      int64_t ng, uint32_t *__restrict__ VAL) {
+    const int64_t tiles = blockIdx.y;
+    const int32_t rl = (int32_t)(tiles / ng);
+    const int64_t tile = tiles % ng;
+    const uint32_t rank = (uint32_t)(rank_lo + rl);
+    const int64_t tlo = tile * pl.L;
+    uint32_t *V = VAL + ((int64_t)rl * pl.G + tile) * pl.P1;
+    for (int64_t s = (int64_t)blockIdx.x * 256 + threadIdx.x; s < pl.P1; s += (int64_t)gridDim.x * 256) {
+        const uint32_t lt = V[s];
+        if (!lt) { V[s] = kNone; continue; }
+        const int64_t t = tlo + (int64_t)lt - 1;
+        uint32_t k[4];
+        window_round_keys(g, rank, 1 + t / g.B, k);
+        V[s] = ins_value_k(g, t, k);
+    }
+}
+
+__global__ __launch_bounds__(256) void k_v2_init_g(V2Plan pl, int64_t g_lo, int64_t ng,
+                                                   const uint32_t *__restrict__ VAL,
+                                                   uint32_t *__restrict__ gbuf) {
+    const int64_t tiles = blockIdx.y;
+    const int32_t rl = (int32_t)(tiles / ng);
+    const int64_t tile = g_lo + tiles % ng;
+    const uint32_t *VALr = VAL + (int64_t)rl * pl.G * pl.P1;
+    uint32_t *b = gbuf + ((int64_t)rl * pl.G + tile) * pl.P1;
+    for (int64_t s = (int64_t)blockIdx.x * 256 + threadIdx.x; s < pl.P1; s += (int64_t)gridDim.x * 256)
+        b[s] = slot_value_after(VALr, pl.P1, tile - 1, s);
+}
+
+// ---- pass B -------------------------------------------------------------------------------
+template <bool GBUF>
+__global__ __launch_bounds__(64) void k_v2_emit(Geometry g, V2Plan pl,
+                                                const RankDesc *__restrict__ ranks,
+                                                int32_t rank_lo, int64_t g_lo, int64_t ng,
+                                                const uint32_t *__restrict__ VAL,
+                                                uint32_t *__restrict__ gbuf,
+                                                int64_t pos_lo, int64_t count,
+                                                int64_t *__restrict__ out) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+    const int64_t P1 = pl.P1;
+    const int64_t nwin_max = pl.L / g.B + 2;
+    uint32_t *rk = smem;                                    // Feistel keys of the tile's windows
+    // collision probe (kMarkBytes, indexed by slot & 4095): volatile so the read-back is never
+    // forwarded from the store, explicitly in LDS (a generic volatile pointer -> flat sc0 sc1)
+    typedef __attribute__((address_space(3))) volatile uint8_t lds_vu8;
+    lds_vu8 *mark = (lds_vu8 *)(rk + 4 * nwin_max);
+    const int lane = threadIdx.x;
+    const int32_t rl = (int32_t)(blockIdx.x / ng);
+    const int64_t tile = g_lo + (int64_t)(blockIdx.x % ng);
+    const uint32_t rank = (uint32_t)(rank_lo + rl);
+    const RankDesc rd = ranks[rank];
+    int64_t tlo, thi;
+    tile_bounds(pl, tile, tlo, thi);
+    const int64_t w_lo = 1 + tlo / g.B;
+    const int nwin = (int)(1 + (thi - 1) / g.B - w_lo + 1);
+    uint32_t *buf;   // slot table: virtual ids held by the P1 slots at the tile's start
+    if (GBUF) {
+        buf = gbuf + ((int64_t)rl * pl.G + tile) * P1;      // filled by k_v2_init_g
+    } else {
+        buf = (uint32_t *)(smem + 4 * nwin_max + kMarkBytes / 4);
+        const uint32_t *VALr = VAL + (int64_t)rl * pl.G * P1;
+        const uint32_t *prev = VALr + (tile - 1) * P1;
+        for (int64_t s0 = lane; s0 < P1; s0 += 256) {       // 4 independent loads in flight
+            uint32_t v[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int64_t s = s0 + 64 * u;
+                v[u] = (tile > 0 && s < P1) ? prev[s] : kNone;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int64_t s = s0 + 64 * u;
+                if (s < P1) buf[s] = v[u] != kNone ? v[u] : slot_value_after(VALr, P1, tile - 2, s);
+            }
+        }
+    }
+    stage_round_keys(g, rank, w_lo, nwin, rk);
+    __syncthreads();
+    const uint64_t lt_mask = (1ull << lane) - 1ull;
+    const int64_t sb_lo = tlo >> 8, sb_hi = (thi - 1) >> 8;
+    // tile-local 32-bit step index tl = t - tlo; the tile emits tl in [e_lo, e_hi)
+    const int64_t pos_hi = pos_lo + count;
+    const uint32_t nvalid = (uint32_t)(thi - tlo);
+    const uint32_t e_lo = (uint32_t)(pos_lo > tlo ? (pos_lo - tlo < nvalid ? pos_lo - tlo : nvalid) : 0);
+    const uint32_t e_hi = (uint32_t)(pos_hi < thi ? (pos_hi > tlo ? pos_hi - tlo : 0) : nvalid);
+    int64_t *o = out + (int64_t)rl * count + (tlo - pos_lo);
+    // ids: v < 2B came from the OLD start, the rest from the NEW one; 32-bit when N allows
+    const bool narrow = g.N + g.ns < (int64_t)UINT32_MAX;
+    const uint32_t twoB = (uint32_t)(2 * g.B < g.ns ? 2 * g.B : g.ns);
+    const uint32_t old32 = (uint32_t)rd.old_start, new32 = (uint32_t)rd.new_start;
+    const uint32_t N32 = (uint32_t)g.N;
+    // pool2 window bookkeeping without per-step division: (w0, p0) = window and insertion
+    // index of the sub-batch's first step t0, advanced by 64 per sub-batch.
+    const uint32_t B = (uint32_t)g.B;
+    const uint32_t hB = feistel_half_bits(B);
+    const uint32_t w_last = (uint32_t)(1 + (pl.T - 1) / g.B);     // last pool2 window (may be short)
+    const uint32_t len_last = (uint32_t)(g.ns - (int64_t)w_last * g.B);
+    const uint32_t h_last = feistel_half_bits(len_last);
+    const uint32_t w_lo32 = (uint32_t)w_lo;
+    const int64_t t_first = sb_lo * 256;
+    uint32_t w0 = (uint32_t)(1 + t_first / g.B);
+    uint32_t p0 = (uint32_t)(t_first - (int64_t)(w0 - 1) * g.B);
+    int32_t tl0 = (int32_t)(t_first - tlo);   // negative while the super-batch starts before the tile
+    for (int64_t sb = sb_lo; sb <= sb_hi; sb++, tl0 += 256) {
+        uint32_t u[4];
+        slot_words(g, rank, sb, lane, u);
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int32_t tl = tl0 + j * 64 + lane;
+            const bool valid = (uint32_t)tl < nvalid;
+            const uint32_t k = scale32(u[j], (uint32_t)P1);
+            // insertion of step t: window w, index p (p0 + lane crosses at most one window
+            // boundary when B >= 64; smaller pools loop)
+            uint32_t p = p0 + (uint32_t)lane;
+            uint32_t w = w0;
+            if (p >= B) {
+                p -= B; w++;
+                while (p >= B) { p -= B; w++; }
+            }
+            uint32_t ins = 0;
+            if (valid) {
+                const bool lastw = w == w_last;
+                const uint32_t *kk = rk + 4 * (w - w_lo32);
+                ins = w * B + feistel(p, lastw ? len_last : B, lastw ? h_last : hB,
+                                      kk[0], kk[1], kk[2], kk[3]);
+            }
+            // collision probe: a lane that reads back another lane's id shares its probe
+            // byte (slot & 4095) with a lane of this sub-batch
+            const uint32_t hk = k & (uint32_t)(kMarkBytes - 1);
+            if (valid) mark[hk] = (uint8_t)lane;
+            const bool clash = valid && mark[hk] != (uint8_t)lane;
+            uint64_t cm = __ballot(clash);
+            uint32_t v;
+            if (cm == 0) {
+                // every valid lane drew a distinct slot: emit its content, insert in one op
+                v = valid ? atomicExch(&buf[k], ins) : 0u;
+            } else {
+                // peers = lanes that drew the same slot; the first of them exchanges the LAST
+                // peer's insertion, the others take the previous peer's insertion
+                uint64_t m = valid ? (1ull << lane) : 0ull;
+                while (cm) {
+                    const int c = __ffsll((long long)cm) - 1;
+                    const uint32_t sc = (uint32_t)__builtin_amdgcn_readlane((int)k, c);
+                    const bool same = valid && k == sc;
+                    const uint64_t mm = __ballot(same);
+                    if (same) m = mm;
+                    cm &= ~mm;
+                }
+                const uint64_t lower = m & lt_mask;
+                const int hi_lane = m ? 63 - __clzll((long long)m) : lane;
+                const int prev_lane = lower ? 63 - __clzll((long long)lower) : lane;
+                const uint32_t ins_last = (uint32_t)__shfl((int)ins, hi_lane);
+                const uint32_t ins_prev = (uint32_t)__shfl((int)ins, prev_lane);
+                v = (valid && !lower) ? atomicExch(&buf[k], ins_last) : ins_prev;
+            }
+            if ((uint32_t)tl >= e_lo && (uint32_t)tl < e_hi) {
+                if (narrow) {
+                    uint32_t id = (v < twoB ? old32 : new32) + v;
+                    id = id >= N32 ? id - N32 : id;
+                    o[tl] = (int64_t)id;
+                } else {
+                    o[tl] = v2_id(v, rd, g);
+                }
+            }
+            p0 += 64;
+            while (p0 >= B) { p0 -= B; w0++; }
+        }
+    }
+}
+
+// ---- tail ---------------------------------------------------------------------------------
+template <int EPT>
+__global__ __launch_bounds__(256) void k_v2_tail(Geometry g, V2Plan pl,
+                                                const RankDesc *__restrict__ ranks,
+                                                int32_t rank_lo, const uint32_t *__restrict__ VAL,
+                                                int64_t pos_lo, int64_t count,
+                                                int64_t *__restrict__ out) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+    uint32_t *S = smem, *hist = smem + 256 * EPT, *tot = hist + 256 * EPT;
+    const int32_t rl = (int32_t)blockIdx.x;
+    const uint32_t rank = (uint32_t)(rank_lo + rl);
+    const RankDesc rd = ranks[rank];
+    const int P1 = (int)pl.P1;
+    const int hb = block_sort_keys<EPT>(g.key0, g.key1, 0u, rank, DOM_V2_TAIL, P1, S, hist, tot);
+    const uint32_t mask = (1u << hb) - 1u;
+    const uint32_t *VALr = VAL + (int64_t)rl * pl.G * P1;
+    const uint32_t *last = VALr + (pl.G - 1) * P1;
+    int64_t *o = out + (int64_t)rl * count - pos_lo;
+    const int64_t pos_hi = pos_lo + count;
+    for (int j0 = threadIdx.x; j0 < P1; j0 += 1024) {        // 4 independent loads in flight
+        int s[4];
+        uint32_t v[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int j = j0 + 256 * u;
+            s[u] = j < P1 ? (int)(S[j] & mask) : 0;
+            v[u] = (j < P1 && pl.G > 0) ? last[s[u]] : kNone;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int j = j0 + 256 * u;
+            const int64_t pos = pl.T + j;
+            if (j >= P1 || pos < pos_lo || pos >= pos_hi) continue;
+            const uint32_t val = v[u] != kNone ? v[u] : slot_value_after(VALr, P1, pl.G - 2, s[u]);
+            o[pos] = v2_id(val, rd, g);
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void k_v2_tail_big(Geometry g, V2Plan pl,
+                                                    const RankDesc *__restrict__ ranks,
+                                                    SortJobs J, int64_t job_lo, BigSortWS ws,
+                                                    const uint32_t *__restrict__ VAL,
+                                                    int64_t pos_lo, int64_t count,
+                                                    int64_t *__restrict__ out) {
+    const int64_t jj = blockIdx.y;
+    const int64_t rl = job_lo + jj;
+    const uint32_t rank = (uint32_t)(J.rank_lo + rl);
+    const RankDesc rd = ranks[rank];
+    const uint32_t *perm = ws.perm + jj * ws.nmax;
+    const uint32_t *VALr = VAL + rl * pl.G * pl.P1;
+    int64_t *o = out + rl * count - pos_lo;
+    const int64_t pos_hi = pos_lo + count;
+    for (int64_t j = (int64_t)blockIdx.x * 1024 + threadIdx.x;
+         j < pl.P1 && j < (int64_t)(blockIdx.x + 1) * 1024; j += 256) {
+        const int64_t pos = pl.T + j;
+        if (pos < pos_lo || pos >= pos_hi) continue;
+        o[pos] = v2_id(slot_value_after(VALr, pl.P1, pl.G - 1, perm[j]), rd, g);
+    }
+}
+
+template <int EPT>
+static void launch_tail_ept(const Geometry &g, const V2Plan &pl, const RankDesc *ranks,
+                     int32_t rank_lo, int32_t nr, const uint32_t *VAL, int64_t pos_lo,
+                     int64_t count, int64_t *out, hipStream_t s) {
+    hipLaunchKernelGGL(k_v2_tail<EPT>, dim3((uint32_t)nr), dim3(256), sort_lds_bytes<EPT>(), s,
+                       g, pl, ranks, rank_lo, VAL, pos_lo, count, out);
+}
+
+static SortJobs tail_jobs(const Geometry &g, const V2Plan &pl, int32_t rank_lo) {
+    SortJobs J{};
+    J.kind = 1; J.rank_lo = rank_lo; J.nw = 1; J.w_lo = 0;
+    J.B = g.B; J.ns = g.ns; J.P1 = pl.P1; J.nmax = pl.P1; J.dom = DOM_V2_TAIL;
+    return J;
+}
+
+
+// ------------------------------------------------------------------------------------------
+// launchers
+// ------------------------------------------------------------------------------------------
+V2Plan v2_plan(const Geometry &g) {
+    V2Plan p{};
+    p.P1 = g.B < g.ns ? g.B : g.ns;
+    p.T = g.ns - p.P1;
+    p.global_buf = p.P1 > kLdsSlotMax;
+    static const int64_t mult_env = [] {
+        const char *e = getenv("PSS_V2_TILE_MULT");   // tuning knob: tile = mult * P1 steps
+        const long v = e ? atol(e) : 0;
+        return (int64_t)(v > 0 ? v : 0);
+    }();
+    const int64_t mult = mult_env ? mult_env : (p.global_buf ? 1 : 16);
+    p.L = cdiv(mult * p.P1, 256) * 256;
+    p.G = p.T > 0 ? cdiv(p.T, p.L) : 0;
+    return p;
+}
+
+size_t v2_val_bytes(const Geometry &g, int32_t nr) {
+    const V2Plan p = v2_plan(g);
+    return (size_t)nr * (size_t)p.G * (size_t)p.P1 * sizeof(uint32_t);
+}
+
+size_t v2_buf_bytes(const Geometry &g, int32_t nr) {
+    const V2Plan p = v2_plan(g);
+    return p.global_buf ? v2_val_bytes(g, nr) : 0;
+}
+
+size_t v2_sort_bytes(const Geometry &g, int32_t nr) {
+    const V2Plan p = v2_plan(g);
+    if (p.P1 <= kLdsSortMax || nr <= 0) return 0;
+    return big_sort_bytes(p.P1, big_sort_batch(p.P1, nr, kBigSortBudget));
+}
+
+hipError_t launch_v2(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, int32_t nr,
+                     int64_t pos_lo, int64_t count, int64_t *out, uint32_t *VAL, uint32_t *gbuf,
+                     uint32_t *sort_ws, int32_t *err, hipStream_t s, const Marker &mk) {
+    const V2Plan pl = v2_plan(g);
+    const int64_t pos_hi = pos_lo + count < g.ns ? pos_lo + count : g.ns;
+    if (nr <= 0 || pos_hi <= pos_lo) return hipSuccess;
+    const int64_t nwin_max = pl.L / g.B + 2;
+    const size_t lds_keys = (size_t)4 * nwin_max * sizeof(uint32_t);
+    const bool need_tail = pos_hi > pl.T;
+    if (pl.G > 0) {
+        // pass A over every tile up to the last one emitted (the tail needs all of them);
+        // VAL is indexed (rl*G + tile), tile < g_need
+        const int64_t last_emit = pos_lo < pl.T ? ((pos_hi < pl.T ? pos_hi : pl.T) - 1) / pl.L : -1;
+        const int64_t g_need = need_tail ? pl.G : last_emit + 1;
+        if (g_need > 0) {
+            mk(K_V2_LASTOCC, s);
+            if (!pl.global_buf) {
+                hipLaunchKernelGGL(k_v2_lastocc, dim3((uint32_t)(nr * g_need)), dim3(256),
+                                   (size_t)pl.P1 * 4 + lds_keys, s, g, pl, rank_lo, g_need, VAL);
+            } else {
+                hipError_t e = hipMemsetAsync(VAL, 0, v2_val_bytes(g, nr), s);
+                if (e != hipSuccess) return e;
+                hipLaunchKernelGGL(k_v2_lastocc_g, dim3((uint32_t)cdiv(pl.L, kLastoccChunk), (uint32_t)(nr * g_need)),
+                                   dim3(256), 0, s, g, pl, rank_lo, g_need, VAL);
+                hipLaunchKernelGGL(k_v2_convert_g, dim3((uint32_t)cdiv(pl.P1, 256), (uint32_t)(nr * g_need)),
+                                   dim3(256), 0, s, g, pl, rank_lo, g_need, VAL);
+            }
+        }
+        if (last_emit >= 0) {
+            const int64_t g_lo = pos_lo / pl.L;
+            const int64_t ng = last_emit - g_lo + 1;
+            if (!pl.global_buf) {
+                mk(K_V2_EMIT, s);
+                hipLaunchKernelGGL(k_v2_emit<false>, dim3((uint32_t)(nr * ng)), dim3(64),
+                                   lds_keys + kMarkBytes + (size_t)pl.P1 * 4, s,
+                                   g, pl, ranks, rank_lo, g_lo, ng, (const uint32_t *)VAL,
+                                   (uint32_t *)nullptr, pos_lo, count, out);
+            } else {
+                hipLaunchKernelGGL(k_v2_init_g, dim3((uint32_t)cdiv(pl.P1, 256), (uint32_t)(nr * ng)),
+                                   dim3(256), 0, s, pl, g_lo, ng, (const uint32_t *)VAL, gbuf);
+                mk(K_V2_EMIT, s);
+                hipLaunchKernelGGL(k_v2_emit<true>, dim3((uint32_t)(nr * ng)), dim3(64),
+                                   lds_keys + kMarkBytes, s,
+                                   g, pl, ranks, rank_lo, g_lo, ng, (const uint32_t *)VAL,
+                                   gbuf, pos_lo, count, out);
+            }
+        }
+    }
+    if (need_tail) {
+        mk(K_V2_TAIL, s);
+        const int64_t P1 = pl.P1;
+        if (P1 <= 1024) launch_tail_ept<4>(g, pl, ranks, rank_lo, nr, VAL, pos_lo, count, out, s);
+        else if (P1 <= 4096) launch_tail_ept<16>(g, pl, ranks, rank_lo, nr, VAL, pos_lo, count, out, s);
+        else if (P1 <= 8192) launch_tail_ept<32>(g, pl, ranks, rank_lo, nr, VAL, pos_lo, count, out, s);
+        else if (P1 <= kLdsSortMax) launch_tail_ept<64>(g, pl, ranks, rank_lo, nr, VAL, pos_lo, count, out, s);
+        else {
+            const SortJobs J = tail_jobs(g, pl, rank_lo);
+            const int64_t jb = big_sort_batch(P1, nr, kBigSortBudget);
+            const BigSortWS ws = big_sort_ws(sort_ws, P1, jb);
+            for (int64_t j0 = 0; j0 < nr; j0 += jb) {
+                const int64_t nj = nr - j0 < jb ? nr - j0 : jb;
+                hipError_t e = launch_big_sort(g, J, j0, nj, ws, err, s);
+                if (e != hipSuccess) return e;
+                hipLaunchKernelGGL(k_v2_tail_big, dim3((uint32_t)cdiv(P1, 1024), (uint32_t)nj), dim3(256), 0, s,
+                                   g, pl, ranks, J, j0, ws, (const uint32_t *)VAL, pos_lo, count, out);
+            }
+        }
+    }
+    mk(-1, s);
+    return hipGetLastError();
+}
+
+hipError_t init_kernel_attributes_v2() {
+    const int big = 160 * 1024;
+    hipError_t e = hipSuccess;
+#define PSS_ATTR(fn) { hipError_t x = hipFuncSetAttribute((const void *)(fn), hipFuncAttributeMaxDynamicSharedMemorySize, big); if (x != hipSuccess) e = x; }
+    PSS_ATTR(k_v2_tail<32>);
+    PSS_ATTR(k_v2_tail<64>);
+    PSS_ATTR(k_v2_lastocc);
+    PSS_ATTR(k_v2_emit<false>);
+    PSS_ATTR(k_v2_emit<true>);
+#undef PSS_ATTR
+    return e;
+}
+
+}  // namespace pss

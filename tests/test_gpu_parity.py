@@ -55,6 +55,9 @@ CONFIGS = [
     (13, (1, 50), 5, 100),        # ns < B
     (9, (20, 40), 2, 70),         # B < ns < 2B
     (100, (1, 3), 8, 7),          # tiny windows
+    (20, (5000, 20000), 2, 20000),      # pools beyond LDS: HBM multi-pass sort / HBM slot table
+    (12, (50000, 100000), 3, 70001),    # ... odd pool size, partial last window
+    (6, (1000, 3000), 2, 100000),       # ns < B with a big pool: tail only
 ]
 
 
