@@ -65,6 +65,18 @@ PSS_HD uint32_t feistel(uint32_t x, uint32_t n, uint32_t h, uint32_t rk0, uint32
     return x;
 }
 
+// One Feistel pass, for domains n == 2^(2h) where cycle walking never triggers.
+PSS_HD uint32_t feistel_once(uint32_t x, uint32_t h, uint32_t rk0, uint32_t rk1, uint32_t rk2,
+                             uint32_t rk3) {
+    const uint32_t mask = (1u << h) - 1u;
+    uint32_t L = x >> h, R = x & mask, t;
+    t = L ^ (lowbias32(R ^ rk0) & mask); L = R; R = t;
+    t = L ^ (lowbias32(R ^ rk1) & mask); L = R; R = t;
+    t = L ^ (lowbias32(R ^ rk2) & mask); L = R; R = t;
+    t = L ^ (lowbias32(R ^ rk3) & mask); L = R; R = t;
+    return (L << h) | R;
+}
+
 PSS_HD uint32_t feistel_half_bits(uint32_t n) {
     const int bits = ceil_log2_u64(n);
     return (uint32_t)((bits + 1) >> 1);

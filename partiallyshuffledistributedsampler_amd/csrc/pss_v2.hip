@@ -132,7 +132,94 @@ __global__ __launch_bounds__(256) void k_v2_init_g(V2Plan pl, int64_t g_lo, int6
 }
 
 // ---- pass B -------------------------------------------------------------------------------
-template <bool GBUF>
+// collision probe bytes live in LDS and are accessed volatile (the read-back must not be
+// forwarded from the store); the explicit address space keeps them ds_write_b8/ds_read_u8
+// (a generic volatile pointer lowers to flat sc0 sc1 accesses)
+typedef __attribute__((address_space(3))) volatile uint8_t lds_vu8;
+
+struct EmitCtx {   // per-tile constants of k_v2_emit + the running pool2 position (w0, p0)
+    uint64_t lt_mask;
+    uint32_t *buf;
+    lds_vu8 *mark;
+    const uint32_t *rk;
+    int64_t *o;
+    const Geometry *g;
+    RankDesc rd;
+    int lane;
+    uint32_t P1, nvalid, e_lo, e_hi;
+    uint32_t twoB, old32, new32, N32;
+    uint32_t B, hB, w_last, len_last, h_last, w_lo;
+    bool walk_full;
+    uint32_t w0, p0;
+
+    // One 64-step sub-batch (lane l = step tl).  FAST: every step valid and emitted.
+    template <bool FAST, bool NARROW>
+    __device__ __forceinline__ void step(uint32_t uword, int32_t tl) {
+        const bool valid = FAST || (uint32_t)tl < nvalid;
+        const uint32_t k = scale32(uword, P1);
+        // collision probe: a lane that reads back another lane's id shares its probe byte
+        // (slot & 4095) with a lane of this sub-batch
+        const uint32_t hk = k & (uint32_t)(kMarkBytes - 1);
+        if (valid) mark[hk] = (uint8_t)lane;
+        const uint8_t probe = mark[hk];
+        // insertion of step t (computed while the probe is in flight): window w, index p;
+        // p0 + lane crosses at most one window boundary when B >= 64, smaller pools loop
+        uint32_t p = p0 + (uint32_t)lane;
+        uint32_t w = w0;
+        if (p0 + 63u >= B) {                    // uniform: this sub-batch crosses a window
+            while (p >= B) { p -= B; w++; }
+        }
+        uint32_t ins = 0;
+        if (valid) {
+            const uint32_t *kk = rk + 4 * (w - w_lo);
+            if (!walk_full && w != w_last) {
+                ins = w * B + feistel_once(p, hB, kk[0], kk[1], kk[2], kk[3]);
+            } else {
+                const bool lastw = w == w_last;
+                ins = w * B + feistel(p, lastw ? len_last : B, lastw ? h_last : hB,
+                                      kk[0], kk[1], kk[2], kk[3]);
+            }
+        }
+        const bool clash = valid && probe != (uint8_t)lane;
+        uint64_t cm = __ballot(clash);
+        uint32_t v;
+        if (cm == 0) {
+            // every valid lane drew a distinct slot: emit its content, insert in one op
+            v = valid ? atomicExch(&buf[k], ins) : 0u;
+        } else {
+            // peers = lanes that drew the same slot; the first of them exchanges the LAST
+            // peer's insertion, the others take the previous peer's insertion
+            uint64_t m = valid ? (1ull << lane) : 0ull;
+            while (cm) {
+                const int cl = __ffsll((long long)cm) - 1;
+                const uint32_t sc = (uint32_t)__builtin_amdgcn_readlane((int)k, cl);
+                const bool same = valid && k == sc;
+                const uint64_t mm = __ballot(same);
+                if (same) m = mm;
+                cm &= ~mm;
+            }
+            const uint64_t lower = m & lt_mask;
+            const int hi_lane = m ? 63 - __clzll((long long)m) : lane;
+            const int prev_lane = lower ? 63 - __clzll((long long)lower) : lane;
+            const uint32_t ins_last = (uint32_t)__shfl((int)ins, hi_lane);
+            const uint32_t ins_prev = (uint32_t)__shfl((int)ins, prev_lane);
+            v = (valid && !lower) ? atomicExch(&buf[k], ins_last) : ins_prev;
+        }
+        if (FAST || ((uint32_t)tl >= e_lo && (uint32_t)tl < e_hi)) {
+            if (NARROW) {
+                uint32_t id = (v < twoB ? old32 : new32) + v;
+                id = id >= N32 ? id - N32 : id;
+                o[tl] = (int64_t)id;
+            } else {
+                o[tl] = v2_id(v, rd, *g);
+            }
+        }
+        p0 += 64;
+        while (p0 >= B) { p0 -= B; w0++; }
+    }
+};
+
+template <bool GBUF, bool NARROW>
 __global__ __launch_bounds__(64) void k_v2_emit(Geometry g, V2Plan pl,
                                                 const RankDesc *__restrict__ ranks,
                                                 int32_t rank_lo, int64_t g_lo, int64_t ng,
@@ -144,10 +231,7 @@ __global__ __launch_bounds__(64) void k_v2_emit(Geometry g, V2Plan pl,
     const int64_t P1 = pl.P1;
     const int64_t nwin_max = pl.L / g.B + 2;
     uint32_t *rk = smem;                                    // Feistel keys of the tile's windows
-    // collision probe (kMarkBytes, indexed by slot & 4095): volatile so the read-back is never
-    // forwarded from the store, explicitly in LDS (a generic volatile pointer -> flat sc0 sc1)
-    typedef __attribute__((address_space(3))) volatile uint8_t lds_vu8;
-    lds_vu8 *mark = (lds_vu8 *)(rk + 4 * nwin_max);
+    lds_vu8 *mark = (lds_vu8 *)(rk + 4 * nwin_max);         // collision probe, kMarkBytes
     const int lane = threadIdx.x;
     const int32_t rl = (int32_t)(blockIdx.x / ng);
     const int64_t tile = g_lo + (int64_t)(blockIdx.x % ng);
@@ -180,94 +264,49 @@ __global__ __launch_bounds__(64) void k_v2_emit(Geometry g, V2Plan pl,
     }
     stage_round_keys(g, rank, w_lo, nwin, rk);
     __syncthreads();
-    const uint64_t lt_mask = (1ull << lane) - 1ull;
+    EmitCtx c;
+    c.lane = lane;
+    c.lt_mask = (1ull << lane) - 1ull;
+    c.P1 = (uint32_t)P1;
+    c.buf = buf;
+    c.mark = mark;
+    c.rk = rk;
     const int64_t sb_lo = tlo >> 8, sb_hi = (thi - 1) >> 8;
     // tile-local 32-bit step index tl = t - tlo; the tile emits tl in [e_lo, e_hi)
     const int64_t pos_hi = pos_lo + count;
-    const uint32_t nvalid = (uint32_t)(thi - tlo);
-    const uint32_t e_lo = (uint32_t)(pos_lo > tlo ? (pos_lo - tlo < nvalid ? pos_lo - tlo : nvalid) : 0);
-    const uint32_t e_hi = (uint32_t)(pos_hi < thi ? (pos_hi > tlo ? pos_hi - tlo : 0) : nvalid);
-    int64_t *o = out + (int64_t)rl * count + (tlo - pos_lo);
-    // ids: v < 2B came from the OLD start, the rest from the NEW one; 32-bit when N allows
-    const bool narrow = g.N + g.ns < (int64_t)UINT32_MAX;
-    const uint32_t twoB = (uint32_t)(2 * g.B < g.ns ? 2 * g.B : g.ns);
-    const uint32_t old32 = (uint32_t)rd.old_start, new32 = (uint32_t)rd.new_start;
-    const uint32_t N32 = (uint32_t)g.N;
+    c.nvalid = (uint32_t)(thi - tlo);
+    c.e_lo = (uint32_t)(pos_lo > tlo ? (pos_lo - tlo < c.nvalid ? pos_lo - tlo : c.nvalid) : 0);
+    c.e_hi = (uint32_t)(pos_hi < thi ? (pos_hi > tlo ? pos_hi - tlo : 0) : c.nvalid);
+    c.o = out + (int64_t)rl * count + (tlo - pos_lo);
+    // ids: v < 2B came from the OLD start, the rest from the NEW one
+    c.twoB = (uint32_t)(2 * g.B < g.ns ? 2 * g.B : g.ns);
+    c.old32 = (uint32_t)rd.old_start; c.new32 = (uint32_t)rd.new_start;
+    c.N32 = (uint32_t)g.N;
+    c.rd = rd;
+    c.g = &g;
     // pool2 window bookkeeping without per-step division: (w0, p0) = window and insertion
     // index of the sub-batch's first step t0, advanced by 64 per sub-batch.
-    const uint32_t B = (uint32_t)g.B;
-    const uint32_t hB = feistel_half_bits(B);
-    const uint32_t w_last = (uint32_t)(1 + (pl.T - 1) / g.B);     // last pool2 window (may be short)
-    const uint32_t len_last = (uint32_t)(g.ns - (int64_t)w_last * g.B);
-    const uint32_t h_last = feistel_half_bits(len_last);
-    const uint32_t w_lo32 = (uint32_t)w_lo;
+    c.B = (uint32_t)g.B;
+    c.hB = feistel_half_bits(c.B);
+    c.walk_full = c.B != (1u << (2 * c.hB));      // full windows need cycle walking
+    c.w_last = (uint32_t)(1 + (pl.T - 1) / g.B);  // last pool2 window (may be short)
+    c.len_last = (uint32_t)(g.ns - (int64_t)c.w_last * g.B);
+    c.h_last = feistel_half_bits(c.len_last);
+    c.w_lo = (uint32_t)w_lo;
     const int64_t t_first = sb_lo * 256;
-    uint32_t w0 = (uint32_t)(1 + t_first / g.B);
-    uint32_t p0 = (uint32_t)(t_first - (int64_t)(w0 - 1) * g.B);
+    c.w0 = (uint32_t)(1 + t_first / g.B);
+    c.p0 = (uint32_t)(t_first - (int64_t)(c.w0 - 1) * g.B);
+    const bool full_emit = c.e_lo == 0 && c.e_hi == c.nvalid;
     int32_t tl0 = (int32_t)(t_first - tlo);   // negative while the super-batch starts before the tile
     for (int64_t sb = sb_lo; sb <= sb_hi; sb++, tl0 += 256) {
         uint32_t u[4];
         slot_words(g, rank, sb, lane, u);
+        if (full_emit && tl0 >= 0 && (uint32_t)tl0 + 256 <= c.nvalid) {   // uniform
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const int32_t tl = tl0 + j * 64 + lane;
-            const bool valid = (uint32_t)tl < nvalid;
-            const uint32_t k = scale32(u[j], (uint32_t)P1);
-            // insertion of step t: window w, index p (p0 + lane crosses at most one window
-            // boundary when B >= 64; smaller pools loop)
-            uint32_t p = p0 + (uint32_t)lane;
-            uint32_t w = w0;
-            if (p >= B) {
-                p -= B; w++;
-                while (p >= B) { p -= B; w++; }
-            }
-            uint32_t ins = 0;
-            if (valid) {
-                const bool lastw = w == w_last;
-                const uint32_t *kk = rk + 4 * (w - w_lo32);
-                ins = w * B + feistel(p, lastw ? len_last : B, lastw ? h_last : hB,
-                                      kk[0], kk[1], kk[2], kk[3]);
-            }
-            // collision probe: a lane that reads back another lane's id shares its probe
-            // byte (slot & 4095) with a lane of this sub-batch
-            const uint32_t hk = k & (uint32_t)(kMarkBytes - 1);
-            if (valid) mark[hk] = (uint8_t)lane;
-            const bool clash = valid && mark[hk] != (uint8_t)lane;
-            uint64_t cm = __ballot(clash);
-            uint32_t v;
-            if (cm == 0) {
-                // every valid lane drew a distinct slot: emit its content, insert in one op
-                v = valid ? atomicExch(&buf[k], ins) : 0u;
-            } else {
-                // peers = lanes that drew the same slot; the first of them exchanges the LAST
-                // peer's insertion, the others take the previous peer's insertion
-                uint64_t m = valid ? (1ull << lane) : 0ull;
-                while (cm) {
-                    const int c = __ffsll((long long)cm) - 1;
-                    const uint32_t sc = (uint32_t)__builtin_amdgcn_readlane((int)k, c);
-                    const bool same = valid && k == sc;
-                    const uint64_t mm = __ballot(same);
-                    if (same) m = mm;
-                    cm &= ~mm;
-                }
-                const uint64_t lower = m & lt_mask;
-                const int hi_lane = m ? 63 - __clzll((long long)m) : lane;
-                const int prev_lane = lower ? 63 - __clzll((long long)lower) : lane;
-                const uint32_t ins_last = (uint32_t)__shfl((int)ins, hi_lane);
-                const uint32_t ins_prev = (uint32_t)__shfl((int)ins, prev_lane);
-                v = (valid && !lower) ? atomicExch(&buf[k], ins_last) : ins_prev;
-            }
-            if ((uint32_t)tl >= e_lo && (uint32_t)tl < e_hi) {
-                if (narrow) {
-                    uint32_t id = (v < twoB ? old32 : new32) + v;
-                    id = id >= N32 ? id - N32 : id;
-                    o[tl] = (int64_t)id;
-                } else {
-                    o[tl] = v2_id(v, rd, g);
-                }
-            }
-            p0 += 64;
-            while (p0 >= B) { p0 -= B; w0++; }
+            for (int j = 0; j < 4; j++) c.step<true, NARROW>(u[j], tl0 + j * 64 + lane);
+        } else {
+#pragma unroll
+            for (int j = 0; j < 4; j++) c.step<false, NARROW>(u[j], tl0 + j * 64 + lane);
         }
     }
 }
@@ -415,20 +454,29 @@ hipError_t launch_v2(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, 
         if (last_emit >= 0) {
             const int64_t g_lo = pos_lo / pl.L;
             const int64_t ng = last_emit - g_lo + 1;
+            // 32-bit id arithmetic whenever every id (and id + ns before the wrap) fits
+            const bool narrow = g.N + g.ns < (int64_t)UINT32_MAX;
+            const dim3 grid((uint32_t)(nr * ng));
             if (!pl.global_buf) {
                 mk(K_V2_EMIT, s);
-                hipLaunchKernelGGL(k_v2_emit<false>, dim3((uint32_t)(nr * ng)), dim3(64),
-                                   lds_keys + kMarkBytes + (size_t)pl.P1 * 4, s,
-                                   g, pl, ranks, rank_lo, g_lo, ng, (const uint32_t *)VAL,
-                                   (uint32_t *)nullptr, pos_lo, count, out);
+                const size_t lds = lds_keys + kMarkBytes + (size_t)pl.P1 * 4;
+                if (narrow)
+                    hipLaunchKernelGGL((k_v2_emit<false, true>), grid, dim3(64), lds, s, g, pl, ranks, rank_lo,
+                                       g_lo, ng, (const uint32_t *)VAL, (uint32_t *)nullptr, pos_lo, count, out);
+                else
+                    hipLaunchKernelGGL((k_v2_emit<false, false>), grid, dim3(64), lds, s, g, pl, ranks, rank_lo,
+                                       g_lo, ng, (const uint32_t *)VAL, (uint32_t *)nullptr, pos_lo, count, out);
             } else {
                 hipLaunchKernelGGL(k_v2_init_g, dim3((uint32_t)cdiv(pl.P1, 256), (uint32_t)(nr * ng)),
                                    dim3(256), 0, s, pl, g_lo, ng, (const uint32_t *)VAL, gbuf);
                 mk(K_V2_EMIT, s);
-                hipLaunchKernelGGL(k_v2_emit<true>, dim3((uint32_t)(nr * ng)), dim3(64),
-                                   lds_keys + kMarkBytes, s,
-                                   g, pl, ranks, rank_lo, g_lo, ng, (const uint32_t *)VAL,
-                                   gbuf, pos_lo, count, out);
+                const size_t lds = lds_keys + kMarkBytes;
+                if (narrow)
+                    hipLaunchKernelGGL((k_v2_emit<true, true>), grid, dim3(64), lds, s, g, pl, ranks, rank_lo,
+                                       g_lo, ng, (const uint32_t *)VAL, gbuf, pos_lo, count, out);
+                else
+                    hipLaunchKernelGGL((k_v2_emit<true, false>), grid, dim3(64), lds, s, g, pl, ranks, rank_lo,
+                                       g_lo, ng, (const uint32_t *)VAL, gbuf, pos_lo, count, out);
             }
         }
     }
@@ -463,8 +511,10 @@ hipError_t init_kernel_attributes_v2() {
     PSS_ATTR(k_v2_tail<32>);
     PSS_ATTR(k_v2_tail<64>);
     PSS_ATTR(k_v2_lastocc);
-    PSS_ATTR(k_v2_emit<false>);
-    PSS_ATTR(k_v2_emit<true>);
+    PSS_ATTR((k_v2_emit<false, true>));
+    PSS_ATTR((k_v2_emit<false, false>));
+    PSS_ATTR((k_v2_emit<true, true>));
+    PSS_ATTR((k_v2_emit<true, false>));
 #undef PSS_ATTR
     return e;
 }
