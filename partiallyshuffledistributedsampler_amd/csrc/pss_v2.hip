@@ -152,48 +152,69 @@ struct EmitCtx {   // per-tile constants of k_v2_emit + the running pool2 positi
     bool walk_full;
     uint32_t w0, p0;
 
-    // One 64-step sub-batch (lane l = step tl).  FAST: every step valid and emitted.
-    template <bool FAST, bool NARROW>
-    __device__ __forceinline__ void step(uint32_t uword, int32_t tl) {
-        const bool valid = FAST || (uint32_t)tl < nvalid;
-        const uint32_t k = scale32(uword, P1);
+    // One 64-step sub-batch (lane l = step tl) in two halves, so that the next sub-batch's
+    // prep (ALU work + probe) can be issued while this one's LDS round trips are in flight.
+    struct Step { uint32_t k, ins, probe; int32_t tl; bool valid; };
+
+    // FAST: every step valid, B >= 64 (at most one window boundary per sub-batch) and no
+    // step in the last (short) window or in a cycle-walking window -- straight-line code.
+    template <bool FAST>
+    __device__ __forceinline__ Step prep(uint32_t uword, int32_t tl) {
+        Step s;
+        s.tl = tl;
+        s.valid = FAST || (uint32_t)tl < nvalid;
+        s.k = scale32(uword, P1);
         // collision probe: a lane that reads back another lane's id shares its probe byte
         // (slot & 4095) with a lane of this sub-batch
-        const uint32_t hk = k & (uint32_t)(kMarkBytes - 1);
-        if (valid) mark[hk] = (uint8_t)lane;
-        const uint8_t probe = mark[hk];
-        // insertion of step t (computed while the probe is in flight): window w, index p;
-        // p0 + lane crosses at most one window boundary when B >= 64, smaller pools loop
+        const uint32_t hk = s.k & (uint32_t)(kMarkBytes - 1);
+        if (s.valid) mark[hk] = (uint8_t)lane;
+        s.probe = mark[hk];
+        // insertion of step t: window w, index p
         uint32_t p = p0 + (uint32_t)lane;
         uint32_t w = w0;
-        if (p0 + 63u >= B) {                    // uniform: this sub-batch crosses a window
-            while (p >= B) { p -= B; w++; }
-        }
-        uint32_t ins = 0;
-        if (valid) {
+        if (FAST) {
+            const bool cross = p >= B;
+            p = cross ? p - B : p;
+            w = cross ? w + 1 : w;
             const uint32_t *kk = rk + 4 * (w - w_lo);
-            if (!walk_full && w != w_last) {
-                ins = w * B + feistel_once(p, hB, kk[0], kk[1], kk[2], kk[3]);
-            } else {
+            s.ins = w * B + feistel_once(p, hB, kk[0], kk[1], kk[2], kk[3]);
+        } else {
+            while (p >= B) { p -= B; w++; }
+            s.ins = 0;
+            if (s.valid) {
+                const uint32_t *kk = rk + 4 * (w - w_lo);
                 const bool lastw = w == w_last;
-                ins = w * B + feistel(p, lastw ? len_last : B, lastw ? h_last : hB,
-                                      kk[0], kk[1], kk[2], kk[3]);
+                s.ins = w * B + feistel(p, lastw ? len_last : B, lastw ? h_last : hB,
+                                        kk[0], kk[1], kk[2], kk[3]);
             }
         }
-        const bool clash = valid && probe != (uint8_t)lane;
+        p0 += 64;
+        if (FAST) {
+            const bool c2 = p0 >= B;
+            p0 = c2 ? p0 - B : p0;
+            w0 = c2 ? w0 + 1 : w0;
+        } else {
+            while (p0 >= B) { p0 -= B; w0++; }
+        }
+        return s;
+    }
+
+    template <bool FAST, bool NARROW>
+    __device__ __forceinline__ void finish(const Step &s) {
+        const bool clash = s.valid && s.probe != (uint32_t)lane;
         uint64_t cm = __ballot(clash);
         uint32_t v;
         if (cm == 0) {
             // every valid lane drew a distinct slot: emit its content, insert in one op
-            v = valid ? atomicExch(&buf[k], ins) : 0u;
+            v = (FAST || s.valid) ? atomicExch(&buf[s.k], s.ins) : 0u;
         } else {
             // peers = lanes that drew the same slot; the first of them exchanges the LAST
             // peer's insertion, the others take the previous peer's insertion
-            uint64_t m = valid ? (1ull << lane) : 0ull;
+            uint64_t m = s.valid ? (1ull << lane) : 0ull;
             while (cm) {
                 const int cl = __ffsll((long long)cm) - 1;
-                const uint32_t sc = (uint32_t)__builtin_amdgcn_readlane((int)k, cl);
-                const bool same = valid && k == sc;
+                const uint32_t sc = (uint32_t)__builtin_amdgcn_readlane((int)s.k, cl);
+                const bool same = s.valid && s.k == sc;
                 const uint64_t mm = __ballot(same);
                 if (same) m = mm;
                 cm &= ~mm;
@@ -201,21 +222,19 @@ struct EmitCtx {   // per-tile constants of k_v2_emit + the running pool2 positi
             const uint64_t lower = m & lt_mask;
             const int hi_lane = m ? 63 - __clzll((long long)m) : lane;
             const int prev_lane = lower ? 63 - __clzll((long long)lower) : lane;
-            const uint32_t ins_last = (uint32_t)__shfl((int)ins, hi_lane);
-            const uint32_t ins_prev = (uint32_t)__shfl((int)ins, prev_lane);
-            v = (valid && !lower) ? atomicExch(&buf[k], ins_last) : ins_prev;
+            const uint32_t ins_last = (uint32_t)__shfl((int)s.ins, hi_lane);
+            const uint32_t ins_prev = (uint32_t)__shfl((int)s.ins, prev_lane);
+            v = (s.valid && !lower) ? atomicExch(&buf[s.k], ins_last) : ins_prev;
         }
-        if (FAST || ((uint32_t)tl >= e_lo && (uint32_t)tl < e_hi)) {
+        if (FAST || ((uint32_t)s.tl >= e_lo && (uint32_t)s.tl < e_hi)) {
             if (NARROW) {
                 uint32_t id = (v < twoB ? old32 : new32) + v;
                 id = id >= N32 ? id - N32 : id;
-                o[tl] = (int64_t)id;
+                o[s.tl] = (int64_t)id;
             } else {
-                o[tl] = v2_id(v, rd, *g);
+                o[s.tl] = v2_id(v, rd, *g);
             }
         }
-        p0 += 64;
-        while (p0 >= B) { p0 -= B; w0++; }
     }
 };
 
@@ -296,17 +315,30 @@ __global__ __launch_bounds__(64) void k_v2_emit(Geometry g, V2Plan pl,
     const int64_t t_first = sb_lo * 256;
     c.w0 = (uint32_t)(1 + t_first / g.B);
     c.p0 = (uint32_t)(t_first - (int64_t)(c.w0 - 1) * g.B);
-    const bool full_emit = c.e_lo == 0 && c.e_hi == c.nvalid;
+    // fast super-batches: fully valid and emitted, B >= 64, and no window touched that is
+    // the last one or needs cycle walking (windows w0 .. w0 + 256/B + 1)
+    const bool fast_tile = c.e_lo == 0 && c.e_hi == c.nvalid && c.B >= 64 && !c.walk_full;
+    const uint32_t w_span = 256 / c.B + 1;
     int32_t tl0 = (int32_t)(t_first - tlo);   // negative while the super-batch starts before the tile
     for (int64_t sb = sb_lo; sb <= sb_hi; sb++, tl0 += 256) {
         uint32_t u[4];
         slot_words(g, rank, sb, lane, u);
-        if (full_emit && tl0 >= 0 && (uint32_t)tl0 + 256 <= c.nvalid) {   // uniform
-#pragma unroll
-            for (int j = 0; j < 4; j++) c.step<true, NARROW>(u[j], tl0 + j * 64 + lane);
+        if (fast_tile && tl0 >= 0 && (uint32_t)tl0 + 256 <= c.nvalid && c.w0 + w_span < c.w_last) {
+            // software-pipelined: sub-batch j+1's prep is in flight before j finishes
+            const EmitCtx::Step s0 = c.prep<true>(u[0], tl0 + lane);
+            const EmitCtx::Step s1 = c.prep<true>(u[1], tl0 + 64 + lane);
+            c.finish<true, NARROW>(s0);
+            const EmitCtx::Step s2 = c.prep<true>(u[2], tl0 + 128 + lane);
+            c.finish<true, NARROW>(s1);
+            const EmitCtx::Step s3 = c.prep<true>(u[3], tl0 + 192 + lane);
+            c.finish<true, NARROW>(s2);
+            c.finish<true, NARROW>(s3);
         } else {
 #pragma unroll
-            for (int j = 0; j < 4; j++) c.step<false, NARROW>(u[j], tl0 + j * 64 + lane);
+            for (int j = 0; j < 4; j++) {
+                const EmitCtx::Step s = c.prep<false>(u[j], tl0 + j * 64 + lane);
+                c.finish<false, NARROW>(s);
+            }
         }
     }
 }
