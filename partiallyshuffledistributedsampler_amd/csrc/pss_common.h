@@ -54,7 +54,12 @@ PSS_HD uint32_t feistel(uint32_t x, uint32_t n, uint32_t h, uint32_t rk0, uint32
                         uint32_t rk2, uint32_t rk3) {
     if (n <= 1) return 0;
     const uint32_t mask = (1u << h) - 1u;
+    // x < n <= 2^(2h): the walk stays on x's cycle and meets a value < n after a few steps
+    // (each step lands below n with probability >= 1/4).  The bound only guards against a
+    // caller passing x >= 2^(2h), which would otherwise never terminate.
+    int guard = 1 << 16;
     do {
+        if (--guard < 0) break;
         uint32_t L = x >> h, R = x & mask, t;
         t = L ^ (lowbias32(R ^ rk0) & mask); L = R; R = t;
         t = L ^ (lowbias32(R ^ rk1) & mask); L = R; R = t;

@@ -73,6 +73,11 @@ __device__ __forceinline__ int64_t wrap_id(int64_t id, int64_t N) { return id >=
 // (low 32-hb key bits << hb | i).  A bucket averages one element, so the in-bucket fix-up is
 // a short insertion sort.  Result: S[p] & (2^hb - 1) = index of the p-th smallest key.
 // ------------------------------------------------------------------------------------------
+// Bucket arrays are padded by one word per 16 buckets: a thread that scans 16 consecutive
+// buckets then hits bank (17*t + i) mod 32 instead of a 32-way conflict on 16*t + i.
+__device__ __forceinline__ int bpad(int b) { return b + (b >> 4); }
+__host__ __device__ constexpr int bpad_size(int nb) { return nb + nb / 16 + 1; }
+
 template <int EPT>
 __device__ __forceinline__ int block_sort_keys(uint32_t k0, uint32_t k1, uint32_t c1,
                                                uint32_t rank, uint32_t dom, int n,
@@ -88,7 +93,7 @@ __device__ __forceinline__ int block_sort_keys(uint32_t k0, uint32_t k1, uint32_
         philox4x32_10(c0, cc1, c2, c3, k0, k1);
         key[j][0] = c0; key[j][1] = cc1; key[j][2] = c2; key[j][3] = c3;
     }
-    for (int i = tid; i < nb; i += 256) hist[i] = 0;
+    for (int i = tid; i < bpad_size(nb); i += 256) hist[i] = 0;
     __syncthreads();
     const int sh = 32 - hb;
 #pragma unroll
@@ -96,17 +101,17 @@ __device__ __forceinline__ int block_sort_keys(uint32_t k0, uint32_t k1, uint32_
 #pragma unroll
         for (int w = 0; w < 4; w++) {
             const int i = 4 * (tid + 256 * j) + w;
-            if (i < n) atomicAdd(&hist[hb ? key[j][w] >> sh : 0], 1u);
+            if (i < n) atomicAdd(&hist[bpad(hb ? key[j][w] >> sh : 0)], 1u);
         }
     __syncthreads();
     const int per = nb >= 256 ? nb / 256 : 1;
     const int blo = tid * per < nb ? tid * per : nb;
     const int bhi = blo + per < nb ? blo + per : nb;
     uint32_t s = 0;
-    for (int b = blo; b < bhi; b++) s += hist[b];
+    for (int b = blo; b < bhi; b++) s += hist[bpad(b)];
     uint32_t total;
     uint32_t run = block_excl_scan<256>(s, tot, total);
-    for (int b = blo; b < bhi; b++) { const uint32_t c = hist[b]; hist[b] = run; run += c; }
+    for (int b = blo; b < bhi; b++) { const uint32_t c = hist[bpad(b)]; hist[bpad(b)] = run; run += c; }
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < NQ; j++)
@@ -115,14 +120,14 @@ __device__ __forceinline__ int block_sort_keys(uint32_t k0, uint32_t k1, uint32_
             const int i = 4 * (tid + 256 * j) + w;
             if (i < n) {
                 const uint32_t k = key[j][w];
-                const uint32_t pos = atomicAdd(&hist[hb ? k >> sh : 0], 1u);
+                const uint32_t pos = atomicAdd(&hist[bpad(hb ? k >> sh : 0)], 1u);
                 S[pos] = hb ? ((k << hb) | (uint32_t)i) : 0u;
             }
         }
     __syncthreads();
-    for (int b = blo; b < bhi; b++) {  // hist[b] is now the END of bucket b
-        const int e = (int)hist[b];
-        const int st = b ? (int)hist[b - 1] : 0;
+    for (int b = tid; b < nb; b += 256) {  // hist[b] is now the END of bucket b
+        const int e = (int)hist[bpad(b)];
+        const int st = b ? (int)hist[bpad(b - 1)] : 0;
         for (int x = st + 1; x < e; x++) {
             const uint32_t v = S[x];
             int y = x - 1;
@@ -135,7 +140,9 @@ __device__ __forceinline__ int block_sort_keys(uint32_t k0, uint32_t k1, uint32_
 }
 
 template <int EPT>
-constexpr size_t sort_lds_bytes() { return (size_t)(2 * 256 * EPT + 16) * sizeof(uint32_t); }
+constexpr size_t sort_lds_bytes() {
+    return (size_t)(256 * EPT + bpad_size(256 * EPT) + 16) * sizeof(uint32_t);
+}
 
 // ------------------------------------------------------------------------------------------
 // V2 helpers

@@ -198,7 +198,7 @@ __global__ __launch_bounds__(256) void k_v1_lds(Geometry g, const RankDesc *__re
                                                int64_t pos_lo, int64_t count,
                                                int64_t *__restrict__ out) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-    uint32_t *S = smem, *hist = smem + 256 * EPT, *tot = hist + 256 * EPT;
+    uint32_t *S = smem, *hist = smem + 256 * EPT, *tot = hist + bpad_size(256 * EPT);
     const int32_t rl = (int32_t)(blockIdx.x / nw);
     const int64_t w = w_lo + (int64_t)(blockIdx.x % nw);
     const int32_t rank = rank_lo + rl;

@@ -343,6 +343,187 @@ __global__ __launch_bounds__(64) void k_v2_emit(Geometry g, V2Plan pl,
     }
 }
 
+// ---- pass B, sorted sub-tiles ---------------------------------------------------------------
+// One 256-thread workgroup per tile; the tile is cut into sub-tiles of S <= 4096 steps
+// (S a multiple of 256, S <= P1).  Per sub-tile, in LDS:
+//   P1 histogram of the drawn slots, P2 exclusive scan, P3 scatter (slot << 16 | step) into
+//   slot buckets, P4 order each bucket by step + flag its first/last entry, P5 insertion value
+//   of every entry, P6 value emitted by each step = slot table (first entry of its bucket) or
+//   the previous entry's insertion, P7 last entries write the slot table back; coalesced ids.
+// Same result as k_v2_emit (the step order inside a slot is what the sequential replay sees).
+constexpr uint32_t kSstFirst = 1u << 31, kSstLast = 1u << 30, kSstPayload = kSstLast - 1;
+
+template <bool NARROW>
+__global__ __launch_bounds__(256) void k_v2_emit_sst(Geometry g, V2Plan pl,
+                                                    const RankDesc *__restrict__ ranks,
+                                                    int32_t rank_lo, int64_t g_lo, int64_t ng,
+                                                    const uint32_t *__restrict__ VAL,
+                                                    int64_t pos_lo, int64_t count,
+                                                    int64_t *__restrict__ out) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+    const int P1 = (int)pl.P1;                       // == B while steps exist
+    const int S = (P1 < 4096 ? P1 : 4096) & ~255;
+    uint32_t *buf = smem;                            // [P1] slot table
+    uint32_t *cnt = buf + P1;                        // [P1] counts -> starts -> ends; then val[S]
+    uint32_t *ord = cnt + bpad_size(P1);             // [S]  (slot << 16 | step) in bucket order
+    uint32_t *insv = ord + S;                        // [S]  insertion value of each entry
+    uint32_t *tot = insv + S;                        // [4]  block-scan scratch
+    uint32_t *val = cnt;
+    const int tid = threadIdx.x;
+    const int32_t rl = (int32_t)(blockIdx.x / ng);
+    const int64_t tile = g_lo + (int64_t)(blockIdx.x % ng);
+    const uint32_t rank = (uint32_t)(rank_lo + rl);
+    const RankDesc rd = ranks[rank];
+    int64_t tlo, thi;
+    tile_bounds(pl, tile, tlo, thi);
+    {   // slot table at the tile's start (4 independent loads in flight per thread)
+        const uint32_t *VALr = VAL + (int64_t)rl * pl.G * P1;
+        const uint32_t *prev = VALr + (tile - 1) * P1;
+        for (int s0 = tid; s0 < P1; s0 += 1024) {
+            uint32_t v[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int s = s0 + 256 * u;
+                v[u] = (tile > 0 && s < P1) ? prev[s] : kNone;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int s = s0 + 256 * u;
+                if (s < P1) buf[s] = v[u] != kNone ? v[u] : slot_value_after(VALr, P1, tile - 2, s);
+            }
+        }
+    }
+    const uint32_t B = (uint32_t)g.B;
+    const uint32_t hB = feistel_half_bits(B);
+    const bool walk_full = B != (1u << (2 * hB));
+    const uint32_t w_last = (uint32_t)(1 + (pl.T - 1) / g.B);
+    const uint32_t len_last = (uint32_t)(g.ns - (int64_t)w_last * g.B);
+    const uint32_t h_last = feistel_half_bits(len_last);
+    const uint32_t twoB = (uint32_t)(2 * g.B < g.ns ? 2 * g.B : g.ns);
+    const uint32_t old32 = (uint32_t)rd.old_start, new32 = (uint32_t)rd.new_start;
+    const uint32_t N32 = (uint32_t)g.N;
+    const int64_t pos_hi = pos_lo + count;
+    int64_t *o = out + (int64_t)rl * count - pos_lo;
+    const int per = (P1 + 255) / 256;                // buckets per thread in P2 / P4
+    const int blo = tid * per < P1 ? tid * per : P1;
+    const int bhi = blo + per < P1 ? blo + per : P1;
+    const int NBLK = (S + 1023) / 1024;              // Philox blocks per thread (<= 4)
+    for (int64_t a = tlo; a < thi; a += S) {
+        const int n = (int)(thi - a < S ? thi - a : S);
+        const uint32_t wa = (uint32_t)(1 + a / g.B);
+        const uint32_t pa = (uint32_t)(a - (int64_t)(wa - 1) * g.B);
+        uint32_t ka[4], kb[4];
+        window_round_keys(g, rank, wa, ka);
+        window_round_keys(g, rank, (int64_t)wa + 1, kb);
+        // P0
+        for (int i = tid; i < bpad_size(P1); i += 256) cnt[i] = 0;
+        __syncthreads();
+        // P1: slots of the sub-tile's steps (a is a multiple of 256: whole super-batches)
+        uint32_t kreg[4][4];
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+            if (b >= NBLK) break;
+            const int ci = tid + 256 * b;            // (super-batch q, lane)
+            const int q = ci >> 6, lane = ci & 63;
+            uint32_t u[4] = {0, 0, 0, 0};
+            if (q * 256 < S) slot_words(g, rank, (a >> 8) + q, lane, u);
+#pragma unroll
+            for (int w = 0; w < 4; w++) {
+                const int tl = q * 256 + w * 64 + lane;
+                const bool valid = q * 256 < S && tl < n;
+                const uint32_t k = scale32(u[w], (uint32_t)P1);
+                kreg[b][w] = valid ? k : 0xFFFFFFFFu;
+                if (valid) atomicAdd(&cnt[bpad(k)], 1u);
+            }
+        }
+        __syncthreads();
+        // P2: exclusive scan of the bucket counts
+        {
+            uint32_t s = 0;
+            for (int i = blo; i < bhi; i++) s += cnt[bpad(i)];
+            uint32_t total;
+            uint32_t run = block_excl_scan<256>(s, tot, total);
+            for (int i = blo; i < bhi; i++) { const uint32_t c = cnt[bpad(i)]; cnt[bpad(i)] = run; run += c; }
+        }
+        __syncthreads();
+        // P3: scatter entries into their buckets (order inside a bucket is fixed in P4)
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+            if (b >= NBLK) break;
+            const int ci = tid + 256 * b;
+            const int q = ci >> 6, lane = ci & 63;
+#pragma unroll
+            for (int w = 0; w < 4; w++) {
+                const uint32_t k = kreg[b][w];
+                if (k != 0xFFFFFFFFu) {
+                    const uint32_t pos = atomicAdd(&cnt[bpad(k)], 1u);
+                    ord[pos] = (k << 16) | (uint32_t)(q * 256 + w * 64 + lane);
+                }
+            }
+        }
+        __syncthreads();
+        // P4: order every bucket by step; flag first and last entries
+        for (int bk = tid; bk < P1; bk += 256) {     // interleaved: conflict-free cnt reads
+            const int e = (int)cnt[bpad(bk)];
+            const int st = bk ? (int)cnt[bpad(bk - 1)] : 0;
+            for (int x = st + 1; x < e; x++) {
+                const uint32_t v = ord[x];
+                int y = x - 1;
+                while (y >= st && ord[y] > v) { ord[y + 1] = ord[y]; y--; }
+                ord[y + 1] = v;
+            }
+            if (e > st) {
+                ord[st] |= kSstFirst;
+                ord[e - 1] |= kSstLast;
+            }
+        }
+        __syncthreads();
+        // P5: insertion value of every entry
+        for (int p = tid; p < n; p += 256) {
+            const uint32_t tl = ord[p] & 0xFFFFu;
+            uint32_t pp = pa + tl, w = wa;
+            const bool cross = pp >= B;
+            pp = cross ? pp - B : pp;
+            w = cross ? w + 1 : w;
+            const uint32_t k0 = cross ? kb[0] : ka[0], k1 = cross ? kb[1] : ka[1];
+            const uint32_t k2 = cross ? kb[2] : ka[2], k3 = cross ? kb[3] : ka[3];
+            uint32_t x;
+            if (!walk_full && w != w_last) {
+                x = feistel_once(pp, hB, k0, k1, k2, k3);
+            } else {
+                const bool lastw = w == w_last;
+                x = feistel(pp, lastw ? len_last : B, lastw ? h_last : hB, k0, k1, k2, k3);
+            }
+            insv[p] = w * B + x;
+        }
+        __syncthreads();
+        // P6: value emitted by each step (val aliases cnt, no longer needed)
+        for (int p = tid; p < n; p += 256) {
+            const uint32_t e = ord[p];
+            const uint32_t k = (e & kSstPayload) >> 16;
+            val[e & 0xFFFFu] = (e & kSstFirst) ? buf[k] : insv[p - 1];
+        }
+        __syncthreads();
+        // P7: slot table after the sub-tile; ids of its steps
+        for (int p = tid; p < n; p += 256) {
+            const uint32_t e = ord[p];
+            if (e & kSstLast) buf[(e & kSstPayload) >> 16] = insv[p];
+        }
+        for (int tl = tid; tl < n; tl += 256) {
+            const int64_t t = a + tl;
+            if (t < pos_lo || t >= pos_hi) continue;
+            const uint32_t v = val[tl];
+            if (NARROW) {
+                uint32_t id = (v < twoB ? old32 : new32) + v;
+                o[t] = (int64_t)(id >= N32 ? id - N32 : id);
+            } else {
+                o[t] = v2_id(v, rd, g);
+            }
+        }
+        __syncthreads();
+    }
+}
+
 // ---- tail ---------------------------------------------------------------------------------
 template <int EPT>
 __global__ __launch_bounds__(256) void k_v2_tail(Geometry g, V2Plan pl,
@@ -351,7 +532,7 @@ __global__ __launch_bounds__(256) void k_v2_tail(Geometry g, V2Plan pl,
                                                 int64_t pos_lo, int64_t count,
                                                 int64_t *__restrict__ out) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-    uint32_t *S = smem, *hist = smem + 256 * EPT, *tot = hist + 256 * EPT;
+    uint32_t *S = smem, *hist = smem + 256 * EPT, *tot = hist + bpad_size(256 * EPT);
     const int32_t rl = (int32_t)blockIdx.x;
     const uint32_t rank = (uint32_t)(rank_lo + rl);
     const RankDesc rd = ranks[rank];
@@ -489,7 +670,24 @@ hipError_t launch_v2(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, 
             // 32-bit id arithmetic whenever every id (and id + ns before the wrap) fits
             const bool narrow = g.N + g.ns < (int64_t)UINT32_MAX;
             const dim3 grid((uint32_t)(nr * ng));
-            if (!pl.global_buf) {
+            static const bool use_sst = [] {
+                // A/B knob: "sst" = sorted sub-tiles (bit-identical; measured 2.8x slower than
+                // the wave replay on C2, kept for experiments -- see DESIGN.md §5)
+                const char *e = getenv("PSS_V2_EMIT");
+                return e && e[0] == 's';
+            }();
+            if (!pl.global_buf && use_sst && pl.P1 >= 1024 && pl.P1 <= 8192) {
+                mk(K_V2_EMIT, s);
+                const int64_t S = (pl.P1 < 4096 ? pl.P1 : 4096) & ~255;
+                const size_t lds = (size_t)4 * (pl.P1 + bpad_size((int)pl.P1) + 2 * S) + 16;
+                const dim3 blk(256);
+                if (narrow)
+                    hipLaunchKernelGGL((k_v2_emit_sst<true>), grid, blk, lds, s, g, pl, ranks, rank_lo,
+                                       g_lo, ng, (const uint32_t *)VAL, pos_lo, count, out);
+                else
+                    hipLaunchKernelGGL((k_v2_emit_sst<false>), grid, blk, lds, s, g, pl, ranks, rank_lo,
+                                       g_lo, ng, (const uint32_t *)VAL, pos_lo, count, out);
+            } else if (!pl.global_buf) {
                 mk(K_V2_EMIT, s);
                 const size_t lds = lds_keys + kMarkBytes + (size_t)pl.P1 * 4;
                 if (narrow)
@@ -543,6 +741,8 @@ hipError_t init_kernel_attributes_v2() {
     PSS_ATTR(k_v2_tail<32>);
     PSS_ATTR(k_v2_tail<64>);
     PSS_ATTR(k_v2_lastocc);
+    PSS_ATTR((k_v2_emit_sst<true>));
+    PSS_ATTR((k_v2_emit_sst<false>));
     PSS_ATTR((k_v2_emit<false, true>));
     PSS_ATTR((k_v2_emit<false, false>));
     PSS_ATTR((k_v2_emit<true, true>));
