@@ -48,7 +48,7 @@ def _pmc_traffic(kernel):
     try:
         with open(p) as f:
             d = json.load(f)
-        return d.get(kernel, {}).get("hbm_bytes_per_launch")
+        return d.get("k_" + kernel, {}).get("hbm_bytes_per_launch")
     except (OSError, ValueError):
         return None
 
