@@ -199,6 +199,36 @@ struct EmitCtx {   // per-tile constants of k_v2_emit + the running pool2 positi
         return s;
     }
 
+    // Fast super-batch, first half: slots + probes of its 4 sub-batches (in order: the probe
+    // of sub-batch j+1 is written after sub-batch j's read-back) ...
+    __device__ __forceinline__ Step probe4(uint32_t uword, int32_t tl) {
+        Step s;
+        s.tl = tl;
+        s.valid = true;
+        s.k = scale32(uword, P1);
+        const uint32_t hk = s.k & (uint32_t)(kMarkBytes - 1);
+        mark[hk] = (uint8_t)lane;
+        s.probe = mark[hk];
+        return s;
+    }
+    // ... second half: insertion value of sub-batch j (B >= 256: at most one window boundary
+    // inside the super-batch; no last / cycle-walking window).  Independent of the other
+    // three, so the four Feistel chains interleave.
+    __device__ __forceinline__ uint32_t ins4(int j) const {
+        uint32_t p = p0 + (uint32_t)(64 * j + lane);
+        const bool cross = p >= B;
+        p = cross ? p - B : p;
+        const uint32_t w = cross ? w0 + 1 : w0;
+        const uint32_t *kk = rk + 4 * (w - w_lo);
+        return w * B + feistel_once(p, hB, kk[0], kk[1], kk[2], kk[3]);
+    }
+    __device__ __forceinline__ void advance256() {
+        p0 += 256;
+        const bool c2 = p0 >= B;
+        p0 = c2 ? p0 - B : p0;
+        w0 = c2 ? w0 + 1 : w0;
+    }
+
     template <bool FAST, bool NARROW>
     __device__ __forceinline__ void finish(const Step &s) {
         const bool clash = s.valid && s.probe != (uint32_t)lane;
@@ -315,31 +345,36 @@ __global__ __launch_bounds__(64) void k_v2_emit(Geometry g, V2Plan pl,
     const int64_t t_first = sb_lo * 256;
     c.w0 = (uint32_t)(1 + t_first / g.B);
     c.p0 = (uint32_t)(t_first - (int64_t)(c.w0 - 1) * g.B);
-    // fast super-batches: fully valid and emitted, B >= 64, and no window touched that is
-    // the last one or needs cycle walking (windows w0 .. w0 + 256/B + 1)
-    const bool fast_tile = c.e_lo == 0 && c.e_hi == c.nvalid && c.B >= 64 && !c.walk_full;
-    const uint32_t w_span = 256 / c.B + 1;
+    // fast super-batches: fully valid and emitted, B >= 256, and no window touched that is
+    // the last one or needs cycle walking (windows w0 .. w0 + 1)
+    const bool fast_tile = c.e_lo == 0 && c.e_hi == c.nvalid && c.B >= 256 && !c.walk_full;
     int32_t tl0 = (int32_t)(t_first - tlo);   // negative while the super-batch starts before the tile
+    uint32_t u[4];
+    slot_words(g, rank, sb_lo, lane, u);
     for (int64_t sb = sb_lo; sb <= sb_hi; sb++, tl0 += 256) {
-        uint32_t u[4];
-        slot_words(g, rank, sb, lane, u);
-        if (fast_tile && tl0 >= 0 && (uint32_t)tl0 + 256 <= c.nvalid && c.w0 + w_span < c.w_last) {
-            // software-pipelined: sub-batch j+1's prep is in flight before j finishes
-            const EmitCtx::Step s0 = c.prep<true>(u[0], tl0 + lane);
-            const EmitCtx::Step s1 = c.prep<true>(u[1], tl0 + 64 + lane);
-            c.finish<true, NARROW>(s0);
-            const EmitCtx::Step s2 = c.prep<true>(u[2], tl0 + 128 + lane);
-            c.finish<true, NARROW>(s1);
-            const EmitCtx::Step s3 = c.prep<true>(u[3], tl0 + 192 + lane);
-            c.finish<true, NARROW>(s2);
-            c.finish<true, NARROW>(s3);
+        uint32_t un[4];   // next super-batch's slot words, computed under this one's work
+        if (fast_tile && tl0 >= 0 && (uint32_t)tl0 + 256 <= c.nvalid && c.w0 + 1 < c.w_last) {
+            // one branch-free block: 4 probes, 4 independent Feistel chains and the next
+            // Philox block interleave; then the 4 sub-batches finish in step order
+            EmitCtx::Step s[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) s[j] = c.probe4(u[j], tl0 + 64 * j + lane);
+#pragma unroll
+            for (int j = 0; j < 4; j++) s[j].ins = c.ins4(j);
+            slot_words(g, rank, sb + 1, lane, un);
+            c.advance256();
+#pragma unroll
+            for (int j = 0; j < 4; j++) c.finish<true, NARROW>(s[j]);
         } else {
 #pragma unroll
             for (int j = 0; j < 4; j++) {
                 const EmitCtx::Step s = c.prep<false>(u[j], tl0 + j * 64 + lane);
                 c.finish<false, NARROW>(s);
             }
+            slot_words(g, rank, sb + 1, lane, un);
         }
+#pragma unroll
+        for (int j = 0; j < 4; j++) u[j] = un[j];
     }
 }
 
