@@ -282,21 +282,17 @@ uint64_t orc_epoch_key(uint64_t seed, int64_t epoch) {
     return orc_mix64(orc_mix64(seed) ^ (uint64_t)epoch);
 }
 
-static inline uint32_t lowbias32(uint32_t x) {
-    x ^= x >> 16; x *= 0x7feb352dU; x ^= x >> 15; x *= 0x846ca68bU; x ^= x >> 16;
-    return x;
-}
-
-/* keyed bijection of [0,n): 4-round balanced Feistel on 2h bits + cycle walking */
-uint32_t orc_feistel(uint32_t x, uint32_t n, const uint32_t rk[4]) {
+/* keyed bijection of [0,n): 6-round balanced Feistel on 2h bits + cycle walking; round
+ * function = top h bits of (R ^ rk[i]) * 0x9E3779B1 (multiplicative hashing) */
+uint32_t orc_feistel(uint32_t x, uint32_t n, const uint32_t rk[6]) {
     if (n <= 1) return 0;
     int bits = 0; while ((1ull << bits) < (uint64_t)n) bits++;
     int h = (bits + 1) >> 1;
     uint32_t mask = (1u << h) - 1u;
     do {
         uint32_t L = x >> h, R = x & mask;
-        for (int i = 0; i < 4; i++) {
-            uint32_t t = L ^ (lowbias32(R ^ rk[i]) & mask);
+        for (int i = 0; i < 6; i++) {
+            uint32_t t = L ^ (uint32_t)(((R ^ rk[i]) * 0x9E3779B1u) >> (32 - h));
             L = R; R = t;
         }
         x = (L << h) | R;
@@ -369,7 +365,7 @@ static inline int64_t v2_vid_to_id(int64_t v, int64_t old_start, int64_t new_sta
  *   P1 = min(B, ns) slots initialised with window 0 (v = s); T = ns - P1 steps;
  *   step t draws slot k_t (Philox DOM_V2_SLOT), emits buf[k_t] and stores the t-th inserted
  *   element there: window w = 1 + t/B, inserted in the order of the Feistel bijection keyed
- *   by Philox (w, 0, rank, DOM_V2_INS);  then the final buffer is emitted in the order of a
+ *   by Philox (w, 0|1, rank, DOM_V2_INS) (6 rounds);  then the final buffer is emitted in the order of a
  *   stable argsort of Philox keys (j>>2, 0, rank, DOM_V2_TAIL).
  * Writes all ns ids (rank order) to out; returns ns. */
 int64_t orc_v2_philox_stream(uint64_t key64, uint32_t rank, int64_t old_start,
@@ -379,14 +375,16 @@ int64_t orc_v2_philox_stream(uint64_t key64, uint32_t rank, int64_t old_start,
     uint32_t *buf = (uint32_t *)malloc(sizeof(uint32_t) * (size_t)P1);
     for (int64_t s = 0; s < P1; s++) buf[s] = (uint32_t)s;
     int64_t cur_w = -1;
-    uint32_t rk[4] = {0, 0, 0, 0};
+    uint32_t rk[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     for (int64_t t = 0; t < T; t++) {
         uint32_t k = v2_slot(key64, rank, t, (uint32_t)P1);
         out[t] = v2_vid_to_id(buf[k], old_start, new_start, B, N);
         int64_t w = 1 + t / B, p = t % B;
-        if (w != cur_w) {
-            uint32_t ctr[4] = {(uint32_t)w, 0, rank, DOM_V2_INS};
-            orc_philox4x32(ctr, key64, rk);
+        if (w != cur_w) {   /* round keys: Philox blocks (w, 0|1, rank, DOM_V2_INS) */
+            uint32_t c0[4] = {(uint32_t)w, 0, rank, DOM_V2_INS};
+            uint32_t c1[4] = {(uint32_t)w, 1, rank, DOM_V2_INS};
+            orc_philox4x32(c0, key64, rk);
+            orc_philox4x32(c1, key64, rk + 4);
             cur_w = w;
         }
         int64_t len = ns - w * B; if (len > B) len = B;

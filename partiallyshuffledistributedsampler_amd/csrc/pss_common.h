@@ -40,46 +40,43 @@ PSS_HD uint64_t epoch_key(uint64_t seed, int64_t epoch) {
     return mix64(mix64(seed) ^ (uint64_t)epoch);
 }
 
-PSS_HD uint32_t lowbias32(uint32_t x) {
-    x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
-    return x;
-}
-
 PSS_HD int ceil_log2_u64(uint64_t n) {  // smallest b with 2^b >= n (n >= 1)
     return n <= 1 ? 0 : 64 - __builtin_clzll(n - 1);
 }
 
-// Keyed bijection of [0, n): 4-round balanced Feistel over 2h bits + cycle walking.
-PSS_HD uint32_t feistel(uint32_t x, uint32_t n, uint32_t h, uint32_t rk0, uint32_t rk1,
-                        uint32_t rk2, uint32_t rk3) {
+// Keyed bijection of [0, n): 6-round balanced Feistel over 2h bits + cycle walking.
+// Round function: multiplicative hashing of the keyed right half, F(R) = top h bits of
+// (R ^ k_i) * 0x9E3779B1 -- one multiply per round (DESIGN.md §3.3 has the quality numbers).
+constexpr int kFeistelRounds = 6;
+
+PSS_HD uint32_t feistel_pass(uint32_t x, uint32_t h, const uint32_t *k) {
+    const uint32_t mask = (1u << h) - 1u, sh = 32u - h;
+    uint32_t L = x >> h, R = x & mask;
+#pragma unroll
+    for (int i = 0; i < kFeistelRounds; i++) {
+        const uint32_t t = L ^ (((R ^ k[i]) * 0x9E3779B1u) >> sh);
+        L = R;
+        R = t;
+    }
+    return (L << h) | R;
+}
+
+PSS_HD uint32_t feistel(uint32_t x, uint32_t n, uint32_t h, const uint32_t *k) {
     if (n <= 1) return 0;
-    const uint32_t mask = (1u << h) - 1u;
     // x < n <= 2^(2h): the walk stays on x's cycle and meets a value < n after a few steps
     // (each step lands below n with probability >= 1/4).  The bound only guards against a
     // caller passing x >= 2^(2h), which would otherwise never terminate.
     int guard = 1 << 16;
     do {
         if (--guard < 0) break;
-        uint32_t L = x >> h, R = x & mask, t;
-        t = L ^ (lowbias32(R ^ rk0) & mask); L = R; R = t;
-        t = L ^ (lowbias32(R ^ rk1) & mask); L = R; R = t;
-        t = L ^ (lowbias32(R ^ rk2) & mask); L = R; R = t;
-        t = L ^ (lowbias32(R ^ rk3) & mask); L = R; R = t;
-        x = (L << h) | R;
+        x = feistel_pass(x, h, k);
     } while (x >= n);
     return x;
 }
 
 // One Feistel pass, for domains n == 2^(2h) where cycle walking never triggers.
-PSS_HD uint32_t feistel_once(uint32_t x, uint32_t h, uint32_t rk0, uint32_t rk1, uint32_t rk2,
-                             uint32_t rk3) {
-    const uint32_t mask = (1u << h) - 1u;
-    uint32_t L = x >> h, R = x & mask, t;
-    t = L ^ (lowbias32(R ^ rk0) & mask); L = R; R = t;
-    t = L ^ (lowbias32(R ^ rk1) & mask); L = R; R = t;
-    t = L ^ (lowbias32(R ^ rk2) & mask); L = R; R = t;
-    t = L ^ (lowbias32(R ^ rk3) & mask); L = R; R = t;
-    return (L << h) | R;
+PSS_HD uint32_t feistel_once(uint32_t x, uint32_t h, const uint32_t *k) {
+    return feistel_pass(x, h, k);
 }
 
 PSS_HD uint32_t feistel_half_bits(uint32_t n) {

@@ -157,11 +157,18 @@ __device__ __forceinline__ void slot_words(const Geometry &g, uint32_t rank, int
     u[0] = c0; u[1] = c1; u[2] = c2; u[3] = c3;
 }
 
+// Feistel round keys of pool2 window w: Philox blocks (w, 0, rank, INS) and (w, 1, rank, INS),
+// 8 words of which the first kFeistelRounds are used
+constexpr int kRoundKeyWords = 8;
+
 __device__ __forceinline__ void window_round_keys(const Geometry &g, uint32_t rank, int64_t w,
-                                                  uint32_t k[4]) {
-    uint32_t c0 = (uint32_t)w, c1 = 0, c2 = rank, c3 = DOM_V2_INS;
-    philox4x32_10(c0, c1, c2, c3, g.key0, g.key1);
-    k[0] = c0; k[1] = c1; k[2] = c2; k[3] = c3;
+                                                  uint32_t k[kRoundKeyWords]) {
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+        uint32_t c0 = (uint32_t)w, c1 = (uint32_t)h, c2 = rank, c3 = DOM_V2_INS;
+        philox4x32_10(c0, c1, c2, c3, g.key0, g.key1);
+        k[4 * h] = c0; k[4 * h + 1] = c1; k[4 * h + 2] = c2; k[4 * h + 3] = c3;
+    }
 }
 
 // virtual index inserted at step t (pool2 window w = 1 + t/B in Feistel order), given the
@@ -171,7 +178,7 @@ __device__ __forceinline__ uint32_t ins_value_k(const Geometry &g, int64_t t, co
     const int64_t p = t - (w - 1) * g.B;
     const int64_t rem = g.ns - w * g.B;
     const uint32_t len = (uint32_t)(rem < g.B ? rem : g.B);
-    return (uint32_t)(w * g.B) + feistel((uint32_t)p, len, feistel_half_bits(len), k[0], k[1], k[2], k[3]);
+    return (uint32_t)(w * g.B) + feistel((uint32_t)p, len, feistel_half_bits(len), k);
 }
 
 __device__ __forceinline__ int64_t v2_id(uint32_t v, const RankDesc &rd, const Geometry &g) {

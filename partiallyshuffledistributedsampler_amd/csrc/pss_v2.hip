@@ -29,7 +29,8 @@ __device__ __forceinline__ void tile_bounds(const V2Plan &pl, int64_t tile, int6
 
 __device__ __forceinline__ void stage_round_keys(const Geometry &g, uint32_t rank, int64_t w_lo,
                                                  int nwin, uint32_t *rk) {
-    for (int j = threadIdx.x; j < nwin; j += blockDim.x) window_round_keys(g, rank, w_lo + j, rk + 4 * j);
+    for (int j = threadIdx.x; j < nwin; j += blockDim.x)
+        window_round_keys(g, rank, w_lo + j, rk + kRoundKeyWords * j);
 }
 
 // ---- pass A, LDS --------------------------------------------------------------------------
@@ -67,7 +68,7 @@ __global__ __launch_bounds__(256) void k_v2_lastocc(Geometry g, V2Plan pl, int32
         const uint32_t lt = lastT[s];
         if (!lt) { V[s] = kNone; continue; }
         const int64_t t = tlo + (int64_t)lt - 1;
-        V[s] = ins_value_k(g, t, rk + 4 * (1 + t / g.B - w_lo));
+        V[s] = ins_value_k(g, t, rk + kRoundKeyWords * (1 + t / g.B - w_lo));
     }
 }
 
@@ -113,7 +114,7 @@ __global__ __launch_bounds__(256) void k_v2_convert_g(Geometry g, V2Plan pl, int
         const uint32_t lt = V[s];
         if (!lt) { V[s] = kNone; continue; }
         const int64_t t = tlo + (int64_t)lt - 1;
-        uint32_t k[4];
+        uint32_t k[kRoundKeyWords];
         window_round_keys(g, rank, 1 + t / g.B, k);
         V[s] = ins_value_k(g, t, k);
     }
@@ -176,16 +177,14 @@ struct EmitCtx {   // per-tile constants of k_v2_emit + the running pool2 positi
             const bool cross = p >= B;
             p = cross ? p - B : p;
             w = cross ? w + 1 : w;
-            const uint32_t *kk = rk + 4 * (w - w_lo);
-            s.ins = w * B + feistel_once(p, hB, kk[0], kk[1], kk[2], kk[3]);
+            s.ins = w * B + feistel_once(p, hB, rk + kRoundKeyWords * (w - w_lo));
         } else {
             while (p >= B) { p -= B; w++; }
             s.ins = 0;
             if (s.valid) {
-                const uint32_t *kk = rk + 4 * (w - w_lo);
                 const bool lastw = w == w_last;
                 s.ins = w * B + feistel(p, lastw ? len_last : B, lastw ? h_last : hB,
-                                        kk[0], kk[1], kk[2], kk[3]);
+                                        rk + kRoundKeyWords * (w - w_lo));
             }
         }
         p0 += 64;
@@ -219,8 +218,7 @@ struct EmitCtx {   // per-tile constants of k_v2_emit + the running pool2 positi
         const bool cross = p >= B;
         p = cross ? p - B : p;
         const uint32_t w = cross ? w0 + 1 : w0;
-        const uint32_t *kk = rk + 4 * (w - w_lo);
-        return w * B + feistel_once(p, hB, kk[0], kk[1], kk[2], kk[3]);
+        return w * B + feistel_once(p, hB, rk + kRoundKeyWords * (w - w_lo));
     }
     __device__ __forceinline__ void advance256() {
         p0 += 256;
@@ -280,7 +278,7 @@ __global__ __launch_bounds__(64) void k_v2_emit(Geometry g, V2Plan pl,
     const int64_t P1 = pl.P1;
     const int64_t nwin_max = pl.L / g.B + 2;
     uint32_t *rk = smem;                                    // Feistel keys of the tile's windows
-    lds_vu8 *mark = (lds_vu8 *)(rk + 4 * nwin_max);         // collision probe, kMarkBytes
+    lds_vu8 *mark = (lds_vu8 *)(rk + kRoundKeyWords * nwin_max);   // collision probe, kMarkBytes
     const int lane = threadIdx.x;
     const int32_t rl = (int32_t)(blockIdx.x / ng);
     const int64_t tile = g_lo + (int64_t)(blockIdx.x % ng);
@@ -294,7 +292,7 @@ __global__ __launch_bounds__(64) void k_v2_emit(Geometry g, V2Plan pl,
     if (GBUF) {
         buf = gbuf + ((int64_t)rl * pl.G + tile) * P1;      // filled by k_v2_init_g
     } else {
-        buf = (uint32_t *)(smem + 4 * nwin_max + kMarkBytes / 4);
+        buf = (uint32_t *)(smem + kRoundKeyWords * nwin_max + kMarkBytes / 4);
         const uint32_t *VALr = VAL + (int64_t)rl * pl.G * P1;
         const uint32_t *prev = VALr + (tile - 1) * P1;
         for (int64_t s0 = lane; s0 < P1; s0 += 256) {       // 4 independent loads in flight
@@ -447,7 +445,7 @@ __global__ __launch_bounds__(256) void k_v2_emit_sst(Geometry g, V2Plan pl,
         const int n = (int)(thi - a < S ? thi - a : S);
         const uint32_t wa = (uint32_t)(1 + a / g.B);
         const uint32_t pa = (uint32_t)(a - (int64_t)(wa - 1) * g.B);
-        uint32_t ka[4], kb[4];
+        uint32_t ka[kRoundKeyWords], kb[kRoundKeyWords];
         window_round_keys(g, rank, wa, ka);
         window_round_keys(g, rank, (int64_t)wa + 1, kb);
         // P0
@@ -520,14 +518,15 @@ __global__ __launch_bounds__(256) void k_v2_emit_sst(Geometry g, V2Plan pl,
             const bool cross = pp >= B;
             pp = cross ? pp - B : pp;
             w = cross ? w + 1 : w;
-            const uint32_t k0 = cross ? kb[0] : ka[0], k1 = cross ? kb[1] : ka[1];
-            const uint32_t k2 = cross ? kb[2] : ka[2], k3 = cross ? kb[3] : ka[3];
+            uint32_t kk[kFeistelRounds];
+#pragma unroll
+            for (int i = 0; i < kFeistelRounds; i++) kk[i] = cross ? kb[i] : ka[i];
             uint32_t x;
             if (!walk_full && w != w_last) {
-                x = feistel_once(pp, hB, k0, k1, k2, k3);
+                x = feistel_once(pp, hB, kk);
             } else {
                 const bool lastw = w == w_last;
-                x = feistel(pp, lastw ? len_last : B, lastw ? h_last : hB, k0, k1, k2, k3);
+                x = feistel(pp, lastw ? len_last : B, lastw ? h_last : hB, kk);
             }
             insv[p] = w * B + x;
         }
@@ -678,7 +677,7 @@ hipError_t launch_v2(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, 
     const int64_t pos_hi = pos_lo + count < g.ns ? pos_lo + count : g.ns;
     if (nr <= 0 || pos_hi <= pos_lo) return hipSuccess;
     const int64_t nwin_max = pl.L / g.B + 2;
-    const size_t lds_keys = (size_t)4 * nwin_max * sizeof(uint32_t);
+    const size_t lds_keys = (size_t)kRoundKeyWords * nwin_max * sizeof(uint32_t);
     const bool need_tail = pos_hi > pl.T;
     if (pl.G > 0) {
         // pass A over every tile up to the last one emitted (the tail needs all of them);
