@@ -28,6 +28,8 @@ struct V2Plan {         // slot-machine tiling of one V2 stream (DESIGN.md §3.3
     int64_t L;          // steps per tile
     int64_t G;          // tiles per rank = ceil(T / L)
     int32_t global_buf; // 1: slot table lives in HBM scratch (P1 beyond the LDS budget)
+    int32_t fold;       // 1: every virtual id < 2^24, probe byte folded into the slot word
+    int64_t emit_lds;   // dynamic LDS of one k_v2_emit wave (padded to cap waves per CU)
 };
 
 // optional per-kernel timing: `mark(ctx, kind, stream)` is called right before each launch
@@ -89,7 +91,8 @@ hipError_t launch_big_sort(const Geometry &g, const SortJobs &J, int64_t job_lo,
 int64_t big_sort_batch(int64_t nmax, int64_t njobs, size_t budget);
 constexpr size_t kBigSortBudget = (size_t)2 << 30;
 
-V2Plan v2_plan(const Geometry &g);
+// tiling of a launch over nr ranks: sized so that k_v2_emit fills every SIMD with two waves
+V2Plan v2_plan(const Geometry &g, int32_t nr);
 
 // exclusive prefix over the shuffled file order: prefix[f] = sum_{j<f} len[order[j]]
 hipError_t launch_scan_prefix(const int64_t *lens, const int32_t *order, int64_t F,

@@ -138,7 +138,15 @@ __global__ __launch_bounds__(256) void k_v2_init_g(V2Plan pl, int64_t g_lo, int6
 // (a generic volatile pointer lowers to flat sc0 sc1 accesses)
 typedef __attribute__((address_space(3))) volatile uint8_t lds_vu8;
 
+// FOLD (every virtual id < 2^24): the probe byte of slot k is the top byte of buf[k] itself
+// (values live in bits 0..23), so the wave needs no separate probe array -- 16 KB of LDS per
+// wave at P1 = 4096 instead of 20 KB, i.e. 8 instead of 7 waves per CU (2 per SIMD)
+template <bool FOLD>
 struct EmitCtx {   // per-tile constants of k_v2_emit + the running pool2 position (w0, p0)
+    static constexpr uint32_t kValMask = FOLD ? 0x00FFFFFFu : 0xFFFFFFFFu;
+    __device__ __forceinline__ static uint32_t probe_ix(uint32_t k) {
+        return FOLD ? (k << 2) : (k & (uint32_t)(kMarkBytes - 1));
+    }
     uint64_t lt_mask;
     uint32_t *buf;
     lds_vu8 *mark;
@@ -167,7 +175,7 @@ struct EmitCtx {   // per-tile constants of k_v2_emit + the running pool2 positi
         s.k = scale32(uword, P1);
         // collision probe: a lane that reads back another lane's id shares its probe byte
         // (slot & 4095) with a lane of this sub-batch
-        const uint32_t hk = s.k & (uint32_t)(kMarkBytes - 1);
+        const uint32_t hk = probe_ix(s.k);
         if (s.valid) mark[hk] = (uint8_t)lane;
         s.probe = mark[hk];
         // insertion of step t: window w, index p
@@ -205,7 +213,7 @@ struct EmitCtx {   // per-tile constants of k_v2_emit + the running pool2 positi
         s.tl = tl;
         s.valid = true;
         s.k = scale32(uword, P1);
-        const uint32_t hk = s.k & (uint32_t)(kMarkBytes - 1);
+        const uint32_t hk = probe_ix(s.k);
         mark[hk] = (uint8_t)lane;
         s.probe = mark[hk];
         return s;
@@ -234,7 +242,7 @@ struct EmitCtx {   // per-tile constants of k_v2_emit + the running pool2 positi
         uint32_t v;
         if (cm == 0) {
             // every valid lane drew a distinct slot: emit its content, insert in one op
-            v = (FAST || s.valid) ? atomicExch(&buf[s.k], s.ins) : 0u;
+            v = (FAST || s.valid) ? atomicExch(&buf[s.k], s.ins) & kValMask : 0u;
         } else {
             // peers = lanes that drew the same slot; the first of them exchanges the LAST
             // peer's insertion, the others take the previous peer's insertion
@@ -252,7 +260,7 @@ struct EmitCtx {   // per-tile constants of k_v2_emit + the running pool2 positi
             const int prev_lane = lower ? 63 - __clzll((long long)lower) : lane;
             const uint32_t ins_last = (uint32_t)__shfl((int)s.ins, hi_lane);
             const uint32_t ins_prev = (uint32_t)__shfl((int)s.ins, prev_lane);
-            v = (s.valid && !lower) ? atomicExch(&buf[s.k], ins_last) : ins_prev;
+            v = (s.valid && !lower) ? atomicExch(&buf[s.k], ins_last) & kValMask : ins_prev;
         }
         if (FAST || ((uint32_t)s.tl >= e_lo && (uint32_t)s.tl < e_hi)) {
             if (NARROW) {
@@ -266,7 +274,7 @@ struct EmitCtx {   // per-tile constants of k_v2_emit + the running pool2 positi
     }
 };
 
-template <bool GBUF, bool NARROW>
+template <bool GBUF, bool NARROW, bool FOLD>
 __global__ __launch_bounds__(64) void k_v2_emit(Geometry g, V2Plan pl,
                                                 const RankDesc *__restrict__ ranks,
                                                 int32_t rank_lo, int64_t g_lo, int64_t ng,
@@ -278,7 +286,9 @@ __global__ __launch_bounds__(64) void k_v2_emit(Geometry g, V2Plan pl,
     const int64_t P1 = pl.P1;
     const int64_t nwin_max = pl.L / g.B + 2;
     uint32_t *rk = smem;                                    // Feistel keys of the tile's windows
-    lds_vu8 *mark = (lds_vu8 *)(rk + kRoundKeyWords * nwin_max);   // collision probe, kMarkBytes
+    // collision probe: kMarkBytes of its own, or (FOLD) the top byte of each slot word
+    const int mark_words = FOLD ? 0 : kMarkBytes / 4;
+    lds_vu8 *mark = (lds_vu8 *)(rk + kRoundKeyWords * nwin_max);
     const int lane = threadIdx.x;
     const int32_t rl = (int32_t)(blockIdx.x / ng);
     const int64_t tile = g_lo + (int64_t)(blockIdx.x % ng);
@@ -292,7 +302,8 @@ __global__ __launch_bounds__(64) void k_v2_emit(Geometry g, V2Plan pl,
     if (GBUF) {
         buf = gbuf + ((int64_t)rl * pl.G + tile) * P1;      // filled by k_v2_init_g
     } else {
-        buf = (uint32_t *)(smem + kRoundKeyWords * nwin_max + kMarkBytes / 4);
+        buf = (uint32_t *)(smem + kRoundKeyWords * nwin_max + mark_words);
+        if (FOLD) mark = (lds_vu8 *)buf + 3;
         const uint32_t *VALr = VAL + (int64_t)rl * pl.G * P1;
         const uint32_t *prev = VALr + (tile - 1) * P1;
         for (int64_t s0 = lane; s0 < P1; s0 += 256) {       // 4 independent loads in flight
@@ -311,7 +322,7 @@ __global__ __launch_bounds__(64) void k_v2_emit(Geometry g, V2Plan pl,
     }
     stage_round_keys(g, rank, w_lo, nwin, rk);
     __syncthreads();
-    EmitCtx c;
+    EmitCtx<FOLD> c;
     c.lane = lane;
     c.lt_mask = (1ull << lane) - 1ull;
     c.P1 = (uint32_t)P1;
@@ -354,7 +365,7 @@ __global__ __launch_bounds__(64) void k_v2_emit(Geometry g, V2Plan pl,
         if (fast_tile && tl0 >= 0 && (uint32_t)tl0 + 256 <= c.nvalid && c.w0 + 1 < c.w_last) {
             // one branch-free block: 4 probes, 4 independent Feistel chains and the next
             // Philox block interleave; then the 4 sub-batches finish in step order
-            EmitCtx::Step s[4];
+            typename EmitCtx<FOLD>::Step s[4];
 #pragma unroll
             for (int j = 0; j < 4; j++) s[j] = c.probe4(u[j], tl0 + 64 * j + lane);
 #pragma unroll
@@ -362,12 +373,12 @@ __global__ __launch_bounds__(64) void k_v2_emit(Geometry g, V2Plan pl,
             slot_words(g, rank, sb + 1, lane, un);
             c.advance256();
 #pragma unroll
-            for (int j = 0; j < 4; j++) c.finish<true, NARROW>(s[j]);
+            for (int j = 0; j < 4; j++) c.template finish<true, NARROW>(s[j]);
         } else {
 #pragma unroll
             for (int j = 0; j < 4; j++) {
-                const EmitCtx::Step s = c.prep<false>(u[j], tl0 + j * 64 + lane);
-                c.finish<false, NARROW>(s);
+                const typename EmitCtx<FOLD>::Step s = c.template prep<false>(u[j], tl0 + j * 64 + lane);
+                c.template finish<false, NARROW>(s);
             }
             slot_words(g, rank, sb + 1, lane, un);
         }
@@ -638,34 +649,74 @@ static SortJobs tail_jobs(const Geometry &g, const V2Plan &pl, int32_t rank_lo) 
 // ------------------------------------------------------------------------------------------
 // launchers
 // ------------------------------------------------------------------------------------------
-V2Plan v2_plan(const Geometry &g) {
+static int device_cus() {
+    static int cache[64] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+    if (!cache[dev]) {
+        int n = 0;
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+            n = 256;
+        cache[dev] = n;
+    }
+    return cache[dev];
+}
+
+constexpr int64_t kCuLdsBytes = 160 * 1024;
+constexpr int64_t kMaxTileMult = 16;   // tile length <= 16 * P1 steps (Feistel key table bound)
+constexpr int64_t kMinTileMult = 4;    // >= 4 * P1: VAL traffic <= 2 B/step, walk-back <= e^-4
+
+V2Plan v2_plan(const Geometry &g, int32_t nr) {
     V2Plan p{};
     p.P1 = g.B < g.ns ? g.B : g.ns;
     p.T = g.ns - p.P1;
     p.global_buf = p.P1 > kLdsSlotMax;
+    p.fold = !p.global_buf && g.ns <= (int64_t)1 << 24;
     static const int64_t mult_env = [] {
         const char *e = getenv("PSS_V2_TILE_MULT");   // tuning knob: tile = mult * P1 steps
         const long v = e ? atol(e) : 0;
         return (int64_t)(v > 0 ? v : 0);
     }();
-    const int64_t mult = mult_env ? mult_env : (p.global_buf ? 1 : 16);
-    p.L = cdiv(mult * p.P1, 256) * 256;
+    // emit wave LDS: Feistel keys of up to kMaxTileMult + 2 windows, the slot table, the probe
+    const int64_t keys = (int64_t)kRoundKeyWords * 4 * (kMaxTileMult + 2);
+    const int64_t lds = keys + (p.global_buf ? 0 : p.P1 * 4) + (p.fold ? 0 : kMarkBytes);
+    // waves per CU the LDS admits, rounded down to whole SIMD quads (balanced SIMDs), <= 16;
+    // the launch pads its LDS so that no CU takes more (dispatch would otherwise stack a 9th)
+    int64_t wpc = kCuLdsBytes / lds;
+    wpc = wpc > 16 ? 16 : wpc;
+    if (wpc >= 4) wpc &= ~3;
+    p.emit_lds = lds;
+    if (wpc >= 1 && kCuLdsBytes / (wpc + 1) >= lds) p.emit_lds = kCuLdsBytes / (wpc + 1) + 16;
+    int64_t L;
+    if (mult_env) {
+        L = mult_env * p.P1;
+    } else if (p.global_buf) {
+        L = p.P1;
+    } else {
+        // one round of waves: tiles = waves per CU x CUs spread over the nr streams
+        const int64_t waves = wpc * device_cus();
+        const int64_t per_rank = cdiv(waves, nr > 0 ? nr : 1);
+        L = p.T > 0 ? cdiv(p.T, per_rank) : p.P1;
+        const int64_t lo = kMinTileMult * p.P1, hi = kMaxTileMult * p.P1;
+        L = L < lo ? lo : (L > hi ? hi : L);
+    }
+    p.L = cdiv(L, 256) * 256;
     p.G = p.T > 0 ? cdiv(p.T, p.L) : 0;
     return p;
 }
 
 size_t v2_val_bytes(const Geometry &g, int32_t nr) {
-    const V2Plan p = v2_plan(g);
+    const V2Plan p = v2_plan(g, nr);
     return (size_t)nr * (size_t)p.G * (size_t)p.P1 * sizeof(uint32_t);
 }
 
 size_t v2_buf_bytes(const Geometry &g, int32_t nr) {
-    const V2Plan p = v2_plan(g);
+    const V2Plan p = v2_plan(g, nr);
     return p.global_buf ? v2_val_bytes(g, nr) : 0;
 }
 
 size_t v2_sort_bytes(const Geometry &g, int32_t nr) {
-    const V2Plan p = v2_plan(g);
+    const V2Plan p = v2_plan(g, nr);
     if (p.P1 <= kLdsSortMax || nr <= 0) return 0;
     return big_sort_bytes(p.P1, big_sort_batch(p.P1, nr, kBigSortBudget));
 }
@@ -673,7 +724,7 @@ size_t v2_sort_bytes(const Geometry &g, int32_t nr) {
 hipError_t launch_v2(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, int32_t nr,
                      int64_t pos_lo, int64_t count, int64_t *out, uint32_t *VAL, uint32_t *gbuf,
                      uint32_t *sort_ws, int32_t *err, hipStream_t s, const Marker &mk) {
-    const V2Plan pl = v2_plan(g);
+    const V2Plan pl = v2_plan(g, nr);
     const int64_t pos_hi = pos_lo + count < g.ns ? pos_lo + count : g.ns;
     if (nr <= 0 || pos_hi <= pos_lo) return hipSuccess;
     const int64_t nwin_max = pl.L / g.B + 2;
@@ -723,23 +774,25 @@ hipError_t launch_v2(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, 
                                        g_lo, ng, (const uint32_t *)VAL, pos_lo, count, out);
             } else if (!pl.global_buf) {
                 mk(K_V2_EMIT, s);
-                const size_t lds = lds_keys + kMarkBytes + (size_t)pl.P1 * 4;
-                if (narrow)
-                    hipLaunchKernelGGL((k_v2_emit<false, true>), grid, dim3(64), lds, s, g, pl, ranks, rank_lo,
-                                       g_lo, ng, (const uint32_t *)VAL, (uint32_t *)nullptr, pos_lo, count, out);
-                else
-                    hipLaunchKernelGGL((k_v2_emit<false, false>), grid, dim3(64), lds, s, g, pl, ranks, rank_lo,
-                                       g_lo, ng, (const uint32_t *)VAL, (uint32_t *)nullptr, pos_lo, count, out);
+                const size_t need = lds_keys + (size_t)pl.P1 * 4 + (pl.fold ? 0 : kMarkBytes);
+                const size_t lds = need > (size_t)pl.emit_lds ? need : (size_t)pl.emit_lds;
+#define PSS_EMIT(N, F) hipLaunchKernelGGL((k_v2_emit<false, N, F>), grid, dim3(64), lds, s, g, pl, ranks, rank_lo, \
+                                          g_lo, ng, (const uint32_t *)VAL, (uint32_t *)nullptr, pos_lo, count, out)
+                if (pl.fold && narrow) PSS_EMIT(true, true);
+                else if (pl.fold) PSS_EMIT(false, true);
+                else if (narrow) PSS_EMIT(true, false);
+                else PSS_EMIT(false, false);
+#undef PSS_EMIT
             } else {
                 hipLaunchKernelGGL(k_v2_init_g, dim3((uint32_t)cdiv(pl.P1, 256), (uint32_t)(nr * ng)),
                                    dim3(256), 0, s, pl, g_lo, ng, (const uint32_t *)VAL, gbuf);
                 mk(K_V2_EMIT, s);
                 const size_t lds = lds_keys + kMarkBytes;
                 if (narrow)
-                    hipLaunchKernelGGL((k_v2_emit<true, true>), grid, dim3(64), lds, s, g, pl, ranks, rank_lo,
+                    hipLaunchKernelGGL((k_v2_emit<true, true, false>), grid, dim3(64), lds, s, g, pl, ranks, rank_lo,
                                        g_lo, ng, (const uint32_t *)VAL, gbuf, pos_lo, count, out);
                 else
-                    hipLaunchKernelGGL((k_v2_emit<true, false>), grid, dim3(64), lds, s, g, pl, ranks, rank_lo,
+                    hipLaunchKernelGGL((k_v2_emit<true, false, false>), grid, dim3(64), lds, s, g, pl, ranks, rank_lo,
                                        g_lo, ng, (const uint32_t *)VAL, gbuf, pos_lo, count, out);
             }
         }
@@ -777,10 +830,12 @@ hipError_t init_kernel_attributes_v2() {
     PSS_ATTR(k_v2_lastocc);
     PSS_ATTR((k_v2_emit_sst<true>));
     PSS_ATTR((k_v2_emit_sst<false>));
-    PSS_ATTR((k_v2_emit<false, true>));
-    PSS_ATTR((k_v2_emit<false, false>));
-    PSS_ATTR((k_v2_emit<true, true>));
-    PSS_ATTR((k_v2_emit<true, false>));
+    PSS_ATTR((k_v2_emit<false, true, false>));
+    PSS_ATTR((k_v2_emit<false, false, false>));
+    PSS_ATTR((k_v2_emit<false, true, true>));
+    PSS_ATTR((k_v2_emit<false, false, true>));
+    PSS_ATTR((k_v2_emit<true, true, false>));
+    PSS_ATTR((k_v2_emit<true, false, false>));
 #undef PSS_ATTR
     return e;
 }
