@@ -346,11 +346,21 @@ int64_t orc_v1_philox_stream(uint64_t key64, uint32_t rank, int64_t start, int64
     return n_out;
 }
 
-static inline uint32_t v2_slot(uint64_t key64, uint32_t rank, int64_t t, uint32_t P1) {
-    uint64_t c = (uint64_t)(t >> 8) * 64u + (uint64_t)(t & 63);
-    uint32_t ctr[4] = {(uint32_t)c, (uint32_t)(c >> 32), rank, DOM_V2_SLOT}, o[4];
-    orc_philox4x32(ctr, key64, o);
-    uint32_t u = o[(t >> 6) & 3];
+/* V2 slot draw of step t (pss_common.h slot_hash): keyed 2-round multiply-xorshift mixer,
+ * key = the first two words of Philox block (0, 0, rank, DOM_V2_SLOT). */
+static inline uint32_t orc_slot_hash(uint32_t t, uint32_t s0, uint32_t s1) {
+    uint32_t x = t ^ s0;
+    x ^= x >> 16;
+    x *= 0x21F0AAADu;
+    x ^= x >> 15;
+    x ^= s1;
+    x *= 0x735A2D97u;
+    x ^= x >> 15;
+    return x;
+}
+
+static inline uint32_t v2_slot(const uint32_t sk[4], int64_t t, uint32_t P1) {
+    uint32_t u = orc_slot_hash((uint32_t)t, sk[0], sk[1]);
     return (uint32_t)(((uint64_t)u * P1) >> 32);
 }
 
@@ -363,7 +373,7 @@ static inline int64_t v2_vid_to_id(int64_t v, int64_t old_start, int64_t new_sta
 
 /* V2 under the Philox schedule (slot-replacement form of V2:96-116):
  *   P1 = min(B, ns) slots initialised with window 0 (v = s); T = ns - P1 steps;
- *   step t draws slot k_t (Philox DOM_V2_SLOT), emits buf[k_t] and stores the t-th inserted
+ *   step t draws slot k_t (slot hash keyed by Philox DOM_V2_SLOT), emits buf[k_t] and stores the t-th inserted
  *   element there: window w = 1 + t/B, inserted in the order of the Feistel bijection keyed
  *   by Philox (w, 0|1, rank, DOM_V2_INS) (6 rounds);  then the final buffer is emitted in the order of a
  *   stable argsort of Philox keys (j>>2, 0, rank, DOM_V2_TAIL).
@@ -376,8 +386,10 @@ int64_t orc_v2_philox_stream(uint64_t key64, uint32_t rank, int64_t old_start,
     for (int64_t s = 0; s < P1; s++) buf[s] = (uint32_t)s;
     int64_t cur_w = -1;
     uint32_t rk[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint32_t sk[4], skc[4] = {0, 0, rank, DOM_V2_SLOT};
+    orc_philox4x32(skc, key64, sk);
     for (int64_t t = 0; t < T; t++) {
-        uint32_t k = v2_slot(key64, rank, t, (uint32_t)P1);
+        uint32_t k = v2_slot(sk, t, (uint32_t)P1);
         out[t] = v2_vid_to_id(buf[k], old_start, new_start, B, N);
         int64_t w = 1 + t / B, p = t % B;
         if (w != cur_w) {   /* round keys: Philox blocks (w, 0|1, rank, DOM_V2_INS) */

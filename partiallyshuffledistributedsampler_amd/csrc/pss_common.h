@@ -84,6 +84,23 @@ PSS_HD uint32_t feistel_half_bits(uint32_t n) {
     return (uint32_t)((bits + 1) >> 1);
 }
 
+// V2 slot draw of step t (t < 2^32: ns >= 2^32 is rejected).  A keyed 32-bit mixer: two
+// multiply-xorshift rounds with the constants of the lowest-bias published 2-round integer
+// hash (16 / 0x21F0AAAD / 15 / 0x735A2D97 / 15), keyed by (s0, s1) = the first two words of the
+// Philox block (0, 0, rank, DOM_V2_SLOT) under the epoch key.  2 multiplies per step instead
+// of a quarter Philox4x32-10 block (5 64-bit multiplies); tests/test_schedule_quality.py
+// checks that the V2 displacement law still matches the reference's.
+PSS_HD uint32_t slot_hash(uint32_t t, uint32_t s0, uint32_t s1) {
+    uint32_t x = t ^ s0;
+    x ^= x >> 16;
+    x *= 0x21F0AAADu;
+    x ^= x >> 15;
+    x ^= s1;
+    x *= 0x735A2D97u;
+    x ^= x >> 15;
+    return x;
+}
+
 // Lemire multiply-shift: uniform-ish slot in [0, n) from one 32-bit word (bias <= n/2^32).
 PSS_HD uint32_t scale32(uint32_t u, uint32_t n) {
     return (uint32_t)(((uint64_t)u * n) >> 32);

@@ -147,14 +147,20 @@ constexpr size_t sort_lds_bytes() {
 // ------------------------------------------------------------------------------------------
 // V2 helpers
 // ------------------------------------------------------------------------------------------
-// slot draw of step t: super-batch sb = t>>8 holds 256 steps; lane l of a wave draws the
-// Philox block (sb*64 + l) and its word j is the slot of step sb*256 + j*64 + l.
-__device__ __forceinline__ void slot_words(const Geometry &g, uint32_t rank, int64_t sb, int lane,
-                                           uint32_t u[4]) {
-    const uint64_t c = (uint64_t)sb * 64u + (uint64_t)lane;
-    uint32_t c0 = (uint32_t)c, c1 = (uint32_t)(c >> 32), c2 = rank, c3 = DOM_V2_SLOT;
+// slot draw of step t = sb*256 + j*64 + lane (super-batch sb, sub-batch j): slot_hash under
+// the rank's key (SlotKey, computed once per wave)
+struct SlotKey { uint32_t s0, s1; };
+
+__device__ __forceinline__ SlotKey slot_key(const Geometry &g, uint32_t rank) {
+    uint32_t c0 = 0, c1 = 0, c2 = rank, c3 = DOM_V2_SLOT;
     philox4x32_10(c0, c1, c2, c3, g.key0, g.key1);
-    u[0] = c0; u[1] = c1; u[2] = c2; u[3] = c3;
+    return SlotKey{c0, c1};
+}
+
+__device__ __forceinline__ void slot_words(const SlotKey &sk, int64_t sb, int lane, uint32_t u[4]) {
+    const uint32_t t0 = (uint32_t)sb * 256u + (uint32_t)lane;
+#pragma unroll
+    for (int j = 0; j < 4; j++) u[j] = slot_hash(t0 + 64u * j, sk.s0, sk.s1);
 }
 
 // Feistel round keys of pool2 window w: Philox blocks (w, 0, rank, INS) and (w, 1, rank, INS),

@@ -48,19 +48,18 @@ __global__ __launch_bounds__(256) void k_v2_lastocc(Geometry g, V2Plan pl, int32
     const int nwin = (int)(1 + (thi - 1) / g.B - w_lo + 1);
     for (int s = threadIdx.x; s < P1; s += 256) lastT[s] = 0;
     stage_round_keys(g, rank, w_lo, nwin, rk);
+    const SlotKey sk = slot_key(g, rank);
     __syncthreads();
-    const int64_t sb_lo = tlo >> 8, sb_hi = (thi - 1) >> 8;
-    const int64_t ncnt = (sb_hi - sb_lo + 1) * 64;
-    for (int64_t ci = threadIdx.x; ci < ncnt; ci += 256) {
-        const int64_t sb = sb_lo + (ci >> 6);
-        const int lane = (int)(ci & 63);
-        uint32_t u[4];
-        slot_words(g, rank, sb, lane, u);
+    // every step of the tile: last step (tile-local, +1) that drew each slot; 4 independent
+    // hashes in flight per thread
+    const uint32_t n = (uint32_t)(thi - tlo), t0 = (uint32_t)tlo;
+    for (uint32_t b = threadIdx.x; b < n; b += 1024) {
+        uint32_t k[4];
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const int64_t t = sb * 256 + j * 64 + lane;
-            if (t >= tlo && t < thi) atomicMax(&lastT[scale32(u[j], (uint32_t)P1)], (uint32_t)(t - tlo + 1));
-        }
+        for (int j = 0; j < 4; j++) k[j] = scale32(slot_hash(t0 + b + 256u * j, sk.s0, sk.s1), (uint32_t)P1);
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+            if (b + 256u * j < n) atomicMax(&lastT[k[j]], b + 256u * j + 1u);
     }
     __syncthreads();
     uint32_t *V = VAL + ((int64_t)rl * pl.G + tile) * P1;
@@ -89,11 +88,12 @@ __global__ __launch_bounds__(256) void k_v2_lastocc_g(Geometry g, V2Plan pl, int
     uint32_t *V = VAL + ((int64_t)rl * pl.G + tile) * pl.P1;
     const int64_t sb_lo = clo >> 8, sb_hi = (chi - 1) >> 8;
     const int64_t ncnt = (sb_hi - sb_lo + 1) * 64;
+    const SlotKey sk = slot_key(g, rank);
     for (int64_t ci = threadIdx.x; ci < ncnt; ci += 256) {
         const int64_t sb = sb_lo + (ci >> 6);
         const int lane = (int)(ci & 63);
         uint32_t u[4];
-        slot_words(g, rank, sb, lane, u);
+        slot_words(sk, sb, lane, u);
 #pragma unroll
         for (int j = 0; j < 4; j++) {
             const int64_t t = sb * 256 + j * 64 + lane;
@@ -358,8 +358,9 @@ __global__ __launch_bounds__(64) void k_v2_emit(Geometry g, V2Plan pl,
     // the last one or needs cycle walking (windows w0 .. w0 + 1)
     const bool fast_tile = c.e_lo == 0 && c.e_hi == c.nvalid && c.B >= 256 && !c.walk_full;
     int32_t tl0 = (int32_t)(t_first - tlo);   // negative while the super-batch starts before the tile
+    const SlotKey sk = slot_key(g, rank);
     uint32_t u[4];
-    slot_words(g, rank, sb_lo, lane, u);
+    slot_words(sk, sb_lo, lane, u);
     for (int64_t sb = sb_lo; sb <= sb_hi; sb++, tl0 += 256) {
         uint32_t un[4];   // next super-batch's slot words, computed under this one's work
         if (fast_tile && tl0 >= 0 && (uint32_t)tl0 + 256 <= c.nvalid && c.w0 + 1 < c.w_last) {
@@ -370,7 +371,7 @@ __global__ __launch_bounds__(64) void k_v2_emit(Geometry g, V2Plan pl,
             for (int j = 0; j < 4; j++) s[j] = c.probe4(u[j], tl0 + 64 * j + lane);
 #pragma unroll
             for (int j = 0; j < 4; j++) s[j].ins = c.ins4(j);
-            slot_words(g, rank, sb + 1, lane, un);
+            slot_words(sk, sb + 1, lane, un);
             c.advance256();
 #pragma unroll
             for (int j = 0; j < 4; j++) c.template finish<true, NARROW>(s[j]);
@@ -380,7 +381,7 @@ __global__ __launch_bounds__(64) void k_v2_emit(Geometry g, V2Plan pl,
                 const typename EmitCtx<FOLD>::Step s = c.template prep<false>(u[j], tl0 + j * 64 + lane);
                 c.template finish<false, NARROW>(s);
             }
-            slot_words(g, rank, sb + 1, lane, un);
+            slot_words(sk, sb + 1, lane, un);
         }
 #pragma unroll
         for (int j = 0; j < 4; j++) u[j] = un[j];
@@ -451,7 +452,8 @@ __global__ __launch_bounds__(256) void k_v2_emit_sst(Geometry g, V2Plan pl,
     const int per = (P1 + 255) / 256;                // buckets per thread in P2 / P4
     const int blo = tid * per < P1 ? tid * per : P1;
     const int bhi = blo + per < P1 ? blo + per : P1;
-    const int NBLK = (S + 1023) / 1024;              // Philox blocks per thread (<= 4)
+    const int NBLK = (S + 1023) / 1024;              // 4-step groups per thread (<= 4)
+    const SlotKey sk = slot_key(g, rank);
     for (int64_t a = tlo; a < thi; a += S) {
         const int n = (int)(thi - a < S ? thi - a : S);
         const uint32_t wa = (uint32_t)(1 + a / g.B);
@@ -470,7 +472,7 @@ __global__ __launch_bounds__(256) void k_v2_emit_sst(Geometry g, V2Plan pl,
             const int ci = tid + 256 * b;            // (super-batch q, lane)
             const int q = ci >> 6, lane = ci & 63;
             uint32_t u[4] = {0, 0, 0, 0};
-            if (q * 256 < S) slot_words(g, rank, (a >> 8) + q, lane, u);
+            if (q * 256 < S) slot_words(sk, (a >> 8) + q, lane, u);
 #pragma unroll
             for (int w = 0; w < 4; w++) {
                 const int tl = q * 256 + w * 64 + lane;
