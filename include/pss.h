@@ -99,6 +99,13 @@ int pss_profile_read(pss_sampler *h, double *total_ms, int64_t *launches, int32_
 /* Synchronise `stream` and report any device-side error flag of the handle. */
 int pss_check(pss_sampler *h, void *stream);
 
+/* V2 replay kernel selection (no effect on results, which are identical on every path):
+ * 0 = auto (one LDS exchange per step when the device passed the start-up lane-order check,
+ * else the collision-probe kernel), 1 = exchange kernel (PSS_ENOTSUP if the check failed),
+ * 2 = collision-probe kernel.  pss_emit_path reports the path `auto` resolves to. */
+int pss_set_emit_path(pss_sampler *h, int32_t path);
+int pss_emit_path(pss_sampler *h, int32_t *path);
+
 /* Self-test of the wave64 DPP scan primitive: out_dev[2i] = 64-bit inclusive wave scan,
  * out_dev[2i+1] = 32-bit one (low words), for n inputs. */
 int pss_debug_wave_scan(const uint64_t *in_dev, uint64_t *out_dev, int64_t n, void *stream);

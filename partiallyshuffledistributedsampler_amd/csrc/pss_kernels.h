@@ -116,11 +116,16 @@ hipError_t launch_v1(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, 
                      int32_t *err, hipStream_t s, const Marker &mk = Marker());
 size_t v1_workspace_bytes(const Geometry &g, int32_t nr, int64_t pos_lo, int64_t count);
 
+// V2 replay kernel: EMIT_XCHG = one LDS exchange per step (needs the lane-ordered exchange the
+// start-up check confirms), EMIT_PROBE = collision probe + per-clash fix-up (any hardware)
+enum EmitPath { EMIT_AUTO = 0, EMIT_XCHG = 1, EMIT_PROBE = 2 };
+bool lds_xchg_ordered();   // result of the start-up check on the current device
+
 // V2: same contract; val_ws holds the per-tile slot tables
 hipError_t launch_v2(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, int32_t nr,
                      int64_t pos_lo, int64_t count, int64_t *out, uint32_t *val_ws,
                      uint32_t *buf_ws, uint32_t *sort_ws, int32_t *err, hipStream_t s,
-                     const Marker &mk = Marker());
+                     const Marker &mk = Marker(), int emit_path = EMIT_AUTO);
 size_t v2_val_bytes(const Geometry &g, int32_t nr);
 size_t v2_buf_bytes(const Geometry &g, int32_t nr);
 size_t v2_sort_bytes(const Geometry &g, int32_t nr);

@@ -151,6 +151,7 @@ struct pss_sampler {
     std::vector<int64_t> files_len;
     int64_t F = 0, N = 0, ns = 0, B = 0;
     int32_t R = 0, version = 1, shuffle = 1, device = 0;
+    int32_t emit_path = 0;        // pss::EmitPath
     uint64_t seed = 0;
     // history state
     std::vector<int32_t> order;   // self.files as dataset positions
@@ -400,8 +401,32 @@ int pss_generate(pss_sampler *h, int32_t rank_lo, int32_t rank_hi, int64_t pos_l
         if (bb) PSS_HIP(h->d_buf.ensure(words(bb)));
         if (sb) PSS_HIP(h->d_sort.ensure(words(sb)));
         PSS_HIP(pss::launch_v2(g, h->d_ranks.p, rank_lo, nr, pos_lo, count, out_dev, h->d_val.p,
-                               h->d_buf.p, h->d_sort.p, h->d_err.p, s, mk));
+                               h->d_buf.p, h->d_sort.p, h->d_err.p, s, mk, h->emit_path));
     }
+    return PSS_OK;
+}
+
+int pss_set_emit_path(pss_sampler *h, int32_t path) {
+    if (!h) return fail(PSS_EINVAL, "NULL handle");
+    if (path < pss::EMIT_AUTO || path > pss::EMIT_PROBE) return fail(PSS_EINVAL, "bad emit path");
+    if (path == pss::EMIT_XCHG) {
+        DeviceGuard dg(h->device);
+        int rc = ensure_device(h);
+        if (rc) return rc;
+        if (!pss::lds_xchg_ordered())
+            return fail(PSS_ENOTSUP, "device failed the LDS exchange-order check");
+    }
+    h->emit_path = path;
+    return PSS_OK;
+}
+
+int pss_emit_path(pss_sampler *h, int32_t *path) {
+    if (!h || !path) return fail(PSS_EINVAL, "NULL argument");
+    if (h->emit_path != pss::EMIT_AUTO) { *path = h->emit_path; return PSS_OK; }
+    DeviceGuard dg(h->device);
+    int rc = ensure_device(h);
+    if (rc) return rc;
+    *path = pss::lds_xchg_ordered() ? pss::EMIT_XCHG : pss::EMIT_PROBE;
     return PSS_OK;
 }
 

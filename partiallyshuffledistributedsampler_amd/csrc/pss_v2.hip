@@ -388,6 +388,157 @@ __global__ __launch_bounds__(64) void k_v2_emit(Geometry g, V2Plan pl,
     }
 }
 
+// ---- pass B, exchange-ordered (the default on gfx950) --------------------------------------
+// One ds_wrxchg_rtn_b32 whose lanes hit the same LDS word behaves on gfx950 like the lanes
+// exchanging one after another in ascending lane order (checked at start-up by
+// k_xchg_order_check below, and tools/lds_xchg_order.hip): lane l gets the value the highest
+// lower lane on that slot inserted, the lowest gets the slot's content, the slot ends with the
+// highest lane's insertion.  That is exactly the sequential replay of 64 consecutive steps, so
+// each step is ONE exchange -- no probe, no ballot, no per-clash fix-up -- and the four
+// exchanges of a super-batch issue back to back behind a single wait.
+template <bool NARROW>
+__device__ __forceinline__ int64_t emit_id(uint32_t v, uint32_t twoB, uint32_t old32, uint32_t new32,
+                                           uint32_t N32, const RankDesc &rd, const Geometry &g) {
+    if (NARROW) {
+        const uint32_t id = (v < twoB ? old32 : new32) + v;
+        const uint32_t idw = id - N32;
+        return (int64_t)(id < N32 ? id : idw);
+    }
+    return v2_id(v, rd, g);
+}
+
+template <bool NARROW>
+__global__ __launch_bounds__(64) void k_v2_emit_x(Geometry g, V2Plan pl,
+                                                  const RankDesc *__restrict__ ranks,
+                                                  int32_t rank_lo, int64_t g_lo, int64_t ng,
+                                                  const uint32_t *__restrict__ VAL,
+                                                  int64_t pos_lo, int64_t count,
+                                                  int64_t *__restrict__ out) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+    const uint32_t P1 = (uint32_t)pl.P1;
+    const int64_t nwin_max = pl.L / g.B + 2;
+    uint32_t *rk = smem;                                    // Feistel keys of the tile's windows
+    uint32_t *buf = smem + kRoundKeyWords * nwin_max;       // slot table
+    const int lane = threadIdx.x;
+    const int32_t rl = (int32_t)(blockIdx.x / ng);
+    const int64_t tile = g_lo + (int64_t)(blockIdx.x % ng);
+    const uint32_t rank = (uint32_t)(rank_lo + rl);
+    const RankDesc rd = ranks[rank];
+    int64_t tlo, thi;
+    tile_bounds(pl, tile, tlo, thi);
+    const int64_t w_lo = 1 + tlo / g.B;
+    const int nwin = (int)(1 + (thi - 1) / g.B - w_lo + 1);
+    {   // slot table at the tile's start (4 independent loads in flight per lane)
+        const uint32_t *VALr = VAL + (int64_t)rl * pl.G * pl.P1;
+        const uint32_t *prev = VALr + (tile - 1) * pl.P1;
+        for (uint32_t s0 = lane; s0 < P1; s0 += 256) {
+            uint32_t v[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const uint32_t s = s0 + 64 * u;
+                v[u] = (tile > 0 && s < P1) ? prev[s] : kNone;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const uint32_t s = s0 + 64 * u;
+                if (s < P1) buf[s] = v[u] != kNone ? v[u] : slot_value_after(VALr, pl.P1, tile - 2, s);
+            }
+        }
+    }
+    stage_round_keys(g, rank, w_lo, nwin, rk);
+    const SlotKey sk = slot_key(g, rank);
+    __syncthreads();
+    // tile-local step tl = t - tlo (tlo is a multiple of 256); the tile emits tl in [e_lo, e_hi)
+    const int64_t pos_hi = pos_lo + count;
+    const uint32_t nvalid = (uint32_t)(thi - tlo);
+    const uint32_t e_lo = (uint32_t)(pos_lo > tlo ? (pos_lo - tlo < nvalid ? pos_lo - tlo : nvalid) : 0);
+    const uint32_t e_hi = (uint32_t)(pos_hi < thi ? (pos_hi > tlo ? pos_hi - tlo : 0) : nvalid);
+    int64_t *o = out + (int64_t)rl * count + (tlo - pos_lo);
+    const uint32_t twoB = (uint32_t)(2 * g.B < g.ns ? 2 * g.B : g.ns);
+    const uint32_t old32 = (uint32_t)rd.old_start, new32 = (uint32_t)rd.new_start;
+    const uint32_t N32 = (uint32_t)g.N;
+    const uint32_t B = (uint32_t)g.B;
+    const uint32_t hB = feistel_half_bits(B);
+    const bool walk_full = B != (1u << (2 * hB));           // full windows need cycle walking
+    const uint32_t w_last = (uint32_t)(1 + (pl.T - 1) / g.B);  // last pool2 window (may be short)
+    const uint32_t len_last = (uint32_t)(g.ns - (int64_t)w_last * g.B);
+    const uint32_t h_last = feistel_half_bits(len_last);
+    const uint32_t wl = (uint32_t)w_lo;
+    const uint32_t t0 = (uint32_t)tlo;
+    // pool2 position (w0, p0) of the super-batch's first step, advanced without division
+    uint32_t w0 = (uint32_t)(1 + tlo / g.B);
+    uint32_t p0 = (uint32_t)(tlo - (int64_t)(w0 - 1) * g.B);
+    // fast super-batches: every step valid and emitted, B >= 256 (at most one window boundary
+    // per super-batch), neither window short nor cycle-walking
+    const bool fast_tile = e_lo == 0 && e_hi == nvalid && B >= 256 && !walk_full;
+    for (uint32_t tl0 = 0; tl0 < nvalid; tl0 += 256) {
+        if (fast_tile && tl0 + 256 <= nvalid && w0 + 1 < w_last) {
+            uint32_t k[4], ins[4], v[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                k[j] = scale32(slot_hash(t0 + tl0 + 64u * j + lane, sk.s0, sk.s1), P1);
+                uint32_t p = p0 + 64u * j + lane;
+                const bool cross = p >= B;
+                p = cross ? p - B : p;
+                const uint32_t w = cross ? w0 + 1 : w0;
+                ins[j] = w * B + feistel_once(p, hB, rk + kRoundKeyWords * (w - wl));
+            }
+#pragma unroll
+            for (int j = 0; j < 4; j++) v[j] = atomicExch(&buf[k[j]], ins[j]);
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+                o[tl0 + 64u * j + lane] = emit_id<NARROW>(v[j], twoB, old32, new32, N32, rd, g);
+        } else {
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const uint32_t tl = tl0 + 64u * j + lane;
+                if (tl < nvalid) {
+                    const uint32_t kk = scale32(slot_hash(t0 + tl, sk.s0, sk.s1), P1);
+                    uint32_t p = p0 + 64u * j + lane, w = w0;
+                    while (p >= B) { p -= B; w++; }
+                    const bool lastw = w == w_last;
+                    const uint32_t in = w * B + feistel(p, lastw ? len_last : B, lastw ? h_last : hB,
+                                                        rk + kRoundKeyWords * (w - wl));
+                    const uint32_t vv = atomicExch(&buf[kk], in);
+                    if (tl >= e_lo && tl < e_hi) o[tl] = emit_id<NARROW>(vv, twoB, old32, new32, N32, rd, g);
+                }
+            }
+        }
+        p0 += 256;
+        while (p0 >= B) { p0 -= B; w0++; }
+    }
+}
+
+// Start-up check of the exchange order k_v2_emit_x relies on: random slot patterns (heavy
+// collisions at 64 slots, sparse at 4096) against the sequential lane-order model.
+__global__ __launch_bounds__(64) void k_xchg_order_check(int iters, uint32_t P, uint32_t *bad) {
+    __shared__ uint32_t buf[4096];
+    __shared__ uint32_t model[4096];
+    const int lane = threadIdx.x;
+    for (uint32_t s = lane; s < P; s += 64) { buf[s] = 0xF0000000u | s; model[s] = 0xF0000000u | s; }
+    __syncthreads();
+    uint32_t nbad = 0;
+    for (int it = 0; it < iters; it++) {
+        const uint32_t kslot = scale32(slot_hash((uint32_t)(blockIdx.x * iters + it) * 64u + lane, 0x9E3779B9u, 0x7F4A7C15u), P);
+        const uint32_t ins = ((uint32_t)it << 8) ^ (uint32_t)lane;
+        const uint32_t got = atomicExch(&buf[kslot], ins);
+        __syncthreads();
+        uint32_t expect = 0;
+        for (int l = 0; l < 64; l++) {          // lane 0 replays the 64 exchanges in lane order
+            const uint32_t kl = (uint32_t)__shfl((int)kslot, l);
+            const uint32_t il = (uint32_t)__shfl((int)ins, l);
+            uint32_t old = 0;
+            if (lane == 0) { old = model[kl]; model[kl] = il; }
+            old = (uint32_t)__shfl((int)old, 0);
+            if (lane == l) expect = old;
+        }
+        __syncthreads();
+        nbad += got != expect;
+    }
+    for (uint32_t s = lane; s < P; s += 64) nbad += buf[s] != model[s];
+    if (nbad) atomicAdd(bad, nbad);
+}
+
 // ---- pass B, sorted sub-tiles ---------------------------------------------------------------
 // One 256-thread workgroup per tile; the tile is cut into sub-tiles of S <= 4096 steps
 // (S a multiple of 256, S <= P1).  Per sub-tile, in LDS:
@@ -725,7 +876,9 @@ size_t v2_sort_bytes(const Geometry &g, int32_t nr) {
 
 hipError_t launch_v2(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, int32_t nr,
                      int64_t pos_lo, int64_t count, int64_t *out, uint32_t *VAL, uint32_t *gbuf,
-                     uint32_t *sort_ws, int32_t *err, hipStream_t s, const Marker &mk) {
+                     uint32_t *sort_ws, int32_t *err, hipStream_t s, const Marker &mk,
+                     int emit_path) {
+    if (emit_path == EMIT_AUTO) emit_path = lds_xchg_ordered() ? EMIT_XCHG : EMIT_PROBE;
     const V2Plan pl = v2_plan(g, nr);
     const int64_t pos_hi = pos_lo + count < g.ns ? pos_lo + count : g.ns;
     if (nr <= 0 || pos_hi <= pos_lo) return hipSuccess;
@@ -774,7 +927,17 @@ hipError_t launch_v2(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, 
                 else
                     hipLaunchKernelGGL((k_v2_emit_sst<false>), grid, blk, lds, s, g, pl, ranks, rank_lo,
                                        g_lo, ng, (const uint32_t *)VAL, pos_lo, count, out);
-            } else if (!pl.global_buf) {
+            } else if (!pl.global_buf && emit_path == EMIT_XCHG) {
+                mk(K_V2_EMIT, s);
+                const size_t need = lds_keys + (size_t)pl.P1 * 4;
+                const size_t lds = need > (size_t)pl.emit_lds ? need : (size_t)pl.emit_lds;
+                if (narrow)
+                    hipLaunchKernelGGL((k_v2_emit_x<true>), grid, dim3(64), lds, s, g, pl, ranks, rank_lo,
+                                       g_lo, ng, (const uint32_t *)VAL, pos_lo, count, out);
+                else
+                    hipLaunchKernelGGL((k_v2_emit_x<false>), grid, dim3(64), lds, s, g, pl, ranks, rank_lo,
+                                       g_lo, ng, (const uint32_t *)VAL, pos_lo, count, out);
+            } else if (!pl.global_buf) {   // probe path (EMIT_PROBE)
                 mk(K_V2_EMIT, s);
                 const size_t need = lds_keys + (size_t)pl.P1 * 4 + (pl.fold ? 0 : kMarkBytes);
                 const size_t lds = need > (size_t)pl.emit_lds ? need : (size_t)pl.emit_lds;
@@ -823,13 +986,45 @@ hipError_t launch_v2(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, 
     return hipGetLastError();
 }
 
+static signed char g_xchg_ordered[64];   // per device: 0 unknown, 1 ordered, -1 not
+
+hipError_t check_lds_xchg_order() {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    if (dev < 0 || dev >= 64 || g_xchg_ordered[dev]) return hipSuccess;
+    uint32_t *bad = nullptr, hbad[2] = {1, 1};
+    e = hipMalloc((void **)&bad, 2 * sizeof(uint32_t));
+    if (e != hipSuccess) return e;
+    e = hipMemset(bad, 0, 2 * sizeof(uint32_t));
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(k_xchg_order_check, dim3(32), dim3(64), 0, 0, 64, 64u, bad);
+        hipLaunchKernelGGL(k_xchg_order_check, dim3(32), dim3(64), 0, 0, 64, 4096u, bad + 1);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpy(hbad, bad, sizeof(hbad), hipMemcpyDeviceToHost);
+    (void)hipFree(bad);
+    if (e != hipSuccess) return e;
+    g_xchg_ordered[dev] = (hbad[0] == 0 && hbad[1] == 0) ? 1 : -1;
+    return hipSuccess;
+}
+
+bool lds_xchg_ordered() {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return false;
+    if (!g_xchg_ordered[dev] && check_lds_xchg_order() != hipSuccess) return false;
+    return g_xchg_ordered[dev] > 0;
+}
+
 hipError_t init_kernel_attributes_v2() {
     const int big = 160 * 1024;
-    hipError_t e = hipSuccess;
+    hipError_t e = check_lds_xchg_order();
 #define PSS_ATTR(fn) { hipError_t x = hipFuncSetAttribute((const void *)(fn), hipFuncAttributeMaxDynamicSharedMemorySize, big); if (x != hipSuccess) e = x; }
     PSS_ATTR(k_v2_tail<32>);
     PSS_ATTR(k_v2_tail<64>);
     PSS_ATTR(k_v2_lastocc);
+    PSS_ATTR((k_v2_emit_x<true>));
+    PSS_ATTR((k_v2_emit_x<false>));
     PSS_ATTR((k_v2_emit_sst<true>));
     PSS_ATTR((k_v2_emit_sst<false>));
     PSS_ATTR((k_v2_emit<false, true, false>));

@@ -144,6 +144,17 @@ class IndexEngine:
         d = self._dev()
         _lib.call("pss_check", self._h, _stream_ptr(stream, d))
 
+    EMIT_PATHS = {"auto": 0, "xchg": 1, "probe": 2}
+
+    def set_emit_path(self, path):
+        """V2 replay kernel: "auto", "xchg" (one LDS exchange per step) or "probe"."""
+        _lib.call("pss_set_emit_path", self._h, self.EMIT_PATHS[path])
+
+    def emit_path(self):
+        v = ctypes.c_int32()
+        _lib.call("pss_emit_path", self._h, ctypes.byref(v))
+        return {1: "xchg", 2: "probe"}[v.value]
+
     KERNEL_KINDS = ("scan", "v1_window", "v2_lastocc", "v2_emit", "v2_tail", "map",
                     "partition", "digest")
 

@@ -203,3 +203,33 @@ def test_v2_displacement_bounds():
         pos = np.arange(ns)
         assert (pos - v).min() >= -2 * B
         assert np.array_equal(np.sort(v), np.arange(ns))
+
+
+def test_exchange_emit_path_is_the_default():
+    # MI355X passes the start-up lane-order check: the one-exchange-per-step kernel runs
+    eng = _engine(np.full(10, 1000), 10000, 2, 256, 2)
+    assert eng.emit_path() == "xchg"
+
+
+@pytest.mark.parametrize("path", ["xchg", "probe"])
+@pytest.mark.parametrize("B,R,F,lo,hi", [(4096, 3, 40, 5000, 9000), (1000, 4, 60, 500, 3000),
+                                         (300, 2, 30, 100, 900), (64, 5, 20, 10, 200),
+                                         (2048, 2, 8, 10000, 40000)])
+def test_v2_emit_paths_match_oracle(path, B, R, F, lo, hi):
+    # both replay kernels, full epochs and ragged position ranges, against the oracle twin
+    rng = np.random.default_rng(B + R)
+    lengths = rng.integers(lo, hi, F)
+    N = int(lengths.sum())
+    eng = _engine(lengths, N, R, B, 2, seed=99)
+    eng.set_emit_path(path)
+    ns = eng.num_samples
+    eng.init_iter(4)
+    old, new = eng.rank_starts()
+    full = eng.generate(0, R).cpu().numpy()
+    key = O.epoch_key(99, 4)
+    for r in range(R):
+        assert np.array_equal(full[r], O.v2_philox_stream(key, r, int(old[r]), int(new[r]), ns, B, N)), r
+    for pos_lo, count in ((0, 63), (5, 300), (B - 1, 2 * B + 7), (ns // 2, 999), (ns - 100, 100)):
+        part = eng.generate(0, R, pos_lo, count).cpu().numpy()
+        c = min(count, ns - pos_lo)
+        assert np.array_equal(part[:, :c], full[:, pos_lo:pos_lo + c]), (pos_lo, count)
