@@ -60,7 +60,8 @@ int pss_blocks(const pss_sampler *h, int32_t *blocks /* [R] */);
 int pss_rank_starts(const pss_sampler *h, int64_t *old_start /* [R] */, int64_t *new_start /* [R] */);
 
 /* Upload the epoch descriptors and run the device prefix scan over the shuffled files_len
- * (replaces the lazy past_files_samples scan, V1:181-190).  Implied by the calls below. */
+ * (replaces the lazy past_files_samples scan, V1:181-190).  Implied by the calls below:
+ * pss_generate needs only the upload; pss_map / pss_partition run the scan on first use. */
 int pss_prepare(pss_sampler *h, void *stream);
 
 /* Index generation (V1:151-172 / V2:96-116,170-176): positions [pos_lo, pos_lo+count) of

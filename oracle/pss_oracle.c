@@ -375,8 +375,8 @@ static inline int64_t v2_vid_to_id(int64_t v, int64_t old_start, int64_t new_sta
  *   P1 = min(B, ns) slots initialised with window 0 (v = s); T = ns - P1 steps;
  *   step t draws slot k_t (slot hash keyed by Philox DOM_V2_SLOT), emits buf[k_t] and stores the t-th inserted
  *   element there: window w = 1 + t/B, inserted in the order of the Feistel bijection keyed
- *   by Philox (w, 0|1, rank, DOM_V2_INS) (6 rounds);  then the final buffer is emitted in the order of a
- *   stable argsort of Philox keys (j>>2, 0, rank, DOM_V2_TAIL).
+ *   by Philox (w, 0|1, rank, DOM_V2_INS) (6 rounds);  then the final buffer is emitted in the
+ *   order of the Feistel bijection of [0, P1) keyed by Philox (0, 0|1, rank, DOM_V2_TAIL).
  * Writes all ns ids (rank order) to out; returns ns. */
 int64_t orc_v2_philox_stream(uint64_t key64, uint32_t rank, int64_t old_start,
                              int64_t new_start, int64_t ns, int64_t B, int64_t N, int64_t *out) {
@@ -402,11 +402,16 @@ int64_t orc_v2_philox_stream(uint64_t key64, uint32_t rank, int64_t old_start,
         int64_t len = ns - w * B; if (len > B) len = B;
         buf[k] = (uint32_t)(w * B + orc_feistel((uint32_t)p, (uint32_t)len, rk));
     }
-    uint32_t *perm = (uint32_t *)malloc(sizeof(uint32_t) * (size_t)P1);
-    orc_sort_perm(key64, 0, rank, DOM_V2_TAIL, P1, perm);
+    /* tail: the final buffer drained in the order of the Feistel bijection of [0, P1) keyed by
+     * Philox blocks (0, 0|1, rank, DOM_V2_TAIL) */
+    uint32_t tk[8];
+    uint32_t t0[4] = {0, 0, rank, DOM_V2_TAIL}, t1[4] = {0, 1, rank, DOM_V2_TAIL};
+    orc_philox4x32(t0, key64, tk);
+    orc_philox4x32(t1, key64, tk + 4);
     for (int64_t j = 0; j < P1; j++)
-        out[T + j] = v2_vid_to_id(buf[perm[j]], old_start, new_start, B, N);
-    free(perm); free(buf);
+        out[T + j] = v2_vid_to_id(buf[orc_feistel((uint32_t)j, (uint32_t)P1, tk)], old_start,
+                                  new_start, B, N);
+    free(buf);
     return ns;
 }
 

@@ -177,6 +177,17 @@ __device__ __forceinline__ void window_round_keys(const Geometry &g, uint32_t ra
     }
 }
 
+// Feistel keys of the final-pool drain (V2 tail): Philox blocks (0, 0|1, rank, DOM_V2_TAIL)
+__device__ __forceinline__ void tail_round_keys(const Geometry &g, uint32_t rank,
+                                                uint32_t k[kRoundKeyWords]) {
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+        uint32_t c0 = 0, c1 = (uint32_t)h, c2 = rank, c3 = DOM_V2_TAIL;
+        philox4x32_10(c0, c1, c2, c3, g.key0, g.key1);
+        k[4 * h] = c0; k[4 * h + 1] = c1; k[4 * h + 2] = c2; k[4 * h + 3] = c3;
+    }
+}
+
 // virtual index inserted at step t (pool2 window w = 1 + t/B in Feistel order), given the
 // window's round keys
 __device__ __forceinline__ uint32_t ins_value_k(const Geometry &g, int64_t t, const uint32_t *k) {

@@ -95,8 +95,10 @@ constexpr size_t kBigSortBudget = (size_t)2 << 30;
 V2Plan v2_plan(const Geometry &g, int32_t nr);
 
 // exclusive prefix over the shuffled file order: prefix[f] = sum_{j<f} len[order[j]]
+// scratch: scan_scratch_words(F) words
 hipError_t launch_scan_prefix(const int64_t *lens, const int32_t *order, int64_t F,
-                              int64_t *prefix, hipStream_t s);
+                              int64_t *prefix, uint64_t *scratch, hipStream_t s);
+size_t scan_scratch_words(int64_t F);
 
 // per-rank file segments of ranks [rank_lo, rank_lo+nr); counts-only when seg_cap == 0
 hipError_t launch_partition(const Geometry &g, const RankDesc *ranks, int32_t rank_lo,

@@ -5,7 +5,7 @@
 // The hot path of the reference (index generation, V1:157-172 / V2:96-116, and the id ->
 // (file, offset) scan, V1:181-221) is restated as integer, HBM-write-bound kernels:
 //
-//   k_scan_prefix      exclusive scan of files_len over the shuffled file order (wave64 DPP)
+//   k_scan_partial/_final  exclusive scan of files_len over the shuffled file order (wave64 DPP)
 //   k_part_*           balanced file -> rank partition (segments of each rank's id block)
 //   k_v1_lds<EPT>      V1: one workgroup per (rank, window); pool permutation = stable sort
 //                      of Philox keys in LDS (bucket pass on the top key bits + fix-up)
@@ -24,23 +24,57 @@ namespace pss {
 // ------------------------------------------------------------------------------------------
 // scan + partition (V1:27-53,181-190 / V2:27-49,184-193)
 // ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(1024) void k_scan_prefix(const int64_t *__restrict__ lens,
-                                                      const int32_t *__restrict__ order,
-                                                      int64_t F, int64_t *__restrict__ prefix) {
-    __shared__ uint64_t tot[16];
-    const int64_t per = (F + 1023) / 1024;
-    int64_t lo = (int64_t)threadIdx.x * per;
-    if (lo > F) lo = F;
-    const int64_t hi = lo + per < F ? lo + per : F;
-    uint64_t s = 0;
-    for (int64_t f = lo; f < hi; f++) s += (uint64_t)lens[order[f]];
+// Two passes over chunks of 4096 files (256 threads x 16, coalesced order reads):
+// k_scan_partial sums each chunk; k_scan_final adds the sums of the chunks before its own and
+// scans its chunk with 16 workgroup DPP scans.  One chunk (F <= 4096) skips the first pass.
+constexpr int kScanChunk = 4096;
+
+__device__ __forceinline__ uint64_t block_sum256(uint64_t x, uint64_t *tot) {
     uint64_t total;
-    uint64_t run = block_excl_scan<1024>(s, tot, total);
-    for (int64_t f = lo; f < hi; f++) {
-        prefix[f] = (int64_t)run;
-        run += (uint64_t)lens[order[f]];
+    (void)block_excl_scan<256>(x, tot, total);
+    return total;
+}
+
+__global__ __launch_bounds__(256) void k_scan_partial(const int64_t *__restrict__ lens,
+                                                      const int32_t *__restrict__ order,
+                                                      int64_t F, uint64_t *__restrict__ part) {
+    __shared__ uint64_t tot[4];
+    const int64_t base = (int64_t)blockIdx.x * kScanChunk;
+    uint64_t s = 0;
+#pragma unroll
+    for (int j = 0; j < kScanChunk / 256; j++) {
+        const int64_t f = base + j * 256 + threadIdx.x;
+        if (f < F) s += (uint64_t)lens[order[f]];
     }
-    if (threadIdx.x == 0) prefix[F] = (int64_t)total;
+    const uint64_t total = block_sum256(s, tot);
+    if (threadIdx.x == 0) part[blockIdx.x] = total;
+}
+
+__global__ __launch_bounds__(256) void k_scan_final(const int64_t *__restrict__ lens,
+                                                    const int32_t *__restrict__ order, int64_t F,
+                                                    const uint64_t *__restrict__ part,
+                                                    int64_t *__restrict__ prefix) {
+    __shared__ uint64_t tot[4];
+    const int64_t c = blockIdx.x;
+    const int64_t base = c * kScanChunk;
+    uint64_t x[kScanChunk / 256];
+#pragma unroll
+    for (int j = 0; j < kScanChunk / 256; j++) {       // all 16 gathers in flight
+        const int64_t f = base + j * 256 + threadIdx.x;
+        x[j] = f < F ? (uint64_t)lens[order[f]] : 0;
+    }
+    uint64_t cs = 0;
+    for (int64_t i = threadIdx.x; i < c; i += 256) cs += part[i];
+    uint64_t carry = block_sum256(cs, tot);
+#pragma unroll
+    for (int j = 0; j < kScanChunk / 256; j++) {
+        const int64_t f = base + j * 256 + threadIdx.x;
+        uint64_t total;
+        const uint64_t ex = block_excl_scan<256>(x[j], tot, total);
+        if (f < F) prefix[f] = (int64_t)(carry + ex);
+        carry += total;
+    }
+    if (c == gridDim.x - 1 && threadIdx.x == 0) prefix[F] = (int64_t)carry;
 }
 
 // largest f in [0, F) with prefix[f] <= id  (the file holding id; empty files are skipped
@@ -243,9 +277,15 @@ __global__ __launch_bounds__(256) void k_v1_write_big(Geometry g, const RankDesc
 // ------------------------------------------------------------------------------------------
 static inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
+size_t scan_scratch_words(int64_t F) { return (size_t)cdiv(F > 0 ? F : 1, kScanChunk); }
+
 hipError_t launch_scan_prefix(const int64_t *lens, const int32_t *order, int64_t F,
-                              int64_t *prefix, hipStream_t s) {
-    hipLaunchKernelGGL(k_scan_prefix, dim3(1), dim3(1024), 0, s, lens, order, F, prefix);
+                              int64_t *prefix, uint64_t *scratch, hipStream_t s) {
+    const int64_t nc = cdiv(F > 0 ? F : 1, kScanChunk);
+    if (nc > 1)
+        hipLaunchKernelGGL(k_scan_partial, dim3((uint32_t)nc), dim3(256), 0, s, lens, order, F, scratch);
+    hipLaunchKernelGGL(k_scan_final, dim3((uint32_t)nc), dim3(256), 0, s, lens, order, F,
+                       (const uint64_t *)scratch, prefix);
     return hipGetLastError();
 }
 

@@ -162,6 +162,7 @@ struct pss_sampler {
     // device state
     bool dev_init = false;
     bool dirty = true;
+    bool prefix_dirty = true;     // prefix scan owed (run lazily by map / partition)
     DevBuf<int64_t> d_lens, d_prefix;
     DevBuf<int32_t> d_order, d_err;
     DevBuf<pss::RankDesc> d_ranks;
@@ -217,7 +218,7 @@ int ensure_device(pss_sampler *h) {
     PSS_HIP(pss::init_kernel_attributes());
     PSS_HIP(h->d_lens.ensure((size_t)h->F));
     PSS_HIP(h->d_order.ensure((size_t)h->F));
-    PSS_HIP(h->d_prefix.ensure((size_t)h->F + 1));
+    PSS_HIP(h->d_prefix.ensure((size_t)h->F + 1 + pss::scan_scratch_words(h->F)));
     PSS_HIP(h->d_ranks.ensure((size_t)h->R));
     PSS_HIP(h->d_err.ensure(1));
     PSS_HIP(hipMemset(h->d_err.p, 0, sizeof(int32_t)));
@@ -241,11 +242,22 @@ int prepare(pss_sampler *h, hipStream_t s) {
     PSS_HIP(hipMemcpyAsync(h->d_ranks.p, h->h_stage_ranks, sizeof(pss::RankDesc) * h->R, hipMemcpyHostToDevice, s));
     PSS_HIP(hipEventRecord(h->upload_done, s));
     h->upload_pending = true;
+    h->dirty = false;
+    h->prefix_dirty = true;
+    return PSS_OK;
+}
+
+// the exclusive prefix over the epoch's file order is needed only by the id -> (file, offset)
+// map and the partition, so it is scanned on first use after an init_iter
+int prepare_prefix(pss_sampler *h, hipStream_t s) {
+    int rc = prepare(h, s);
+    if (rc || !h->prefix_dirty) return rc;
     const pss::Marker mk = marker_of(h);
     mk(pss::K_SCAN, s);
-    PSS_HIP(pss::launch_scan_prefix(h->d_lens.p, h->d_order.p, h->F, h->d_prefix.p, s));
+    PSS_HIP(pss::launch_scan_prefix(h->d_lens.p, h->d_order.p, h->F, h->d_prefix.p,
+                                    (uint64_t *)(h->d_prefix.p + h->F + 1), s));
     mk(-1, s);
-    h->dirty = false;
+    h->prefix_dirty = false;
     return PSS_OK;
 }
 
@@ -373,7 +385,7 @@ int pss_rank_starts(const pss_sampler *h, int64_t *old_start, int64_t *new_start
 int pss_prepare(pss_sampler *h, void *stream) {
     if (!h) return fail(PSS_EINVAL, "NULL handle");
     DeviceGuard dg(h->device);
-    return prepare(h, (hipStream_t)stream);
+    return prepare_prefix(h, (hipStream_t)stream);
 }
 
 int pss_generate(pss_sampler *h, int32_t rank_lo, int32_t rank_hi, int64_t pos_lo,
@@ -462,7 +474,7 @@ int pss_map(pss_sampler *h, const int64_t *ids_dev, int64_t n, int32_t *file_pos
     if (h->F == 0) return fail(PSS_ESTATE, "no files to map into");
     DeviceGuard dg(h->device);
     hipStream_t s = (hipStream_t)stream;
-    int rc = prepare(h, s);
+    int rc = prepare_prefix(h, s);
     if (rc) return rc;
     PSS_HIP(pss::launch_map(h->d_prefix.p, h->F, ids_dev, n, file_pos_dev, offset_dev, s));
     return PSS_OK;
@@ -478,7 +490,7 @@ int pss_partition(pss_sampler *h, int32_t rank_lo, int32_t rank_hi, int64_t *seg
     if (h->F == 0) return fail(PSS_ESTATE, "no files to partition");
     DeviceGuard dg(h->device);
     hipStream_t s = (hipStream_t)stream;
-    int rc = prepare(h, s);
+    int rc = prepare_prefix(h, s);
     if (rc) return rc;
     PSS_HIP(pss::launch_partition(h->geometry(), h->d_ranks.p, rank_lo, rank_hi - rank_lo,
                                   h->d_prefix.p, h->F, seg_off_dev, seg_file_dev, seg_lo_dev,

@@ -10,8 +10,11 @@
 //                    each step exchanges its insertion into the drawn slot (ds_wrxchg_rtn /
 //                    global_atomic_swap) and emits what it held; lanes of one iteration that
 //                    drew the same slot are chained through ds_bpermute instead
-//   k_v2_tail<EPT>   the final pool1 drained in Philox-sorted order (LDS sort)
-//   k_v2_tail_big    ... or from the HBM multi-pass sort (pss_bigsort.hip)
+//   k_v2_emit_x      pass B on gfx950: one lane-ordered LDS exchange per step; the wave of a
+//                    rank's last tile also drains the final pool (the tail) from LDS
+//   k_v2_tail_f      the tail from the VAL tables, when the last tile is not replayed in the
+//                    same launch (or on the probe / HBM paths): final pool1 drained in the
+//                    order of a keyed Feistel bijection of [0, P1)
 #include <cstdlib>
 
 #include "pss_device.h"
@@ -50,17 +53,19 @@ __global__ __launch_bounds__(256) void k_v2_lastocc(Geometry g, V2Plan pl, int32
     stage_round_keys(g, rank, w_lo, nwin, rk);
     const SlotKey sk = slot_key(g, rank);
     __syncthreads();
-    // every step of the tile: last step (tile-local, +1) that drew each slot; 4 independent
-    // hashes in flight per thread
+    // every step of the tile: last step (tile-local, +1) that drew each slot.  Whole blocks of
+    // 2048 steps run branch-free with 8 independent hashes per thread, then the remainder.
     const uint32_t n = (uint32_t)(thi - tlo), t0 = (uint32_t)tlo;
-    for (uint32_t b = threadIdx.x; b < n; b += 1024) {
-        uint32_t k[4];
+    const uint32_t nfull = n & ~2047u;
+    for (uint32_t b = threadIdx.x; b < nfull; b += 2048) {
+        uint32_t k[8];
 #pragma unroll
-        for (int j = 0; j < 4; j++) k[j] = scale32(slot_hash(t0 + b + 256u * j, sk.s0, sk.s1), (uint32_t)P1);
+        for (int j = 0; j < 8; j++) k[j] = scale32(slot_hash(t0 + b + 256u * j, sk.s0, sk.s1), (uint32_t)P1);
 #pragma unroll
-        for (int j = 0; j < 4; j++)
-            if (b + 256u * j < n) atomicMax(&lastT[k[j]], b + 256u * j + 1u);
+        for (int j = 0; j < 8; j++) atomicMax(&lastT[k[j]], b + 256u * j + 1u);
     }
+    for (uint32_t b = nfull + threadIdx.x; b < n; b += 256)
+        atomicMax(&lastT[scale32(slot_hash(t0 + b, sk.s0, sk.s1), (uint32_t)P1)], b + 1u);
     __syncthreads();
     uint32_t *V = VAL + ((int64_t)rl * pl.G + tile) * P1;
     for (int s = threadIdx.x; s < P1; s += 256) {
@@ -412,7 +417,7 @@ __global__ __launch_bounds__(64) void k_v2_emit_x(Geometry g, V2Plan pl,
                                                   const RankDesc *__restrict__ ranks,
                                                   int32_t rank_lo, int64_t g_lo, int64_t ng,
                                                   const uint32_t *__restrict__ VAL,
-                                                  int64_t pos_lo, int64_t count,
+                                                  int64_t pos_lo, int64_t count, int do_tail,
                                                   int64_t *__restrict__ out) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     const uint32_t P1 = (uint32_t)pl.P1;
@@ -471,17 +476,34 @@ __global__ __launch_bounds__(64) void k_v2_emit_x(Geometry g, V2Plan pl,
     // fast super-batches: every step valid and emitted, B >= 256 (at most one window boundary
     // per super-batch), neither window short nor cycle-walking
     const bool fast_tile = e_lo == 0 && e_hi == nvalid && B >= 256 && !walk_full;
+    uint32_t kw[kFeistelRounds];     // round keys of window w0 (wave-uniform: SGPRs)
+    uint32_t kw_w = 0xFFFFFFFFu;
     for (uint32_t tl0 = 0; tl0 < nvalid; tl0 += 256) {
         if (fast_tile && tl0 + 256 <= nvalid && w0 + 1 < w_last) {
-            uint32_t k[4], ins[4], v[4];
+            if (kw_w != w0) {
 #pragma unroll
-            for (int j = 0; j < 4; j++) {
-                k[j] = scale32(slot_hash(t0 + tl0 + 64u * j + lane, sk.s0, sk.s1), P1);
-                uint32_t p = p0 + 64u * j + lane;
-                const bool cross = p >= B;
-                p = cross ? p - B : p;
-                const uint32_t w = cross ? w0 + 1 : w0;
-                ins[j] = w * B + feistel_once(p, hB, rk + kRoundKeyWords * (w - wl));
+                for (int i = 0; i < kFeistelRounds; i++)
+                    kw[i] = __builtin_amdgcn_readfirstlane(rk[kRoundKeyWords * (w0 - wl) + i]);
+                kw_w = w0;
+            }
+            uint32_t k[4], ins[4], v[4];
+            if (p0 + 256 <= B) {
+                // the whole super-batch inserts from window w0: scalar round keys
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    k[j] = scale32(slot_hash(t0 + tl0 + 64u * j + lane, sk.s0, sk.s1), P1);
+                    ins[j] = w0 * B + feistel_once(p0 + 64u * j + lane, hB, kw);
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    k[j] = scale32(slot_hash(t0 + tl0 + 64u * j + lane, sk.s0, sk.s1), P1);
+                    uint32_t p = p0 + 64u * j + lane;
+                    const bool cross = p >= B;
+                    p = cross ? p - B : p;
+                    const uint32_t w = cross ? w0 + 1 : w0;
+                    ins[j] = w * B + feistel_once(p, hB, rk + kRoundKeyWords * (w - wl));
+                }
             }
 #pragma unroll
             for (int j = 0; j < 4; j++) v[j] = atomicExch(&buf[k[j]], ins[j]);
@@ -506,6 +528,20 @@ __global__ __launch_bounds__(64) void k_v2_emit_x(Geometry g, V2Plan pl,
         }
         p0 += 256;
         while (p0 >= B) { p0 -= B; w0++; }
+    }
+    if (do_tail && tile == pl.G - 1) {
+        // the rank's final pool is this wave's slot table: drain it in tail order (positions
+        // T + j, j < P1).  One wave: its own LDS exchanges above are complete in order.
+        __syncthreads();
+        uint32_t tk[kRoundKeyWords];
+        tail_round_keys(g, rank, tk);
+        const uint32_t hT = feistel_half_bits(P1);
+        int64_t *ot = out + (int64_t)rl * count - pos_lo + pl.T;
+        for (uint32_t j = lane; j < P1; j += 64) {
+            const int64_t pos = pl.T + j;
+            if (pos < pos_lo || pos >= pos_hi) continue;
+            ot[j] = emit_id<NARROW>(buf[feistel(j, P1, hT, tk)], twoB, old32, new32, N32, rd, g);
+        }
     }
 }
 
@@ -723,81 +759,30 @@ __global__ __launch_bounds__(256) void k_v2_emit_sst(Geometry g, V2Plan pl,
 }
 
 // ---- tail ---------------------------------------------------------------------------------
-template <int EPT>
-__global__ __launch_bounds__(256) void k_v2_tail(Geometry g, V2Plan pl,
-                                                const RankDesc *__restrict__ ranks,
-                                                int32_t rank_lo, const uint32_t *__restrict__ VAL,
-                                                int64_t pos_lo, int64_t count,
-                                                int64_t *__restrict__ out) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-    uint32_t *S = smem, *hist = smem + 256 * EPT, *tot = hist + bpad_size(256 * EPT);
-    const int32_t rl = (int32_t)blockIdx.x;
+// position T + j of a rank emits the final pool1 slot pi(j), pi = Feistel bijection of [0, P1)
+// keyed by tail_round_keys; the final content of a slot is the VAL walk-back from the last tile
+__global__ __launch_bounds__(256) void k_v2_tail_f(Geometry g, V2Plan pl,
+                                                  const RankDesc *__restrict__ ranks,
+                                                  int32_t rank_lo, const uint32_t *__restrict__ VAL,
+                                                  int64_t pos_lo, int64_t count,
+                                                  int64_t *__restrict__ out) {
+    const int32_t rl = (int32_t)blockIdx.y;
     const uint32_t rank = (uint32_t)(rank_lo + rl);
     const RankDesc rd = ranks[rank];
-    const int P1 = (int)pl.P1;
-    const int hb = block_sort_keys<EPT>(g.key0, g.key1, 0u, rank, DOM_V2_TAIL, P1, S, hist, tot);
-    const uint32_t mask = (1u << hb) - 1u;
-    const uint32_t *VALr = VAL + (int64_t)rl * pl.G * P1;
-    const uint32_t *last = VALr + (pl.G - 1) * P1;
+    const uint32_t P1 = (uint32_t)pl.P1;
+    uint32_t tk[kRoundKeyWords];
+    tail_round_keys(g, rank, tk);
+    const uint32_t hT = feistel_half_bits(P1);
+    const uint32_t *VALr = VAL + (int64_t)rl * pl.G * pl.P1;
     int64_t *o = out + (int64_t)rl * count - pos_lo;
     const int64_t pos_hi = pos_lo + count;
-    for (int j0 = threadIdx.x; j0 < P1; j0 += 1024) {        // 4 independent loads in flight
-        int s[4];
-        uint32_t v[4];
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-            const int j = j0 + 256 * u;
-            s[u] = j < P1 ? (int)(S[j] & mask) : 0;
-            v[u] = (j < P1 && pl.G > 0) ? last[s[u]] : kNone;
-        }
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-            const int j = j0 + 256 * u;
-            const int64_t pos = pl.T + j;
-            if (j >= P1 || pos < pos_lo || pos >= pos_hi) continue;
-            const uint32_t val = v[u] != kNone ? v[u] : slot_value_after(VALr, P1, pl.G - 2, s[u]);
-            o[pos] = v2_id(val, rd, g);
-        }
-    }
-}
-
-__global__ __launch_bounds__(256) void k_v2_tail_big(Geometry g, V2Plan pl,
-                                                    const RankDesc *__restrict__ ranks,
-                                                    SortJobs J, int64_t job_lo, BigSortWS ws,
-                                                    const uint32_t *__restrict__ VAL,
-                                                    int64_t pos_lo, int64_t count,
-                                                    int64_t *__restrict__ out) {
-    const int64_t jj = blockIdx.y;
-    const int64_t rl = job_lo + jj;
-    const uint32_t rank = (uint32_t)(J.rank_lo + rl);
-    const RankDesc rd = ranks[rank];
-    const uint32_t *perm = ws.perm + jj * ws.nmax;
-    const uint32_t *VALr = VAL + rl * pl.G * pl.P1;
-    int64_t *o = out + rl * count - pos_lo;
-    const int64_t pos_hi = pos_lo + count;
-    for (int64_t j = (int64_t)blockIdx.x * 1024 + threadIdx.x;
-         j < pl.P1 && j < (int64_t)(blockIdx.x + 1) * 1024; j += 256) {
+    for (uint32_t j = blockIdx.x * 256u + threadIdx.x; j < P1; j += gridDim.x * 256u) {
         const int64_t pos = pl.T + j;
         if (pos < pos_lo || pos >= pos_hi) continue;
-        o[pos] = v2_id(slot_value_after(VALr, pl.P1, pl.G - 1, perm[j]), rd, g);
+        const uint32_t s = feistel(j, P1, hT, tk);
+        o[pos] = v2_id(slot_value_after(VALr, pl.P1, pl.G - 1, s), rd, g);
     }
 }
-
-template <int EPT>
-static void launch_tail_ept(const Geometry &g, const V2Plan &pl, const RankDesc *ranks,
-                     int32_t rank_lo, int32_t nr, const uint32_t *VAL, int64_t pos_lo,
-                     int64_t count, int64_t *out, hipStream_t s) {
-    hipLaunchKernelGGL(k_v2_tail<EPT>, dim3((uint32_t)nr), dim3(256), sort_lds_bytes<EPT>(), s,
-                       g, pl, ranks, rank_lo, VAL, pos_lo, count, out);
-}
-
-static SortJobs tail_jobs(const Geometry &g, const V2Plan &pl, int32_t rank_lo) {
-    SortJobs J{};
-    J.kind = 1; J.rank_lo = rank_lo; J.nw = 1; J.w_lo = 0;
-    J.B = g.B; J.ns = g.ns; J.P1 = pl.P1; J.nmax = pl.P1; J.dom = DOM_V2_TAIL;
-    return J;
-}
-
 
 // ------------------------------------------------------------------------------------------
 // launchers
@@ -868,10 +853,8 @@ size_t v2_buf_bytes(const Geometry &g, int32_t nr) {
     return p.global_buf ? v2_val_bytes(g, nr) : 0;
 }
 
-size_t v2_sort_bytes(const Geometry &g, int32_t nr) {
-    const V2Plan p = v2_plan(g, nr);
-    if (p.P1 <= kLdsSortMax || nr <= 0) return 0;
-    return big_sort_bytes(p.P1, big_sort_batch(p.P1, nr, kBigSortBudget));
+size_t v2_sort_bytes(const Geometry &, int32_t) {
+    return 0;   // the tail order is a Feistel bijection: no sort workspace
 }
 
 hipError_t launch_v2(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, int32_t nr,
@@ -885,6 +868,7 @@ hipError_t launch_v2(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, 
     const int64_t nwin_max = pl.L / g.B + 2;
     const size_t lds_keys = (size_t)kRoundKeyWords * nwin_max * sizeof(uint32_t);
     const bool need_tail = pos_hi > pl.T;
+    bool tail_fused = false;   // drained by the last tile's k_v2_emit_x wave
     if (pl.G > 0) {
         // pass A over every tile up to the last one emitted (the tail needs all of them);
         // VAL is indexed (rl*G + tile), tile < g_need
@@ -931,12 +915,14 @@ hipError_t launch_v2(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, 
                 mk(K_V2_EMIT, s);
                 const size_t need = lds_keys + (size_t)pl.P1 * 4;
                 const size_t lds = need > (size_t)pl.emit_lds ? need : (size_t)pl.emit_lds;
+                tail_fused = need_tail && last_emit == pl.G - 1;
+                const int dt = tail_fused ? 1 : 0;
                 if (narrow)
                     hipLaunchKernelGGL((k_v2_emit_x<true>), grid, dim3(64), lds, s, g, pl, ranks, rank_lo,
-                                       g_lo, ng, (const uint32_t *)VAL, pos_lo, count, out);
+                                       g_lo, ng, (const uint32_t *)VAL, pos_lo, count, dt, out);
                 else
                     hipLaunchKernelGGL((k_v2_emit_x<false>), grid, dim3(64), lds, s, g, pl, ranks, rank_lo,
-                                       g_lo, ng, (const uint32_t *)VAL, pos_lo, count, out);
+                                       g_lo, ng, (const uint32_t *)VAL, pos_lo, count, dt, out);
             } else if (!pl.global_buf) {   // probe path (EMIT_PROBE)
                 mk(K_V2_EMIT, s);
                 const size_t need = lds_keys + (size_t)pl.P1 * 4 + (pl.fold ? 0 : kMarkBytes);
@@ -962,25 +948,11 @@ hipError_t launch_v2(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, 
             }
         }
     }
-    if (need_tail) {
+    if (need_tail && !tail_fused) {
         mk(K_V2_TAIL, s);
-        const int64_t P1 = pl.P1;
-        if (P1 <= 1024) launch_tail_ept<4>(g, pl, ranks, rank_lo, nr, VAL, pos_lo, count, out, s);
-        else if (P1 <= 4096) launch_tail_ept<16>(g, pl, ranks, rank_lo, nr, VAL, pos_lo, count, out, s);
-        else if (P1 <= 8192) launch_tail_ept<32>(g, pl, ranks, rank_lo, nr, VAL, pos_lo, count, out, s);
-        else if (P1 <= kLdsSortMax) launch_tail_ept<64>(g, pl, ranks, rank_lo, nr, VAL, pos_lo, count, out, s);
-        else {
-            const SortJobs J = tail_jobs(g, pl, rank_lo);
-            const int64_t jb = big_sort_batch(P1, nr, kBigSortBudget);
-            const BigSortWS ws = big_sort_ws(sort_ws, P1, jb);
-            for (int64_t j0 = 0; j0 < nr; j0 += jb) {
-                const int64_t nj = nr - j0 < jb ? nr - j0 : jb;
-                hipError_t e = launch_big_sort(g, J, j0, nj, ws, err, s);
-                if (e != hipSuccess) return e;
-                hipLaunchKernelGGL(k_v2_tail_big, dim3((uint32_t)cdiv(P1, 1024), (uint32_t)nj), dim3(256), 0, s,
-                                   g, pl, ranks, J, j0, ws, (const uint32_t *)VAL, pos_lo, count, out);
-            }
-        }
+        const dim3 grid((uint32_t)cdiv(pl.P1 < 65536 ? pl.P1 : 65536, 256), (uint32_t)nr);
+        hipLaunchKernelGGL(k_v2_tail_f, grid, dim3(256), 0, s, g, pl, ranks, rank_lo,
+                           (const uint32_t *)VAL, pos_lo, count, out);
     }
     mk(-1, s);
     return hipGetLastError();
@@ -1020,8 +992,6 @@ hipError_t init_kernel_attributes_v2() {
     const int big = 160 * 1024;
     hipError_t e = check_lds_xchg_order();
 #define PSS_ATTR(fn) { hipError_t x = hipFuncSetAttribute((const void *)(fn), hipFuncAttributeMaxDynamicSharedMemorySize, big); if (x != hipSuccess) e = x; }
-    PSS_ATTR(k_v2_tail<32>);
-    PSS_ATTR(k_v2_tail<64>);
     PSS_ATTR(k_v2_lastocc);
     PSS_ATTR((k_v2_emit_x<true>));
     PSS_ATTR((k_v2_emit_x<false>));

@@ -132,9 +132,11 @@ def test_reference_assignment_and_multiset(name):
                 assert out[r][:len(rec)].tolist() == rec
 
 
-def test_map_and_partition_match_oracle():
-    rng = np.random.default_rng(11)
-    lengths = rng.integers(0, 500, 300)      # includes empty files
+@pytest.mark.parametrize("F,hi", [(300, 500), (4096, 40), (4097, 40), (20_000, 60)])
+def test_map_and_partition_match_oracle(F, hi):
+    # one scan chunk (F <= 4096) and several (two-pass scan); empty files included
+    rng = np.random.default_rng(11 + F)
+    lengths = rng.integers(0, hi, F)
     N, R, B = int(lengths.sum()), 6, 256
     for version in (1, 2):
         eng = _engine(lengths, N, R, B, version)
