@@ -24,6 +24,29 @@ namespace pss {
 
 static inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
+// Progress-based wave priority.  Co-resident waves with equal work are arbitrated by age, so
+// the older one runs ahead and the younger finishes alone at half the issue rate.  A wave
+// lowers its own priority as it passes 1/4, 1/2 and 3/4 of its work: whoever is behind wins
+// arbitration, and the waves of a SIMD finish together.
+struct Pacer {
+    uint32_t next, quarter;
+    int stage;
+    __device__ __forceinline__ explicit Pacer(uint32_t total) {
+        quarter = total / 4 + 1;
+        next = quarter;
+        stage = 0;
+        __builtin_amdgcn_s_setprio(3);
+    }
+    __device__ __forceinline__ void step(uint32_t done) {
+        if (done < next) return;
+        next += quarter;
+        stage++;
+        if (stage == 1) __builtin_amdgcn_s_setprio(2);
+        else if (stage == 2) __builtin_amdgcn_s_setprio(1);
+        else __builtin_amdgcn_s_setprio(0);
+    }
+};
+
 __device__ __forceinline__ void tile_bounds(const V2Plan &pl, int64_t tile, int64_t &tlo,
                                             int64_t &thi) {
     tlo = tile * pl.L;
@@ -57,7 +80,9 @@ __global__ __launch_bounds__(256) void k_v2_lastocc(Geometry g, V2Plan pl, int32
     // 2048 steps run branch-free with 8 independent hashes per thread, then the remainder.
     const uint32_t n = (uint32_t)(thi - tlo), t0 = (uint32_t)tlo;
     const uint32_t nfull = n & ~2047u;
+    Pacer pace(nfull);
     for (uint32_t b = threadIdx.x; b < nfull; b += 2048) {
+        pace.step(b);
         uint32_t k[8];
 #pragma unroll
         for (int j = 0; j < 8; j++) k[j] = scale32(slot_hash(t0 + b + 256u * j, sk.s0, sk.s1), (uint32_t)P1);
@@ -67,12 +92,22 @@ __global__ __launch_bounds__(256) void k_v2_lastocc(Geometry g, V2Plan pl, int32
     for (uint32_t b = nfull + threadIdx.x; b < n; b += 256)
         atomicMax(&lastT[scale32(slot_hash(t0 + b, sk.s0, sk.s1), (uint32_t)P1)], b + 1u);
     __syncthreads();
+    // last step -> inserted value, in 32-bit tile-local arithmetic (no 64-bit division)
     uint32_t *V = VAL + ((int64_t)rl * pl.G + tile) * P1;
+    const uint32_t B = (uint32_t)g.B, hB = feistel_half_bits(B);
+    const uint32_t w_last = (uint32_t)(1 + (pl.T - 1) / g.B);
+    const uint32_t len_last = (uint32_t)(g.ns - (int64_t)w_last * g.B);
+    const uint32_t h_last = feistel_half_bits(len_last);
+    const uint32_t p_lo = (uint32_t)(tlo - (w_lo - 1) * g.B);   // index of step tlo in window w_lo
     for (int s = threadIdx.x; s < P1; s += 256) {
         const uint32_t lt = lastT[s];
         if (!lt) { V[s] = kNone; continue; }
-        const int64_t t = tlo + (int64_t)lt - 1;
-        V[s] = ins_value_k(g, t, rk + kRoundKeyWords * (1 + t / g.B - w_lo));
+        uint32_t p = p_lo + lt - 1u;
+        const uint32_t dw = p / B;
+        p -= dw * B;
+        const uint32_t w = (uint32_t)w_lo + dw;
+        const bool lastw = w == w_last;
+        V[s] = w * B + feistel(p, lastw ? len_last : B, lastw ? h_last : hB, rk + kRoundKeyWords * dw);
     }
 }
 
@@ -478,7 +513,9 @@ __global__ __launch_bounds__(64) void k_v2_emit_x(Geometry g, V2Plan pl,
     const bool fast_tile = e_lo == 0 && e_hi == nvalid && B >= 256 && !walk_full;
     uint32_t kw[kFeistelRounds];     // round keys of window w0 (wave-uniform: SGPRs)
     uint32_t kw_w = 0xFFFFFFFFu;
+    Pacer pace(nvalid);
     for (uint32_t tl0 = 0; tl0 < nvalid; tl0 += 256) {
+        pace.step(tl0);
         if (fast_tile && tl0 + 256 <= nvalid && w0 + 1 < w_last) {
             if (kw_w != w0) {
 #pragma unroll
