@@ -153,7 +153,7 @@ struct SlotKey { uint32_t s0, s1; };
 
 __device__ __forceinline__ SlotKey slot_key(const Geometry &g, uint32_t rank) {
     uint32_t c0 = 0, c1 = 0, c2 = rank, c3 = DOM_V2_SLOT;
-    philox4x32_10(c0, c1, c2, c3, g.key0, g.key1);
+    philox4x32_10_rolled(c0, c1, c2, c3, g.key0, g.key1);
     return SlotKey{c0, c1};
 }
 
@@ -169,10 +169,10 @@ constexpr int kRoundKeyWords = 8;
 
 __device__ __forceinline__ void window_round_keys(const Geometry &g, uint32_t rank, int64_t w,
                                                   uint32_t k[kRoundKeyWords]) {
-#pragma unroll
+#pragma unroll 1
     for (int h = 0; h < 2; h++) {
         uint32_t c0 = (uint32_t)w, c1 = (uint32_t)h, c2 = rank, c3 = DOM_V2_INS;
-        philox4x32_10(c0, c1, c2, c3, g.key0, g.key1);
+        philox4x32_10_rolled(c0, c1, c2, c3, g.key0, g.key1);
         k[4 * h] = c0; k[4 * h + 1] = c1; k[4 * h + 2] = c2; k[4 * h + 3] = c3;
     }
 }
@@ -180,10 +180,10 @@ __device__ __forceinline__ void window_round_keys(const Geometry &g, uint32_t ra
 // Feistel keys of the final-pool drain (V2 tail): Philox blocks (0, 0|1, rank, DOM_V2_TAIL)
 __device__ __forceinline__ void tail_round_keys(const Geometry &g, uint32_t rank,
                                                 uint32_t k[kRoundKeyWords]) {
-#pragma unroll
+#pragma unroll 1
     for (int h = 0; h < 2; h++) {
         uint32_t c0 = 0, c1 = (uint32_t)h, c2 = rank, c3 = DOM_V2_TAIL;
-        philox4x32_10(c0, c1, c2, c3, g.key0, g.key1);
+        philox4x32_10_rolled(c0, c1, c2, c3, g.key0, g.key1);
         k[4 * h] = c0; k[4 * h + 1] = c1; k[4 * h + 2] = c2; k[4 * h + 3] = c3;
     }
 }

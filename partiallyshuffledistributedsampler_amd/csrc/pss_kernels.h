@@ -122,6 +122,7 @@ size_t v1_workspace_bytes(const Geometry &g, int32_t nr, int64_t pos_lo, int64_t
 // start-up check confirms), EMIT_PROBE = collision probe + per-clash fix-up (any hardware)
 enum EmitPath { EMIT_AUTO = 0, EMIT_XCHG = 1, EMIT_PROBE = 2 };
 bool lds_xchg_ordered();   // result of the start-up check on the current device
+bool lds_write_ordered();  // same-word lanes of one plain LDS store: the highest lane wins
 
 // V2: same contract; val_ws holds the per-tile slot tables
 hipError_t launch_v2(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, int32_t nr,

@@ -59,56 +59,126 @@ __device__ __forceinline__ void stage_round_keys(const Geometry &g, uint32_t ran
         window_round_keys(g, rank, w_lo + j, rk + kRoundKeyWords * j);
 }
 
-// ---- pass A, LDS --------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_v2_lastocc(Geometry g, V2Plan pl, int32_t rank_lo,
-                                                    int64_t ng, uint32_t *__restrict__ VAL) {
+#ifdef PSS_STAMPS   // diagnostic build only (tools/stamp_v2.hip): per-workgroup phase clocks
+__device__ uint64_t pss_stamps[1 << 16][8];
+#define PSS_STAMP(i) do { if (threadIdx.x == 0 && blockIdx.x < (1u << 16)) pss_stamps[blockIdx.x][i] = __builtin_amdgcn_s_memtime(); } while (0)
+#define PSS_STAMPW(i) do { if ((threadIdx.x & 63) == 0 && blockIdx.x < (1u << 16)) pss_stamps[blockIdx.x][i] = __builtin_amdgcn_s_memtime(); } while (0)
+#else
+#define PSS_STAMP(i) do { } while (0)
+#endif
+
+// ---- pass A, LDS ----------------------------------------------------------------------------
+// Per tile: the last step (tile-local, +1) that drew each slot, then that step's inserted value.
+//   ORDERED (NT = 64, one wave per tile): the wave walks its steps in order with PLAIN stores
+//     -- a later instruction overwrites an earlier one and, inside one store, the highest lane
+//     wins (start-up check), so each slot ends with its last step.  No LDS atomics.
+//   otherwise (NT = 256): any order, ds_max.
+template <int NT, bool ORDERED>
+__global__ __launch_bounds__(NT) void k_v2_lastocc(Geometry g, V2Plan pl, int32_t rank_lo,
+                                                   int64_t ng, uint32_t *__restrict__ VAL) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+    PSS_STAMP(0);
     const int P1 = (int)pl.P1;
     uint32_t *lastT = smem, *rk = smem + P1;
-    const int32_t rl = (int32_t)(blockIdx.x / ng);
-    const int64_t tile = (int64_t)(blockIdx.x % ng);
+    // 32-bit tile arithmetic (T < 2^32: num_samples >= 2^32 is rejected)
+    const uint32_t ngu = (uint32_t)ng, B = (uint32_t)g.B;
+    const int32_t rl = (int32_t)(blockIdx.x / ngu);
+    const uint32_t tile = blockIdx.x - (uint32_t)rl * ngu;
     const uint32_t rank = (uint32_t)(rank_lo + rl);
-    int64_t tlo, thi;
-    tile_bounds(pl, tile, tlo, thi);
-    const int64_t w_lo = 1 + tlo / g.B;
-    const int nwin = (int)(1 + (thi - 1) / g.B - w_lo + 1);
-    for (int s = threadIdx.x; s < P1; s += 256) lastT[s] = 0;
+    const uint32_t tlo = tile * (uint32_t)pl.L;
+    const uint32_t thi = (uint32_t)(pl.T - tlo < pl.L ? pl.T : tlo + pl.L);
+    const uint32_t w_lo = 1 + tlo / B;
+    const int nwin = (int)(1 + (thi - 1) / B - w_lo + 1);
+#ifdef PSS_STAMPS
+    if (threadIdx.x == 0) pss_stamps[blockIdx.x][4] = __builtin_amdgcn_s_memrealtime();
+#endif
+    for (int s = threadIdx.x; s < P1; s += NT) lastT[s] = 0;
     stage_round_keys(g, rank, w_lo, nwin, rk);
     const SlotKey sk = slot_key(g, rank);
     __syncthreads();
-    // every step of the tile: last step (tile-local, +1) that drew each slot.  Whole blocks of
-    // 2048 steps run branch-free with 8 independent hashes per thread, then the remainder.
+    PSS_STAMP(1);
+    // whole blocks of 8*NT steps run branch-free with 8 independent hashes per thread
     const uint32_t n = (uint32_t)(thi - tlo), t0 = (uint32_t)tlo;
-    const uint32_t nfull = n & ~2047u;
+    constexpr uint32_t BLK = 8 * NT;
+    const uint32_t nfull = n / BLK * BLK;
+    // Loop counters are workgroup-uniform (base), never per-lane: with a per-lane trip count the
+    // compiler may unroll per thread, and lanes would then run different steps in one store.
     Pacer pace(nfull);
-    for (uint32_t b = threadIdx.x; b < nfull; b += 2048) {
-        pace.step(b);
+    for (uint32_t base = 0; base < nfull; base += BLK) {
+        pace.step(base);
+        const uint32_t b = base + threadIdx.x;
         uint32_t k[8];
 #pragma unroll
-        for (int j = 0; j < 8; j++) k[j] = scale32(slot_hash(t0 + b + 256u * j, sk.s0, sk.s1), (uint32_t)P1);
+        for (int j = 0; j < 8; j++) k[j] = scale32(slot_hash(t0 + b + NT * j, sk.s0, sk.s1), (uint32_t)P1);
 #pragma unroll
-        for (int j = 0; j < 8; j++) atomicMax(&lastT[k[j]], b + 256u * j + 1u);
+        for (int j = 0; j < 8; j++) {
+            if (ORDERED) lastT[k[j]] = b + NT * j + 1u;
+            else atomicMax(&lastT[k[j]], b + NT * j + 1u);
+        }
     }
-    for (uint32_t b = nfull + threadIdx.x; b < n; b += 256)
-        atomicMax(&lastT[scale32(slot_hash(t0 + b, sk.s0, sk.s1), (uint32_t)P1)], b + 1u);
+    for (uint32_t base = nfull; base < n; base += NT) {
+        const uint32_t b = base + threadIdx.x;
+        if (b < n) {
+            const uint32_t kk = scale32(slot_hash(t0 + b, sk.s0, sk.s1), (uint32_t)P1);
+            if (ORDERED) lastT[kk] = b + 1u;
+            else atomicMax(&lastT[kk], b + 1u);
+        }
+    }
     __syncthreads();
+    PSS_STAMP(2);
     // last step -> inserted value, in 32-bit tile-local arithmetic (no 64-bit division)
     uint32_t *V = VAL + ((int64_t)rl * pl.G + tile) * P1;
-    const uint32_t B = (uint32_t)g.B, hB = feistel_half_bits(B);
+    const uint32_t hB = feistel_half_bits(B);
     const uint32_t w_last = (uint32_t)(1 + (pl.T - 1) / g.B);
     const uint32_t len_last = (uint32_t)(g.ns - (int64_t)w_last * g.B);
     const uint32_t h_last = feistel_half_bits(len_last);
-    const uint32_t p_lo = (uint32_t)(tlo - (w_lo - 1) * g.B);   // index of step tlo in window w_lo
-    for (int s = threadIdx.x; s < P1; s += 256) {
-        const uint32_t lt = lastT[s];
-        if (!lt) { V[s] = kNone; continue; }
-        uint32_t p = p_lo + lt - 1u;
-        const uint32_t dw = p / B;
-        p -= dw * B;
-        const uint32_t w = (uint32_t)w_lo + dw;
-        const bool lastw = w == w_last;
-        V[s] = w * B + feistel(p, lastw ? len_last : B, lastw ? h_last : hB, rk + kRoundKeyWords * dw);
+    const uint32_t p_lo = tlo - (w_lo - 1) * B;                 // index of step tlo in window w_lo
+    const bool walk_full = B != (1u << (2 * hB));
+    const float invB = 1.0f / (float)B;
+    // 4 slots per thread per pass (independent chains); a whole pass takes the one-pass
+    // Feistel unless one of its slots lies in the short last window or B needs cycle walking
+    for (int s0 = threadIdx.x; s0 < P1; s0 += 4 * NT) {
+        uint32_t lt[4], pp[4], dw[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int s = s0 + u * NT;
+            lt[u] = s < P1 ? lastT[s] : 0u;
+            const uint32_t p = p_lo + lt[u] - 1u;        // < L + B < 2^24: exact in float
+            uint32_t d = (uint32_t)((float)p * invB);    // p / B to within one, then corrected
+            int32_t r = (int32_t)(p - d * B);
+            if (r < 0) { d--; r += (int32_t)B; }
+            if (r >= (int32_t)B) { d++; r -= (int32_t)B; }
+            pp[u] = (uint32_t)r;
+            dw[u] = lt[u] ? d : 0u;
+        }
+        bool slow = walk_full;
+#pragma unroll
+        for (int u = 0; u < 4; u++) slow |= lt[u] && (uint32_t)w_lo + dw[u] == w_last;
+        uint32_t x[4];
+        if (!slow) {
+#pragma unroll
+            for (int u = 0; u < 4; u++) x[u] = feistel_once(pp[u], hB, rk + kRoundKeyWords * dw[u]);
+        } else {
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const bool lastw = (uint32_t)w_lo + dw[u] == w_last;
+                x[u] = lt[u] ? feistel(pp[u], lastw ? len_last : B, lastw ? h_last : hB, rk + kRoundKeyWords * dw[u]) : 0u;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int s = s0 + u * NT;
+            if (s < P1) V[s] = lt[u] ? ((uint32_t)w_lo + dw[u]) * B + x[u] : kNone;
+        }
     }
+    PSS_STAMP(3);
+#ifdef PSS_STAMPS
+    if (threadIdx.x == 0) {
+        pss_stamps[blockIdx.x][5] = __builtin_amdgcn_s_memrealtime();
+        pss_stamps[blockIdx.x][6] = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));
+        pss_stamps[blockIdx.x][7] = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (15 << 11));
+    }
+#endif
 }
 
 // ---- pass A, HBM ----------------------------------------------------------------------------
@@ -585,31 +655,47 @@ __global__ __launch_bounds__(64) void k_v2_emit_x(Geometry g, V2Plan pl,
 // Start-up check of the exchange order k_v2_emit_x relies on: random slot patterns (heavy
 // collisions at 64 slots, sparse at 4096) against the sequential lane-order model.
 __global__ __launch_bounds__(64) void k_xchg_order_check(int iters, uint32_t P, uint32_t *bad) {
+    // two exchanges and two plain stores per iteration, back to back (no wait in between), as
+    // the replay kernels issue them; the model replays them in (instruction, lane) order
     __shared__ uint32_t buf[4096];
     __shared__ uint32_t model[4096];
+    __shared__ uint32_t wbuf[4096];
     const int lane = threadIdx.x;
-    for (uint32_t s = lane; s < P; s += 64) { buf[s] = 0xF0000000u | s; model[s] = 0xF0000000u | s; }
+    for (uint32_t s = lane; s < P; s += 64) { buf[s] = 0xF0000000u | s; model[s] = buf[s]; wbuf[s] = buf[s]; }
     __syncthreads();
-    uint32_t nbad = 0;
+    uint32_t nbad = 0, nbadw = 0;
     for (int it = 0; it < iters; it++) {
-        const uint32_t kslot = scale32(slot_hash((uint32_t)(blockIdx.x * iters + it) * 64u + lane, 0x9E3779B9u, 0x7F4A7C15u), P);
-        const uint32_t ins = ((uint32_t)it << 8) ^ (uint32_t)lane;
-        const uint32_t got = atomicExch(&buf[kslot], ins);
+        uint32_t ks[2], ins[2], got[2];
+#pragma unroll
+        for (int q = 0; q < 2; q++) {
+            ks[q] = scale32(slot_hash((uint32_t)((blockIdx.x * iters + it) * 2 + q) * 64u + lane, 0x9E3779B9u, 0x7F4A7C15u), P);
+            ins[q] = ((uint32_t)it << 9) ^ ((uint32_t)q << 8) ^ (uint32_t)lane;
+        }
+#pragma unroll
+        for (int q = 0; q < 2; q++) got[q] = atomicExch(&buf[ks[q]], ins[q]);
+#pragma unroll
+        for (int q = 0; q < 2; q++) wbuf[ks[q]] = ins[q];
         __syncthreads();
-        uint32_t expect = 0;
-        for (int l = 0; l < 64; l++) {          // lane 0 replays the 64 exchanges in lane order
-            const uint32_t kl = (uint32_t)__shfl((int)kslot, l);
-            const uint32_t il = (uint32_t)__shfl((int)ins, l);
-            uint32_t old = 0;
-            if (lane == 0) { old = model[kl]; model[kl] = il; }
-            old = (uint32_t)__shfl((int)old, 0);
-            if (lane == l) expect = old;
+        uint32_t expect[2] = {0, 0};
+        for (int q = 0; q < 2; q++) {
+            for (int l = 0; l < 64; l++) {      // lane 0 replays the exchanges in lane order
+                const uint32_t kl = (uint32_t)__shfl((int)ks[q], l);
+                const uint32_t il = (uint32_t)__shfl((int)ins[q], l);
+                uint32_t old = 0;
+                if (lane == 0) { old = model[kl]; model[kl] = il; }
+                old = (uint32_t)__shfl((int)old, 0);
+                if (lane == l) expect[q] = old;
+            }
         }
         __syncthreads();
-        nbad += got != expect;
+        nbad += (got[0] != expect[0]) + (got[1] != expect[1]);
     }
-    for (uint32_t s = lane; s < P; s += 64) nbad += buf[s] != model[s];
+    for (uint32_t s = lane; s < P; s += 64) {
+        nbad += buf[s] != model[s];
+        nbadw += wbuf[s] != model[s];
+    }
     if (nbad) atomicAdd(bad, nbad);
+    if (nbadw) atomicAdd(bad + 2, nbadw);
 }
 
 // ---- pass B, sorted sub-tiles ---------------------------------------------------------------
@@ -914,8 +1000,27 @@ hipError_t launch_v2(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, 
         if (g_need > 0) {
             mk(K_V2_LASTOCC, s);
             if (!pl.global_buf) {
-                hipLaunchKernelGGL(k_v2_lastocc, dim3((uint32_t)(nr * g_need)), dim3(256),
-                                   (size_t)pl.P1 * 4 + lds_keys, s, g, pl, rank_lo, g_need, VAL);
+                static const int lo_mode = [] {   // A/B knob: "ordered" = one-wave plain-store kernel
+                    const char *e = getenv("PSS_V2_LASTOCC");  // (measured 15% slower than ds_max on C2)
+                    return e && e[0] == 'o' ? 1 : 0;
+                }();
+                const size_t lds = (size_t)pl.P1 * 4 + lds_keys;
+                static const int lo_nt = [] {   // A/B knob: threads per last-occurrence workgroup
+                    const char *e = getenv("PSS_V2_LASTOCC_NT");
+                    return e ? atoi(e) : 256;
+                }();
+                if (lds_write_ordered() && lo_mode)
+                    hipLaunchKernelGGL((k_v2_lastocc<64, true>), dim3((uint32_t)(nr * g_need)), dim3(64),
+                                       lds, s, g, pl, rank_lo, g_need, VAL);
+                else if (lo_nt == 1024)
+                    hipLaunchKernelGGL((k_v2_lastocc<1024, false>), dim3((uint32_t)(nr * g_need)), dim3(1024),
+                                       lds, s, g, pl, rank_lo, g_need, VAL);
+                else if (lo_nt == 512)
+                    hipLaunchKernelGGL((k_v2_lastocc<512, false>), dim3((uint32_t)(nr * g_need)), dim3(512),
+                                       lds, s, g, pl, rank_lo, g_need, VAL);
+                else
+                    hipLaunchKernelGGL((k_v2_lastocc<256, false>), dim3((uint32_t)(nr * g_need)), dim3(256),
+                                       lds, s, g, pl, rank_lo, g_need, VAL);
             } else {
                 hipError_t e = hipMemsetAsync(VAL, 0, v2_val_bytes(g, nr), s);
                 if (e != hipSuccess) return e;
@@ -996,16 +1101,18 @@ hipError_t launch_v2(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, 
 }
 
 static signed char g_xchg_ordered[64];   // per device: 0 unknown, 1 ordered, -1 not
+static signed char g_write_ordered[64];
 
 hipError_t check_lds_xchg_order() {
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return e;
     if (dev < 0 || dev >= 64 || g_xchg_ordered[dev]) return hipSuccess;
-    uint32_t *bad = nullptr, hbad[2] = {1, 1};
-    e = hipMalloc((void **)&bad, 2 * sizeof(uint32_t));
+    // bad[0..1]: exchange mismatches at 64 / 4096 slots; bad[2..3]: plain-store mismatches
+    uint32_t *bad = nullptr, hbad[4] = {1, 1, 1, 1};
+    e = hipMalloc((void **)&bad, sizeof(hbad));
     if (e != hipSuccess) return e;
-    e = hipMemset(bad, 0, 2 * sizeof(uint32_t));
+    e = hipMemset(bad, 0, sizeof(hbad));
     if (e == hipSuccess) {
         hipLaunchKernelGGL(k_xchg_order_check, dim3(32), dim3(64), 0, 0, 64, 64u, bad);
         hipLaunchKernelGGL(k_xchg_order_check, dim3(32), dim3(64), 0, 0, 64, 4096u, bad + 1);
@@ -1015,7 +1122,15 @@ hipError_t check_lds_xchg_order() {
     (void)hipFree(bad);
     if (e != hipSuccess) return e;
     g_xchg_ordered[dev] = (hbad[0] == 0 && hbad[1] == 0) ? 1 : -1;
+    g_write_ordered[dev] = (hbad[2] == 0 && hbad[3] == 0) ? 1 : -1;
     return hipSuccess;
+}
+
+bool lds_write_ordered() {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return false;
+    if (!g_write_ordered[dev] && check_lds_xchg_order() != hipSuccess) return false;
+    return g_write_ordered[dev] > 0;
 }
 
 bool lds_xchg_ordered() {
@@ -1029,7 +1144,10 @@ hipError_t init_kernel_attributes_v2() {
     const int big = 160 * 1024;
     hipError_t e = check_lds_xchg_order();
 #define PSS_ATTR(fn) { hipError_t x = hipFuncSetAttribute((const void *)(fn), hipFuncAttributeMaxDynamicSharedMemorySize, big); if (x != hipSuccess) e = x; }
-    PSS_ATTR(k_v2_lastocc);
+    PSS_ATTR((k_v2_lastocc<64, true>));
+    PSS_ATTR((k_v2_lastocc<256, false>));
+    PSS_ATTR((k_v2_lastocc<512, false>));
+    PSS_ATTR((k_v2_lastocc<1024, false>));
     PSS_ATTR((k_v2_emit_x<true>));
     PSS_ATTR((k_v2_emit_x<false>));
     PSS_ATTR((k_v2_emit_sst<true>));
