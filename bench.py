@@ -3,8 +3,9 @@
 
 Workload (BASELINE.json configs[1]): V2 two-pool sampler, 10,000 files x
 10,000 samples = 100M samples, 8 logical ranks, shuffle_buffer 4096 -- per GPU.  One step =
-one epoch: set_epoch + init_iter (host CPython-MT file/block history, epoch upload, device
-prefix scan) + generation of every id of the GPU's 8 logical ranks into HBM.  With --gpus N
+one epoch: set_epoch + init_iter (host CPython-MT file/block history, epoch upload) +
+generation of every id of the GPU's 8 logical ranks into HBM (the id -> file prefix scan is
+run by the first map after an epoch change, not by generation).  With --gpus N
 (torchrun, one process per GPU) GPU g owns logical ranks [8g, 8g+8) of an 8N-rank sampler over
 N x 100M samples (weak scaling, no data-path collective); after the timed loop the ranks
 all-gather (count, coverage digest) over RCCL and rank 0 checks exact coverage.
@@ -41,16 +42,21 @@ WORKLOADS = {
 }
 
 
-def _pmc_traffic(kernel):
-    """HBM bytes per launch of `kernel` from profiles/pmc_traffic.json (written by
-    tools/pmc_summary.py from rocprofv3 --pmc passes), or None."""
+def _pmc_traffic(symbols):
+    """HBM bytes per launch of the first kernel symbol found in profiles/pmc_traffic.json
+    (written by tools/pmc_summary.py from separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE
+    passes over this same bench), or None."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(p) as f:
             d = json.load(f)
-        return d.get("k_" + kernel, {}).get("hbm_bytes_per_launch")
     except (OSError, ValueError):
         return None
+    for sym in symbols:
+        v = d.get(sym, {}).get("hbm_bytes_per_launch")
+        if v is not None:
+            return v
+    return None
 
 
 def cpu_baseline(seconds_budget=12.0):
@@ -184,7 +190,11 @@ def main():
     else:
         units = RG * ns
     achieved = units * BYTES_PER_ID / (per_launch_ms * 1e-3) / 1e9 if per_launch_ms > 0 else 0.0
-    traffic = _pmc_traffic(kname)
+    if ver == 2:
+        syms = ["k_v2_emit_x"] if eng.emit_path() == "xchg" else ["k_v2_emit"]
+    else:
+        syms = ["k_v1_lds"]
+    traffic = _pmc_traffic(syms)
     line = {
         "metric": METRIC,
         "value": value,
