@@ -212,4 +212,40 @@ __device__ __forceinline__ uint32_t slot_value_after(const uint32_t *VALr, int64
     return (uint32_t)s;  // initial pool1 = window 0 in slot order
 }
 
+// Progress-based wave priority.  Co-resident waves with equal work are arbitrated by age, so
+// the older one runs ahead and the younger finishes alone at half the issue rate.  A wave
+// lowers its own priority as it passes 1/4, 1/2 and 3/4 of its work: whoever is behind wins
+// arbitration, and the waves of a SIMD finish together.
+struct Pacer {
+    uint32_t next, quarter;
+    int stage;
+    __device__ __forceinline__ explicit Pacer(uint32_t total) {
+        quarter = total / 4 + 1;
+        next = quarter;
+        stage = 0;
+        __builtin_amdgcn_s_setprio(3);
+    }
+    __device__ __forceinline__ void step(uint32_t done) {
+        if (done < next) return;
+        next += quarter;
+        stage++;
+        if (stage == 1) __builtin_amdgcn_s_setprio(2);
+        else if (stage == 2) __builtin_amdgcn_s_setprio(1);
+        else __builtin_amdgcn_s_setprio(0);
+    }
+};
+
+
+// global id of virtual index v (NARROW: every id and id + ns fits in 32 bits)
+template <bool NARROW>
+__device__ __forceinline__ int64_t emit_id(uint32_t v, uint32_t twoB, uint32_t old32, uint32_t new32,
+                                           uint32_t N32, const RankDesc &rd, const Geometry &g) {
+    if (NARROW) {
+        const uint32_t id = (v < twoB ? old32 : new32) + v;
+        const uint32_t idw = id - N32;
+        return (int64_t)(id < N32 ? id : idw);
+    }
+    return v2_id(v, rd, g);
+}
+
 }  // namespace pss

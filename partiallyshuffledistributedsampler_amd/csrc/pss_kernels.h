@@ -123,6 +123,7 @@ size_t v1_workspace_bytes(const Geometry &g, int32_t nr, int64_t pos_lo, int64_t
 enum EmitPath { EMIT_AUTO = 0, EMIT_XCHG = 1, EMIT_PROBE = 2 };
 bool lds_xchg_ordered();   // result of the start-up check on the current device
 bool lds_write_ordered();  // same-word lanes of one plain LDS store: the highest lane wins
+bool lds_add_ordered();    // same-word lanes of one ds_add_rtn are served in lane order
 
 // V2: same contract; val_ws holds the per-tile slot tables
 hipError_t launch_v2(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, int32_t nr,
@@ -130,6 +131,18 @@ hipError_t launch_v2(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, 
                      uint32_t *buf_ws, uint32_t *sort_ws, int32_t *err, hipStream_t s,
                      const Marker &mk = Marker(), int emit_path = EMIT_AUTO);
 size_t v2_val_bytes(const Geometry &g, int32_t nr);
+// V2 tail from per-tile VAL tables (walk-back), positions [pos_lo, pos_lo+count) past T
+hipError_t launch_v2_tail_vals(const Geometry &g, const V2Plan &pl, const RankDesc *ranks,
+                               int32_t rank_lo, int32_t nr, const uint32_t *VAL, int64_t pos_lo,
+                               int64_t count, int64_t *out, hipStream_t s);
+// pools beyond LDS (P1 in (16384, 2^22]): slot-chunked replay (pss_v2big.hip); workspace in
+// buf_ws (v2_buf_bytes covers it)
+bool v2_big_applicable(const Geometry &g);
+size_t v2_big_bytes(const Geometry &g, int32_t nr);
+hipError_t launch_v2_big(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, int32_t nr,
+                         int64_t pos_lo, int64_t count, int64_t *out, void *ws, hipStream_t s,
+                         const Marker &mk);
+hipError_t init_kernel_attributes_v2big();
 size_t v2_buf_bytes(const Geometry &g, int32_t nr);
 size_t v2_sort_bytes(const Geometry &g, int32_t nr);
 

@@ -24,29 +24,6 @@ namespace pss {
 
 static inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
-// Progress-based wave priority.  Co-resident waves with equal work are arbitrated by age, so
-// the older one runs ahead and the younger finishes alone at half the issue rate.  A wave
-// lowers its own priority as it passes 1/4, 1/2 and 3/4 of its work: whoever is behind wins
-// arbitration, and the waves of a SIMD finish together.
-struct Pacer {
-    uint32_t next, quarter;
-    int stage;
-    __device__ __forceinline__ explicit Pacer(uint32_t total) {
-        quarter = total / 4 + 1;
-        next = quarter;
-        stage = 0;
-        __builtin_amdgcn_s_setprio(3);
-    }
-    __device__ __forceinline__ void step(uint32_t done) {
-        if (done < next) return;
-        next += quarter;
-        stage++;
-        if (stage == 1) __builtin_amdgcn_s_setprio(2);
-        else if (stage == 2) __builtin_amdgcn_s_setprio(1);
-        else __builtin_amdgcn_s_setprio(0);
-    }
-};
-
 __device__ __forceinline__ void tile_bounds(const V2Plan &pl, int64_t tile, int64_t &tlo,
                                             int64_t &thi) {
     tlo = tile * pl.L;
@@ -507,17 +484,6 @@ __global__ __launch_bounds__(64) void k_v2_emit(Geometry g, V2Plan pl,
 // each step is ONE exchange -- no probe, no ballot, no per-clash fix-up -- and the four
 // exchanges of a super-batch issue back to back behind a single wait.
 template <bool NARROW>
-__device__ __forceinline__ int64_t emit_id(uint32_t v, uint32_t twoB, uint32_t old32, uint32_t new32,
-                                           uint32_t N32, const RankDesc &rd, const Geometry &g) {
-    if (NARROW) {
-        const uint32_t id = (v < twoB ? old32 : new32) + v;
-        const uint32_t idw = id - N32;
-        return (int64_t)(id < N32 ? id : idw);
-    }
-    return v2_id(v, rd, g);
-}
-
-template <bool NARROW>
 __global__ __launch_bounds__(64) void k_v2_emit_x(Geometry g, V2Plan pl,
                                                   const RankDesc *__restrict__ ranks,
                                                   int32_t rank_lo, int64_t g_lo, int64_t ng,
@@ -660,10 +626,14 @@ __global__ __launch_bounds__(64) void k_xchg_order_check(int iters, uint32_t P, 
     __shared__ uint32_t buf[4096];
     __shared__ uint32_t model[4096];
     __shared__ uint32_t wbuf[4096];
+    __shared__ uint32_t cnt[4096];
+    __shared__ uint32_t mcnt[4096];
     const int lane = threadIdx.x;
-    for (uint32_t s = lane; s < P; s += 64) { buf[s] = 0xF0000000u | s; model[s] = buf[s]; wbuf[s] = buf[s]; }
+    for (uint32_t s = lane; s < P; s += 64) {
+        buf[s] = 0xF0000000u | s; model[s] = buf[s]; wbuf[s] = buf[s]; cnt[s] = 0; mcnt[s] = 0;
+    }
     __syncthreads();
-    uint32_t nbad = 0, nbadw = 0;
+    uint32_t nbad = 0, nbadw = 0, nbada = 0;
     for (int it = 0; it < iters; it++) {
         uint32_t ks[2], ins[2], got[2];
 #pragma unroll
@@ -671,31 +641,38 @@ __global__ __launch_bounds__(64) void k_xchg_order_check(int iters, uint32_t P, 
             ks[q] = scale32(slot_hash((uint32_t)((blockIdx.x * iters + it) * 2 + q) * 64u + lane, 0x9E3779B9u, 0x7F4A7C15u), P);
             ins[q] = ((uint32_t)it << 9) ^ ((uint32_t)q << 8) ^ (uint32_t)lane;
         }
+        uint32_t pos[2];
 #pragma unroll
         for (int q = 0; q < 2; q++) got[q] = atomicExch(&buf[ks[q]], ins[q]);
 #pragma unroll
         for (int q = 0; q < 2; q++) wbuf[ks[q]] = ins[q];
+#pragma unroll
+        for (int q = 0; q < 2; q++) pos[q] = atomicAdd(&cnt[ks[q]], 1u);
         __syncthreads();
-        uint32_t expect[2] = {0, 0};
+        uint32_t expect[2] = {0, 0}, expc[2] = {0, 0};
         for (int q = 0; q < 2; q++) {
-            for (int l = 0; l < 64; l++) {      // lane 0 replays the exchanges in lane order
+            for (int l = 0; l < 64; l++) {      // lane 0 replays the exchanges / adds in lane order
                 const uint32_t kl = (uint32_t)__shfl((int)ks[q], l);
                 const uint32_t il = (uint32_t)__shfl((int)ins[q], l);
-                uint32_t old = 0;
-                if (lane == 0) { old = model[kl]; model[kl] = il; }
+                uint32_t old = 0, oc = 0;
+                if (lane == 0) { old = model[kl]; model[kl] = il; oc = mcnt[kl]; mcnt[kl] = oc + 1; }
                 old = (uint32_t)__shfl((int)old, 0);
-                if (lane == l) expect[q] = old;
+                oc = (uint32_t)__shfl((int)oc, 0);
+                if (lane == l) { expect[q] = old; expc[q] = oc; }
             }
         }
         __syncthreads();
         nbad += (got[0] != expect[0]) + (got[1] != expect[1]);
+        nbada += (pos[0] != expc[0]) + (pos[1] != expc[1]);
     }
     for (uint32_t s = lane; s < P; s += 64) {
         nbad += buf[s] != model[s];
         nbadw += wbuf[s] != model[s];
     }
+    for (uint32_t s = lane; s < P; s += 64) nbada += cnt[s] != mcnt[s];
     if (nbad) atomicAdd(bad, nbad);
     if (nbadw) atomicAdd(bad + 2, nbadw);
+    if (nbada) atomicAdd(bad + 4, nbada);
 }
 
 // ---- pass B, sorted sub-tiles ---------------------------------------------------------------
@@ -973,11 +950,24 @@ size_t v2_val_bytes(const Geometry &g, int32_t nr) {
 
 size_t v2_buf_bytes(const Geometry &g, int32_t nr) {
     const V2Plan p = v2_plan(g, nr);
-    return p.global_buf ? v2_val_bytes(g, nr) : 0;
+    if (!p.global_buf) return 0;
+    const size_t legacy = v2_val_bytes(g, nr);
+    if (!v2_big_applicable(g)) return legacy;
+    const size_t big = v2_big_bytes(g, nr);
+    return big > legacy ? big : legacy;
 }
 
 size_t v2_sort_bytes(const Geometry &, int32_t) {
     return 0;   // the tail order is a Feistel bijection: no sort workspace
+}
+
+hipError_t launch_v2_tail_vals(const Geometry &g, const V2Plan &pl, const RankDesc *ranks,
+                               int32_t rank_lo, int32_t nr, const uint32_t *VAL, int64_t pos_lo,
+                               int64_t count, int64_t *out, hipStream_t s) {
+    const dim3 grid((uint32_t)cdiv(pl.P1 < 65536 ? pl.P1 : 65536, 256), (uint32_t)nr);
+    hipLaunchKernelGGL(k_v2_tail_f, grid, dim3(256), 0, s, g, pl, ranks, rank_lo, VAL, pos_lo,
+                       count, out);
+    return hipGetLastError();
 }
 
 hipError_t launch_v2(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, int32_t nr,
@@ -985,6 +975,8 @@ hipError_t launch_v2(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, 
                      uint32_t *sort_ws, int32_t *err, hipStream_t s, const Marker &mk,
                      int emit_path) {
     if (emit_path == EMIT_AUTO) emit_path = lds_xchg_ordered() ? EMIT_XCHG : EMIT_PROBE;
+    if (emit_path == EMIT_XCHG && v2_big_applicable(g))   // pools beyond LDS: chunked replay
+        return launch_v2_big(g, ranks, rank_lo, nr, pos_lo, count, out, gbuf, s, mk);
     const V2Plan pl = v2_plan(g, nr);
     const int64_t pos_hi = pos_lo + count < g.ns ? pos_lo + count : g.ns;
     if (nr <= 0 || pos_hi <= pos_lo) return hipSuccess;
@@ -1092,9 +1084,8 @@ hipError_t launch_v2(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, 
     }
     if (need_tail && !tail_fused) {
         mk(K_V2_TAIL, s);
-        const dim3 grid((uint32_t)cdiv(pl.P1 < 65536 ? pl.P1 : 65536, 256), (uint32_t)nr);
-        hipLaunchKernelGGL(k_v2_tail_f, grid, dim3(256), 0, s, g, pl, ranks, rank_lo,
-                           (const uint32_t *)VAL, pos_lo, count, out);
+        hipError_t e = launch_v2_tail_vals(g, pl, ranks, rank_lo, nr, VAL, pos_lo, count, out, s);
+        if (e != hipSuccess) return e;
     }
     mk(-1, s);
     return hipGetLastError();
@@ -1102,20 +1093,22 @@ hipError_t launch_v2(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, 
 
 static signed char g_xchg_ordered[64];   // per device: 0 unknown, 1 ordered, -1 not
 static signed char g_write_ordered[64];
+static signed char g_add_ordered[64];
 
 hipError_t check_lds_xchg_order() {
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return e;
     if (dev < 0 || dev >= 64 || g_xchg_ordered[dev]) return hipSuccess;
-    // bad[0..1]: exchange mismatches at 64 / 4096 slots; bad[2..3]: plain-store mismatches
-    uint32_t *bad = nullptr, hbad[4] = {1, 1, 1, 1};
+    // bad[0..1]: exchange mismatches at 64 / 4096 slots; bad[2..3]: plain-store mismatches;
+    // bad[4..5]: returning-add mismatches
+    uint32_t *bad = nullptr, hbad[6] = {1, 1, 1, 1, 1, 1};
     e = hipMalloc((void **)&bad, sizeof(hbad));
     if (e != hipSuccess) return e;
     e = hipMemset(bad, 0, sizeof(hbad));
     if (e == hipSuccess) {
-        hipLaunchKernelGGL(k_xchg_order_check, dim3(32), dim3(64), 0, 0, 64, 64u, bad);
-        hipLaunchKernelGGL(k_xchg_order_check, dim3(32), dim3(64), 0, 0, 64, 4096u, bad + 1);
+        hipLaunchKernelGGL(k_xchg_order_check, dim3(64), dim3(64), 0, 0, 24, 64u, bad);
+        hipLaunchKernelGGL(k_xchg_order_check, dim3(64), dim3(64), 0, 0, 24, 4096u, bad + 1);
         e = hipGetLastError();
     }
     if (e == hipSuccess) e = hipMemcpy(hbad, bad, sizeof(hbad), hipMemcpyDeviceToHost);
@@ -1123,7 +1116,15 @@ hipError_t check_lds_xchg_order() {
     if (e != hipSuccess) return e;
     g_xchg_ordered[dev] = (hbad[0] == 0 && hbad[1] == 0) ? 1 : -1;
     g_write_ordered[dev] = (hbad[2] == 0 && hbad[3] == 0) ? 1 : -1;
+    g_add_ordered[dev] = (hbad[4] == 0 && hbad[5] == 0) ? 1 : -1;
     return hipSuccess;
+}
+
+bool lds_add_ordered() {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return false;
+    if (!g_add_ordered[dev] && check_lds_xchg_order() != hipSuccess) return false;
+    return g_add_ordered[dev] > 0;
 }
 
 bool lds_write_ordered() {
@@ -1143,6 +1144,7 @@ bool lds_xchg_ordered() {
 hipError_t init_kernel_attributes_v2() {
     const int big = 160 * 1024;
     hipError_t e = check_lds_xchg_order();
+    if (e == hipSuccess) e = init_kernel_attributes_v2big();
 #define PSS_ATTR(fn) { hipError_t x = hipFuncSetAttribute((const void *)(fn), hipFuncAttributeMaxDynamicSharedMemorySize, big); if (x != hipSuccess) e = x; }
     PSS_ATTR((k_v2_lastocc<64, true>));
     PSS_ATTR((k_v2_lastocc<256, false>));

@@ -235,3 +235,30 @@ def test_v2_emit_paths_match_oracle(path, B, R, F, lo, hi):
         part = eng.generate(0, R, pos_lo, count).cpu().numpy()
         c = min(count, ns - pos_lo)
         assert np.array_equal(part[:, :c], full[:, pos_lo:pos_lo + c]), (pos_lo, count)
+
+
+@pytest.mark.parametrize("path", ["xchg", "probe"])
+@pytest.mark.parametrize("B,R,F,lo,hi", [(20000, 3, 30, 5000, 20000), (65536, 2, 40, 10000, 30000),
+                                         (16385, 4, 20, 3000, 9000), (131072, 2, 12, 40000, 80000)])
+def test_v2_large_pool_paths_match_oracle(path, B, R, F, lo, hi):
+    # pools beyond the LDS slot table: slot-chunked replay ("xchg") and the HBM slot table
+    # ("probe"), full epochs and ragged position ranges, against the oracle twin
+    rng = np.random.default_rng(B + R + F)
+    lengths = rng.integers(lo, hi, F)
+    N = int(lengths.sum())
+    eng = _engine(lengths, N, R, B, 2, seed=5)
+    eng.set_emit_path(path)
+    ns = eng.num_samples
+    assert ns > B
+    for epoch in (0, 2):
+        eng.init_iter(epoch)
+        old, new = eng.rank_starts()
+        full = eng.generate(0, R).cpu().numpy()
+        key = O.epoch_key(5, epoch)
+        for r in range(R):
+            ref = O.v2_philox_stream(key, r, int(old[r]), int(new[r]), ns, B, N)
+            assert np.array_equal(full[r], ref), (epoch, r, int(np.argmax(full[r] != ref)))
+    for pos_lo, count in ((0, 100), (B - 5, 3 * B), (ns // 3, 12345), (ns - B - 10, 50), (ns - 7, 7)):
+        part = eng.generate(0, R, pos_lo, count).cpu().numpy()
+        c = min(count, ns - pos_lo)
+        assert np.array_equal(part[:, :c], full[:, pos_lo:pos_lo + c]), (pos_lo, count)
