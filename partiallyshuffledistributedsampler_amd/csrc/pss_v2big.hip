@@ -8,7 +8,7 @@
 // tile (L = mult * P1 steps) and rank:
 //
 //   k_bk_count     one wave per segment of 4096 steps: histogram of the chunk of every step
-//   k_bk_scan      per tile: exclusive scan of the (chunk, segment) counts, chunk-major
+//   k_bk_scan_*    per tile: exclusive scan of the (chunk, segment) counts, chunk-major
 //   k_bk_scatter   per segment: each step's tile-local index into its chunk's list, in step
 //                  order (lane-ordered ds_add_rtn, checked at start-up: stable)
 //   k_bk_lastocc   per (tile, chunk): last step of each slot (plain stores in list order) ->
@@ -19,6 +19,8 @@
 //   k_v2_tail_f    (pss_v2.hip) the final pool from the VAL walk-back
 //
 // Same schedule as the LDS path: the output is bit-identical.
+#include <cstdlib>
+
 #include "pss_device.h"
 
 namespace pss {
@@ -43,8 +45,14 @@ BigPlan big_plan(const Geometry &g, int32_t nr) {
     p.C = cdiv(p.P1, kChunk);
     // tiles of mult * P1 steps: long enough that a slot is rarely untouched by a whole tile
     // (walk-back e^-mult), short enough that nr * G * C jobs fill the chip
-    int64_t mult = 4;
+    static const int64_t mult_env = [] {   // tuning knob
+        const char *e = getenv("PSS_V2BIG_MULT");
+        const long v = e ? atol(e) : 0;
+        return (int64_t)(v >= 1 && v <= 4 ? v : 0);
+    }();
+    int64_t mult = mult_env ? mult_env : 4;
     for (;;) {
+        if (mult_env) break;
         const int64_t L = cdiv(mult * p.P1, kSeg) * kSeg;
         const int64_t G = p.T > 0 ? cdiv(p.T, L) : 0;
         if (mult == 2 || (int64_t)nr * G * p.C >= 4096) break;
@@ -121,25 +129,45 @@ __global__ __launch_bounds__(64) void k_bk_count(Geometry g, BigPlan p, int32_t 
     for (uint32_t c = threadIdx.x; c < C; c += 64) cnt[(size_t)c * p.nseg] = hist[c];
 }
 
-// grid: nr * G blocks of 1024; scans the tile's counts in (chunk, segment) order in place
-__global__ __launch_bounds__(1024) void k_bk_scan(BigPlan p, BigWS w) {
-    __shared__ uint32_t tot[16];
-    const uint32_t rt = blockIdx.x;
+// Two-level scan of the (chunk, segment) counts:
+//   k_bk_scan_seg   one 256-thread block per (rank-tile, chunk): exclusive scan over the
+//                   chunk's segments in place; the chunk's total -> cst[c]
+//   k_bk_scan_chunk one block per rank-tile: exclusive scan of the chunk totals (cst[0..C])
+// k_bk_scatter then starts segment sg of chunk c at cst[c] + cnt[c][sg].
+__global__ __launch_bounds__(256) void k_bk_scan_seg(BigPlan p, BigWS w) {
+    __shared__ uint32_t tot[4];
     const uint32_t C = (uint32_t)p.C, S = (uint32_t)p.nseg;
-    uint32_t *cnt = w.cnt + (size_t)rt * S * C;
-    uint32_t *cst = w.cst + (size_t)rt * (C + 1);
-    const uint32_t n = C * S;                          // linear index i = c * S + s
-    const uint32_t per = (n + 1023) / 1024;
-    const uint32_t lo = threadIdx.x * per < n ? threadIdx.x * per : n;
-    const uint32_t hi = lo + per < n ? lo + per : n;
+    const uint32_t rt = blockIdx.x / C, c = blockIdx.x - rt * C;
+    uint32_t *cnt = w.cnt + ((size_t)rt * C + c) * S;
+    const uint32_t per = (S + 255) / 256;
+    const uint32_t lo = threadIdx.x * per < S ? threadIdx.x * per : S;
+    const uint32_t hi = lo + per < S ? lo + per : S;
     uint32_t sum = 0;
     for (uint32_t i = lo; i < hi; i++) sum += cnt[i];
     uint32_t total;
-    uint32_t run = block_excl_scan<1024>(sum, tot, total);
+    uint32_t run = block_excl_scan<256>(sum, tot, total);
     for (uint32_t i = lo; i < hi; i++) {
         const uint32_t v = cnt[i];
-        if (i % S == 0) cst[i / S] = run;
         cnt[i] = run;
+        run += v;
+    }
+    if (threadIdx.x == 0) w.cst[(size_t)rt * (C + 1) + c] = total;
+}
+
+__global__ __launch_bounds__(1024) void k_bk_scan_chunk(BigPlan p, BigWS w) {
+    __shared__ uint32_t tot[16];
+    const uint32_t C = (uint32_t)p.C;
+    uint32_t *cst = w.cst + (size_t)blockIdx.x * (C + 1);
+    const uint32_t per = (C + 1023) / 1024;
+    const uint32_t lo = threadIdx.x * per < C ? threadIdx.x * per : C;
+    const uint32_t hi = lo + per < C ? lo + per : C;
+    uint32_t sum = 0;
+    for (uint32_t i = lo; i < hi; i++) sum += cst[i];
+    uint32_t total;
+    uint32_t run = block_excl_scan<1024>(sum, tot, total);
+    for (uint32_t i = lo; i < hi; i++) {
+        const uint32_t v = cst[i];
+        cst[i] = run;
         run += v;
     }
     if (threadIdx.x == 0) cst[C] = total;
@@ -153,7 +181,8 @@ __global__ __launch_bounds__(64) void k_bk_scatter(Geometry g, BigPlan p, int32_
     const TileInfo ti = tile_info(p, rank_lo, rt);
     const uint32_t C = (uint32_t)p.C, P1 = (uint32_t)p.P1;
     const uint32_t *cnt = w.cnt + (size_t)rt * p.nseg * C + sg;
-    for (uint32_t c = threadIdx.x; c < C; c += 64) off[c] = cnt[(size_t)c * p.nseg];
+    const uint32_t *cst = w.cst + (size_t)rt * (C + 1);
+    for (uint32_t c = threadIdx.x; c < C; c += 64) off[c] = cst[c] + cnt[(size_t)c * p.nseg];
     __syncthreads();
     const SlotKey sk = slot_key(g, ti.rank);
     uint32_t *list = w.list + (size_t)rt * p.L;
@@ -336,7 +365,8 @@ hipError_t launch_v2_big(const Geometry &g, const RankDesc *ranks, int32_t rank_
         const size_t lds_c = (size_t)p.C * 4;
         mk(K_V2_LASTOCC, s);
         hipLaunchKernelGGL(k_bk_count, dim3(rts * (uint32_t)p.nseg), dim3(64), lds_c, s, g, p, rank_lo, w);
-        hipLaunchKernelGGL(k_bk_scan, dim3(rts), dim3(1024), 0, s, p, w);
+        hipLaunchKernelGGL(k_bk_scan_seg, dim3(rts * (uint32_t)p.C), dim3(256), 0, s, p, w);
+        hipLaunchKernelGGL(k_bk_scan_chunk, dim3(rts), dim3(1024), 0, s, p, w);
         hipLaunchKernelGGL(k_bk_scatter, dim3(rts * (uint32_t)p.nseg), dim3(64), lds_c, s, g, p, rank_lo, w);
         hipLaunchKernelGGL(k_bk_lastocc, dim3(rts * (uint32_t)p.C), dim3(64), 0, s, g, p, rank_lo, w);
         const int64_t last_emit = pos_lo < p.T ? ((pos_hi < p.T ? pos_hi : p.T) - 1) / p.L : -1;
