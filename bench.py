@@ -129,6 +129,8 @@ def main():
     ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-latency", action="store_true")
+    ap.add_argument("--no-kernel-timing", action="store_true",
+                    help="time the steps without the per-launch HIP events (roofline omitted)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -158,7 +160,7 @@ def main():
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
-    eng.profile(True)
+    eng.profile(not args.no_kernel_timing)
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for i in range(args.steps):

@@ -163,6 +163,13 @@ __device__ __forceinline__ void slot_words(const SlotKey &sk, int64_t sb, int la
     for (int j = 0; j < 4; j++) u[j] = slot_hash(t0 + 64u * j, sk.s0, sk.s1);
 }
 
+// slot of a 32-bit draw: Lemire multiply-shift, or a plain shift when P1 is a power of two
+// (exactly the same value: (u * 2^k) >> 32 == u >> (32 - k)), one quarter-rate multiply less
+template <bool POW2>
+__device__ __forceinline__ uint32_t slot_scale(uint32_t u, uint32_t P1, uint32_t sh) {
+    return POW2 ? (u >> sh) : scale32(u, P1);
+}
+
 // Feistel round keys of pool2 window w: Philox blocks (w, 0, rank, INS) and (w, 1, rank, INS),
 // 8 words of which the first kFeistelRounds are used
 constexpr int kRoundKeyWords = 8;
@@ -186,6 +193,37 @@ __device__ __forceinline__ void tail_round_keys(const Geometry &g, uint32_t rank
         philox4x32_10_rolled(c0, c1, c2, c3, g.key0, g.key1);
         k[4 * h] = c0; k[4 * h + 1] = c1; k[4 * h + 2] = c2; k[4 * h + 3] = c3;
     }
+}
+
+// Per-launch key table (k_v2_keys): for local rank rl at p + rl * stride:
+//   [0, 2) slot key, [8, 16) tail round keys, [16 + 8 (w - 1), +8) round keys of pool2 window w.
+// p == nullptr: the kernels derive the keys with Philox themselves.
+
+__device__ __forceinline__ SlotKey slot_key_t(const Geometry &g, uint32_t rank, const KeyTab &kt,
+                                              int32_t rl) {
+    if (!kt.p) return slot_key(g, rank);
+    const uint32_t *b = kt.p + rl * kt.stride;
+    return SlotKey{b[0], b[1]};
+}
+
+__device__ __forceinline__ void tail_keys_t(const Geometry &g, uint32_t rank, const KeyTab &kt,
+                                            int32_t rl, uint32_t k[kRoundKeyWords]) {
+    if (!kt.p) { tail_round_keys(g, rank, k); return; }
+    const uint32_t *b = kt.p + rl * kt.stride + 8;
+#pragma unroll
+    for (int i = 0; i < kRoundKeyWords; i++) k[i] = b[i];
+}
+
+// round keys of windows [w_lo, w_lo + nwin) into LDS (all threads of the block take part)
+__device__ __forceinline__ void stage_keys_t(const Geometry &g, uint32_t rank, int64_t w_lo, int nwin,
+                                             uint32_t *rk, const KeyTab &kt, int32_t rl) {
+    if (!kt.p) {
+        for (int j = threadIdx.x; j < nwin; j += blockDim.x)
+            window_round_keys(g, rank, w_lo + j, rk + kRoundKeyWords * j);
+        return;
+    }
+    const uint32_t *b = kt.p + rl * kt.stride + 16 + kRoundKeyWords * (w_lo - 1);
+    for (int i = threadIdx.x; i < nwin * kRoundKeyWords; i += blockDim.x) rk[i] = b[i];
 }
 
 // virtual index inserted at step t (pool2 window w = 1 + t/B in Feistel order), given the

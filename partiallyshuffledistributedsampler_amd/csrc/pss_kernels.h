@@ -22,6 +22,11 @@ struct Geometry {       // per-epoch constants of one sampler
     uint32_t key0, key1;  // Philox key = epoch_key(seed, epoch)
 };
 
+struct KeyTab {         // per-launch table of Philox-derived keys (pss_device.h layout)
+    const uint32_t *p;  // nullptr: kernels derive the keys themselves
+    int64_t stride;     // words per local rank
+};
+
 struct V2Plan {         // slot-machine tiling of one V2 stream
     int64_t P1;         // slots = min(B, ns)
     int64_t T;          // replacement steps = ns - P1
@@ -30,6 +35,12 @@ struct V2Plan {         // slot-machine tiling of one V2 stream (DESIGN.md §3.3
     int32_t global_buf; // 1: slot table lives in HBM scratch (P1 beyond the LDS budget)
     int32_t fold;       // 1: every virtual id < 2^24, probe byte folded into the slot word
     int64_t emit_lds;   // dynamic LDS of one k_v2_emit wave (padded to cap waves per CU)
+    // 32-bit constants of the replay, computed on the host so that no kernel prologue runs a
+    // 64-bit division (each one is ~100 scalar instructions of cold code per wave)
+    uint32_t B32, L32, T32;    // shuffle_buffer, tile length, steps (T < 2^32)
+    uint32_t hB, walk_full;    // Feistel half width of a full window; 1 if it needs walking
+    uint32_t w_last, len_last, h_last;   // last pool2 window (may be short)
+    uint32_t twoB;             // min(2B, ns): virtual ids below come from the OLD start
 };
 
 // optional per-kernel timing: `mark(ctx, kind, stream)` is called right before each launch
@@ -94,6 +105,11 @@ constexpr size_t kBigSortBudget = (size_t)2 << 30;
 // tiling of a launch over nr ranks: sized so that k_v2_emit fills every SIMD with two waves
 V2Plan v2_plan(const Geometry &g, int32_t nr);
 
+// rank descriptors host -> device through kernel arguments (128 per launch), R <= kArgRanksMax
+constexpr int32_t kArgRanks = 128;
+constexpr int32_t kArgRanksMax = 1024;
+hipError_t launch_put_ranks(const RankDesc *host, int32_t R, RankDesc *dst, hipStream_t s);
+
 // exclusive prefix over the shuffled file order: prefix[f] = sum_{j<f} len[order[j]]
 // scratch: scan_scratch_words(F) words
 hipError_t launch_scan_prefix(const int64_t *lens, const int32_t *order, int64_t F,
@@ -121,6 +137,7 @@ size_t v1_workspace_bytes(const Geometry &g, int32_t nr, int64_t pos_lo, int64_t
 // V2 replay kernel: EMIT_XCHG = one LDS exchange per step (needs the lane-ordered exchange the
 // start-up check confirms), EMIT_PROBE = collision probe + per-clash fix-up (any hardware)
 enum EmitPath { EMIT_AUTO = 0, EMIT_XCHG = 1, EMIT_PROBE = 2 };
+enum V2Stage { V2_STAGE_ALL = 0, V2_STAGE_PRE = 1, V2_STAGE_EMIT = 2 };
 bool lds_xchg_ordered();   // result of the start-up check on the current device
 bool lds_write_ordered();  // same-word lanes of one plain LDS store: the highest lane wins
 bool lds_add_ordered();    // same-word lanes of one ds_add_rtn are served in lane order
@@ -129,12 +146,14 @@ bool lds_add_ordered();    // same-word lanes of one ds_add_rtn are served in la
 hipError_t launch_v2(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, int32_t nr,
                      int64_t pos_lo, int64_t count, int64_t *out, uint32_t *val_ws,
                      uint32_t *buf_ws, uint32_t *sort_ws, int32_t *err, hipStream_t s,
-                     const Marker &mk = Marker(), int emit_path = EMIT_AUTO);
+                     const Marker &mk = Marker(), int emit_path = EMIT_AUTO,
+                     int stage = V2_STAGE_ALL);
 size_t v2_val_bytes(const Geometry &g, int32_t nr);
 // V2 tail from per-tile VAL tables (walk-back), positions [pos_lo, pos_lo+count) past T
 hipError_t launch_v2_tail_vals(const Geometry &g, const V2Plan &pl, const RankDesc *ranks,
                                int32_t rank_lo, int32_t nr, const uint32_t *VAL, int64_t pos_lo,
-                               int64_t count, int64_t *out, hipStream_t s);
+                               int64_t count, int64_t *out, hipStream_t s,
+                               KeyTab kt);
 // pools beyond LDS (P1 in (16384, 2^22]): slot-chunked replay (pss_v2big.hip); workspace in
 // buf_ws (v2_buf_bytes covers it)
 bool v2_big_applicable(const Geometry &g);

@@ -277,6 +277,22 @@ __global__ __launch_bounds__(256) void k_v1_write_big(Geometry g, const RankDesc
 // ------------------------------------------------------------------------------------------
 static inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
+struct RankArgs { RankDesc r[kArgRanks]; };
+
+__global__ __launch_bounds__(kArgRanks) void k_put_ranks(RankArgs a, int32_t n, RankDesc *dst) {
+    if ((int32_t)threadIdx.x < n) dst[threadIdx.x] = a.r[threadIdx.x];
+}
+
+hipError_t launch_put_ranks(const RankDesc *host, int32_t R, RankDesc *dst, hipStream_t s) {
+    for (int32_t r0 = 0; r0 < R; r0 += kArgRanks) {
+        RankArgs a;
+        const int32_t n = R - r0 < kArgRanks ? R - r0 : kArgRanks;
+        for (int32_t i = 0; i < n; i++) a.r[i] = host[r0 + i];
+        hipLaunchKernelGGL(k_put_ranks, dim3(1), dim3(kArgRanks), 0, s, a, n, dst + r0);
+    }
+    return hipGetLastError();
+}
+
 size_t scan_scratch_words(int64_t F) { return (size_t)cdiv(F > 0 ? F : 1, kScanChunk); }
 
 hipError_t launch_scan_prefix(const int64_t *lens, const int32_t *order, int64_t F,

@@ -46,24 +46,20 @@ class CPythonMT {
         init_by_array(key, key[1] ? 2 : 1);
     }
     uint32_t next() {
-        if (mti_ >= kN) twist();
-        uint32_t y = mt_[mti_++];
-        y ^= y >> 11;
-        y ^= (y << 7) & 0x9d2c5680u;
-        y ^= (y << 15) & 0xefc60000u;
-        y ^= y >> 18;
-        return y;
+        if (__builtin_expect(mti_ >= kN, 0)) twist();
+        return out_[mti_++];
     }
+    // random.py:239-249 (_randbelow_with_getrandbits): k = n.bit_length(), draw getrandbits(k)
+    // (the top k bits of one 32-bit output) until below n
     uint32_t randbelow(uint32_t n) {  // n < 2^32
         if (n == 0) return 0;
-        int k = 0;
-        for (uint64_t v = n; v; v >>= 1) k++;
+        const int sh = __builtin_clz(n);                 // 32 - k
         uint32_t r;
-        do { r = next() >> (32 - k); } while (r >= n);
+        do { r = next() >> sh; } while (r >= n);
         return r;
     }
     template <typename T>
-    void shuffle(T *x, int64_t n) {
+    void shuffle(T *x, int64_t n) {   // random.py:380-396
         for (int64_t i = n - 1; i >= 1; i--) {
             const int64_t j = randbelow((uint32_t)(i + 1));
             const T t = x[i]; x[i] = x[j]; x[j] = t;
@@ -73,6 +69,7 @@ class CPythonMT {
   private:
     static constexpr int kN = 624, kM = 397;
     uint32_t mt_[kN];
+    uint32_t out_[kN];   // tempered outputs of the current block
     int mti_ = kN + 1;
 
     void init_genrand(uint32_t s) {
@@ -111,6 +108,14 @@ class CPythonMT {
         }
         y = (mt_[kN - 1] & 0x80000000u) | (mt_[0] & 0x7fffffffu);
         mt_[kN - 1] = mt_[kM - 1] ^ (y >> 1) ^ mag01[y & 1u];
+        for (int i = 0; i < kN; i++) {   // temper the whole block at once (vectorises)
+            uint32_t t = mt_[i];
+            t ^= t >> 11;
+            t ^= (t << 7) & 0x9d2c5680u;
+            t ^= (t << 15) & 0xefc60000u;
+            t ^= t >> 18;
+            out_[i] = t;
+        }
         mti_ = 0;
     }
 };
@@ -161,7 +166,8 @@ struct pss_sampler {
     bool iterated = false;
     // device state
     bool dev_init = false;
-    bool dirty = true;
+    bool dirty = true;            // rank descriptors of the epoch not on the device yet
+    bool order_dirty = true;      // file order not uploaded (only map / partition need it)
     bool prefix_dirty = true;     // prefix scan owed (run lazily by map / partition)
     DevBuf<int64_t> d_lens, d_prefix;
     DevBuf<int32_t> d_order, d_err;
@@ -235,14 +241,31 @@ int prepare(pss_sampler *h, hipStream_t s) {
     int rc = ensure_device(h);
     if (rc) return rc;
     if (!h->dirty) return PSS_OK;
+    // generation needs only the R rank descriptors: small tables travel as kernel arguments
+    // (no copy-engine round trip on the epoch path), large ones through pinned staging
+    if (h->R <= pss::kArgRanksMax) {
+        PSS_HIP(pss::launch_put_ranks(h->ranks.data(), h->R, h->d_ranks.p, s));
+    } else {
+        if (h->upload_pending) PSS_HIP(hipEventSynchronize(h->upload_done));
+        std::memcpy(h->h_stage_ranks, h->ranks.data(), sizeof(pss::RankDesc) * h->R);
+        PSS_HIP(hipMemcpyAsync(h->d_ranks.p, h->h_stage_ranks, sizeof(pss::RankDesc) * h->R, hipMemcpyHostToDevice, s));
+        PSS_HIP(hipEventRecord(h->upload_done, s));
+        h->upload_pending = true;
+    }
+    h->dirty = false;
+    return PSS_OK;
+}
+
+// the shuffled file order, uploaded on first use after an init_iter
+int prepare_order(pss_sampler *h, hipStream_t s) {
+    int rc = prepare(h, s);
+    if (rc || !h->order_dirty) return rc;
     if (h->upload_pending) PSS_HIP(hipEventSynchronize(h->upload_done));
     std::memcpy(h->h_stage_order, h->order.data(), sizeof(int32_t) * h->F);
-    std::memcpy(h->h_stage_ranks, h->ranks.data(), sizeof(pss::RankDesc) * h->R);
     if (h->F) PSS_HIP(hipMemcpyAsync(h->d_order.p, h->h_stage_order, sizeof(int32_t) * h->F, hipMemcpyHostToDevice, s));
-    PSS_HIP(hipMemcpyAsync(h->d_ranks.p, h->h_stage_ranks, sizeof(pss::RankDesc) * h->R, hipMemcpyHostToDevice, s));
     PSS_HIP(hipEventRecord(h->upload_done, s));
     h->upload_pending = true;
-    h->dirty = false;
+    h->order_dirty = false;
     h->prefix_dirty = true;
     return PSS_OK;
 }
@@ -250,7 +273,7 @@ int prepare(pss_sampler *h, hipStream_t s) {
 // the exclusive prefix over the epoch's file order is needed only by the id -> (file, offset)
 // map and the partition, so it is scanned on first use after an init_iter
 int prepare_prefix(pss_sampler *h, hipStream_t s) {
-    int rc = prepare(h, s);
+    int rc = prepare_order(h, s);
     if (rc || !h->prefix_dirty) return rc;
     const pss::Marker mk = marker_of(h);
     mk(pss::K_SCAN, s);
@@ -358,6 +381,8 @@ int pss_init_iter(pss_sampler *h, int64_t epoch) {
     h->epoch = epoch;
     h->iterated = true;
     h->dirty = true;
+    h->order_dirty = true;
+    h->prefix_dirty = true;
     return PSS_OK;
 }
 

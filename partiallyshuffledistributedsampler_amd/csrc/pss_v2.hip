@@ -30,10 +30,27 @@ __device__ __forceinline__ void tile_bounds(const V2Plan &pl, int64_t tile, int6
     thi = tlo + pl.L < pl.T ? tlo + pl.L : pl.T;
 }
 
-__device__ __forceinline__ void stage_round_keys(const Geometry &g, uint32_t rank, int64_t w_lo,
-                                                 int nwin, uint32_t *rk) {
-    for (int j = threadIdx.x; j < nwin; j += blockDim.x)
-        window_round_keys(g, rank, w_lo + j, rk + kRoundKeyWords * j);
+// ---- key table: one thread per (local rank, item) --------------------------------------------
+__global__ __launch_bounds__(256) void k_v2_keys(Geometry g, int32_t rank_lo, int64_t nwin_tot,
+                                                 int64_t stride, uint32_t *__restrict__ kt) {
+    const int32_t rl = (int32_t)blockIdx.y;
+    const uint32_t rank = (uint32_t)(rank_lo + rl);
+    const int64_t item = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    uint32_t *b = kt + rl * stride;
+    if (item == 0) {
+        const SlotKey sk = slot_key(g, rank);
+        b[0] = sk.s0; b[1] = sk.s1;
+    } else if (item == 1) {
+        uint32_t k[kRoundKeyWords];
+        tail_round_keys(g, rank, k);
+#pragma unroll
+        for (int i = 0; i < kRoundKeyWords; i++) b[8 + i] = k[i];
+    } else if (item < nwin_tot + 2) {
+        uint32_t k[kRoundKeyWords];
+        window_round_keys(g, rank, item - 1, k);
+#pragma unroll
+        for (int i = 0; i < kRoundKeyWords; i++) b[16 + kRoundKeyWords * (item - 2) + i] = k[i];
+    }
 }
 
 #ifdef PSS_STAMPS   // diagnostic build only (tools/stamp_v2.hip): per-workgroup phase clocks
@@ -50,32 +67,34 @@ __device__ uint64_t pss_stamps[1 << 16][8];
 //     -- a later instruction overwrites an earlier one and, inside one store, the highest lane
 //     wins (start-up check), so each slot ends with its last step.  No LDS atomics.
 //   otherwise (NT = 256): any order, ds_max.
-template <int NT, bool ORDERED>
+template <int NT, bool ORDERED, bool POW2>
 __global__ __launch_bounds__(NT) void k_v2_lastocc(Geometry g, V2Plan pl, int32_t rank_lo,
-                                                   int64_t ng, uint32_t *__restrict__ VAL) {
+                                                   int64_t ng, uint32_t *__restrict__ VAL,
+                                                   KeyTab kt) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     PSS_STAMP(0);
     const int P1 = (int)pl.P1;
     uint32_t *lastT = smem, *rk = smem + P1;
-    // 32-bit tile arithmetic (T < 2^32: num_samples >= 2^32 is rejected)
-    const uint32_t ngu = (uint32_t)ng, B = (uint32_t)g.B;
+    // 32-bit tile arithmetic from the plan's host-computed constants (T < 2^32)
+    const uint32_t ngu = (uint32_t)ng, B = pl.B32;
     const int32_t rl = (int32_t)(blockIdx.x / ngu);
     const uint32_t tile = blockIdx.x - (uint32_t)rl * ngu;
     const uint32_t rank = (uint32_t)(rank_lo + rl);
-    const uint32_t tlo = tile * (uint32_t)pl.L;
-    const uint32_t thi = (uint32_t)(pl.T - tlo < pl.L ? pl.T : tlo + pl.L);
+    const uint32_t tlo = tile * pl.L32;
+    const uint32_t thi = pl.T32 - tlo < pl.L32 ? pl.T32 : tlo + pl.L32;
     const uint32_t w_lo = 1 + tlo / B;
     const int nwin = (int)(1 + (thi - 1) / B - w_lo + 1);
 #ifdef PSS_STAMPS
     if (threadIdx.x == 0) pss_stamps[blockIdx.x][4] = __builtin_amdgcn_s_memrealtime();
 #endif
     for (int s = threadIdx.x; s < P1; s += NT) lastT[s] = 0;
-    stage_round_keys(g, rank, w_lo, nwin, rk);
-    const SlotKey sk = slot_key(g, rank);
+    stage_keys_t(g, rank, w_lo, nwin, rk, kt, rl);
+    const SlotKey sk = slot_key_t(g, rank, kt, rl);
     __syncthreads();
     PSS_STAMP(1);
     // whole blocks of 8*NT steps run branch-free with 8 independent hashes per thread
     const uint32_t n = (uint32_t)(thi - tlo), t0 = (uint32_t)tlo;
+    const uint32_t sh = 32u - (uint32_t)ceil_log2_u64((uint64_t)P1);   // POW2 only
     constexpr uint32_t BLK = 8 * NT;
     const uint32_t nfull = n / BLK * BLK;
     // Loop counters are workgroup-uniform (base), never per-lane: with a per-lane trip count the
@@ -86,7 +105,7 @@ __global__ __launch_bounds__(NT) void k_v2_lastocc(Geometry g, V2Plan pl, int32_
         const uint32_t b = base + threadIdx.x;
         uint32_t k[8];
 #pragma unroll
-        for (int j = 0; j < 8; j++) k[j] = scale32(slot_hash(t0 + b + NT * j, sk.s0, sk.s1), (uint32_t)P1);
+        for (int j = 0; j < 8; j++) k[j] = slot_scale<POW2>(slot_hash(t0 + b + NT * j, sk.s0, sk.s1), (uint32_t)P1, sh);
 #pragma unroll
         for (int j = 0; j < 8; j++) {
             if (ORDERED) lastT[k[j]] = b + NT * j + 1u;
@@ -96,7 +115,7 @@ __global__ __launch_bounds__(NT) void k_v2_lastocc(Geometry g, V2Plan pl, int32_
     for (uint32_t base = nfull; base < n; base += NT) {
         const uint32_t b = base + threadIdx.x;
         if (b < n) {
-            const uint32_t kk = scale32(slot_hash(t0 + b, sk.s0, sk.s1), (uint32_t)P1);
+            const uint32_t kk = slot_scale<POW2>(slot_hash(t0 + b, sk.s0, sk.s1), (uint32_t)P1, sh);
             if (ORDERED) lastT[kk] = b + 1u;
             else atomicMax(&lastT[kk], b + 1u);
         }
@@ -105,12 +124,9 @@ __global__ __launch_bounds__(NT) void k_v2_lastocc(Geometry g, V2Plan pl, int32_
     PSS_STAMP(2);
     // last step -> inserted value, in 32-bit tile-local arithmetic (no 64-bit division)
     uint32_t *V = VAL + ((int64_t)rl * pl.G + tile) * P1;
-    const uint32_t hB = feistel_half_bits(B);
-    const uint32_t w_last = (uint32_t)(1 + (pl.T - 1) / g.B);
-    const uint32_t len_last = (uint32_t)(g.ns - (int64_t)w_last * g.B);
-    const uint32_t h_last = feistel_half_bits(len_last);
+    const uint32_t hB = pl.hB, w_last = pl.w_last, len_last = pl.len_last, h_last = pl.h_last;
     const uint32_t p_lo = tlo - (w_lo - 1) * B;                 // index of step tlo in window w_lo
-    const bool walk_full = B != (1u << (2 * hB));
+    const bool walk_full = pl.walk_full;
     const float invB = 1.0f / (float)B;
     // 4 slots per thread per pass (independent chains); a whole pass takes the one-pass
     // Feistel unless one of its slots lies in the short last window or B needs cycle walking
@@ -407,7 +423,7 @@ __global__ __launch_bounds__(64) void k_v2_emit(Geometry g, V2Plan pl,
             }
         }
     }
-    stage_round_keys(g, rank, w_lo, nwin, rk);
+    stage_keys_t(g, rank, w_lo, nwin, rk, KeyTab{nullptr, 0}, rl);
     __syncthreads();
     EmitCtx<FOLD> c;
     c.lane = lane;
@@ -483,30 +499,33 @@ __global__ __launch_bounds__(64) void k_v2_emit(Geometry g, V2Plan pl,
 // highest lane's insertion.  That is exactly the sequential replay of 64 consecutive steps, so
 // each step is ONE exchange -- no probe, no ballot, no per-clash fix-up -- and the four
 // exchanges of a super-batch issue back to back behind a single wait.
-template <bool NARROW>
+template <bool NARROW, bool POW2>
 __global__ __launch_bounds__(64) void k_v2_emit_x(Geometry g, V2Plan pl,
                                                   const RankDesc *__restrict__ ranks,
                                                   int32_t rank_lo, int64_t g_lo, int64_t ng,
                                                   const uint32_t *__restrict__ VAL,
                                                   int64_t pos_lo, int64_t count, int do_tail,
-                                                  int64_t *__restrict__ out) {
+                                                  int64_t *__restrict__ out, KeyTab kt) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     const uint32_t P1 = (uint32_t)pl.P1;
-    const int64_t nwin_max = pl.L / g.B + 2;
+    const uint32_t B = pl.B32;
+    const uint32_t nwin_max = pl.L32 / B + 2;
     uint32_t *rk = smem;                                    // Feistel keys of the tile's windows
     uint32_t *buf = smem + kRoundKeyWords * nwin_max;       // slot table
     const int lane = threadIdx.x;
-    const int32_t rl = (int32_t)(blockIdx.x / ng);
-    const int64_t tile = g_lo + (int64_t)(blockIdx.x % ng);
+    // 32-bit tile arithmetic from the plan's host-computed constants (T < 2^32)
+    const uint32_t ngu = (uint32_t)ng;
+    const int32_t rl = (int32_t)(blockIdx.x / ngu);
+    const uint32_t tile = (uint32_t)g_lo + (blockIdx.x - (uint32_t)rl * ngu);
     const uint32_t rank = (uint32_t)(rank_lo + rl);
     const RankDesc rd = ranks[rank];
-    int64_t tlo, thi;
-    tile_bounds(pl, tile, tlo, thi);
-    const int64_t w_lo = 1 + tlo / g.B;
-    const int nwin = (int)(1 + (thi - 1) / g.B - w_lo + 1);
+    const uint32_t tlo = tile * pl.L32;
+    const uint32_t thi = pl.T32 - tlo < pl.L32 ? pl.T32 : tlo + pl.L32;
+    const uint32_t w_lo = 1 + tlo / B;
+    const int nwin = (int)(1 + (thi - 1) / B - w_lo + 1);
     {   // slot table at the tile's start (4 independent loads in flight per lane)
         const uint32_t *VALr = VAL + (int64_t)rl * pl.G * pl.P1;
-        const uint32_t *prev = VALr + (tile - 1) * pl.P1;
+        const uint32_t *prev = VALr + ((int64_t)tile - 1) * pl.P1;   // tile 0: never read
         for (uint32_t s0 = lane; s0 < P1; s0 += 256) {
             uint32_t v[4];
 #pragma unroll
@@ -517,33 +536,35 @@ __global__ __launch_bounds__(64) void k_v2_emit_x(Geometry g, V2Plan pl,
 #pragma unroll
             for (int u = 0; u < 4; u++) {
                 const uint32_t s = s0 + 64 * u;
-                if (s < P1) buf[s] = v[u] != kNone ? v[u] : slot_value_after(VALr, pl.P1, tile - 2, s);
+                if (s < P1) buf[s] = v[u] != kNone ? v[u] : slot_value_after(VALr, pl.P1, (int64_t)tile - 2, s);
             }
         }
     }
-    stage_round_keys(g, rank, w_lo, nwin, rk);
-    const SlotKey sk = slot_key(g, rank);
+    stage_keys_t(g, rank, w_lo, nwin, rk, kt, rl);
+    const SlotKey sk = slot_key_t(g, rank, kt, rl);
     __syncthreads();
     // tile-local step tl = t - tlo (tlo is a multiple of 256); the tile emits tl in [e_lo, e_hi)
     const int64_t pos_hi = pos_lo + count;
-    const uint32_t nvalid = (uint32_t)(thi - tlo);
+    const uint32_t nvalid = thi - tlo;
     const uint32_t e_lo = (uint32_t)(pos_lo > tlo ? (pos_lo - tlo < nvalid ? pos_lo - tlo : nvalid) : 0);
     const uint32_t e_hi = (uint32_t)(pos_hi < thi ? (pos_hi > tlo ? pos_hi - tlo : 0) : nvalid);
-    int64_t *o = out + (int64_t)rl * count + (tlo - pos_lo);
-    const uint32_t twoB = (uint32_t)(2 * g.B < g.ns ? 2 * g.B : g.ns);
+    int64_t *o = out + (int64_t)rl * count + ((int64_t)tlo - pos_lo);
+    const uint32_t twoB = pl.twoB;
     const uint32_t old32 = (uint32_t)rd.old_start, new32 = (uint32_t)rd.new_start;
     const uint32_t N32 = (uint32_t)g.N;
-    const uint32_t B = (uint32_t)g.B;
-    const uint32_t hB = feistel_half_bits(B);
-    const bool walk_full = B != (1u << (2 * hB));           // full windows need cycle walking
-    const uint32_t w_last = (uint32_t)(1 + (pl.T - 1) / g.B);  // last pool2 window (may be short)
-    const uint32_t len_last = (uint32_t)(g.ns - (int64_t)w_last * g.B);
-    const uint32_t h_last = feistel_half_bits(len_last);
-    const uint32_t wl = (uint32_t)w_lo;
-    const uint32_t t0 = (uint32_t)tlo;
+    const uint32_t hB = pl.hB;
+    const bool walk_full = pl.walk_full;                     // full windows need cycle walking
+    const uint32_t w_last = pl.w_last;                       // last pool2 window (may be short)
+    const uint32_t len_last = pl.len_last, h_last = pl.h_last;
+    const uint32_t wl = w_lo;
+    const uint32_t t0 = tlo;
+    const uint32_t sh = 32u - (uint32_t)ceil_log2_u64((uint64_t)P1);   // POW2 only
+#ifdef PSS_STAMPS
+    const uint64_t st_clk = __builtin_amdgcn_s_memtime(), st_rt = __builtin_amdgcn_s_memrealtime();
+#endif
     // pool2 position (w0, p0) of the super-batch's first step, advanced without division
-    uint32_t w0 = (uint32_t)(1 + tlo / g.B);
-    uint32_t p0 = (uint32_t)(tlo - (int64_t)(w0 - 1) * g.B);
+    uint32_t w0 = w_lo;
+    uint32_t p0 = tlo - (w0 - 1) * B;
     // fast super-batches: every step valid and emitted, B >= 256 (at most one window boundary
     // per super-batch), neither window short nor cycle-walking
     const bool fast_tile = e_lo == 0 && e_hi == nvalid && B >= 256 && !walk_full;
@@ -564,13 +585,13 @@ __global__ __launch_bounds__(64) void k_v2_emit_x(Geometry g, V2Plan pl,
                 // the whole super-batch inserts from window w0: scalar round keys
 #pragma unroll
                 for (int j = 0; j < 4; j++) {
-                    k[j] = scale32(slot_hash(t0 + tl0 + 64u * j + lane, sk.s0, sk.s1), P1);
+                    k[j] = slot_scale<POW2>(slot_hash(t0 + tl0 + 64u * j + lane, sk.s0, sk.s1), P1, sh);
                     ins[j] = w0 * B + feistel_once(p0 + 64u * j + lane, hB, kw);
                 }
             } else {
 #pragma unroll
                 for (int j = 0; j < 4; j++) {
-                    k[j] = scale32(slot_hash(t0 + tl0 + 64u * j + lane, sk.s0, sk.s1), P1);
+                    k[j] = slot_scale<POW2>(slot_hash(t0 + tl0 + 64u * j + lane, sk.s0, sk.s1), P1, sh);
                     uint32_t p = p0 + 64u * j + lane;
                     const bool cross = p >= B;
                     p = cross ? p - B : p;
@@ -588,7 +609,7 @@ __global__ __launch_bounds__(64) void k_v2_emit_x(Geometry g, V2Plan pl,
             for (int j = 0; j < 4; j++) {
                 const uint32_t tl = tl0 + 64u * j + lane;
                 if (tl < nvalid) {
-                    const uint32_t kk = scale32(slot_hash(t0 + tl, sk.s0, sk.s1), P1);
+                    const uint32_t kk = slot_scale<POW2>(slot_hash(t0 + tl, sk.s0, sk.s1), P1, sh);
                     uint32_t p = p0 + 64u * j + lane, w = w0;
                     while (p >= B) { p -= B; w++; }
                     const bool lastw = w == w_last;
@@ -602,12 +623,18 @@ __global__ __launch_bounds__(64) void k_v2_emit_x(Geometry g, V2Plan pl,
         p0 += 256;
         while (p0 >= B) { p0 -= B; w0++; }
     }
-    if (do_tail && tile == pl.G - 1) {
+#ifdef PSS_STAMPS
+    if (lane == 0 && blockIdx.x < (1u << 16)) {
+        pss_stamps[blockIdx.x][0] = __builtin_amdgcn_s_memtime() - st_clk;
+        pss_stamps[blockIdx.x][1] = __builtin_amdgcn_s_memrealtime() - st_rt;
+    }
+#endif
+    if (do_tail && (int64_t)tile == pl.G - 1) {
         // the rank's final pool is this wave's slot table: drain it in tail order (positions
         // T + j, j < P1).  One wave: its own LDS exchanges above are complete in order.
         __syncthreads();
         uint32_t tk[kRoundKeyWords];
-        tail_round_keys(g, rank, tk);
+        tail_keys_t(g, rank, kt, rl, tk);
         const uint32_t hT = feistel_half_bits(P1);
         int64_t *ot = out + (int64_t)rl * count - pos_lo + pl.T;
         for (uint32_t j = lane; j < P1; j += 64) {
@@ -865,13 +892,13 @@ __global__ __launch_bounds__(256) void k_v2_tail_f(Geometry g, V2Plan pl,
                                                   const RankDesc *__restrict__ ranks,
                                                   int32_t rank_lo, const uint32_t *__restrict__ VAL,
                                                   int64_t pos_lo, int64_t count,
-                                                  int64_t *__restrict__ out) {
+                                                  int64_t *__restrict__ out, KeyTab kt) {
     const int32_t rl = (int32_t)blockIdx.y;
     const uint32_t rank = (uint32_t)(rank_lo + rl);
     const RankDesc rd = ranks[rank];
     const uint32_t P1 = (uint32_t)pl.P1;
     uint32_t tk[kRoundKeyWords];
-    tail_round_keys(g, rank, tk);
+    tail_keys_t(g, rank, kt, rl, tk);
     const uint32_t hT = feistel_half_bits(P1);
     const uint32_t *VALr = VAL + (int64_t)rl * pl.G * pl.P1;
     int64_t *o = out + (int64_t)rl * count - pos_lo;
@@ -925,6 +952,11 @@ V2Plan v2_plan(const Geometry &g, int32_t nr) {
     if (wpc >= 4) wpc &= ~3;
     p.emit_lds = lds;
     if (wpc >= 1 && kCuLdsBytes / (wpc + 1) >= lds) p.emit_lds = kCuLdsBytes / (wpc + 1) + 16;
+    static const int64_t lds_env = [] {   // experiment knob: explicit emit LDS bytes per wave
+        const char *e = getenv("PSS_V2_EMIT_LDS");
+        return (int64_t)(e ? atol(e) : 0);
+    }();
+    if (lds_env > lds) p.emit_lds = lds_env;
     int64_t L;
     if (mult_env) {
         L = mult_env * p.P1;
@@ -940,12 +972,30 @@ V2Plan v2_plan(const Geometry &g, int32_t nr) {
     }
     p.L = cdiv(L, 256) * 256;
     p.G = p.T > 0 ? cdiv(p.T, p.L) : 0;
+    p.B32 = (uint32_t)g.B;
+    p.L32 = (uint32_t)p.L;
+    p.T32 = (uint32_t)p.T;
+    p.hB = feistel_half_bits(p.B32);
+    p.walk_full = p.B32 != (1u << (2 * p.hB));
+    p.w_last = p.T > 0 ? (uint32_t)(1 + (p.T - 1) / g.B) : 0;
+    p.len_last = p.T > 0 ? (uint32_t)(g.ns - (int64_t)p.w_last * g.B) : 0;
+    p.h_last = feistel_half_bits(p.len_last > 0 ? p.len_last : 1);
+    p.twoB = (uint32_t)(2 * g.B < g.ns ? 2 * g.B : g.ns);
     return p;
+}
+
+// key table: pool2 windows 1..W of every rank + slot and tail keys; none when it would be big
+static int64_t keytab_windows(const V2Plan &pl, const Geometry &g) {
+    return pl.T > 0 ? 1 + (pl.T - 1) / g.B : 0;
+}
+static size_t keytab_words(const V2Plan &pl, const Geometry &g, int32_t nr) {
+    const size_t w = (size_t)nr * (size_t)(16 + kRoundKeyWords * keytab_windows(pl, g));
+    return w <= ((size_t)64 << 20) ? w : 0;     // <= 256 MB
 }
 
 size_t v2_val_bytes(const Geometry &g, int32_t nr) {
     const V2Plan p = v2_plan(g, nr);
-    return (size_t)nr * (size_t)p.G * (size_t)p.P1 * sizeof(uint32_t);
+    return ((size_t)nr * (size_t)p.G * (size_t)p.P1 + keytab_words(p, g, nr)) * sizeof(uint32_t);
 }
 
 size_t v2_buf_bytes(const Geometry &g, int32_t nr) {
@@ -963,18 +1013,28 @@ size_t v2_sort_bytes(const Geometry &, int32_t) {
 
 hipError_t launch_v2_tail_vals(const Geometry &g, const V2Plan &pl, const RankDesc *ranks,
                                int32_t rank_lo, int32_t nr, const uint32_t *VAL, int64_t pos_lo,
-                               int64_t count, int64_t *out, hipStream_t s) {
+                               int64_t count, int64_t *out, hipStream_t s, KeyTab kt) {
     const dim3 grid((uint32_t)cdiv(pl.P1 < 65536 ? pl.P1 : 65536, 256), (uint32_t)nr);
     hipLaunchKernelGGL(k_v2_tail_f, grid, dim3(256), 0, s, g, pl, ranks, rank_lo, VAL, pos_lo,
-                       count, out);
+                       count, out, kt);
     return hipGetLastError();
 }
 
 hipError_t launch_v2(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, int32_t nr,
                      int64_t pos_lo, int64_t count, int64_t *out, uint32_t *VAL, uint32_t *gbuf,
                      uint32_t *sort_ws, int32_t *err, hipStream_t s, const Marker &mk,
-                     int emit_path) {
+                     int emit_path, int stage) {
     if (emit_path == EMIT_AUTO) emit_path = lds_xchg_ordered() ? EMIT_XCHG : EMIT_PROBE;
+    // stage: V2_STAGE_ALL, or the split the runtime pipelines over two streams --
+    // V2_STAGE_PRE (key table + last-occurrence pass, writes VAL) then V2_STAGE_EMIT (replay +
+    // tail, reads VAL).  Only the LDS exchange path splits; everything else runs whole in the
+    // PRE call and the EMIT call is a no-op.
+    const bool splittable = emit_path == EMIT_XCHG && !v2_big_applicable(g) && !v2_plan(g, nr).global_buf;
+    if (!splittable) {
+        if (stage == V2_STAGE_EMIT) return hipSuccess;
+        stage = V2_STAGE_ALL;
+    }
+    const bool do_pre = stage != V2_STAGE_EMIT, do_emit = stage != V2_STAGE_PRE;
     if (emit_path == EMIT_XCHG && v2_big_applicable(g))   // pools beyond LDS: chunked replay
         return launch_v2_big(g, ranks, rank_lo, nr, pos_lo, count, out, gbuf, s, mk);
     const V2Plan pl = v2_plan(g, nr);
@@ -984,12 +1044,22 @@ hipError_t launch_v2(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, 
     const size_t lds_keys = (size_t)kRoundKeyWords * nwin_max * sizeof(uint32_t);
     const bool need_tail = pos_hi > pl.T;
     bool tail_fused = false;   // drained by the last tile's k_v2_emit_x wave
+    KeyTab kt{nullptr, 0};
+    if (keytab_words(pl, g, nr)) {   // keys of every window once, after the VAL tables
+        uint32_t *ktp = VAL + (size_t)nr * (size_t)pl.G * (size_t)pl.P1;
+        kt.p = ktp;
+        kt.stride = 16 + kRoundKeyWords * keytab_windows(pl, g);
+        const int64_t items = keytab_windows(pl, g) + 2;
+        if (do_pre)
+            hipLaunchKernelGGL(k_v2_keys, dim3((uint32_t)cdiv(items, 256), (uint32_t)nr), dim3(256), 0, s,
+                               g, rank_lo, keytab_windows(pl, g), kt.stride, ktp);
+    }
     if (pl.G > 0) {
         // pass A over every tile up to the last one emitted (the tail needs all of them);
         // VAL is indexed (rl*G + tile), tile < g_need
         const int64_t last_emit = pos_lo < pl.T ? ((pos_hi < pl.T ? pos_hi : pl.T) - 1) / pl.L : -1;
         const int64_t g_need = need_tail ? pl.G : last_emit + 1;
-        if (g_need > 0) {
+        if (g_need > 0 && do_pre) {
             mk(K_V2_LASTOCC, s);
             if (!pl.global_buf) {
                 static const int lo_mode = [] {   // A/B knob: "ordered" = one-wave plain-store kernel
@@ -1001,20 +1071,17 @@ hipError_t launch_v2(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, 
                     const char *e = getenv("PSS_V2_LASTOCC_NT");
                     return e ? atoi(e) : 256;
                 }();
-                if (lds_write_ordered() && lo_mode)
-                    hipLaunchKernelGGL((k_v2_lastocc<64, true>), dim3((uint32_t)(nr * g_need)), dim3(64),
-                                       lds, s, g, pl, rank_lo, g_need, VAL);
-                else if (lo_nt == 1024)
-                    hipLaunchKernelGGL((k_v2_lastocc<1024, false>), dim3((uint32_t)(nr * g_need)), dim3(1024),
-                                       lds, s, g, pl, rank_lo, g_need, VAL);
-                else if (lo_nt == 512)
-                    hipLaunchKernelGGL((k_v2_lastocc<512, false>), dim3((uint32_t)(nr * g_need)), dim3(512),
-                                       lds, s, g, pl, rank_lo, g_need, VAL);
-                else
-                    hipLaunchKernelGGL((k_v2_lastocc<256, false>), dim3((uint32_t)(nr * g_need)), dim3(256),
-                                       lds, s, g, pl, rank_lo, g_need, VAL);
+                const bool pow2 = (pl.P1 & (pl.P1 - 1)) == 0;
+                const dim3 grid((uint32_t)(nr * g_need));
+#define PSS_LO(NT, ORD) do { if (pow2) hipLaunchKernelGGL((k_v2_lastocc<NT, ORD, true>), grid, dim3(NT), lds, s, g, pl, rank_lo, g_need, VAL, kt); \
+                             else hipLaunchKernelGGL((k_v2_lastocc<NT, ORD, false>), grid, dim3(NT), lds, s, g, pl, rank_lo, g_need, VAL, kt); } while (0)
+                if (lds_write_ordered() && lo_mode) PSS_LO(64, true);
+                else if (lo_nt == 1024) PSS_LO(1024, false);
+                else if (lo_nt == 512) PSS_LO(512, false);
+                else PSS_LO(256, false);
+#undef PSS_LO
             } else {
-                hipError_t e = hipMemsetAsync(VAL, 0, v2_val_bytes(g, nr), s);
+                hipError_t e = hipMemsetAsync(VAL, 0, (size_t)nr * (size_t)pl.G * (size_t)pl.P1 * sizeof(uint32_t), s);
                 if (e != hipSuccess) return e;
                 hipLaunchKernelGGL(k_v2_lastocc_g, dim3((uint32_t)cdiv(pl.L, kLastoccChunk), (uint32_t)(nr * g_need)),
                                    dim3(256), 0, s, g, pl, rank_lo, g_need, VAL);
@@ -1022,7 +1089,8 @@ hipError_t launch_v2(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, 
                                    dim3(256), 0, s, g, pl, rank_lo, g_need, VAL);
             }
         }
-        if (last_emit >= 0) {
+        if (do_pre && !do_emit) mk(-1, s);
+        if (last_emit >= 0 && do_emit) {
             const int64_t g_lo = pos_lo / pl.L;
             const int64_t ng = last_emit - g_lo + 1;
             // 32-bit id arithmetic whenever every id (and id + ns before the wrap) fits
@@ -1051,12 +1119,14 @@ hipError_t launch_v2(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, 
                 const size_t lds = need > (size_t)pl.emit_lds ? need : (size_t)pl.emit_lds;
                 tail_fused = need_tail && last_emit == pl.G - 1;
                 const int dt = tail_fused ? 1 : 0;
-                if (narrow)
-                    hipLaunchKernelGGL((k_v2_emit_x<true>), grid, dim3(64), lds, s, g, pl, ranks, rank_lo,
-                                       g_lo, ng, (const uint32_t *)VAL, pos_lo, count, dt, out);
-                else
-                    hipLaunchKernelGGL((k_v2_emit_x<false>), grid, dim3(64), lds, s, g, pl, ranks, rank_lo,
-                                       g_lo, ng, (const uint32_t *)VAL, pos_lo, count, dt, out);
+                const bool pow2 = (pl.P1 & (pl.P1 - 1)) == 0;
+#define PSS_EX(N, P2) hipLaunchKernelGGL((k_v2_emit_x<N, P2>), grid, dim3(64), lds, s, g, pl, ranks, rank_lo, \
+                                         g_lo, ng, (const uint32_t *)VAL, pos_lo, count, dt, out, kt)
+                if (narrow && pow2) PSS_EX(true, true);
+                else if (narrow) PSS_EX(true, false);
+                else if (pow2) PSS_EX(false, true);
+                else PSS_EX(false, false);
+#undef PSS_EX
             } else if (!pl.global_buf) {   // probe path (EMIT_PROBE)
                 mk(K_V2_EMIT, s);
                 const size_t need = lds_keys + (size_t)pl.P1 * 4 + (pl.fold ? 0 : kMarkBytes);
@@ -1082,9 +1152,10 @@ hipError_t launch_v2(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, 
             }
         }
     }
+    if (!do_emit) return hipGetLastError();
     if (need_tail && !tail_fused) {
         mk(K_V2_TAIL, s);
-        hipError_t e = launch_v2_tail_vals(g, pl, ranks, rank_lo, nr, VAL, pos_lo, count, out, s);
+        hipError_t e = launch_v2_tail_vals(g, pl, ranks, rank_lo, nr, VAL, pos_lo, count, out, s, kt);
         if (e != hipSuccess) return e;
     }
     mk(-1, s);
@@ -1146,12 +1217,18 @@ hipError_t init_kernel_attributes_v2() {
     hipError_t e = check_lds_xchg_order();
     if (e == hipSuccess) e = init_kernel_attributes_v2big();
 #define PSS_ATTR(fn) { hipError_t x = hipFuncSetAttribute((const void *)(fn), hipFuncAttributeMaxDynamicSharedMemorySize, big); if (x != hipSuccess) e = x; }
-    PSS_ATTR((k_v2_lastocc<64, true>));
-    PSS_ATTR((k_v2_lastocc<256, false>));
-    PSS_ATTR((k_v2_lastocc<512, false>));
-    PSS_ATTR((k_v2_lastocc<1024, false>));
-    PSS_ATTR((k_v2_emit_x<true>));
-    PSS_ATTR((k_v2_emit_x<false>));
+    PSS_ATTR((k_v2_lastocc<64, true, true>));
+    PSS_ATTR((k_v2_lastocc<64, true, false>));
+    PSS_ATTR((k_v2_lastocc<256, false, true>));
+    PSS_ATTR((k_v2_lastocc<256, false, false>));
+    PSS_ATTR((k_v2_lastocc<512, false, true>));
+    PSS_ATTR((k_v2_lastocc<512, false, false>));
+    PSS_ATTR((k_v2_lastocc<1024, false, true>));
+    PSS_ATTR((k_v2_lastocc<1024, false, false>));
+    PSS_ATTR((k_v2_emit_x<true, true>));
+    PSS_ATTR((k_v2_emit_x<true, false>));
+    PSS_ATTR((k_v2_emit_x<false, true>));
+    PSS_ATTR((k_v2_emit_x<false, false>));
     PSS_ATTR((k_v2_emit_sst<true>));
     PSS_ATTR((k_v2_emit_sst<false>));
     PSS_ATTR((k_v2_emit<false, true, false>));

@@ -388,7 +388,7 @@ hipError_t launch_v2_big(const Geometry &g, const RankDesc *ranks, int32_t rank_
         mk(K_V2_TAIL, s);
         V2Plan vp{};
         vp.P1 = p.P1; vp.T = p.T; vp.L = p.L; vp.G = p.G; vp.global_buf = 1;
-        hipError_t e = launch_v2_tail_vals(g, vp, ranks, rank_lo, nr, w.val, pos_lo, count, out, s);
+        hipError_t e = launch_v2_tail_vals(g, vp, ranks, rank_lo, nr, w.val, pos_lo, count, out, s, KeyTab{nullptr, 0});
         if (e != hipSuccess) return e;
     }
     mk(-1, s);
