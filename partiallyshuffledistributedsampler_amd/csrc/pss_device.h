@@ -78,7 +78,7 @@ __device__ __forceinline__ int64_t wrap_id(int64_t id, int64_t N) { return id >=
 __device__ __forceinline__ int bpad(int b) { return b + (b >> 4); }
 __host__ __device__ constexpr int bpad_size(int nb) { return nb + nb / 16 + 1; }
 
-template <int EPT>
+template <int EPT, int NT = 256>
 __device__ __forceinline__ int block_sort_keys(uint32_t k0, uint32_t k1, uint32_t c1,
                                                uint32_t rank, uint32_t dom, int n,
                                                uint32_t *S, uint32_t *hist, uint32_t *tot) {
@@ -89,35 +89,35 @@ __device__ __forceinline__ int block_sort_keys(uint32_t k0, uint32_t k1, uint32_
     uint32_t key[NQ][4];
 #pragma unroll
     for (int j = 0; j < NQ; j++) {
-        uint32_t c0 = (uint32_t)(tid + 256 * j), cc1 = c1, c2 = rank, c3 = dom;
+        uint32_t c0 = (uint32_t)(tid + NT * j), cc1 = c1, c2 = rank, c3 = dom;
         philox4x32_10(c0, cc1, c2, c3, k0, k1);
         key[j][0] = c0; key[j][1] = cc1; key[j][2] = c2; key[j][3] = c3;
     }
-    for (int i = tid; i < bpad_size(nb); i += 256) hist[i] = 0;
+    for (int i = tid; i < bpad_size(nb); i += NT) hist[i] = 0;
     __syncthreads();
     const int sh = 32 - hb;
 #pragma unroll
     for (int j = 0; j < NQ; j++)
 #pragma unroll
         for (int w = 0; w < 4; w++) {
-            const int i = 4 * (tid + 256 * j) + w;
+            const int i = 4 * (tid + NT * j) + w;
             if (i < n) atomicAdd(&hist[bpad(hb ? key[j][w] >> sh : 0)], 1u);
         }
     __syncthreads();
-    const int per = nb >= 256 ? nb / 256 : 1;
+    const int per = nb >= NT ? nb / NT : 1;
     const int blo = tid * per < nb ? tid * per : nb;
     const int bhi = blo + per < nb ? blo + per : nb;
     uint32_t s = 0;
     for (int b = blo; b < bhi; b++) s += hist[bpad(b)];
     uint32_t total;
-    uint32_t run = block_excl_scan<256>(s, tot, total);
+    uint32_t run = block_excl_scan<NT>(s, tot, total);
     for (int b = blo; b < bhi; b++) { const uint32_t c = hist[bpad(b)]; hist[bpad(b)] = run; run += c; }
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < NQ; j++)
 #pragma unroll
         for (int w = 0; w < 4; w++) {
-            const int i = 4 * (tid + 256 * j) + w;
+            const int i = 4 * (tid + NT * j) + w;
             if (i < n) {
                 const uint32_t k = key[j][w];
                 const uint32_t pos = atomicAdd(&hist[bpad(hb ? k >> sh : 0)], 1u);
@@ -125,7 +125,7 @@ __device__ __forceinline__ int block_sort_keys(uint32_t k0, uint32_t k1, uint32_
             }
         }
     __syncthreads();
-    for (int b = tid; b < nb; b += 256) {  // hist[b] is now the END of bucket b
+    for (int b = tid; b < nb; b += NT) {  // hist[b] is now the END of bucket b
         const int e = (int)hist[bpad(b)];
         const int st = b ? (int)hist[bpad(b - 1)] : 0;
         for (int x = st + 1; x < e; x++) {
@@ -139,9 +139,9 @@ __device__ __forceinline__ int block_sort_keys(uint32_t k0, uint32_t k1, uint32_
     return hb;
 }
 
-template <int EPT>
+template <int EPT, int NT = 256>
 constexpr size_t sort_lds_bytes() {
-    return (size_t)(256 * EPT + bpad_size(256 * EPT) + 16) * sizeof(uint32_t);
+    return (size_t)(NT * EPT + bpad_size(NT * EPT) + 16) * sizeof(uint32_t);
 }
 
 // ------------------------------------------------------------------------------------------

@@ -226,13 +226,13 @@ __global__ void k_debug_wave_scan(const uint64_t *in, uint64_t *out, int64_t n) 
 // ------------------------------------------------------------------------------------------
 // V1 (V1:157-172): window w of rank r -> ids start + w*B + perm_w[p], wrap at N
 // ------------------------------------------------------------------------------------------
-template <int EPT>
-__global__ __launch_bounds__(256) void k_v1_lds(Geometry g, const RankDesc *__restrict__ ranks,
+template <int EPT, int NT>
+__global__ __launch_bounds__(NT) void k_v1_lds(Geometry g, const RankDesc *__restrict__ ranks,
                                                int32_t rank_lo, int64_t w_lo, int64_t nw,
                                                int64_t pos_lo, int64_t count,
                                                int64_t *__restrict__ out) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-    uint32_t *S = smem, *hist = smem + 256 * EPT, *tot = hist + bpad_size(256 * EPT);
+    uint32_t *S = smem, *hist = smem + NT * EPT, *tot = hist + bpad_size(NT * EPT);
     const int32_t rl = (int32_t)(blockIdx.x / nw);
     const int64_t w = w_lo + (int64_t)(blockIdx.x % nw);
     const int32_t rank = rank_lo + rl;
@@ -240,13 +240,13 @@ __global__ __launch_bounds__(256) void k_v1_lds(Geometry g, const RankDesc *__re
     const int64_t n = g.ns - wb < g.B ? g.ns - wb : g.B;
     const int64_t base = ranks[rank].new_start + wb;
     int hb = 0;
-    if (g.shuffle) hb = block_sort_keys<EPT>(g.key0, g.key1, (uint32_t)w, (uint32_t)rank, DOM_V1_WIN, (int)n, S, hist, tot);
+    if (g.shuffle) hb = block_sort_keys<EPT, NT>(g.key0, g.key1, (uint32_t)w, (uint32_t)rank, DOM_V1_WIN, (int)n, S, hist, tot);
     const uint32_t mask = (1u << hb) - 1u;
     int64_t *o = out + (int64_t)rl * count - pos_lo;
     int64_t p0 = 0, p1 = n;
     if (wb < pos_lo) p0 = pos_lo - wb;
     if (wb + n > pos_lo + count) p1 = pos_lo + count - wb;
-    for (int64_t p = p0 + threadIdx.x; p < p1; p += 256) {
+    for (int64_t p = p0 + threadIdx.x; p < p1; p += NT) {
         const uint32_t idx = g.shuffle ? (S[p] & mask) : (uint32_t)p;
         o[wb + p] = wrap_id(base + idx, g.N);
     }
@@ -350,12 +350,12 @@ hipError_t launch_debug_wave_scan(const uint64_t *in, uint64_t *out, int64_t n, 
     return hipGetLastError();
 }
 
-template <int EPT>
+template <int EPT, int NT = 256>
 static void launch_v1_ept(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, int32_t nr,
                           int64_t w_lo, int64_t nw, int64_t pos_lo, int64_t count, int64_t *out,
                           hipStream_t s) {
-    hipLaunchKernelGGL(k_v1_lds<EPT>, dim3((uint32_t)(nr * nw)), dim3(256),
-                       g.shuffle ? sort_lds_bytes<EPT>() : 16, s,
+    const size_t lds = g.shuffle ? sort_lds_bytes<EPT, NT>() : 16;
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_v1_lds<EPT, NT>), dim3((uint32_t)(nr * nw)), dim3(NT), lds, s,
                        g, ranks, rank_lo, w_lo, nw, pos_lo, count, out);
 }
 
@@ -392,8 +392,15 @@ hipError_t launch_v1(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, 
     if (nr <= 0 || !v1_window_range(g, pos_lo, count, w_lo, nw)) return hipSuccess;
     const int64_t nmax = g.B < g.ns ? g.B : g.ns;
     mk(K_V1, s);
+    static const int v1_nt = [] {   // experiment knob: threads per window workgroup
+        const char *e = getenv("PSS_V1_NT");   // 512 measured fastest at B = 4096 (C2 V1: 0.39 ms
+        return e ? atoi(e) : 512;              // vs 0.51 ms at 256 and 1024 threads)
+    }();
     if (!g.shuffle || nmax <= 1024) launch_v1_ept<4>(g, ranks, rank_lo, nr, w_lo, nw, pos_lo, count, out, s);
+    else if (nmax <= 4096 && v1_nt == 1024) launch_v1_ept<4, 1024>(g, ranks, rank_lo, nr, w_lo, nw, pos_lo, count, out, s);
+    else if (nmax <= 4096 && v1_nt == 512) launch_v1_ept<8, 512>(g, ranks, rank_lo, nr, w_lo, nw, pos_lo, count, out, s);
     else if (nmax <= 4096) launch_v1_ept<16>(g, ranks, rank_lo, nr, w_lo, nw, pos_lo, count, out, s);
+    else if (nmax <= 8192 && v1_nt == 512) launch_v1_ept<16, 512>(g, ranks, rank_lo, nr, w_lo, nw, pos_lo, count, out, s);
     else if (nmax <= 8192) launch_v1_ept<32>(g, ranks, rank_lo, nr, w_lo, nw, pos_lo, count, out, s);
     else if (nmax <= kLdsSortMax) launch_v1_ept<64>(g, ranks, rank_lo, nr, w_lo, nw, pos_lo, count, out, s);
     else {
@@ -418,8 +425,9 @@ hipError_t init_kernel_attributes() {
     const int big = 160 * 1024;
     hipError_t e = hipSuccess;
 #define PSS_ATTR(fn) { hipError_t x = hipFuncSetAttribute((const void *)(fn), hipFuncAttributeMaxDynamicSharedMemorySize, big); if (x != hipSuccess) e = x; }
-    PSS_ATTR(k_v1_lds<32>);
-    PSS_ATTR(k_v1_lds<64>);
+    PSS_ATTR((k_v1_lds<32, 256>));
+    PSS_ATTR((k_v1_lds<64, 256>));
+    PSS_ATTR((k_v1_lds<16, 512>));
 #undef PSS_ATTR
     hipError_t e2 = init_kernel_attributes_v2();
     hipError_t e3 = init_kernel_attributes_bigsort();
