@@ -359,7 +359,19 @@ static inline uint32_t orc_slot_hash(uint32_t t, uint32_t s0, uint32_t s1) {
     return x;
 }
 
+/* P1 = 2^b, b <= 16: steps t and t + 64 of each 128-step block share the hash of index
+ * (t >> 7) * 64 + (t & 63); step t takes the top b bits of the high half-word, t + 64 those of
+ * the low half-word.  Other P1: one hash per step, multiply-shift scaled. */
 static inline uint32_t v2_slot(const uint32_t sk[4], int64_t t, uint32_t P1) {
+    if (P1 <= 65536u && (P1 & (P1 - 1u)) == 0u) {
+        if (P1 == 1u) return 0u;
+        int b = 0;
+        while ((1u << b) < P1) b++;
+        uint32_t tt = (uint32_t)t;
+        uint32_t u = orc_slot_hash(((tt >> 7) << 6) | (tt & 63u), sk[0], sk[1]);
+        if (tt & 64u) u <<= 16;
+        return u >> (32 - b);
+    }
     uint32_t u = orc_slot_hash((uint32_t)t, sk[0], sk[1]);
     return (uint32_t)(((uint64_t)u * P1) >> 32);
 }

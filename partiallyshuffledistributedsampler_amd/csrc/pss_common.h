@@ -121,4 +121,22 @@ PSS_HD uint32_t scale32(uint32_t u, uint32_t n) {
     return (uint32_t)(((uint64_t)u * n) >> 32);
 }
 
+// Slot drawn at V2 step t.  P1 = 2^b with b <= 16 ("paired"): one hash serves two steps -- t
+// and t + 64 of each 128-step block, the top b bits of its high and of its low half-word (both
+// exactly uniform).  Otherwise every step hashes its own index and scales it to [0, P1).
+PSS_HD bool slot_paired(uint32_t P1) { return P1 <= 65536u && (P1 & (P1 - 1u)) == 0u; }
+
+PSS_HD uint32_t slot_pair_index(uint32_t t) { return ((t >> 7) << 6) | (t & 63u); }
+
+PSS_HD uint32_t slot_draw(uint32_t t, uint32_t s0, uint32_t s1, uint32_t P1) {
+    if (slot_paired(P1)) {
+        if (P1 == 1u) return 0u;
+        const uint32_t sh = 32u - (uint32_t)ceil_log2_u64(P1);
+        uint32_t u = slot_hash(slot_pair_index(t), s0, s1);
+        if (t & 64u) u <<= 16;
+        return u >> sh;
+    }
+    return scale32(slot_hash(t, s0, s1), P1);
+}
+
 }  // namespace pss

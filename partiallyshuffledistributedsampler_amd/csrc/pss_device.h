@@ -157,10 +157,12 @@ __device__ __forceinline__ SlotKey slot_key(const Geometry &g, uint32_t rank) {
     return SlotKey{c0, c1};
 }
 
-__device__ __forceinline__ void slot_words(const SlotKey &sk, int64_t sb, int lane, uint32_t u[4]) {
+// slots of the 4 steps sb*256 + 64 j + lane (j < 4) of super-batch sb
+__device__ __forceinline__ void slot_ks(const SlotKey &sk, int64_t sb, int lane, uint32_t P1,
+                                        uint32_t k[4]) {
     const uint32_t t0 = (uint32_t)sb * 256u + (uint32_t)lane;
 #pragma unroll
-    for (int j = 0; j < 4; j++) u[j] = slot_hash(t0 + 64u * j, sk.s0, sk.s1);
+    for (int j = 0; j < 4; j++) k[j] = slot_draw(t0 + 64u * j, sk.s0, sk.s1, P1);
 }
 
 // slot of a 32-bit draw: Lemire multiply-shift, or a plain shift when P1 is a power of two
@@ -168,6 +170,24 @@ __device__ __forceinline__ void slot_words(const SlotKey &sk, int64_t sb, int la
 template <bool POW2>
 __device__ __forceinline__ uint32_t slot_scale(uint32_t u, uint32_t P1, uint32_t sh) {
     return POW2 ? (u >> sh) : scale32(u, P1);
+}
+
+// slots of steps t, t + 64, t + 128, t + 192 (t = a lane's step of a 256-aligned super-batch):
+// POW2 (P1 = 2^b <= 65536, paired draw) -- two hashes for the four steps
+template <bool POW2>
+__device__ __forceinline__ void slot4(uint32_t t, const SlotKey &sk, uint32_t P1, uint32_t sh,
+                                      uint32_t k[4]) {
+    if (POW2) {
+#pragma unroll
+        for (int j = 0; j < 4; j += 2) {
+            const uint32_t u = slot_hash(slot_pair_index(t + 64u * j), sk.s0, sk.s1);
+            k[j] = u >> sh;
+            k[j + 1] = (u << 16) >> sh;
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < 4; j++) k[j] = scale32(slot_hash(t + 64u * j, sk.s0, sk.s1), P1);
+    }
 }
 
 // Feistel round keys of pool2 window w: Philox blocks (w, 0, rank, INS) and (w, 1, rank, INS),

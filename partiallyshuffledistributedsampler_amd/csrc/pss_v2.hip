@@ -102,20 +102,36 @@ __global__ __launch_bounds__(NT) void k_v2_lastocc(Geometry g, V2Plan pl, int32_
     Pacer pace(nfull);
     for (uint32_t base = 0; base < nfull; base += BLK) {
         pace.step(base);
-        const uint32_t b = base + threadIdx.x;
-        uint32_t k[8];
-#pragma unroll
-        for (int j = 0; j < 8; j++) k[j] = slot_scale<POW2>(slot_hash(t0 + b + NT * j, sk.s0, sk.s1), (uint32_t)P1, sh);
+        // thread -> 8 steps: (t, t + 64) pairs of 4 different 128-step groups, so that with
+        // a paired draw (POW2) one hash serves two steps.  ORDERED (one wave) keeps step order:
+        // j-th store covers steps base + 64 j + lane.
+        uint32_t st[8], k[8];
 #pragma unroll
         for (int j = 0; j < 8; j++) {
-            if (ORDERED) lastT[k[j]] = b + NT * j + 1u;
-            else atomicMax(&lastT[k[j]], b + NT * j + 1u);
+            if (ORDERED) st[j] = base + 64u * j + threadIdx.x;
+            else st[j] = base + 128u * ((threadIdx.x >> 6) + (NT / 64) * (j >> 1)) + 64u * (j & 1) + (threadIdx.x & 63u);
+        }
+        if (POW2 && !ORDERED) {
+#pragma unroll
+            for (int j = 0; j < 8; j += 2) {
+                const uint32_t u = slot_hash(slot_pair_index(t0 + st[j]), sk.s0, sk.s1);
+                k[j] = u >> sh;
+                k[j + 1] = (u << 16) >> sh;
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < 8; j++) k[j] = slot_draw(t0 + st[j], sk.s0, sk.s1, (uint32_t)P1);
+        }
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            if (ORDERED) lastT[k[j]] = st[j] + 1u;
+            else atomicMax(&lastT[k[j]], st[j] + 1u);
         }
     }
     for (uint32_t base = nfull; base < n; base += NT) {
         const uint32_t b = base + threadIdx.x;
         if (b < n) {
-            const uint32_t kk = slot_scale<POW2>(slot_hash(t0 + b, sk.s0, sk.s1), (uint32_t)P1, sh);
+            const uint32_t kk = slot_draw(t0 + b, sk.s0, sk.s1, (uint32_t)P1);
             if (ORDERED) lastT[kk] = b + 1u;
             else atomicMax(&lastT[kk], b + 1u);
         }
@@ -196,11 +212,11 @@ __global__ __launch_bounds__(256) void k_v2_lastocc_g(Geometry g, V2Plan pl, int
         const int64_t sb = sb_lo + (ci >> 6);
         const int lane = (int)(ci & 63);
         uint32_t u[4];
-        slot_words(sk, sb, lane, u);
+        slot_ks(sk, sb, lane, (uint32_t)pl.P1, u);
 #pragma unroll
         for (int j = 0; j < 4; j++) {
             const int64_t t = sb * 256 + j * 64 + lane;
-            if (t >= clo && t < chi) atomicMax(&V[scale32(u[j], (uint32_t)pl.P1)], (uint32_t)(t - tlo + 1));
+            if (t >= clo && t < chi) atomicMax(&V[u[j]], (uint32_t)(t - tlo + 1));
         }
     }
 }
@@ -275,7 +291,7 @@ struct EmitCtx {   // per-tile constants of k_v2_emit + the running pool2 positi
         Step s;
         s.tl = tl;
         s.valid = FAST || (uint32_t)tl < nvalid;
-        s.k = scale32(uword, P1);
+        s.k = uword;   // the step's slot (slot_ks)
         // collision probe: a lane that reads back another lane's id shares its probe byte
         // (slot & 4095) with a lane of this sub-batch
         const uint32_t hk = probe_ix(s.k);
@@ -315,7 +331,7 @@ struct EmitCtx {   // per-tile constants of k_v2_emit + the running pool2 positi
         Step s;
         s.tl = tl;
         s.valid = true;
-        s.k = scale32(uword, P1);
+        s.k = uword;   // the step's slot (slot_ks)
         const uint32_t hk = probe_ix(s.k);
         mark[hk] = (uint8_t)lane;
         s.probe = mark[hk];
@@ -463,7 +479,7 @@ __global__ __launch_bounds__(64) void k_v2_emit(Geometry g, V2Plan pl,
     int32_t tl0 = (int32_t)(t_first - tlo);   // negative while the super-batch starts before the tile
     const SlotKey sk = slot_key(g, rank);
     uint32_t u[4];
-    slot_words(sk, sb_lo, lane, u);
+    slot_ks(sk, sb_lo, lane, c.P1, u);
     for (int64_t sb = sb_lo; sb <= sb_hi; sb++, tl0 += 256) {
         uint32_t un[4];   // next super-batch's slot words, computed under this one's work
         if (fast_tile && tl0 >= 0 && (uint32_t)tl0 + 256 <= c.nvalid && c.w0 + 1 < c.w_last) {
@@ -474,7 +490,7 @@ __global__ __launch_bounds__(64) void k_v2_emit(Geometry g, V2Plan pl,
             for (int j = 0; j < 4; j++) s[j] = c.probe4(u[j], tl0 + 64 * j + lane);
 #pragma unroll
             for (int j = 0; j < 4; j++) s[j].ins = c.ins4(j);
-            slot_words(sk, sb + 1, lane, un);
+            slot_ks(sk, sb + 1, lane, c.P1, un);
             c.advance256();
 #pragma unroll
             for (int j = 0; j < 4; j++) c.template finish<true, NARROW>(s[j]);
@@ -484,7 +500,7 @@ __global__ __launch_bounds__(64) void k_v2_emit(Geometry g, V2Plan pl,
                 const typename EmitCtx<FOLD>::Step s = c.template prep<false>(u[j], tl0 + j * 64 + lane);
                 c.template finish<false, NARROW>(s);
             }
-            slot_words(sk, sb + 1, lane, un);
+            slot_ks(sk, sb + 1, lane, c.P1, un);
         }
 #pragma unroll
         for (int j = 0; j < 4; j++) u[j] = un[j];
@@ -583,15 +599,13 @@ __global__ __launch_bounds__(64) void k_v2_emit_x(Geometry g, V2Plan pl,
             uint32_t k[4], ins[4], v[4];
             if (p0 + 256 <= B) {
                 // the whole super-batch inserts from window w0: scalar round keys
+                slot4<POW2>(t0 + tl0 + lane, sk, P1, sh, k);
 #pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    k[j] = slot_scale<POW2>(slot_hash(t0 + tl0 + 64u * j + lane, sk.s0, sk.s1), P1, sh);
-                    ins[j] = w0 * B + feistel_once(p0 + 64u * j + lane, hB, kw);
-                }
+                for (int j = 0; j < 4; j++) ins[j] = w0 * B + feistel_once(p0 + 64u * j + lane, hB, kw);
             } else {
+                slot4<POW2>(t0 + tl0 + lane, sk, P1, sh, k);
 #pragma unroll
                 for (int j = 0; j < 4; j++) {
-                    k[j] = slot_scale<POW2>(slot_hash(t0 + tl0 + 64u * j + lane, sk.s0, sk.s1), P1, sh);
                     uint32_t p = p0 + 64u * j + lane;
                     const bool cross = p >= B;
                     p = cross ? p - B : p;
@@ -609,7 +623,7 @@ __global__ __launch_bounds__(64) void k_v2_emit_x(Geometry g, V2Plan pl,
             for (int j = 0; j < 4; j++) {
                 const uint32_t tl = tl0 + 64u * j + lane;
                 if (tl < nvalid) {
-                    const uint32_t kk = slot_scale<POW2>(slot_hash(t0 + tl, sk.s0, sk.s1), P1, sh);
+                    const uint32_t kk = slot_draw(t0 + tl, sk.s0, sk.s1, P1);
                     uint32_t p = p0 + 64u * j + lane, w = w0;
                     while (p >= B) { p -= B; w++; }
                     const bool lastw = w == w_last;
@@ -700,189 +714,6 @@ __global__ __launch_bounds__(64) void k_xchg_order_check(int iters, uint32_t P, 
     if (nbad) atomicAdd(bad, nbad);
     if (nbadw) atomicAdd(bad + 2, nbadw);
     if (nbada) atomicAdd(bad + 4, nbada);
-}
-
-// ---- pass B, sorted sub-tiles ---------------------------------------------------------------
-// One 256-thread workgroup per tile; the tile is cut into sub-tiles of S <= 4096 steps
-// (S a multiple of 256, S <= P1).  Per sub-tile, in LDS:
-//   P1 histogram of the drawn slots, P2 exclusive scan, P3 scatter (slot << 16 | step) into
-//   slot buckets, P4 order each bucket by step + flag its first/last entry, P5 insertion value
-//   of every entry, P6 value emitted by each step = slot table (first entry of its bucket) or
-//   the previous entry's insertion, P7 last entries write the slot table back; coalesced ids.
-// Same result as k_v2_emit (the step order inside a slot is what the sequential replay sees).
-constexpr uint32_t kSstFirst = 1u << 31, kSstLast = 1u << 30, kSstPayload = kSstLast - 1;
-
-template <bool NARROW>
-__global__ __launch_bounds__(256) void k_v2_emit_sst(Geometry g, V2Plan pl,
-                                                    const RankDesc *__restrict__ ranks,
-                                                    int32_t rank_lo, int64_t g_lo, int64_t ng,
-                                                    const uint32_t *__restrict__ VAL,
-                                                    int64_t pos_lo, int64_t count,
-                                                    int64_t *__restrict__ out) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-    const int P1 = (int)pl.P1;                       // == B while steps exist
-    const int S = (P1 < 4096 ? P1 : 4096) & ~255;
-    uint32_t *buf = smem;                            // [P1] slot table
-    uint32_t *cnt = buf + P1;                        // [P1] counts -> starts -> ends; then val[S]
-    uint32_t *ord = cnt + bpad_size(P1);             // [S]  (slot << 16 | step) in bucket order
-    uint32_t *insv = ord + S;                        // [S]  insertion value of each entry
-    uint32_t *tot = insv + S;                        // [4]  block-scan scratch
-    uint32_t *val = cnt;
-    const int tid = threadIdx.x;
-    const int32_t rl = (int32_t)(blockIdx.x / ng);
-    const int64_t tile = g_lo + (int64_t)(blockIdx.x % ng);
-    const uint32_t rank = (uint32_t)(rank_lo + rl);
-    const RankDesc rd = ranks[rank];
-    int64_t tlo, thi;
-    tile_bounds(pl, tile, tlo, thi);
-    {   // slot table at the tile's start (4 independent loads in flight per thread)
-        const uint32_t *VALr = VAL + (int64_t)rl * pl.G * P1;
-        const uint32_t *prev = VALr + (tile - 1) * P1;
-        for (int s0 = tid; s0 < P1; s0 += 1024) {
-            uint32_t v[4];
-#pragma unroll
-            for (int u = 0; u < 4; u++) {
-                const int s = s0 + 256 * u;
-                v[u] = (tile > 0 && s < P1) ? prev[s] : kNone;
-            }
-#pragma unroll
-            for (int u = 0; u < 4; u++) {
-                const int s = s0 + 256 * u;
-                if (s < P1) buf[s] = v[u] != kNone ? v[u] : slot_value_after(VALr, P1, tile - 2, s);
-            }
-        }
-    }
-    const uint32_t B = (uint32_t)g.B;
-    const uint32_t hB = feistel_half_bits(B);
-    const bool walk_full = B != (1u << (2 * hB));
-    const uint32_t w_last = (uint32_t)(1 + (pl.T - 1) / g.B);
-    const uint32_t len_last = (uint32_t)(g.ns - (int64_t)w_last * g.B);
-    const uint32_t h_last = feistel_half_bits(len_last);
-    const uint32_t twoB = (uint32_t)(2 * g.B < g.ns ? 2 * g.B : g.ns);
-    const uint32_t old32 = (uint32_t)rd.old_start, new32 = (uint32_t)rd.new_start;
-    const uint32_t N32 = (uint32_t)g.N;
-    const int64_t pos_hi = pos_lo + count;
-    int64_t *o = out + (int64_t)rl * count - pos_lo;
-    const int per = (P1 + 255) / 256;                // buckets per thread in P2 / P4
-    const int blo = tid * per < P1 ? tid * per : P1;
-    const int bhi = blo + per < P1 ? blo + per : P1;
-    const int NBLK = (S + 1023) / 1024;              // 4-step groups per thread (<= 4)
-    const SlotKey sk = slot_key(g, rank);
-    for (int64_t a = tlo; a < thi; a += S) {
-        const int n = (int)(thi - a < S ? thi - a : S);
-        const uint32_t wa = (uint32_t)(1 + a / g.B);
-        const uint32_t pa = (uint32_t)(a - (int64_t)(wa - 1) * g.B);
-        uint32_t ka[kRoundKeyWords], kb[kRoundKeyWords];
-        window_round_keys(g, rank, wa, ka);
-        window_round_keys(g, rank, (int64_t)wa + 1, kb);
-        // P0
-        for (int i = tid; i < bpad_size(P1); i += 256) cnt[i] = 0;
-        __syncthreads();
-        // P1: slots of the sub-tile's steps (a is a multiple of 256: whole super-batches)
-        uint32_t kreg[4][4];
-#pragma unroll
-        for (int b = 0; b < 4; b++) {
-            if (b >= NBLK) break;
-            const int ci = tid + 256 * b;            // (super-batch q, lane)
-            const int q = ci >> 6, lane = ci & 63;
-            uint32_t u[4] = {0, 0, 0, 0};
-            if (q * 256 < S) slot_words(sk, (a >> 8) + q, lane, u);
-#pragma unroll
-            for (int w = 0; w < 4; w++) {
-                const int tl = q * 256 + w * 64 + lane;
-                const bool valid = q * 256 < S && tl < n;
-                const uint32_t k = scale32(u[w], (uint32_t)P1);
-                kreg[b][w] = valid ? k : 0xFFFFFFFFu;
-                if (valid) atomicAdd(&cnt[bpad(k)], 1u);
-            }
-        }
-        __syncthreads();
-        // P2: exclusive scan of the bucket counts
-        {
-            uint32_t s = 0;
-            for (int i = blo; i < bhi; i++) s += cnt[bpad(i)];
-            uint32_t total;
-            uint32_t run = block_excl_scan<256>(s, tot, total);
-            for (int i = blo; i < bhi; i++) { const uint32_t c = cnt[bpad(i)]; cnt[bpad(i)] = run; run += c; }
-        }
-        __syncthreads();
-        // P3: scatter entries into their buckets (order inside a bucket is fixed in P4)
-#pragma unroll
-        for (int b = 0; b < 4; b++) {
-            if (b >= NBLK) break;
-            const int ci = tid + 256 * b;
-            const int q = ci >> 6, lane = ci & 63;
-#pragma unroll
-            for (int w = 0; w < 4; w++) {
-                const uint32_t k = kreg[b][w];
-                if (k != 0xFFFFFFFFu) {
-                    const uint32_t pos = atomicAdd(&cnt[bpad(k)], 1u);
-                    ord[pos] = (k << 16) | (uint32_t)(q * 256 + w * 64 + lane);
-                }
-            }
-        }
-        __syncthreads();
-        // P4: order every bucket by step; flag first and last entries
-        for (int bk = tid; bk < P1; bk += 256) {     // interleaved: conflict-free cnt reads
-            const int e = (int)cnt[bpad(bk)];
-            const int st = bk ? (int)cnt[bpad(bk - 1)] : 0;
-            for (int x = st + 1; x < e; x++) {
-                const uint32_t v = ord[x];
-                int y = x - 1;
-                while (y >= st && ord[y] > v) { ord[y + 1] = ord[y]; y--; }
-                ord[y + 1] = v;
-            }
-            if (e > st) {
-                ord[st] |= kSstFirst;
-                ord[e - 1] |= kSstLast;
-            }
-        }
-        __syncthreads();
-        // P5: insertion value of every entry
-        for (int p = tid; p < n; p += 256) {
-            const uint32_t tl = ord[p] & 0xFFFFu;
-            uint32_t pp = pa + tl, w = wa;
-            const bool cross = pp >= B;
-            pp = cross ? pp - B : pp;
-            w = cross ? w + 1 : w;
-            uint32_t kk[kFeistelRounds];
-#pragma unroll
-            for (int i = 0; i < kFeistelRounds; i++) kk[i] = cross ? kb[i] : ka[i];
-            uint32_t x;
-            if (!walk_full && w != w_last) {
-                x = feistel_once(pp, hB, kk);
-            } else {
-                const bool lastw = w == w_last;
-                x = feistel(pp, lastw ? len_last : B, lastw ? h_last : hB, kk);
-            }
-            insv[p] = w * B + x;
-        }
-        __syncthreads();
-        // P6: value emitted by each step (val aliases cnt, no longer needed)
-        for (int p = tid; p < n; p += 256) {
-            const uint32_t e = ord[p];
-            const uint32_t k = (e & kSstPayload) >> 16;
-            val[e & 0xFFFFu] = (e & kSstFirst) ? buf[k] : insv[p - 1];
-        }
-        __syncthreads();
-        // P7: slot table after the sub-tile; ids of its steps
-        for (int p = tid; p < n; p += 256) {
-            const uint32_t e = ord[p];
-            if (e & kSstLast) buf[(e & kSstPayload) >> 16] = insv[p];
-        }
-        for (int tl = tid; tl < n; tl += 256) {
-            const int64_t t = a + tl;
-            if (t < pos_lo || t >= pos_hi) continue;
-            const uint32_t v = val[tl];
-            if (NARROW) {
-                uint32_t id = (v < twoB ? old32 : new32) + v;
-                o[t] = (int64_t)(id >= N32 ? id - N32 : id);
-            } else {
-                o[t] = v2_id(v, rd, g);
-            }
-        }
-        __syncthreads();
-    }
 }
 
 // ---- tail ---------------------------------------------------------------------------------
@@ -1071,7 +902,7 @@ hipError_t launch_v2(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, 
                     const char *e = getenv("PSS_V2_LASTOCC_NT");
                     return e ? atoi(e) : 256;
                 }();
-                const bool pow2 = (pl.P1 & (pl.P1 - 1)) == 0;
+                const bool pow2 = pl.P1 >= 2 && slot_paired((uint32_t)pl.P1);   // paired draws
                 const dim3 grid((uint32_t)(nr * g_need));
 #define PSS_LO(NT, ORD) do { if (pow2) hipLaunchKernelGGL((k_v2_lastocc<NT, ORD, true>), grid, dim3(NT), lds, s, g, pl, rank_lo, g_need, VAL, kt); \
                              else hipLaunchKernelGGL((k_v2_lastocc<NT, ORD, false>), grid, dim3(NT), lds, s, g, pl, rank_lo, g_need, VAL, kt); } while (0)
@@ -1096,30 +927,13 @@ hipError_t launch_v2(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, 
             // 32-bit id arithmetic whenever every id (and id + ns before the wrap) fits
             const bool narrow = g.N + g.ns < (int64_t)UINT32_MAX;
             const dim3 grid((uint32_t)(nr * ng));
-            static const bool use_sst = [] {
-                // A/B knob: "sst" = sorted sub-tiles (bit-identical; measured 2.8x slower than
-                // the wave replay on C2, kept for experiments -- see DESIGN.md §5)
-                const char *e = getenv("PSS_V2_EMIT");
-                return e && e[0] == 's';
-            }();
-            if (!pl.global_buf && use_sst && pl.P1 >= 1024 && pl.P1 <= 8192) {
-                mk(K_V2_EMIT, s);
-                const int64_t S = (pl.P1 < 4096 ? pl.P1 : 4096) & ~255;
-                const size_t lds = (size_t)4 * (pl.P1 + bpad_size((int)pl.P1) + 2 * S) + 16;
-                const dim3 blk(256);
-                if (narrow)
-                    hipLaunchKernelGGL((k_v2_emit_sst<true>), grid, blk, lds, s, g, pl, ranks, rank_lo,
-                                       g_lo, ng, (const uint32_t *)VAL, pos_lo, count, out);
-                else
-                    hipLaunchKernelGGL((k_v2_emit_sst<false>), grid, blk, lds, s, g, pl, ranks, rank_lo,
-                                       g_lo, ng, (const uint32_t *)VAL, pos_lo, count, out);
-            } else if (!pl.global_buf && emit_path == EMIT_XCHG) {
+            if (!pl.global_buf && emit_path == EMIT_XCHG) {
                 mk(K_V2_EMIT, s);
                 const size_t need = lds_keys + (size_t)pl.P1 * 4;
                 const size_t lds = need > (size_t)pl.emit_lds ? need : (size_t)pl.emit_lds;
                 tail_fused = need_tail && last_emit == pl.G - 1;
                 const int dt = tail_fused ? 1 : 0;
-                const bool pow2 = (pl.P1 & (pl.P1 - 1)) == 0;
+                const bool pow2 = pl.P1 >= 2 && slot_paired((uint32_t)pl.P1);   // paired draws
 #define PSS_EX(N, P2) hipLaunchKernelGGL((k_v2_emit_x<N, P2>), grid, dim3(64), lds, s, g, pl, ranks, rank_lo, \
                                          g_lo, ng, (const uint32_t *)VAL, pos_lo, count, dt, out, kt)
                 if (narrow && pow2) PSS_EX(true, true);
@@ -1229,8 +1043,6 @@ hipError_t init_kernel_attributes_v2() {
     PSS_ATTR((k_v2_emit_x<true, false>));
     PSS_ATTR((k_v2_emit_x<false, true>));
     PSS_ATTR((k_v2_emit_x<false, false>));
-    PSS_ATTR((k_v2_emit_sst<true>));
-    PSS_ATTR((k_v2_emit_sst<false>));
     PSS_ATTR((k_v2_emit<false, true, false>));
     PSS_ATTR((k_v2_emit<false, false, false>));
     PSS_ATTR((k_v2_emit<false, true, true>));

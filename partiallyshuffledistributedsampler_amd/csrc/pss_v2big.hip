@@ -102,7 +102,7 @@ __device__ __forceinline__ TileInfo tile_info(const BigPlan &p, int32_t rank_lo,
 }
 
 __device__ __forceinline__ uint32_t slot_of(uint32_t t, const SlotKey &sk, uint32_t P1) {
-    return scale32(slot_hash(t, sk.s0, sk.s1), P1);
+    return slot_draw(t, sk.s0, sk.s1, P1);
 }
 
 // ---- bucketing ------------------------------------------------------------------------------
