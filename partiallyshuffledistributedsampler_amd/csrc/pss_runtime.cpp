@@ -6,9 +6,14 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <condition_variable>
 #include <cstdio>
 #include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/pss.h"
@@ -120,6 +125,90 @@ class CPythonMT {
     }
 };
 
+// The file-order permutation of an epoch (V1:114-117 seed(e + 1), V2:143-144 seed(e)):
+// MT19937 Fisher-Yates of range(F).  A pure function of (version, epoch, F), so it can be
+// computed ahead of time: the sampler prefetches the next two epochs' permutations on worker
+// threads while the current epoch runs (init_iter then only composes it with the current
+// order), and the O(F) host shuffle leaves the epoch's critical path.
+std::shared_ptr<std::vector<int32_t>> file_permutation(int32_t version, int64_t epoch, int64_t F) {
+    auto v = std::make_shared<std::vector<int32_t>>(F);
+    for (int64_t i = 0; i < F; i++) (*v)[i] = (int32_t)i;
+    CPythonMT mt;
+    mt.seed(version == 1 ? epoch + 1 : epoch);
+    mt.shuffle(v->data(), F);
+    return v;
+}
+
+class PermPrefetcher {
+  public:
+    PermPrefetcher(int32_t version, int64_t F) : version_(version), F_(F) {}
+    ~PermPrefetcher() {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto &t : workers_) t.join();
+    }
+    // the permutation of `epoch`: from the cache, or computed here (waiting for a worker that
+    // is already on it); afterwards epochs epoch+1, epoch+2 are queued for the workers
+    std::shared_ptr<std::vector<int32_t>> take(int64_t epoch) {
+        std::shared_ptr<std::vector<int32_t>> r;
+        {
+            std::unique_lock<std::mutex> lk(mu_);
+            cv_.wait(lk, [&] { return !busy_.count(epoch); });
+            auto it = done_.find(epoch);
+            if (it != done_.end()) { r = it->second; done_.erase(it); }
+            // drop stale entries (epochs behind the caller, or far ahead)
+            for (auto j = done_.begin(); j != done_.end();)
+                j = (j->first < epoch || j->first > epoch + kAhead) ? done_.erase(j) : std::next(j);
+        }
+        if (!r) r = file_permutation(version_, epoch, F_);
+        request(epoch + 1);
+        request(epoch + 2);
+        return r;
+    }
+
+  private:
+    static constexpr int64_t kAhead = 2;
+    int32_t version_;
+    int64_t F_;
+    std::mutex mu_;
+    std::condition_variable cv_;
+    std::map<int64_t, std::shared_ptr<std::vector<int32_t>>> done_;
+    std::map<int64_t, bool> busy_;
+    std::vector<int64_t> queue_;
+    std::vector<std::thread> workers_;
+    bool stop_ = false;
+
+    void request(int64_t e) {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            if (done_.count(e) || busy_.count(e)) return;
+            for (int64_t q : queue_) if (q == e) return;
+            queue_.push_back(e);
+            if (workers_.size() < (size_t)kAhead) workers_.emplace_back([this] { run(); });
+        }
+        cv_.notify_all();
+    }
+    void run() {
+        std::unique_lock<std::mutex> lk(mu_);
+        for (;;) {
+            cv_.wait(lk, [&] { return stop_ || !queue_.empty(); });
+            if (stop_) return;
+            const int64_t e = queue_.front();
+            queue_.erase(queue_.begin());
+            busy_[e] = true;
+            lk.unlock();
+            auto v = file_permutation(version_, e, F_);
+            lk.lock();
+            busy_.erase(e);
+            done_[e] = v;
+            cv_.notify_all();
+        }
+    }
+};
+
 class DeviceGuard {  // run on the handle's device, restore the caller's afterwards
   public:
     explicit DeviceGuard(int dev) {
@@ -157,6 +246,7 @@ struct pss_sampler {
     int64_t F = 0, N = 0, ns = 0, B = 0;
     int32_t R = 0, version = 1, shuffle = 1, device = 0;
     int32_t emit_path = 0;        // pss::EmitPath
+    std::unique_ptr<PermPrefetcher> perms;   // file permutations of the coming epochs
     uint64_t seed = 0;
     // history state
     std::vector<int32_t> order;   // self.files as dataset positions
@@ -354,27 +444,27 @@ int pss_num_samples(const pss_sampler *h, int64_t *ns) {
 int pss_init_iter(pss_sampler *h, int64_t epoch) {
     if (!h) return fail(PSS_EINVAL, "NULL handle");
     CPythonMT mt;
-    std::vector<int32_t> fid(h->F);
-    for (int64_t i = 0; i < h->F; i++) fid[i] = (int32_t)i;
     for (int32_t r = 0; r < h->R; r++) h->ranks[r].old_start = h->ranks[r].new_start;
+    const bool files = h->version == 2 || h->shuffle;
+    std::shared_ptr<std::vector<int32_t>> fid;
+    if (files) {
+        if (!h->perms) h->perms.reset(new PermPrefetcher(h->version, h->F));
+        fid = h->perms->take(epoch);                    // V1:114-117 / V2:143-144
+    }
     if (h->version == 1) {
         if (h->shuffle) {                              // V1:113-125
-            mt.seed(epoch + 1);
-            mt.shuffle(fid.data(), h->F);
             mt.seed(epoch + 2);
             mt.shuffle(h->blocks.data(), h->R);        // cumulative: self.blocks is kept
-            std::vector<int32_t> o(h->F);
-            for (int64_t i = 0; i < h->F; i++) o[i] = h->order[fid[i]];
-            h->order.swap(o);
         }
     } else {                                           // V2:142-152
-        mt.seed(epoch);
-        mt.shuffle(fid.data(), h->F);
         for (int32_t r = 0; r < h->R; r++) h->blocks[r] = r;
         mt.seed(epoch + 1);
         mt.shuffle(h->blocks.data(), h->R);
+    }
+    if (files) {                                       // cumulative: self.files is re-shuffled
         std::vector<int32_t> o(h->F);
-        for (int64_t i = 0; i < h->F; i++) o[i] = h->order[fid[i]];
+        const int32_t *f = fid->data();
+        for (int64_t i = 0; i < h->F; i++) o[i] = h->order[f[i]];
         h->order.swap(o);
     }
     for (int32_t r = 0; r < h->R; r++) h->ranks[r].new_start = h->ns * (int64_t)h->blocks[r];
