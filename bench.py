@@ -136,10 +136,19 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal of the multi-process path on a one-GPU box: every rank on cuda:0, gloo for the
+    # (count, digest) exchange.  The real N-GPU run uses RCCL ("nccl") with one GPU per rank.
+    rehearse = os.environ.get("PSS_BENCH_SAME_GPU") == "1"
+    if rehearse:
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    cdev = torch.device("cpu") if rehearse else dev     # device of the collective tensors
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
 
     F1, L, RG, B, ver = WORKLOADS[args.workload]
     F, R = F1 * world, RG * world
@@ -169,14 +178,14 @@ def main():
     dt = time.perf_counter() - t0
     if world > 1:
         dist.barrier()
-        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        t = torch.tensor([dt], dtype=torch.float64, device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     prof = eng.profile_read()
     eng.profile(False)
 
     # coverage of the last epoch across all GPUs: (count, digest) all-gather over RCCL
-    pairs = gather_pairs(out.numel(), as_u64(digest(out.view(-1))), device=dev)
+    pairs = gather_pairs(out.numel(), as_u64(digest(out.view(-1))), device=cdev)
     coverage = None
     if rank == 0:
         coverage = coverage_ok(pairs, ns, R, expected_digest_gpu(N, ns, R, dev))
