@@ -292,7 +292,11 @@ uint32_t orc_feistel(uint32_t x, uint32_t n, const uint32_t rk[6]) {
     do {
         uint32_t L = x >> h, R = x & mask;
         for (int i = 0; i < 6; i++) {
-            uint32_t t = L ^ (uint32_t)(((R ^ rk[i]) * 0x9E3779B1u) >> (32 - h));
+            /* halves of <= 8 bits: 16-bit multiplicative hash (top h bits of the low 16 bits
+             * of (R ^ k) * 0x9E37); wider halves: top h bits of (R ^ k) * 0x9E3779B1 */
+            uint32_t f = h <= 8 ? ((((R ^ rk[i]) * 0x9E37u) & 0xFFFFu) >> (16 - h))
+                                : (uint32_t)(((R ^ rk[i]) * 0x9E3779B1u) >> (32 - h));
+            uint32_t t = L ^ f;
             L = R; R = t;
         }
         x = (L << h) | R;

@@ -60,18 +60,34 @@ PSS_HD int ceil_log2_u64(uint64_t n) {  // smallest b with 2^b >= n (n >= 1)
 }
 
 // Keyed bijection of [0, n): 6-round balanced Feistel over 2h bits + cycle walking.
-// Round function: multiplicative hashing of the keyed right half, F(R) = top h bits of
-// (R ^ k_i) * 0x9E3779B1 -- one multiply per round (DESIGN.md §3.3 has the quality numbers).
+// Round function: multiplicative hashing of the keyed right half (one multiply per round).
 constexpr int kFeistelRounds = 6;
 
+// Round function for halves of h <= 8 bits (windows up to 65536): the top h bits of the low
+// 16 bits of (R ^ k) * 0x9E37 -- a 16-bit multiplicative hash, so two chains fit one 32-bit
+// register and run on packed 16-bit ops (feistel2_pk16).  Wider halves: top h bits of the
+// 32-bit product (R ^ k) * 0x9E3779B1.
+constexpr uint32_t kFeistelM16 = 0x9E37u, kFeistelM32 = 0x9E3779B1u;
+
 PSS_HD uint32_t feistel_pass(uint32_t x, uint32_t h, const uint32_t *k) {
-    const uint32_t mask = (1u << h) - 1u, sh = 32u - h;
+    const uint32_t mask = (1u << h) - 1u;
     uint32_t L = x >> h, R = x & mask;
+    if (h <= 8) {
+        const uint32_t sh = 16u - h;
 #pragma unroll
-    for (int i = 0; i < kFeistelRounds; i++) {
-        const uint32_t t = L ^ (((R ^ k[i]) * 0x9E3779B1u) >> sh);
-        L = R;
-        R = t;
+        for (int i = 0; i < kFeistelRounds; i++) {
+            const uint32_t t = L ^ ((((R ^ k[i]) * kFeistelM16) & 0xFFFFu) >> sh);
+            L = R;
+            R = t;
+        }
+    } else {
+        const uint32_t sh = 32u - h;
+#pragma unroll
+        for (int i = 0; i < kFeistelRounds; i++) {
+            const uint32_t t = L ^ (((R ^ k[i]) * kFeistelM32) >> sh);
+            L = R;
+            R = t;
+        }
     }
     return (L << h) | R;
 }

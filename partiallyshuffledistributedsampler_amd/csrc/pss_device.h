@@ -190,6 +190,30 @@ __device__ __forceinline__ void slot4(uint32_t t, const SlotKey &sk, uint32_t P1
     }
 }
 
+// Two one-pass Feistel chains (feistel_pass with h <= 8) in one register, on packed 16-bit ops:
+// chain 0 in the low half-word, chain 1 in the high one; kp[i] = (k[i] & 0xFFFF) * 0x10001
+// (both chains under the same round keys).  Same values as feistel_once on each chain.
+typedef unsigned short pss_u16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ void feistel2_pk16(uint32_t x0, uint32_t x1, uint32_t h, const uint32_t *kp,
+                                              uint32_t &y0, uint32_t &y1) {
+    const uint32_t mask = (1u << h) - 1u;
+    uint32_t L = (x0 >> h) | ((x1 >> h) << 16);
+    uint32_t R = (x0 & mask) | ((x1 & mask) << 16);
+    const pss_u16x2 M = {(unsigned short)kFeistelM16, (unsigned short)kFeistelM16};
+    const pss_u16x2 SH = {(unsigned short)(16u - h), (unsigned short)(16u - h)};
+#pragma unroll
+    for (int i = 0; i < kFeistelRounds; i++) {
+        const pss_u16x2 a = __builtin_bit_cast(pss_u16x2, R ^ kp[i]);
+        const pss_u16x2 f = (a * M) >> SH;
+        const uint32_t t = L ^ __builtin_bit_cast(uint32_t, f);
+        L = R;
+        R = t;
+    }
+    y0 = ((L & 0xFFFFu) << h) | (R & 0xFFFFu);
+    y1 = ((L >> 16) << h) | (R >> 16);
+}
+
 // Feistel round keys of pool2 window w: Philox blocks (w, 0, rank, INS) and (w, 1, rank, INS),
 // 8 words of which the first kFeistelRounds are used
 constexpr int kRoundKeyWords = 8;

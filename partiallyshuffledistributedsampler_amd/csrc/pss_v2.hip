@@ -584,8 +584,8 @@ __global__ __launch_bounds__(64) void k_v2_emit_x(Geometry g, V2Plan pl,
     // fast super-batches: every step valid and emitted, B >= 256 (at most one window boundary
     // per super-batch), neither window short nor cycle-walking
     const bool fast_tile = e_lo == 0 && e_hi == nvalid && B >= 256 && !walk_full;
-    uint32_t kw[kFeistelRounds];     // round keys of window w0 (wave-uniform: SGPRs)
-    uint32_t kw_w = 0xFFFFFFFFu;
+    uint32_t kw[kFeistelRounds];     // round keys of window w0 (wave-uniform: SGPRs), packed
+    uint32_t kw_w = 0xFFFFFFFFu;     // twice into 16-bit halves (hB <= 7 on this path)
     Pacer pace(nvalid);
     for (uint32_t tl0 = 0; tl0 < nvalid; tl0 += 256) {
         pace.step(tl0);
@@ -593,7 +593,7 @@ __global__ __launch_bounds__(64) void k_v2_emit_x(Geometry g, V2Plan pl,
             if (kw_w != w0) {
 #pragma unroll
                 for (int i = 0; i < kFeistelRounds; i++)
-                    kw[i] = __builtin_amdgcn_readfirstlane(rk[kRoundKeyWords * (w0 - wl) + i]);
+                    kw[i] = (__builtin_amdgcn_readfirstlane(rk[kRoundKeyWords * (w0 - wl) + i]) & 0xFFFFu) * 0x10001u;
                 kw_w = w0;
             }
             uint32_t k[4], ins[4], v[4];
@@ -601,7 +601,12 @@ __global__ __launch_bounds__(64) void k_v2_emit_x(Geometry g, V2Plan pl,
                 // the whole super-batch inserts from window w0: scalar round keys
                 slot4<POW2>(t0 + tl0 + lane, sk, P1, sh, k);
 #pragma unroll
-                for (int j = 0; j < 4; j++) ins[j] = w0 * B + feistel_once(p0 + 64u * j + lane, hB, kw);
+                for (int j = 0; j < 4; j += 2) {
+                    uint32_t y0, y1;
+                    feistel2_pk16(p0 + 64u * j + lane, p0 + 64u * (j + 1) + lane, hB, kw, y0, y1);
+                    ins[j] = w0 * B + y0;
+                    ins[j + 1] = w0 * B + y1;
+                }
             } else {
                 slot4<POW2>(t0 + tl0 + lane, sk, P1, sh, k);
 #pragma unroll
