@@ -523,6 +523,9 @@ __global__ __launch_bounds__(64) void k_v2_emit_x(Geometry g, V2Plan pl,
                                                   int64_t pos_lo, int64_t count, int do_tail,
                                                   int64_t *__restrict__ out, KeyTab kt) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+#ifdef PSS_STAMPS
+    if (threadIdx.x == 0 && blockIdx.x < (1u << 16)) pss_stamps[blockIdx.x][2] = __builtin_amdgcn_s_memrealtime();
+#endif
     const uint32_t P1 = (uint32_t)pl.P1;
     const uint32_t B = pl.B32;
     const uint32_t nwin_max = pl.L32 / B + 2;
@@ -539,20 +542,46 @@ __global__ __launch_bounds__(64) void k_v2_emit_x(Geometry g, V2Plan pl,
     const uint32_t thi = pl.T32 - tlo < pl.L32 ? pl.T32 : tlo + pl.L32;
     const uint32_t w_lo = 1 + tlo / B;
     const int nwin = (int)(1 + (thi - 1) / B - w_lo + 1);
-    {   // slot table at the tile's start (4 independent loads in flight per lane)
+    {   // slot table at the tile's start: 16-byte loads, up to 16 per lane in flight (the whole
+        // 16 KB table of P1 = 4096 in one round trip); slots the previous tile never drew walk
+        // back further (probability e^-(L/P1))
         const uint32_t *VALr = VAL + (int64_t)rl * pl.G * pl.P1;
         const uint32_t *prev = VALr + ((int64_t)tile - 1) * pl.P1;   // tile 0: never read
-        for (uint32_t s0 = lane; s0 < P1; s0 += 256) {
-            uint32_t v[4];
+        if (tile == 0) {
+            for (uint32_t s = lane; s < P1; s += 64) buf[s] = s;
+        } else if ((P1 & 1023u) == 0) {
+            const uint4 *p4 = (const uint4 *)prev;
+            for (uint32_t q0 = 0; q0 < P1 / 4; q0 += 1024) {
+                uint4 v[16];
 #pragma unroll
-            for (int u = 0; u < 4; u++) {
-                const uint32_t s = s0 + 64 * u;
-                v[u] = (tile > 0 && s < P1) ? prev[s] : kNone;
+                for (int u = 0; u < 16; u++) {
+                    const uint32_t q = q0 + 64u * u + lane;
+                    v[u] = q < P1 / 4 ? p4[q] : make_uint4(0, 0, 0, 0);
+                }
+#pragma unroll
+                for (int u = 0; u < 16; u++) {
+                    const uint32_t q = q0 + 64u * u + lane;
+                    if (q >= P1 / 4) continue;
+                    uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+                    for (int c = 0; c < 4; c++)
+                        if (w[c] == kNone) w[c] = slot_value_after(VALr, pl.P1, (int64_t)tile - 2, 4 * q + c);
+                    *(uint4 *)(buf + 4 * q) = make_uint4(w[0], w[1], w[2], w[3]);
+                }
             }
+        } else {
+            for (uint32_t s0 = lane; s0 < P1; s0 += 256) {
+                uint32_t v[4];
 #pragma unroll
-            for (int u = 0; u < 4; u++) {
-                const uint32_t s = s0 + 64 * u;
-                if (s < P1) buf[s] = v[u] != kNone ? v[u] : slot_value_after(VALr, pl.P1, (int64_t)tile - 2, s);
+                for (int u = 0; u < 4; u++) {
+                    const uint32_t s = s0 + 64 * u;
+                    v[u] = s < P1 ? prev[s] : kNone;
+                }
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    const uint32_t s = s0 + 64 * u;
+                    if (s < P1) buf[s] = v[u] != kNone ? v[u] : slot_value_after(VALr, pl.P1, (int64_t)tile - 2, s);
+                }
             }
         }
     }
@@ -577,6 +606,7 @@ __global__ __launch_bounds__(64) void k_v2_emit_x(Geometry g, V2Plan pl,
     const uint32_t sh = 32u - (uint32_t)ceil_log2_u64((uint64_t)P1);   // POW2 only
 #ifdef PSS_STAMPS
     const uint64_t st_clk = __builtin_amdgcn_s_memtime(), st_rt = __builtin_amdgcn_s_memrealtime();
+    if (lane == 0 && blockIdx.x < (1u << 16)) pss_stamps[blockIdx.x][3] = st_rt;
 #endif
     // pool2 position (w0, p0) of the super-batch's first step, advanced without division
     uint32_t w0 = w_lo;
@@ -620,9 +650,11 @@ __global__ __launch_bounds__(64) void k_v2_emit_x(Geometry g, V2Plan pl,
             }
 #pragma unroll
             for (int j = 0; j < 4; j++) v[j] = atomicExch(&buf[k[j]], ins[j]);
+            // wave-uniform base: the stores take (lane * 8 + 512 j) as offset, no 64-bit adds
+            int64_t *ob = o + tl0;
 #pragma unroll
             for (int j = 0; j < 4; j++)
-                o[tl0 + 64u * j + lane] = emit_id<NARROW>(v[j], twoB, old32, new32, N32, rd, g);
+                ob[64u * j + lane] = emit_id<NARROW>(v[j], twoB, old32, new32, N32, rd, g);
         } else {
 #pragma unroll
             for (int j = 0; j < 4; j++) {
@@ -646,6 +678,9 @@ __global__ __launch_bounds__(64) void k_v2_emit_x(Geometry g, V2Plan pl,
     if (lane == 0 && blockIdx.x < (1u << 16)) {
         pss_stamps[blockIdx.x][0] = __builtin_amdgcn_s_memtime() - st_clk;
         pss_stamps[blockIdx.x][1] = __builtin_amdgcn_s_memrealtime() - st_rt;
+        pss_stamps[blockIdx.x][4] = __builtin_amdgcn_s_memrealtime();
+        pss_stamps[blockIdx.x][6] = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));   // HW_ID
+        pss_stamps[blockIdx.x][7] = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (15 << 11));  // XCC_ID
     }
 #endif
     if (do_tail && (int64_t)tile == pl.G - 1) {
@@ -662,6 +697,9 @@ __global__ __launch_bounds__(64) void k_v2_emit_x(Geometry g, V2Plan pl,
             ot[j] = emit_id<NARROW>(buf[feistel(j, P1, hT, tk)], twoB, old32, new32, N32, rd, g);
         }
     }
+#ifdef PSS_STAMPS
+    if (lane == 0 && blockIdx.x < (1u << 16)) pss_stamps[blockIdx.x][5] = __builtin_amdgcn_s_memrealtime();
+#endif
 }
 
 // Start-up check of the exchange order k_v2_emit_x relies on: random slot patterns (heavy

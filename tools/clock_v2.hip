@@ -4,6 +4,8 @@
 #include <cstdio>
 #include <vector>
 #include <unistd.h>
+#include <algorithm>
+#include <map>
 
 int main() {
     using namespace pss;
@@ -28,9 +30,38 @@ int main() {
         (void)hipDeviceSynchronize();
         (void)hipMemcpyFromSymbol(st.data(), HIP_SYMBOL(pss_stamps), st.size() * 8);
         double clk = 0, rt = 0;
-        for (int b = 0; b < 2048; b++) { clk += (double)st[(size_t)b * 8]; rt += (double)st[(size_t)b * 8 + 1]; }
-        printf("%s: mean wave %.1f us, shader clock %.2f GHz\n", mode ? "300us gaps" : "back-to-back", rt / 2048 / 100.0,
-               clk / rt * 0.1);
+        std::vector<double> life;
+        for (int b = 0; b < 2048; b++) {
+            clk += (double)st[(size_t)b * 8]; rt += (double)st[(size_t)b * 8 + 1];
+            life.push_back(st[(size_t)b * 8 + 1] / 100.0);
+        }
+        std::sort(life.begin(), life.end());
+        uint64_t t0 = ~0ull, t1 = 0;
+        double pro = 0, epi = 0;
+        for (int b = 0; b < 2048; b++) {
+            const uint64_t *x = &st[(size_t)b * 8];
+            t0 = std::min(t0, x[2]); t1 = std::max(t1, x[5]);
+            pro += (double)(x[3] - x[2]); epi += (double)(x[5] - x[4]);
+        }
+        // waves per SIMD and the mean life of waves by their SIMD's wave count
+        std::map<uint64_t, int> per;
+        for (int b = 0; b < 2048; b++) {
+            const uint64_t *x = &st[(size_t)b * 8];
+            const uint64_t hw = x[6], key = (x[7] << 32) | (hw & 0xFF30);   // xcc | se,sh,cu | simd
+            per[key]++;
+        }
+        std::map<int, std::pair<double, int>> bycount;
+        for (int b = 0; b < 2048; b++) {
+            const uint64_t *x = &st[(size_t)b * 8];
+            const uint64_t key = (x[7] << 32) | (x[6] & 0xFF30);
+            auto &e = bycount[per[key]];
+            e.first += x[1] / 100.0; e.second++;
+        }
+        for (auto &kv : bycount) printf("  SIMDs with %d waves: %d waves, mean loop %.1f us\n", kv.first, kv.second.second, kv.second.first / kv.second.second);
+        printf("  span %.1f us; mean prologue %.1f us, epilogue (tail) %.1f us\n", (t1 - t0) / 100.0, pro / 2048 / 100.0, epi / 2048 / 100.0);
+        printf("%s: wave us mean %.1f p10 %.1f p50 %.1f p90 %.1f max %.1f, shader clock %.2f GHz\n",
+               mode ? "300us gaps" : "back-to-back", rt / 2048 / 100.0, life[204], life[1024], life[1843],
+               life[2047], clk / rt * 0.1);
     }
     return 0;
 }
