@@ -298,19 +298,37 @@ __device__ __forceinline__ uint32_t slot_value_after(const uint32_t *VALr, int64
 // the older one runs ahead and the younger finishes alone at half the issue rate.  A wave
 // lowers its own priority as it passes 1/4, 1/2 and 3/4 of its work: whoever is behind wins
 // arbitration, and the waves of a SIMD finish together.
+#ifndef PSS_PACER_MODE
+#define PSS_PACER_MODE 0
+#endif
 struct Pacer {
     uint32_t next, quarter;
     int stage;
+    uint32_t total_;
     __device__ __forceinline__ explicit Pacer(uint32_t total) {
+        total_ = total;
         quarter = total / 4 + 1;
+#if PSS_PACER_MODE == 1
+        next = total - total / 4;
+#else
         next = quarter;
+#endif
         stage = 0;
+#if PSS_PACER_MODE != 2
         __builtin_amdgcn_s_setprio(3);
+#endif
     }
     __device__ __forceinline__ void step(uint32_t done) {
+#if PSS_PACER_MODE == 2
+        return;
+#endif
         if (done < next) return;
-        next += quarter;
         stage++;
+#if PSS_PACER_MODE == 1
+        next = stage == 1 ? total_ - total_ / 16 : stage == 2 ? total_ - total_ / 64 : ~0u;
+#else
+        next += quarter;
+#endif
         if (stage == 1) __builtin_amdgcn_s_setprio(2);
         else if (stage == 2) __builtin_amdgcn_s_setprio(1);
         else __builtin_amdgcn_s_setprio(0);

@@ -685,16 +685,38 @@ __global__ __launch_bounds__(64) void k_v2_emit_x(Geometry g, V2Plan pl,
 #endif
     if (do_tail && (int64_t)tile == pl.G - 1) {
         // the rank's final pool is this wave's slot table: drain it in tail order (positions
-        // T + j, j < P1).  One wave: its own LDS exchanges above are complete in order.
+        // T + j, j < P1).  One wave: its own LDS exchanges above are complete in order.  The
+        // last tile is short, so its wave reaches this point while its SIMD partner still runs
+        // at a higher Pacer priority: take the top priority, the tail is on the critical path.
+        __builtin_amdgcn_s_setprio(3);
         __syncthreads();
         uint32_t tk[kRoundKeyWords];
         tail_keys_t(g, rank, kt, rl, tk);
         const uint32_t hT = feistel_half_bits(P1);
         int64_t *ot = out + (int64_t)rl * count - pos_lo + pl.T;
-        for (uint32_t j = lane; j < P1; j += 64) {
-            const int64_t pos = pl.T + j;
-            if (pos < pos_lo || pos >= pos_hi) continue;
-            ot[j] = emit_id<NARROW>(buf[feistel(j, P1, hT, tk)], twoB, old32, new32, N32, rd, g);
+        const bool whole = pl.T >= pos_lo && pl.T + pl.P1 <= pos_hi;
+        if (whole && (P1 & 255u) == 0 && hT <= 8 && P1 == (1u << (2 * hT))) {
+            // P1 = 4^hT: no cycle walking; four independent chains per lane, packed in pairs
+            uint32_t kp[kFeistelRounds];
+#pragma unroll
+            for (int i = 0; i < kFeistelRounds; i++) kp[i] = (tk[i] & 0xFFFFu) * 0x10001u;
+            for (uint32_t j0 = 0; j0 < P1; j0 += 256) {
+                uint32_t y[4];
+                feistel2_pk16(j0 + lane, j0 + 64u + lane, hT, kp, y[0], y[1]);
+                feistel2_pk16(j0 + 128u + lane, j0 + 192u + lane, hT, kp, y[2], y[3]);
+                uint32_t v[4];
+#pragma unroll
+                for (int u = 0; u < 4; u++) v[u] = buf[y[u]];
+#pragma unroll
+                for (int u = 0; u < 4; u++)
+                    ot[j0 + 64u * u + lane] = emit_id<NARROW>(v[u], twoB, old32, new32, N32, rd, g);
+            }
+        } else {
+            for (uint32_t j = lane; j < P1; j += 64) {
+                const int64_t pos = pl.T + j;
+                if (pos < pos_lo || pos >= pos_hi) continue;
+                ot[j] = emit_id<NARROW>(buf[feistel(j, P1, hT, tk)], twoB, old32, new32, N32, rd, g);
+            }
         }
     }
 #ifdef PSS_STAMPS

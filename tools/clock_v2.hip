@@ -6,6 +6,7 @@
 #include <unistd.h>
 #include <algorithm>
 #include <map>
+#include <cmath>
 
 int main() {
     using namespace pss;
@@ -56,6 +57,43 @@ int main() {
             const uint64_t key = (x[7] << 32) | (x[6] & 0xFF30);
             auto &e = bycount[per[key]];
             e.first += x[1] / 100.0; e.second++;
+        }
+        // pairs of waves sharing a SIMD: loop-start and loop-end skew
+        std::map<uint64_t, std::vector<const uint64_t *>> simd;
+        for (int b = 0; b < 2048; b++) {
+            const uint64_t *x = &st[(size_t)b * 8];
+            simd[(x[7] << 32) | (x[6] & 0xFF30)].push_back(x);
+        }
+        double dstart = 0, dend = 0, pspan = 0; int np = 0;
+        for (auto &kv : simd) if (kv.second.size() == 2) {
+            const uint64_t *a = kv.second[0], *c = kv.second[1];
+            dstart += std::fabs((double)a[3] - (double)c[3]);
+            dend += std::fabs((double)a[4] - (double)c[4]);
+            pspan += (double)(std::max(a[4], c[4]) - std::min(a[3], c[3]));
+            np++;
+        }
+        if (np) printf("  SIMD pairs %d: |start skew| %.1f us, |end skew| %.1f us, pair span %.1f us\n", np, dstart / np / 100.0, dend / np / 100.0, pspan / np / 100.0);
+        {   // timeline quantiles (us from the first wave's entry): entry, loop start, loop end, exit
+            std::vector<double> q[4];
+            for (int b = 0; b < 2048; b++) {
+                const uint64_t *x = &st[(size_t)b * 8];
+                for (int k = 0; k < 4; k++) q[k].push_back((double)(x[2 + k] - t0) / 100.0);
+            }
+            const char *nm[4] = {"entry", "loop start", "loop end", "exit"};
+            for (int k = 0; k < 4; k++) {
+                std::sort(q[k].begin(), q[k].end());
+                printf("  %-10s min %.1f p10 %.1f p50 %.1f p90 %.1f max %.1f\n", nm[k], q[k][0], q[k][204], q[k][1024], q[k][1843], q[k][2047]);
+            }
+            // by XCC: mean loop and mean loop end
+            double ml[8] = {0}, me[8] = {0}; int nx[8] = {0};
+            for (int b = 0; b < 2048; b++) {
+                const uint64_t *x = &st[(size_t)b * 8];
+                int xc = (int)(x[7] & 7);
+                ml[xc] += (double)(x[4] - x[3]) / 100.0; me[xc] += (double)(x[4] - t0) / 100.0; nx[xc]++;
+            }
+            printf("  by XCC (waves, loop us, loop end us):");
+            for (int k = 0; k < 8; k++) if (nx[k]) printf(" [%d: %d %.0f %.0f]", k, nx[k], ml[k] / nx[k], me[k] / nx[k]);
+            printf("\n");
         }
         for (auto &kv : bycount) printf("  SIMDs with %d waves: %d waves, mean loop %.1f us\n", kv.first, kv.second.second, kv.second.first / kv.second.second);
         printf("  span %.1f us; mean prologue %.1f us, epilogue (tail) %.1f us\n", (t1 - t0) / 100.0, pro / 2048 / 100.0, epi / 2048 / 100.0);
