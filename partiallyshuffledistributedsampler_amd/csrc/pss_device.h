@@ -214,6 +214,32 @@ __device__ __forceinline__ void feistel2_pk16(uint32_t x0, uint32_t x1, uint32_t
     y1 = ((L >> 16) << h) | (R >> 16);
 }
 
+// Four chains in two registers, rounds interleaved so that neither packed multiply waits on
+// the other's result (no dependency stalls between the pk ops).  Same values as feistel2_pk16.
+__device__ __forceinline__ void feistel4_pk16(const uint32_t x[4], uint32_t h, const uint32_t *kp,
+                                              uint32_t y[4]) {
+    const uint32_t mask = (1u << h) - 1u;
+    uint32_t L0 = (x[0] >> h) | ((x[1] >> h) << 16), R0 = (x[0] & mask) | ((x[1] & mask) << 16);
+    uint32_t L1 = (x[2] >> h) | ((x[3] >> h) << 16), R1 = (x[2] & mask) | ((x[3] & mask) << 16);
+    const pss_u16x2 M = {(unsigned short)kFeistelM16, (unsigned short)kFeistelM16};
+    const pss_u16x2 SH = {(unsigned short)(16u - h), (unsigned short)(16u - h)};
+#pragma unroll
+    for (int i = 0; i < kFeistelRounds; i++) {
+        const pss_u16x2 a0 = __builtin_bit_cast(pss_u16x2, R0 ^ kp[i]);
+        const pss_u16x2 a1 = __builtin_bit_cast(pss_u16x2, R1 ^ kp[i]);
+        const pss_u16x2 f0 = (a0 * M) >> SH;
+        const pss_u16x2 f1 = (a1 * M) >> SH;
+        const uint32_t t0 = L0 ^ __builtin_bit_cast(uint32_t, f0);
+        const uint32_t t1 = L1 ^ __builtin_bit_cast(uint32_t, f1);
+        L0 = R0; R0 = t0;
+        L1 = R1; R1 = t1;
+    }
+    y[0] = ((L0 & 0xFFFFu) << h) | (R0 & 0xFFFFu);
+    y[1] = ((L0 >> 16) << h) | (R0 >> 16);
+    y[2] = ((L1 & 0xFFFFu) << h) | (R1 & 0xFFFFu);
+    y[3] = ((L1 >> 16) << h) | (R1 >> 16);
+}
+
 // Feistel round keys of pool2 window w: Philox blocks (w, 0, rank, INS) and (w, 1, rank, INS),
 // 8 words of which the first kFeistelRounds are used
 constexpr int kRoundKeyWords = 8;

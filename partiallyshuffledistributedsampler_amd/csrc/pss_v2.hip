@@ -16,6 +16,7 @@
 //                    same launch (or on the probe / HBM paths): final pool1 drained in the
 //                    order of a keyed Feistel bijection of [0, P1)
 #include <cstdlib>
+#include <type_traits>
 
 #include "pss_device.h"
 
@@ -529,8 +530,11 @@ __global__ __launch_bounds__(64) void k_v2_emit_x(Geometry g, V2Plan pl,
     const uint32_t P1 = (uint32_t)pl.P1;
     const uint32_t B = pl.B32;
     const uint32_t nwin_max = pl.L32 / B + 2;
-    uint32_t *rk = smem;                                    // Feistel keys of the tile's windows
-    uint32_t *buf = smem + kRoundKeyWords * nwin_max;       // slot table
+    // slot table at LDS offset 0 (exchange addresses are 4 * slot, no base add), then the
+    // Feistel keys of the tile's windows
+    uint32_t *buf = smem;
+    uint32_t *rk = smem + ((P1 + 3u) & ~3u);
+    (void)nwin_max;
     const int lane = threadIdx.x;
     // 32-bit tile arithmetic from the plan's host-computed constants (T < 2^32)
     const uint32_t ngu = (uint32_t)ng;
@@ -538,6 +542,19 @@ __global__ __launch_bounds__(64) void k_v2_emit_x(Geometry g, V2Plan pl,
     const uint32_t tile = (uint32_t)g_lo + (blockIdx.x - (uint32_t)rl * ngu);
     const uint32_t rank = (uint32_t)(rank_lo + rl);
     const RankDesc rd = ranks[rank];
+    const uint32_t twoB = pl.twoB;
+    const uint32_t old32 = (uint32_t)rd.old_start, new32 = (uint32_t)rd.new_start;
+    const uint32_t N32 = (uint32_t)g.N;
+    // NARROW: the slot table holds final ids (converted on insertion, emitted as they come out
+    // of the exchange); otherwise virtual indices, converted on emission
+    auto to_slot = [&](uint32_t v) -> uint32_t {
+        if constexpr (NARROW) return (uint32_t)emit_id<true>(v, twoB, old32, new32, N32, rd, g);
+        else return v;
+    };
+    auto from_slot = [&](uint32_t x) -> int64_t {
+        if constexpr (NARROW) return (int64_t)x;
+        else return emit_id<false>(x, twoB, old32, new32, N32, rd, g);
+    };
     const uint32_t tlo = tile * pl.L32;
     const uint32_t thi = pl.T32 - tlo < pl.L32 ? pl.T32 : tlo + pl.L32;
     const uint32_t w_lo = 1 + tlo / B;
@@ -548,7 +565,7 @@ __global__ __launch_bounds__(64) void k_v2_emit_x(Geometry g, V2Plan pl,
         const uint32_t *VALr = VAL + (int64_t)rl * pl.G * pl.P1;
         const uint32_t *prev = VALr + ((int64_t)tile - 1) * pl.P1;   // tile 0: never read
         if (tile == 0) {
-            for (uint32_t s = lane; s < P1; s += 64) buf[s] = s;
+            for (uint32_t s = lane; s < P1; s += 64) buf[s] = to_slot(s);
         } else if ((P1 & 1023u) == 0) {
             const uint4 *p4 = (const uint4 *)prev;
             for (uint32_t q0 = 0; q0 < P1 / 4; q0 += 1024) {
@@ -565,7 +582,7 @@ __global__ __launch_bounds__(64) void k_v2_emit_x(Geometry g, V2Plan pl,
                     uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
 #pragma unroll
                     for (int c = 0; c < 4; c++)
-                        if (w[c] == kNone) w[c] = slot_value_after(VALr, pl.P1, (int64_t)tile - 2, 4 * q + c);
+                        w[c] = to_slot(w[c] != kNone ? w[c] : slot_value_after(VALr, pl.P1, (int64_t)tile - 2, 4 * q + c));
                     *(uint4 *)(buf + 4 * q) = make_uint4(w[0], w[1], w[2], w[3]);
                 }
             }
@@ -580,7 +597,7 @@ __global__ __launch_bounds__(64) void k_v2_emit_x(Geometry g, V2Plan pl,
 #pragma unroll
                 for (int u = 0; u < 4; u++) {
                     const uint32_t s = s0 + 64 * u;
-                    if (s < P1) buf[s] = v[u] != kNone ? v[u] : slot_value_after(VALr, pl.P1, (int64_t)tile - 2, s);
+                    if (s < P1) buf[s] = to_slot(v[u] != kNone ? v[u] : slot_value_after(VALr, pl.P1, (int64_t)tile - 2, s));
                 }
             }
         }
@@ -594,9 +611,6 @@ __global__ __launch_bounds__(64) void k_v2_emit_x(Geometry g, V2Plan pl,
     const uint32_t e_lo = (uint32_t)(pos_lo > tlo ? (pos_lo - tlo < nvalid ? pos_lo - tlo : nvalid) : 0);
     const uint32_t e_hi = (uint32_t)(pos_hi < thi ? (pos_hi > tlo ? pos_hi - tlo : 0) : nvalid);
     int64_t *o = out + (int64_t)rl * count + ((int64_t)tlo - pos_lo);
-    const uint32_t twoB = pl.twoB;
-    const uint32_t old32 = (uint32_t)rd.old_start, new32 = (uint32_t)rd.new_start;
-    const uint32_t N32 = (uint32_t)g.N;
     const uint32_t hB = pl.hB;
     const bool walk_full = pl.walk_full;                     // full windows need cycle walking
     const uint32_t w_last = pl.w_last;                       // last pool2 window (may be short)
@@ -614,61 +628,141 @@ __global__ __launch_bounds__(64) void k_v2_emit_x(Geometry g, V2Plan pl,
     // fast super-batches: every step valid and emitted, B >= 256 (at most one window boundary
     // per super-batch), neither window short nor cycle-walking
     const bool fast_tile = e_lo == 0 && e_hi == nvalid && B >= 256 && !walk_full;
-    uint32_t kw[kFeistelRounds];     // round keys of window w0 (wave-uniform: SGPRs), packed
-    uint32_t kw_w = 0xFFFFFFFFu;     // twice into 16-bit halves (hB <= 7 on this path)
     Pacer pace(nvalid);
-    for (uint32_t tl0 = 0; tl0 < nvalid; tl0 += 256) {
-        pace.step(tl0);
-        if (fast_tile && tl0 + 256 <= nvalid && w0 + 1 < w_last) {
-            if (kw_w != w0) {
+    uint32_t tl0 = 0;
+    if (fast_tile && (B & 255u) == 0 && w_last > w_lo + 1) {
+        // Fast phase: whole super-batches of windows w_lo .. w_last - 2 (full, no cycle walk),
+        // as one counted loop per window with the window's round keys in SGPRs.  B % 256 == 0
+        // and tlo % 256 == 0 put every super-batch inside one window.
+        const uint32_t avail = (w_last - 1 - w_lo) * B - p0;     // steps before window w_last-1
+        uint32_t left = (avail < nvalid ? avail : nvalid) >> 8;  // super-batches
+        if constexpr (NARROW && POW2) {
+            // Keyed-carry form of the packed Feistel (feistel4_pk16's values): with
+            // A_i = R_i ^ K_i, A_{i+1} = A_{i-1} ^ F(A_i) ^ (K_{i-1} ^ K_{i+1}), one 3-input xor
+            // per round; the output is L = A_5 ^ K_5, R = A_4 ^ F(A_5) ^ K_4.  p0 is a multiple
+            // of 256 >= 2^hB, so R_0 = (64 j + lane) & mask is loop-invariant, L_0 = (p0 >> hB)
+            // | ((64 j + lane) >> hB) has disjoint halves, and A_0, F(A_0) are per-window
+            // constants: A_1 = C ^ (p0 >> hB) costs one xor.  The paired slot hashes take
+            // (pb | 64 q | lane) ^ s0 with pb = (t0 + tl0) / 2, again one xor of a constant.
+            const uint32_t h = hB, mask = (1u << h) - 1u;
+            const uint32_t j1 = 64u + lane, j2 = 128u + lane, j3 = 192u + lane;
+            const uint32_t Li0 = ((uint32_t)lane >> h) | ((j1 >> h) << 16);
+            const uint32_t Li1 = (j2 >> h) | ((j3 >> h) << 16);
+            const uint32_t Ri0 = ((uint32_t)lane & mask) | ((j1 & mask) << 16);
+            const uint32_t Ri1 = (j2 & mask) | ((j3 & mask) << 16);
+            const uint32_t hx0 = (uint32_t)lane ^ sk.s0, hx2 = (64u | (uint32_t)lane) ^ sk.s0;
+            const pss_u16x2 M = {(unsigned short)kFeistelM16, (unsigned short)kFeistelM16};
+            const pss_u16x2 SH = {(unsigned short)(16u - h), (unsigned short)(16u - h)};
+            const pss_u16x2 HS = {(unsigned short)h, (unsigned short)h};
+            auto F = [&](uint32_t a) -> uint32_t {
+                return __builtin_bit_cast(uint32_t, (__builtin_bit_cast(pss_u16x2, a) * M) >> SH);
+            };
+            auto hash2 = [&](uint32_t x) -> uint32_t {   // slot_hash after the s0 xor
+                x ^= x >> 16;
+                x *= 0x21F0AAADu;
+                x ^= x >> 15;
+                x ^= sk.s1;
+                x *= 0x735A2D97u;
+                x ^= x >> 15;
+                return x;
+            };
+            while (left) {
+                const uint32_t room = (B - p0) >> 8;
+                const uint32_t n = left < room ? left : room;
+                uint32_t kw[kFeistelRounds];
 #pragma unroll
                 for (int i = 0; i < kFeistelRounds; i++)
                     kw[i] = (__builtin_amdgcn_readfirstlane(rk[kRoundKeyWords * (w0 - wl) + i]) & 0xFFFFu) * 0x10001u;
-                kw_w = w0;
+                const uint32_t K02 = kw[0] ^ kw[2], K13 = kw[1] ^ kw[3];
+                const uint32_t K24 = kw[2] ^ kw[4], K35 = kw[3] ^ kw[5];
+                const uint32_t KY = kw[4] ^ ((((kw[5] & 0xFFFFu) << h) & 0xFFFFu) * 0x10001u);
+                const uint32_t A00 = Ri0 ^ kw[0], A01 = Ri1 ^ kw[0];
+                const uint32_t C0 = Li0 ^ F(A00) ^ kw[1], C1 = Li1 ^ F(A01) ^ kw[1];
+                // ids of the window's values wB + y: one add when the window maps contiguously
+                const uint32_t wB = w0 * B;
+                const uint32_t id_first = to_slot(wB), id_last = to_slot(wB + B - 1);
+                const bool contiguous = id_last - id_first == B - 1 && ((wB < twoB) == (wB + B - 1 < twoB));
+                pace.step(tl0);
+                auto run = [&](auto contig) {
+                    for (uint32_t i = 0; i < n; i++) {
+                        const uint32_t pb = (t0 + tl0) >> 1;
+                        const uint32_t u0 = hash2(hx0 ^ pb), u2 = hash2(hx2 ^ pb);
+                        const uint32_t k[4] = {u0 >> sh, (u0 << 16) >> sh, u2 >> sh, (u2 << 16) >> sh};
+                        const uint32_t s = (p0 >> h) * 0x10001u;
+                        const uint32_t A10 = C0 ^ s, A11 = C1 ^ s;
+                        const uint32_t F10 = F(A10), F11 = F(A11);
+                        const uint32_t A20 = A00 ^ F10 ^ K02, A21 = A01 ^ F11 ^ K02;
+                        const uint32_t F20 = F(A20), F21 = F(A21);
+                        const uint32_t A30 = A10 ^ F20 ^ K13, A31 = A11 ^ F21 ^ K13;
+                        const uint32_t F30 = F(A30), F31 = F(A31);
+                        const uint32_t A40 = A20 ^ F30 ^ K24, A41 = A21 ^ F31 ^ K24;
+                        const uint32_t F40 = F(A40), F41 = F(A41);
+                        const uint32_t A50 = A30 ^ F40 ^ K35, A51 = A31 ^ F41 ^ K35;
+                        const uint32_t F50 = F(A50), F51 = F(A51);
+                        const uint32_t S0 = __builtin_bit_cast(uint32_t, __builtin_bit_cast(pss_u16x2, A50) << HS);
+                        const uint32_t S1 = __builtin_bit_cast(uint32_t, __builtin_bit_cast(pss_u16x2, A51) << HS);
+                        const uint32_t Y0 = S0 ^ (A40 ^ F50 ^ KY), Y1 = S1 ^ (A41 ^ F51 ^ KY);
+                        const uint32_t y[4] = {Y0 & 0xFFFFu, Y0 >> 16, Y1 & 0xFFFFu, Y1 >> 16};
+                        uint32_t ins[4], v[4];
+#pragma unroll
+                        for (int j = 0; j < 4; j++) ins[j] = contig ? id_first + y[j] : to_slot(wB + y[j]);
+#pragma unroll
+                        for (int j = 0; j < 4; j++) v[j] = atomicExch(&buf[k[j]], ins[j]);
+                        int64_t *ob = o + tl0;
+#pragma unroll
+                        for (int j = 0; j < 4; j++) ob[64u * j + lane] = (int64_t)v[j];
+                        tl0 += 256;
+                        p0 += 256;
+                    }
+                };
+                if (contiguous) run(std::true_type{});
+                else run(std::false_type{});
+                left -= n;
+                if (p0 == B) { p0 = 0; w0++; }
             }
-            uint32_t k[4], ins[4], v[4];
-            if (p0 + 256 <= B) {
-                // the whole super-batch inserts from window w0: scalar round keys
-                slot4<POW2>(t0 + tl0 + lane, sk, P1, sh, k);
-#pragma unroll
-                for (int j = 0; j < 4; j += 2) {
-                    uint32_t y0, y1;
-                    feistel2_pk16(p0 + 64u * j + lane, p0 + 64u * (j + 1) + lane, hB, kw, y0, y1);
-                    ins[j] = w0 * B + y0;
-                    ins[j + 1] = w0 * B + y1;
-                }
-            } else {
-                slot4<POW2>(t0 + tl0 + lane, sk, P1, sh, k);
-#pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    uint32_t p = p0 + 64u * j + lane;
-                    const bool cross = p >= B;
-                    p = cross ? p - B : p;
-                    const uint32_t w = cross ? w0 + 1 : w0;
-                    ins[j] = w * B + feistel_once(p, hB, rk + kRoundKeyWords * (w - wl));
-                }
-            }
-#pragma unroll
-            for (int j = 0; j < 4; j++) v[j] = atomicExch(&buf[k[j]], ins[j]);
-            // wave-uniform base: the stores take (lane * 8 + 512 j) as offset, no 64-bit adds
-            int64_t *ob = o + tl0;
-#pragma unroll
-            for (int j = 0; j < 4; j++)
-                ob[64u * j + lane] = emit_id<NARROW>(v[j], twoB, old32, new32, N32, rd, g);
         } else {
+            while (left) {
+                const uint32_t room = (B - p0) >> 8;
+                const uint32_t n = left < room ? left : room;
+                uint32_t kw[kFeistelRounds];   // window w0's round keys, packed twice into 16 bits
 #pragma unroll
-            for (int j = 0; j < 4; j++) {
-                const uint32_t tl = tl0 + 64u * j + lane;
-                if (tl < nvalid) {
-                    const uint32_t kk = slot_draw(t0 + tl, sk.s0, sk.s1, P1);
-                    uint32_t p = p0 + 64u * j + lane, w = w0;
-                    while (p >= B) { p -= B; w++; }
-                    const bool lastw = w == w_last;
-                    const uint32_t in = w * B + feistel(p, lastw ? len_last : B, lastw ? h_last : hB,
-                                                        rk + kRoundKeyWords * (w - wl));
-                    const uint32_t vv = atomicExch(&buf[kk], in);
-                    if (tl >= e_lo && tl < e_hi) o[tl] = emit_id<NARROW>(vv, twoB, old32, new32, N32, rd, g);
+                for (int i = 0; i < kFeistelRounds; i++)
+                    kw[i] = (__builtin_amdgcn_readfirstlane(rk[kRoundKeyWords * (w0 - wl) + i]) & 0xFFFFu) * 0x10001u;
+                const uint32_t wB = w0 * B;
+                pace.step(tl0);
+                for (uint32_t i = 0; i < n; i++) {
+                    uint32_t k[4], ins[4], v[4];
+                    slot4<POW2>(t0 + tl0 + lane, sk, P1, sh, k);
+                    const uint32_t x[4] = {p0 + lane, p0 + 64u + lane, p0 + 128u + lane, p0 + 192u + lane};
+                    feistel4_pk16(x, hB, kw, ins);
+#pragma unroll
+                    for (int j = 0; j < 4; j++) v[j] = atomicExch(&buf[k[j]], to_slot(wB + ins[j]));
+                    // wave-uniform base: the stores take (lane * 8 + 512 j) as offset
+                    int64_t *ob = o + tl0;
+#pragma unroll
+                    for (int j = 0; j < 4; j++) ob[64u * j + lane] = from_slot(v[j]);
+                    tl0 += 256;
+                    p0 += 256;
                 }
+                left -= n;
+                if (p0 == B) { p0 = 0; w0++; }
+            }
+        }
+    }
+    for (; tl0 < nvalid; tl0 += 256) {
+        pace.step(tl0);
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const uint32_t tl = tl0 + 64u * j + lane;
+            if (tl < nvalid) {
+                const uint32_t kk = slot_draw(t0 + tl, sk.s0, sk.s1, P1);
+                uint32_t p = p0 + 64u * j + lane, w = w0;
+                while (p >= B) { p -= B; w++; }
+                const bool lastw = w == w_last;
+                const uint32_t in = w * B + feistel(p, lastw ? len_last : B, lastw ? h_last : hB,
+                                                    rk + kRoundKeyWords * (w - wl));
+                const uint32_t vv = atomicExch(&buf[kk], to_slot(in));
+                if (tl >= e_lo && tl < e_hi) o[tl] = from_slot(vv);
             }
         }
         p0 += 256;
@@ -709,13 +803,13 @@ __global__ __launch_bounds__(64) void k_v2_emit_x(Geometry g, V2Plan pl,
                 for (int u = 0; u < 4; u++) v[u] = buf[y[u]];
 #pragma unroll
                 for (int u = 0; u < 4; u++)
-                    ot[j0 + 64u * u + lane] = emit_id<NARROW>(v[u], twoB, old32, new32, N32, rd, g);
+                    ot[j0 + 64u * u + lane] = from_slot(v[u]);
             }
         } else {
             for (uint32_t j = lane; j < P1; j += 64) {
                 const int64_t pos = pl.T + j;
                 if (pos < pos_lo || pos >= pos_hi) continue;
-                ot[j] = emit_id<NARROW>(buf[feistel(j, P1, hT, tk)], twoB, old32, new32, N32, rd, g);
+                ot[j] = from_slot(buf[feistel(j, P1, hT, tk)]);
             }
         }
     }
@@ -994,7 +1088,7 @@ hipError_t launch_v2(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, 
             const dim3 grid((uint32_t)(nr * ng));
             if (!pl.global_buf && emit_path == EMIT_XCHG) {
                 mk(K_V2_EMIT, s);
-                const size_t need = lds_keys + (size_t)pl.P1 * 4;
+                const size_t need = lds_keys + (size_t)((pl.P1 + 3) & ~3) * 4;
                 const size_t lds = need > (size_t)pl.emit_lds ? need : (size_t)pl.emit_lds;
                 tail_fused = need_tail && last_emit == pl.G - 1;
                 const int dt = tail_fused ? 1 : 0;

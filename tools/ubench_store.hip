@@ -24,6 +24,17 @@ __global__ __launch_bounds__(64) void k(int64_t *out, uint32_t n, uint32_t salt)
                 longlong2 v; v.x = s + salt; v.y = s + 1 + salt;
                 *(longlong2 *)(o + s) = v;
             }
+    } else if (MODE == 3) {     // dwordx2, grid-interleaved: wave b writes 2 KB chunks b, b+grid, ...
+        const uint32_t G = gridDim.x;
+        for (uint32_t b = 0; b < n; b += 256)
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+                out[((size_t)(b >> 8) * G + blockIdx.x) * 256 + 64 * j + lane] = (int64_t)(b + 64 * j + lane + salt);
+    } else if (MODE == 4) {     // dwordx2, contiguous runs at a padded stride (n + 512 ids)
+        int64_t *op = out + (size_t)blockIdx.x * (n + 512);
+        for (uint32_t b = 0; b < n; b += 256)
+#pragma unroll
+            for (int j = 0; j < 4; j++) op[b + 64 * j + lane] = (int64_t)(b + 64 * j + lane + salt);
     } else {                    // dwordx2 with nontemporal hint
         for (uint32_t b = 0; b < n; b += 256)
 #pragma unroll
@@ -51,10 +62,14 @@ void run(const char *name, int64_t *out, int blocks, uint32_t n, int lds) {
 int main() {
     const uint32_t n = 48896;
     int64_t *out;
-    hipMalloc(&out, (size_t)8192 * n * 8);
+    hipMalloc(&out, (size_t)8192 * (n + 1024) * 8);
     run<0>("dwordx2", out, 2048, n, 18220);
     run<1>("dwordx4", out, 2048, n, 18220);
     run<2>("dwordx2-nt", out, 2048, n, 18220);
+    run<3>("interleaved", out, 2048, n, 18220);
+    run<4>("stride+4K", out, 2048, n, 18220);
+    run<0>("dwordx2 49152", out, 2048, 49152, 18220);
+    run<0>("dwordx2 48640", out, 2048, 48640, 18220);
     run<0>("dwordx2", out, 4096, n / 2, 9000);
     run<1>("dwordx4", out, 4096, n / 2, 9000);
     run<0>("dwordx2", out, 8192, n / 4, 4000);
