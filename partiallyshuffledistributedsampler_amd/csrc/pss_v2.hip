@@ -559,6 +559,22 @@ __global__ __launch_bounds__(64) void k_v2_emit_x(Geometry g, V2Plan pl,
     const uint32_t thi = pl.T32 - tlo < pl.L32 ? pl.T32 : tlo + pl.L32;
     const uint32_t w_lo = 1 + tlo / B;
     const int nwin = (int)(1 + (thi - 1) / B - w_lo + 1);
+    // the tile's window keys and the slot key are independent of the slot table: their loads
+    // are issued first and land while the table streams in
+    constexpr int kKeyPre = 3;                    // nwin <= L / B + 2 <= 18 windows of 8 words
+    const int nkw = nwin * kRoundKeyWords;
+    uint32_t kpre[kKeyPre];
+    SlotKey sk;
+    const bool key_pre = kt.p && nkw <= 64 * kKeyPre;
+    if (key_pre) {
+        const uint32_t *kb = kt.p + rl * kt.stride;
+        sk = SlotKey{kb[0], kb[1]};
+        kb += 16 + kRoundKeyWords * (w_lo - 1);
+#pragma unroll
+        for (int i = 0; i < kKeyPre; i++) kpre[i] = lane + 64 * i < nkw ? kb[lane + 64 * i] : 0u;
+    } else {
+        sk = slot_key_t(g, rank, kt, rl);
+    }
     {   // slot table at the tile's start: 16-byte loads, up to 16 per lane in flight (the whole
         // 16 KB table of P1 = 4096 in one round trip); slots the previous tile never drew walk
         // back further (probability e^-(L/P1))
@@ -571,14 +587,10 @@ __global__ __launch_bounds__(64) void k_v2_emit_x(Geometry g, V2Plan pl,
             for (uint32_t q0 = 0; q0 < P1 / 4; q0 += 1024) {
                 uint4 v[16];
 #pragma unroll
-                for (int u = 0; u < 16; u++) {
-                    const uint32_t q = q0 + 64u * u + lane;
-                    v[u] = q < P1 / 4 ? p4[q] : make_uint4(0, 0, 0, 0);
-                }
+                for (int u = 0; u < 16; u++) v[u] = p4[q0 + 64u * u + lane];   // q < P1/4: P1 % 1024 == 0
 #pragma unroll
                 for (int u = 0; u < 16; u++) {
                     const uint32_t q = q0 + 64u * u + lane;
-                    if (q >= P1 / 4) continue;
                     uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
 #pragma unroll
                     for (int c = 0; c < 4; c++)
@@ -602,8 +614,13 @@ __global__ __launch_bounds__(64) void k_v2_emit_x(Geometry g, V2Plan pl,
             }
         }
     }
-    stage_keys_t(g, rank, w_lo, nwin, rk, kt, rl);
-    const SlotKey sk = slot_key_t(g, rank, kt, rl);
+    if (key_pre) {
+#pragma unroll
+        for (int i = 0; i < kKeyPre; i++)
+            if (lane + 64 * i < nkw) rk[lane + 64 * i] = kpre[i];
+    } else {
+        stage_keys_t(g, rank, w_lo, nwin, rk, kt, rl);
+    }
     __syncthreads();
     // tile-local step tl = t - tlo (tlo is a multiple of 256); the tile emits tl in [e_lo, e_hi)
     const int64_t pos_hi = pos_lo + count;
