@@ -21,8 +21,12 @@ int main() {
     init_kernel_attributes_v2();
     int64_t *out; hipMalloc(&out, sizeof(int64_t) * 8 * g.ns);
     uint32_t *val; hipMalloc(&val, v2_val_bytes(g, 8));
+    // full replays, then the last-occurrence pass alone (the emit kernel writes the same stamp
+    // slots), back to back
     for (int it = 0; it < 3; it++)
         launch_v2(g, d_rd, 0, 8, 0, g.ns, out, val, nullptr, nullptr, nullptr, 0, Marker(), EMIT_XCHG);
+    for (int it = 0; it < 5; it++)
+        launch_v2(g, d_rd, 0, 8, 0, g.ns, out, val, nullptr, nullptr, nullptr, 0, Marker(), EMIT_XCHG, V2_STAGE_PRE);
     hipDeviceSynchronize();
     const V2Plan pl = v2_plan(g, 8);
     const int nwg = (int)(8 * pl.G);
