@@ -947,6 +947,11 @@ V2Plan v2_plan(const Geometry &g, int32_t nr) {
     static const int64_t mult_env = [] {
         const char *e = getenv("PSS_V2_TILE_MULT");   // tuning knob: tile = mult * P1 steps
         const long v = e ? atol(e) : 0;
+        return (int64_t)(v > 0 ? (v < kMaxTileMult ? v : kMaxTileMult) : 0);
+    }();
+    static const int64_t wpc_env = [] {   // tuning knob: emit waves per CU the tiling targets
+        const char *e = getenv("PSS_V2_WPC");
+        const long v = e ? atol(e) : 0;
         return (int64_t)(v > 0 ? v : 0);
     }();
     // emit wave LDS: Feistel keys of up to kMaxTileMult + 2 windows, the slot table, the probe
@@ -957,6 +962,7 @@ V2Plan v2_plan(const Geometry &g, int32_t nr) {
     int64_t wpc = kCuLdsBytes / lds;
     wpc = wpc > 16 ? 16 : wpc;
     if (wpc >= 4) wpc &= ~3;
+    if (wpc_env && wpc_env < wpc) wpc = wpc_env;
     p.emit_lds = lds;
     if (wpc >= 1 && kCuLdsBytes / (wpc + 1) >= lds) p.emit_lds = kCuLdsBytes / (wpc + 1) + 16;
     static const int64_t lds_env = [] {   // experiment knob: explicit emit LDS bytes per wave

@@ -70,6 +70,8 @@ int main() {
     run<4>("stride+4K", out, 2048, n, 18220);
     run<0>("dwordx2 49152", out, 2048, 49152, 18220);
     run<0>("dwordx2 48640", out, 2048, 48640, 18220);
+    run<0>("dwordx2 4/CU", out, 1024, 2 * n, 36000);
+    run<0>("dwordx2 2/CU", out, 512, 4 * n, 72000);
     run<0>("dwordx2", out, 4096, n / 2, 9000);
     run<1>("dwordx4", out, 4096, n / 2, 9000);
     run<0>("dwordx2", out, 8192, n / 4, 4000);
