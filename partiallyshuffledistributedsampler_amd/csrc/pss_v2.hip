@@ -113,11 +113,15 @@ __global__ __launch_bounds__(NT) void k_v2_lastocc(Geometry g, V2Plan pl, int32_
             else st[j] = base + 128u * ((threadIdx.x >> 6) + (NT / 64) * (j >> 1)) + 64u * (j & 1) + (threadIdx.x & 63u);
         }
         if (POW2 && !ORDERED) {
+            // t0 + base is a multiple of 256, so the pair index of st[j] (j even) is
+            // (t0 + base) / 2 + 64 (wave + NT/64 (j/2)) + lane: one add of a per-thread constant
+            const uint32_t pb = (t0 + base) >> 1;
 #pragma unroll
             for (int j = 0; j < 8; j += 2) {
-                const uint32_t u = slot_hash(slot_pair_index(t0 + st[j]), sk.s0, sk.s1);
+                const uint32_t c = 64u * ((threadIdx.x >> 6) + (NT / 64) * (j >> 1)) + (threadIdx.x & 63u);
+                const uint32_t u = slot_hash(pb + c, sk.s0, sk.s1);
                 k[j] = u >> sh;
-                k[j + 1] = (u << 16) >> sh;
+                k[j + 1] = (u & 0xFFFFu) >> (sh - 16u);
             }
         } else {
 #pragma unroll
