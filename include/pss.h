@@ -107,6 +107,19 @@ int pss_check(pss_sampler *h, void *stream);
 int pss_set_emit_path(pss_sampler *h, int32_t path);
 int pss_emit_path(pss_sampler *h, int32_t *path);
 
+/* Order of the ids inside a pool (extension; the multiset and the file / rank assignment are
+ * the reference's in both modes):
+ *   PSS_ORDER_COUNTER (0, default) -- the counter-based schedule (Philox / Feistel, DESIGN.md
+ *       §3): per-sampler, independent of the process-global `random` state;
+ *   PSS_ORDER_EXACT   (1) -- V1 only: each window is `seed(epoch + b*10000); shuffle(range(n))`
+ *       with CPython's MT19937 exactly as V1:102,114-115,165-171 draws it, so the id stream is
+ *       bit-identical to the reference's.  PSS_ENOTSUP for V2 and for shuffle_buffer > 8192.
+ * Replaces nothing in the reference: its order IS the exact one. */
+#define PSS_ORDER_COUNTER 0
+#define PSS_ORDER_EXACT 1
+int pss_set_order_mode(pss_sampler *h, int32_t mode);
+int pss_order_mode(const pss_sampler *h, int32_t *mode);
+
 /* Self-test of the wave64 DPP scan primitive: out_dev[2i] = 64-bit inclusive wave scan,
  * out_dev[2i+1] = 32-bit one (low words), for n inputs. */
 int pss_debug_wave_scan(const uint64_t *in_dev, uint64_t *out_dev, int64_t n, void *stream);

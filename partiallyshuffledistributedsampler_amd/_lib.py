@@ -37,6 +37,8 @@ SIGNATURES = {
     "pss_profile": ([_vp, _i32], ctypes.c_int),
     "pss_set_emit_path": ([_vp, _i32], ctypes.c_int),
     "pss_emit_path": ([_vp, _c_i32p], ctypes.c_int),
+    "pss_set_order_mode": ([_vp, _i32], ctypes.c_int),
+    "pss_order_mode": ([_vp, _c_i32p], ctypes.c_int),
     "pss_profile_read": ([_vp, ctypes.POINTER(ctypes.c_double), _c_i64p, _i32], ctypes.c_int),
     "pss_debug_wave_scan": ([_vp, _vp, _i64, _vp], ctypes.c_int),
 }

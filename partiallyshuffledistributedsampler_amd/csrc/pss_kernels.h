@@ -134,6 +134,13 @@ hipError_t launch_v1(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, 
                      int32_t *err, hipStream_t s, const Marker &mk = Marker());
 size_t v1_workspace_bytes(const Geometry &g, int32_t nr, int64_t pos_lo, int64_t count);
 
+// V1 in the reference's exact order (CPython MT19937 per window, pss_v1exact.hip): windows up
+// to kV1ExactMaxB elements (LDS-resident draw and bucket arrays)
+constexpr int64_t kV1ExactMaxB = 8192;
+bool v1_exact_supported(const Geometry &g);
+hipError_t launch_v1_exact(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, int32_t nr,
+                           int64_t pos_lo, int64_t count, int64_t epoch, int64_t *out, hipStream_t s);
+
 // V2 replay kernel: EMIT_XCHG = one LDS exchange per step (needs the lane-ordered exchange the
 // start-up check confirms), EMIT_PROBE = collision probe + per-clash fix-up (any hardware)
 enum EmitPath { EMIT_AUTO = 0, EMIT_XCHG = 1, EMIT_PROBE = 2 };

@@ -246,6 +246,7 @@ struct pss_sampler {
     int64_t F = 0, N = 0, ns = 0, B = 0;
     int32_t R = 0, version = 1, shuffle = 1, device = 0;
     int32_t emit_path = 0;        // pss::EmitPath
+    int32_t order_mode = 0;       // PSS_ORDER_COUNTER / PSS_ORDER_EXACT
     std::unique_ptr<PermPrefetcher> perms;   // file permutations of the coming epochs
     uint64_t seed = 0;
     // history state
@@ -518,7 +519,10 @@ int pss_generate(pss_sampler *h, int32_t rank_lo, int32_t rank_hi, int64_t pos_l
     const pss::Geometry g = h->geometry();
     const pss::Marker mk = marker_of(h);
     auto words = [](size_t bytes) { return (bytes + sizeof(uint32_t) - 1) / sizeof(uint32_t); };
-    if (h->version == 1) {
+    if (h->version == 1 && h->order_mode == PSS_ORDER_EXACT && g.shuffle) {
+        mk(pss::K_V1, s);
+        PSS_HIP(pss::launch_v1_exact(g, h->d_ranks.p, rank_lo, nr, pos_lo, count, h->epoch, out_dev, s));
+    } else if (h->version == 1) {
         const size_t sb = pss::v1_workspace_bytes(g, nr, pos_lo, count);
         if (sb) PSS_HIP(h->d_sort.ensure(words(sb)));
         PSS_HIP(pss::launch_v1(g, h->d_ranks.p, rank_lo, nr, pos_lo, count, out_dev, h->d_sort.p, h->d_err.p, s, mk));
@@ -544,6 +548,24 @@ int pss_set_emit_path(pss_sampler *h, int32_t path) {
             return fail(PSS_ENOTSUP, "device failed the LDS exchange-order check");
     }
     h->emit_path = path;
+    return PSS_OK;
+}
+
+int pss_set_order_mode(pss_sampler *h, int32_t mode) {
+    if (!h) return fail(PSS_EINVAL, "NULL handle");
+    if (mode != PSS_ORDER_COUNTER && mode != PSS_ORDER_EXACT) return fail(PSS_EINVAL, "bad order mode");
+    if (mode == PSS_ORDER_EXACT) {
+        if (h->version != 1) return fail(PSS_ENOTSUP, "exact order is implemented for V1 windows only");
+        if (!pss::v1_exact_supported(h->geometry()))
+            return fail(PSS_ENOTSUP, "exact order needs shuffle_buffer <= 8192");
+    }
+    h->order_mode = mode;
+    return PSS_OK;
+}
+
+int pss_order_mode(const pss_sampler *h, int32_t *mode) {
+    if (!h || !mode) return fail(PSS_EINVAL, "NULL argument");
+    *mode = h->order_mode;
     return PSS_OK;
 }
 

@@ -32,7 +32,7 @@ class IndexEngine:
     """Device index generator of one sampler configuration (all R logical ranks)."""
 
     def __init__(self, files_len, total_size, num_replicas, shuffle_buffer, version,
-                 shuffle=True, seed=0, device=0):
+                 shuffle=True, seed=0, device=0, order="counter"):
         lib = _lib.load()
         fl = np.ascontiguousarray(files_len, dtype=np.int64)
         self.num_files = len(fl)
@@ -51,6 +51,8 @@ class IndexEngine:
         _lib.check(lib.pss_num_samples(h, ctypes.byref(ns)), "pss_num_samples")
         self.num_samples = ns.value
         self.epoch = None
+        if order != "counter":
+            self.set_order_mode(order)
 
     def close(self):
         if getattr(self, "_h", None):
@@ -154,6 +156,19 @@ class IndexEngine:
         v = ctypes.c_int32()
         _lib.call("pss_emit_path", self._h, ctypes.byref(v))
         return {1: "xchg", 2: "probe"}[v.value]
+
+    ORDER_MODES = {"counter": 0, "exact": 1}
+
+    def set_order_mode(self, mode):
+        """Order of ids inside a pool: "counter" (the counter-based schedule, default) or
+        "exact" (V1 only: each window shuffled with CPython's MT19937 exactly as the reference
+        does, V1:102,114-115,165-171 -- the id stream is bit-identical to the reference's)."""
+        _lib.call("pss_set_order_mode", self._h, self.ORDER_MODES[mode])
+
+    def order_mode(self):
+        v = ctypes.c_int32()
+        _lib.call("pss_order_mode", self._h, ctypes.byref(v))
+        return {0: "counter", 1: "exact"}[v.value]
 
     KERNEL_KINDS = ("scan", "v1_window", "v2_lastocc", "v2_emit", "v2_tail", "map",
                     "partition", "digest")

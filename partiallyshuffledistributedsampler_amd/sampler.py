@@ -10,6 +10,8 @@ Differences from the reference, all deliberate:
     `random` module: file order, blocks, start_num (the file -> rank assignment) and every
     rank's per-epoch multiset are bit-identical to the reference, the order inside a pool is
     an independent uniform shuffle.  The global `random` state is never touched.
+    `order="exact"` (V1) instead shuffles every window with CPython's MT19937 exactly as the
+    reference does (V1:102,114-115,165-171): the id stream is then bit-identical too.
   * find_ckpt_position is an O(1) skip-ahead on the same stream (V1's reference resume
     leaves the current window unshuffled, V1:139; V2's replays every draw, V2:121-122).
   * file lengths missing from files_len are probed for every file at the first __iter__
@@ -33,7 +35,7 @@ class _PartialShuffleSampler(Sampler):
     def __init__(self, dataset, reader, num_replicas=None, rank=None, shuffle=True,
                  shuffle_buffer=None, total_size=None, batch_size=1, file_buffer=10,
                  debug=False, files_len=None, *, seed=0, device=None, copy_chunk=1 << 18,
-                 gc_on_evict=False):
+                 gc_on_evict=False, order="counter"):
         if num_replicas is None:                                    # V1:19-26
             if not dist.is_available():
                 raise RuntimeError("Requires distributed package to be available")
@@ -69,6 +71,7 @@ class _PartialShuffleSampler(Sampler):
         self.count_batches = 0
         self.warm_start = False
         self.seed = seed
+        self.order = order     # "counter" or "exact" (V1: the reference's own window order)
         self.device = device
         self.copy_chunk = int(copy_chunk)
         self._engine = None
@@ -94,7 +97,7 @@ class _PartialShuffleSampler(Sampler):
             self.device = int(dev.index if isinstance(dev, torch.device) else dev)
             self._engine = IndexEngine(self._lengths(), self.ori_total_size, self.num_replicas,
                                        self.shuffle_buffer, self._VERSION, shuffle=self.shuffle,
-                                       seed=self.seed, device=self.device)
+                                       seed=self.seed, device=self.device, order=self.order)
         return self._engine
 
     # ---- epoch ----------------------------------------------------------------------------

@@ -262,3 +262,64 @@ def test_v2_large_pool_paths_match_oracle(path, B, R, F, lo, hi):
         part = eng.generate(0, R, pos_lo, count).cpu().numpy()
         c = min(count, ns - pos_lo)
         assert np.array_equal(part[:, :c], full[:, pos_lo:pos_lo + c]), (pos_lo, count)
+
+
+# ---- exact-order mode (V1): the reference's own CPython-MT window shuffles ----------------
+@pytest.mark.parametrize("name", scenario_names("v1"))
+def test_v1_exact_order_matches_reference_streams(name):
+    """order="exact": every rank's id stream equals the stream the reference itself produced
+    (tests/golden, captured from V1:178), not only its multiset."""
+    fx = load(name)
+    files, lengths, fl, N, R, B, bs, shuffle = fixture_params(fx)
+    lens = [fl.get(p, lengths[p]) if fl else lengths[p] for p in files]
+    eng = pss.IndexEngine(lens, N, R, B, 1, shuffle=shuffle, seed=0, device=0, order="exact")
+    assert eng.order_mode() == "exact"
+    for ep_i, er0 in enumerate(fx["ranks"][0]["epochs"]):
+        eng.init_iter(er0["epoch"])
+        out = eng.generate(0, R).cpu().numpy()
+        for rrec in fx["ranks"]:
+            er = rrec["epochs"][ep_i]
+            if er.get("resume_step") is not None:
+                continue   # the reference's lossy resume (V1:139) is not reproduced
+            # the reference's recorded raw stream (its batches, in order) is a prefix of ours
+            rec = [x for b in er["batches"] for x in b]
+            assert out[rrec["rank"]][:len(rec)].tolist() == rec, (name, rrec["rank"], er["epoch"])
+            ref = O.v1_exact_stream(er["epoch"], er["start_num"], eng.num_samples, B, N, shuffle)
+            assert np.array_equal(out[rrec["rank"]], ref), (name, rrec["rank"], er["epoch"])
+
+
+@pytest.mark.parametrize("F,lo,hi,R,B,epochs", [
+    (64, 10000, 10001, 2, 4096, (0, 1)),            # C1 (BASELINE configs[0])
+    (37, 1, 900, 7, 40, (0, 5)),
+    (50, 1000, 5000, 3, 3000, (2,)),                # partial last window
+    (40, 2000, 9000, 2, 8192, (1,)),                # largest exact window
+    (13, 1, 50, 5, 100, (0, 9)),                    # ns < B
+    (100, 1, 3, 8, 7, (0,)),                        # tiny windows
+    (30, 100, 400, 3, 257, (2 ** 32 - 30000,)),     # window seeds cross 2^32 (two-word MT keys)
+])
+def test_v1_exact_order_matches_exact_oracle(F, lo, hi, R, B, epochs):
+    rng = np.random.default_rng(F + B)
+    lengths = rng.integers(lo, hi, F)
+    N = int(lengths.sum())
+    eng = pss.IndexEngine(lengths, N, R, B, 1, seed=7, device=0, order="exact")
+    ns = eng.num_samples
+    for epoch in epochs:
+        eng.init_iter(epoch)
+        _, new = eng.rank_starts()
+        out = eng.generate(0, R).cpu().numpy()
+        for r in range(R):
+            ref = O.v1_exact_stream(epoch, int(new[r]), ns, B, N, True)
+            assert np.array_equal(out[r], ref), (F, B, epoch, r)
+        if ns > 3:   # position sub-ranges come out of the same windows
+            lo_p, cnt = ns // 3, ns // 2
+            part = eng.generate(1, R, lo_p, cnt).cpu().numpy()
+            assert np.array_equal(part, out[1:, lo_p:lo_p + cnt])
+
+
+def test_exact_order_unsupported_configs():
+    from partiallyshuffledistributedsampler_amd import _lib
+    lengths = np.full(10, 1000)
+    with pytest.raises(_lib.PSSError):
+        pss.IndexEngine(lengths, 10000, 2, 100, 2, device=0, order="exact")      # V2
+    with pytest.raises(_lib.PSSError):
+        pss.IndexEngine(lengths, 10000, 2, 16384, 1, device=0, order="exact")    # B > 8192

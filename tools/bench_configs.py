@@ -3,8 +3,11 @@
 
 Not the driver's bench line (that is bench.py, C2); this measures the other configurations the
 survey names, each as the share one of 8 GPUs would generate:
+  c1     V1, 64 files x 10K, R=2 (BASELINE configs[0])              B=4096
+  c1x    C1 with order="exact" (the reference's CPython-MT window order)
   c2     V2, 10K files x 10K, R=8 (all 8 ranks)                      B=4096
   c2v1   V1 on the same files                                        B=4096
+  c2v1x  c2v1 with order="exact"
   c3     V2, 100K files x 10K = 1B, R=1024 -> ranks [0, 128)         B=4096
   c4     V2, Zipf(1.5)*150 files (N=2.59e9 > 2^31), R=4096 -> [0, 512)  B=4096
   c5     V2, C2 files, B=2^20 (HBM slot-table path), 100 epochs       (reports per-epoch mean)
@@ -23,9 +26,9 @@ sys.path.insert(0, ROOT)
 from partiallyshuffledistributedsampler_amd.engine import IndexEngine  # noqa: E402
 
 
-def run(name, lengths, R, r_hi, B, ver, steps, warmup=2):
+def run(name, lengths, R, r_hi, B, ver, steps, warmup=2, order="counter"):
     N = int(lengths.sum())
-    eng = IndexEngine(lengths, N, R, B, ver, seed=0, device=0)
+    eng = IndexEngine(lengths, N, R, B, ver, seed=0, device=0, order=order)
     ns = eng.num_samples
     out = torch.empty((r_hi, ns), dtype=torch.int64, device="cuda")
     for e in range(warmup):
@@ -43,16 +46,22 @@ def run(name, lengths, R, r_hi, B, ver, steps, warmup=2):
     eng.close()
     ids = r_hi * ns
     print(json.dumps({"config": name, "N": N, "R": R, "ranks_generated": r_hi, "B": B,
-                      "version": ver, "ids_per_step": ids, "ms_per_step": dt * 1e3,
+                      "version": ver, "order": order, "ids_per_step": ids, "ms_per_step": dt * 1e3,
                       "G_idx_per_s": ids / dt / 1e9,
                       "kernels_ms": {k: v[0] / steps for k, v in prof.items()}}), flush=True)
 
 
 def main():
-    which = sys.argv[1:] or ["c2", "c2v1", "c3", "c4", "c5"]
+    which = sys.argv[1:] or ["c1", "c1x", "c2", "c2v1", "c2v1x", "c3", "c4", "c5"]
     c2 = np.full(10_000, 10_000, dtype=np.int64)
     for w in which:
-        if w == "c2":
+        if w == "c1":      # BASELINE configs[0]: V1, 64 files x 10K, R=2
+            run(w, np.full(64, 10_000, dtype=np.int64), 2, 2, 4096, 1, 50)
+        elif w == "c1x":   # C1 in the reference's exact order (CPython MT per window)
+            run(w, np.full(64, 10_000, dtype=np.int64), 2, 2, 4096, 1, 50, order="exact")
+        elif w == "c2v1x":
+            run(w, c2, 8, 8, 4096, 1, 5, order="exact")
+        elif w == "c2":
             run(w, c2, 8, 8, 4096, 2, 20)
         elif w == "c2v1":
             run(w, c2, 8, 8, 4096, 1, 20)
