@@ -526,6 +526,11 @@ int pss_generate(pss_sampler *h, int32_t rank_lo, int32_t rank_hi, int64_t pos_l
         const size_t sb = pss::v1_workspace_bytes(g, nr, pos_lo, count);
         if (sb) PSS_HIP(h->d_sort.ensure(words(sb)));
         PSS_HIP(pss::launch_v1(g, h->d_ranks.p, rank_lo, nr, pos_lo, count, out_dev, h->d_sort.p, h->d_err.p, s, mk));
+    } else if (h->order_mode == PSS_ORDER_EXACT) {
+        PSS_HIP(h->d_sort.ensure(words(pss::v2_exact_ws_bytes(g, nr))));
+        mk(pss::K_V2_EMIT, s);
+        PSS_HIP(pss::launch_v2_exact(g, h->d_ranks.p, rank_lo, nr, pos_lo, count, h->epoch, out_dev,
+                                     h->d_sort.p, s));
     } else {
         PSS_HIP(h->d_val.ensure(words(pss::v2_val_bytes(g, nr))));
         const size_t bb = pss::v2_buf_bytes(g, nr), sb = pss::v2_sort_bytes(g, nr);
@@ -555,9 +560,10 @@ int pss_set_order_mode(pss_sampler *h, int32_t mode) {
     if (!h) return fail(PSS_EINVAL, "NULL handle");
     if (mode != PSS_ORDER_COUNTER && mode != PSS_ORDER_EXACT) return fail(PSS_EINVAL, "bad order mode");
     if (mode == PSS_ORDER_EXACT) {
-        if (h->version != 1) return fail(PSS_ENOTSUP, "exact order is implemented for V1 windows only");
-        if (!pss::v1_exact_supported(h->geometry()))
-            return fail(PSS_ENOTSUP, "exact order needs shuffle_buffer <= 8192");
+        if (h->version == 1 && !pss::v1_exact_supported(h->geometry()))
+            return fail(PSS_ENOTSUP, "V1 exact order needs shuffle_buffer <= 8192");
+        if (h->version == 2 && !pss::v2_exact_supported(h->geometry()))
+            return fail(PSS_ENOTSUP, "V2 exact order needs shuffle_buffer <= 4096 and num_samples < 2^31");
     }
     h->order_mode = mode;
     return PSS_OK;

@@ -1,0 +1,270 @@
+// pss_v2exact.hip -- V2 in the reference's EXACT order (order mode PSS_ORDER_EXACT): the id
+// stream of get_index (V2:96-116) bit for bit, CPython MT19937 included.
+//
+// The reference's loop, per step: k1 = _randbelow(len(pool1)), emit and `remove` pool1[k1];
+// while pool2 is non-empty, k2 = _randbelow(len(pool2)), move pool2[k2] to the END of pool1;
+// when pool2 runs dry, `seed(epoch + buffers*10000)` and refill it with the next window of the
+// new start (V2:108-112).  That splits into independent pieces:
+//
+//   draws   every pool2 window is drawn from its own freshly seeded stream (segment 0 from
+//           seed(e+2) of init_iter, V2:147; segment s >= 1 from seed(e + (s-1)*10000)), k1 and
+//           k2 alternating; once pool2 stays empty every step reseeds, so each tail step's k1
+//           is the first draw of its own stream.  One wave per stream (pss_mt.h).
+//   decode  "remove the k-th, append at the end" is a rank-deletion problem: with the
+//           elements numbered in insertion order, step t removes the k_t-th alive one.  A block
+//           of steps [a, b) is solved in the frame of its start (alive elements 0..B_a-1, its
+//           own insertions after them); two sibling blocks combine by mapping the right
+//           block's answers through the left block's deletions -- the q-th survivor of the
+//           left block is q + #{i : D_i - i <= q} for its sorted deletions D -- and merging
+//           the sorted deletion lists.  Bottom-up, this is a merge sort of (position, step)
+//           pairs: 12 levels in LDS per 4096-step tile, then global levels.  pool2 windows
+//           (no insertions) finish inside one tile.
+//   output  position p < P is old_start + p (initial pool1, V2:135-136); position P + u is
+//           the element step u moved over from pool2: window base + its decoded pool2 rank.
+//
+// tests/test_gpu_parity.py checks the streams against oracle/pss_oracle.c's exact V2 (pinned
+// by the reference's recorded streams).
+#include <cstdlib>
+
+#include "pss_mt.h"
+
+namespace pss {
+
+namespace {
+constexpr int kTile = 4096;       // steps per LDS decode tile; also the largest pool2 window
+constexpr int kTileNT = 256;
+
+struct V2xGeo {                   // one rank's stream, host-computed
+    uint32_t P, T, S, B;          // pool1 size, main steps, pool2 windows, shuffle_buffer
+    uint32_t ns, tiles1;          // steps, pool1 decode tiles
+};
+
+__device__ __forceinline__ uint32_t alive_at(uint32_t B0, uint32_t insu, uint32_t x) {
+    return B0 - (x > insu ? x - insu : 0u);
+}
+__device__ __forceinline__ uint32_t ins_in(uint32_t insu, uint32_t a, uint32_t b) {
+    const uint32_t e = b < insu ? b : insu;
+    return e > a ? e - a : 0u;
+}
+// #{i < n : D[i] - i <= q} for sorted distinct D (D[i] - i is non-decreasing)
+__device__ __forceinline__ uint32_t count_e_le(const uint32_t *D, uint32_t n, uint32_t q) {
+    uint32_t lo = 0, hi = n;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (D[mid] - mid <= q) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+}
+// #{i < n : D[i] < y}
+__device__ __forceinline__ uint32_t count_lt(const uint32_t *D, uint32_t n, uint32_t y) {
+    uint32_t lo = 0, hi = n;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (D[mid] < y) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+}
+// position q of the frame at m (sibling-right block) in the frame at a (left block start)
+__device__ __forceinline__ uint32_t map_right(const uint32_t *DL, uint32_t nL, uint32_t q, uint32_t Ba,
+                                              uint32_t Bm, uint32_t insL) {
+    return q < Bm ? q + count_e_le(DL, nL, q) : q - Bm + Ba + insL;
+}
+}  // namespace
+
+// ---- draws: one wave per MT stream (pool2 windows, then tail steps) -------------------------
+__global__ __launch_bounds__(64) void k_v2x_draws(V2xGeo x, int64_t epoch, uint32_t jobs,
+                                                  uint32_t *__restrict__ K1, uint32_t *__restrict__ K2) {
+    __shared__ uint32_t mt[kMtN];
+    const uint32_t rl = blockIdx.x / jobs, job = blockIdx.x % jobs;
+    uint32_t *k1 = K1 + (size_t)rl * x.ns;
+    uint32_t *k2 = K2 + (size_t)rl * x.T;
+    if (job < x.S) {          // pool2 window s: k1, k2 alternating from its own stream
+        const uint32_t s = job;
+        const uint32_t W = x.T - s * x.B < x.B ? x.T - s * x.B : x.B, t0 = s * x.B;
+        mt_seed_int(mt, s == 0 ? epoch + 2 : epoch + (int64_t)(s - 1) * 10000);
+        const uint32_t P = x.P;
+        mt_draws(mt, 2u * W, [&](uint32_t d) { return (d & 1u) ? W - (d >> 1) : P; },
+                 [&](uint32_t d, uint32_t r) {
+                     if (d & 1u) k2[t0 + (d >> 1)] = r;
+                     else k1[t0 + (d >> 1)] = r;
+                 });
+    } else {                  // tail step j: the first draw after its reseed
+        const uint32_t j = job - x.S;
+        const int64_t seed = x.S >= 1 ? epoch + (int64_t)(x.S - 1 + j) * 10000
+                                      : (j == 0 ? epoch + 2 : epoch + (int64_t)(j - 1) * 10000);
+        mt_seed_int(mt, seed);
+        const uint32_t n = x.P - j, t = x.T + j;
+        mt_draws(mt, 1u, [&](uint32_t) { return n; }, [&](uint32_t, uint32_t r) { k1[t] = r; });
+    }
+}
+
+// ---- decode tiles in LDS: pool1 tiles of kTile steps and whole pool2 windows ---------------
+__global__ __launch_bounds__(kTileNT) void k_v2x_tile(V2xGeo x, uint32_t per_rank,
+                                                      const uint32_t *__restrict__ K1,
+                                                      const uint32_t *__restrict__ K2,
+                                                      uint32_t *__restrict__ V, uint32_t *__restrict__ O,
+                                                      uint32_t *__restrict__ Q2) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+    uint32_t *va = smem, *oa = smem + kTile, *vb = smem + 2 * kTile, *ob = smem + 3 * kTile;
+    const uint32_t rl = blockIdx.x / per_rank, job = blockIdx.x % per_rank;
+    const bool pool1 = job < x.tiles1;
+    uint32_t t0, n, B0, insu;
+    const uint32_t *src;
+    if (pool1) {
+        t0 = job * kTile;
+        n = x.ns - t0 < (uint32_t)kTile ? x.ns - t0 : (uint32_t)kTile;
+        B0 = x.P; insu = x.T;
+        src = K1 + (size_t)rl * x.ns + t0;
+    } else {
+        const uint32_t s = job - x.tiles1;
+        t0 = 0;
+        n = x.T - s * x.B < x.B ? x.T - s * x.B : x.B;
+        B0 = n; insu = 0;
+        src = K2 + (size_t)rl * x.T + (size_t)s * x.B;
+    }
+    for (uint32_t u = threadIdx.x; u < n; u += kTileNT) { va[u] = src[u]; oa[u] = u; }
+    __syncthreads();
+    for (uint32_t w = 1; w < n; w <<= 1) {
+        for (uint32_t u = threadIdx.x; u < n; u += kTileNT) {     // right blocks -> left frame
+            const uint32_t blk = u / w;
+            if (blk & 1u) {
+                const uint32_t a = (blk - 1) * w, m = blk * w;
+                va[u] = map_right(va + a, m - a, va[u], alive_at(B0, insu, t0 + a),
+                                  alive_at(B0, insu, t0 + m), ins_in(insu, t0 + a, t0 + m));
+            }
+        }
+        __syncthreads();
+        for (uint32_t u = threadIdx.x; u < n; u += kTileNT) {     // merge sibling lists
+            const uint32_t a = (u / (2 * w)) * (2 * w), m = a + w;
+            if (m >= n) { vb[u] = va[u]; ob[u] = oa[u]; continue; }
+            const uint32_t e = m + w < n ? m + w : n;
+            const uint32_t pos = u < m ? (u - a) + count_lt(va + m, e - m, va[u])
+                                       : (u - m) + count_lt(va + a, m - a, va[u]);
+            vb[a + pos] = va[u];
+            ob[a + pos] = oa[u];
+        }
+        __syncthreads();
+        uint32_t *t = va; va = vb; vb = t;
+        t = oa; oa = ob; ob = t;
+    }
+    if (pool1) {
+        uint32_t *v = V + (size_t)rl * x.ns + t0, *o = O + (size_t)rl * x.ns + t0;
+        for (uint32_t u = threadIdx.x; u < n; u += kTileNT) { v[u] = va[u]; o[u] = t0 + oa[u]; }
+    } else {
+        uint32_t *q = Q2 + (size_t)rl * x.T + (size_t)(job - x.tiles1) * x.B;
+        for (uint32_t u = threadIdx.x; u < n; u += kTileNT) q[oa[u]] = va[u];
+    }
+}
+
+// ---- global levels of the pool1 decode: blocks of w steps -> 2w -----------------------------
+__global__ __launch_bounds__(256) void k_v2x_gmap(V2xGeo x, uint32_t nr, uint32_t w, uint32_t *__restrict__ V) {
+    const uint64_t gi = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    const uint32_t rl = (uint32_t)(gi / x.ns), u = (uint32_t)(gi % x.ns);
+    if (rl >= nr) return;
+    const uint32_t blk = u / w;
+    if (!(blk & 1u)) return;
+    uint32_t *v = V + (size_t)rl * x.ns;
+    const uint32_t a = (blk - 1) * w, m = blk * w;
+    v[u] = map_right(v + a, m - a, v[u], alive_at(x.P, x.T, a), alive_at(x.P, x.T, m), ins_in(x.T, a, m));
+}
+
+__global__ __launch_bounds__(256) void k_v2x_gmerge(V2xGeo x, uint32_t nr, uint32_t w, const uint32_t *__restrict__ V,
+                                                    const uint32_t *__restrict__ O, uint32_t *__restrict__ Vd,
+                                                    uint32_t *__restrict__ Od) {
+    const uint64_t gi = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    const uint32_t rl = (uint32_t)(gi / x.ns), u = (uint32_t)(gi % x.ns);
+    if (rl >= nr) return;
+    const size_t base = (size_t)rl * x.ns;
+    const uint32_t *v = V + base;
+    const uint32_t a = (u / (2 * w)) * (2 * w), m = a + w;
+    uint32_t dst = u;
+    if (m < x.ns) {
+        const uint32_t e = m + w < x.ns ? m + w : x.ns;
+        dst = a + (u < m ? (u - a) + count_lt(v + m, e - m, v[u]) : (u - m) + count_lt(v + a, m - a, v[u]));
+    }
+    Vd[base + dst] = v[u];
+    Od[base + dst] = O[base + u];
+}
+
+// ---- ids of the decoded positions ------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_v2x_out(Geometry g, V2xGeo x, uint32_t nr, const RankDesc *__restrict__ ranks,
+                                                 int32_t rank_lo, const uint32_t *__restrict__ V,
+                                                 const uint32_t *__restrict__ O, const uint32_t *__restrict__ Q2,
+                                                 int64_t pos_lo, int64_t count, int64_t *__restrict__ out) {
+    const uint64_t gi = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    const uint32_t rl = (uint32_t)(gi / x.ns), i = (uint32_t)(gi % x.ns);
+    if (rl >= nr) return;
+    const size_t base = (size_t)rl * x.ns;
+    const int64_t t = O[base + i];
+    if (t < pos_lo || t >= pos_lo + count) return;
+    const RankDesc rd = ranks[rank_lo + (int32_t)rl];
+    const uint32_t q = V[base + i];
+    int64_t id;
+    if (q < x.P) {
+        id = rd.old_start + q;
+    } else {
+        const uint32_t uu = q - x.P, s = uu / x.B;
+        const int64_t wbase = s == 0 ? rd.old_start + x.B : rd.new_start + (int64_t)(s + 1) * x.B;
+        id = wbase + Q2[(size_t)rl * x.T + uu];
+    }
+    out[(int64_t)rl * count + (t - pos_lo)] = wrap_id(id, g.N);
+}
+
+static int64_t v2x_cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+static V2xGeo v2x_geo(const Geometry &g) {
+    V2xGeo x{};
+    const int64_t P = g.B < g.ns ? g.B : g.ns;
+    x.P = (uint32_t)P;
+    x.T = (uint32_t)(g.ns - P);
+    x.B = (uint32_t)g.B;
+    x.S = x.T ? (uint32_t)v2x_cdiv(x.T, g.B) : 0u;
+    x.ns = (uint32_t)g.ns;
+    x.tiles1 = (uint32_t)v2x_cdiv(g.ns, kTile);
+    return x;
+}
+
+bool v2_exact_supported(const Geometry &g) {
+    return g.B <= kTile && g.ns < ((int64_t)1 << 31);
+}
+
+size_t v2_exact_ws_bytes(const Geometry &g, int32_t nr) {
+    if (!v2_exact_supported(g)) return 0;
+    const V2xGeo x = v2x_geo(g);
+    // K1, V, O, Vd, Od (ns each) + K2, Q2 (T each), per local rank
+    return (size_t)nr * ((size_t)5 * x.ns + (size_t)2 * x.T) * sizeof(uint32_t);
+}
+
+hipError_t launch_v2_exact(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, int32_t nr,
+                           int64_t pos_lo, int64_t count, int64_t epoch, int64_t *out, uint32_t *ws,
+                           hipStream_t s) {
+    const int64_t pos_hi = pos_lo + count < g.ns ? pos_lo + count : g.ns;
+    if (nr <= 0 || pos_hi <= pos_lo) return hipSuccess;
+    if (!v2_exact_supported(g) || !ws) return hipErrorInvalidValue;
+    const V2xGeo x = v2x_geo(g);
+    const size_t nsr = (size_t)nr * x.ns, tr = (size_t)nr * x.T;
+    uint32_t *K1 = ws, *V = K1 + nsr, *O = V + nsr, *Vd = O + nsr, *Od = Vd + nsr;
+    uint32_t *K2 = Od + nsr, *Q2 = K2 + tr;
+    static const hipError_t attr = hipFuncSetAttribute((const void *)k_v2x_tile,
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                       4 * kTile * (int)sizeof(uint32_t));
+    if (attr != hipSuccess) return attr;
+    const uint32_t jobs = x.S + x.P;
+    hipLaunchKernelGGL(k_v2x_draws, dim3(jobs * (uint32_t)nr), dim3(64), 0, s, x, epoch, jobs, K1, K2);
+    const uint32_t per_rank = x.tiles1 + x.S;
+    hipLaunchKernelGGL(k_v2x_tile, dim3(per_rank * (uint32_t)nr), dim3(kTileNT),
+                       4 * kTile * sizeof(uint32_t), s, x, per_rank, K1, K2, V, O, Q2);
+    const dim3 grid((uint32_t)v2x_cdiv((int64_t)nsr, 256));   // one thread per (rank, step)
+    const uint32_t nru = (uint32_t)nr;
+    for (uint32_t w = kTile; w < x.ns; w <<= 1) {
+        hipLaunchKernelGGL(k_v2x_gmap, grid, dim3(256), 0, s, x, nru, w, V);
+        hipLaunchKernelGGL(k_v2x_gmerge, grid, dim3(256), 0, s, x, nru, w, V, O, Vd, Od);
+        uint32_t *t = V; V = Vd; Vd = t;
+        t = O; O = Od; Od = t;
+    }
+    hipLaunchKernelGGL(k_v2x_out, grid, dim3(256), 0, s, g, x, nru, ranks, rank_lo, V, O, Q2,
+                       pos_lo, count, out);
+    return hipGetLastError();
+}
+
+}  // namespace pss

@@ -320,6 +320,55 @@ def test_exact_order_unsupported_configs():
     from partiallyshuffledistributedsampler_amd import _lib
     lengths = np.full(10, 1000)
     with pytest.raises(_lib.PSSError):
-        pss.IndexEngine(lengths, 10000, 2, 100, 2, device=0, order="exact")      # V2
+        pss.IndexEngine(lengths, 10000, 2, 8192, 2, device=0, order="exact")     # V2, B > 4096
     with pytest.raises(_lib.PSSError):
-        pss.IndexEngine(lengths, 10000, 2, 16384, 1, device=0, order="exact")    # B > 8192
+        pss.IndexEngine(lengths, 10000, 2, 16384, 1, device=0, order="exact")    # V1, B > 8192
+
+
+@pytest.mark.parametrize("name", scenario_names("v2"))
+def test_v2_exact_order_matches_reference_streams(name):
+    """order="exact" on V2: each rank's id stream equals the one the reference produced
+    (tests/golden, captured at V2:181) and the exact oracle's."""
+    fx = load(name)
+    files, lengths, fl, N, R, B, bs, shuffle = fixture_params(fx)
+    lens = [fl.get(p, lengths[p]) if fl else lengths[p] for p in files]
+    eng = pss.IndexEngine(lens, N, R, B, 2, seed=0, device=0, order="exact")
+    for ep_i, er0 in enumerate(fx["ranks"][0]["epochs"]):
+        eng.init_iter(er0["epoch"])
+        out = eng.generate(0, R).cpu().numpy()
+        for rrec in fx["ranks"]:
+            er = rrec["epochs"][ep_i]
+            ref = O.v2_exact_stream(er["epoch"], er["old_start"], er["start_num"], eng.num_samples, B, N)
+            assert np.array_equal(out[rrec["rank"]], ref), (name, rrec["rank"], er["epoch"])
+            if er.get("resume_step") is not None:
+                continue   # the recorded batches start at the resume point
+            rec = [x for b in er["batches"] for x in b]
+            assert out[rrec["rank"]][:len(rec)].tolist() == rec, (name, rrec["rank"], er["epoch"])
+
+
+@pytest.mark.parametrize("F,lo,hi,R,B,epochs", [
+    (37, 1, 900, 7, 40, (0, 5)),
+    (50, 1000, 5000, 3, 3000, (2,)),                # partial last pool2 window
+    (40, 2000, 9000, 2, 4096, (1,)),                # largest exact pool
+    (13, 1, 50, 5, 100, (0, 9)),                    # ns < B: tail only
+    (9, 20, 40, 2, 70, (3,)),                       # B < ns < 2B
+    (100, 1, 3, 8, 7, (0,)),                        # tiny pools
+    (64, 3000, 3001, 2, 1000, (4,)),                # many global decode levels (ns = 96000)
+])
+def test_v2_exact_order_matches_exact_oracle(F, lo, hi, R, B, epochs):
+    rng = np.random.default_rng(F * 7 + B)
+    lengths = rng.integers(lo, hi, F)
+    N = int(lengths.sum())
+    eng = pss.IndexEngine(lengths, N, R, B, 2, seed=7, device=0, order="exact")
+    ns = eng.num_samples
+    for epoch in epochs:
+        eng.init_iter(epoch)
+        old, new = eng.rank_starts()
+        out = eng.generate(0, R).cpu().numpy()
+        for r in range(R):
+            ref = O.v2_exact_stream(epoch, int(old[r]), int(new[r]), ns, B, N)
+            assert np.array_equal(out[r], ref), (F, B, epoch, r)
+        if ns > 3:
+            lo_p, cnt = ns // 3, ns // 2
+            part = eng.generate(1, R, lo_p, cnt).cpu().numpy()
+            assert np.array_equal(part, out[1:, lo_p:lo_p + cnt])

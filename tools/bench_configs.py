@@ -8,6 +8,7 @@ survey names, each as the share one of 8 GPUs would generate:
   c2     V2, 10K files x 10K, R=8 (all 8 ranks)                      B=4096
   c2v1   V1 on the same files                                        B=4096
   c2v1x  c2v1 with order="exact"
+  c2x    c2 with order="exact" (the reference's own V2 stream)
   c3     V2, 100K files x 10K = 1B, R=1024 -> ranks [0, 128)         B=4096
   c4     V2, Zipf(1.5)*150 files (N=2.59e9 > 2^31), R=4096 -> [0, 512)  B=4096
   c5     V2, C2 files, B=2^20 (HBM slot-table path), 100 epochs       (reports per-epoch mean)
@@ -52,13 +53,15 @@ def run(name, lengths, R, r_hi, B, ver, steps, warmup=2, order="counter"):
 
 
 def main():
-    which = sys.argv[1:] or ["c1", "c1x", "c2", "c2v1", "c2v1x", "c3", "c4", "c5"]
+    which = sys.argv[1:] or ["c1", "c1x", "c2", "c2x", "c2v1", "c2v1x", "c3", "c4", "c5"]
     c2 = np.full(10_000, 10_000, dtype=np.int64)
     for w in which:
         if w == "c1":      # BASELINE configs[0]: V1, 64 files x 10K, R=2
             run(w, np.full(64, 10_000, dtype=np.int64), 2, 2, 4096, 1, 50)
         elif w == "c1x":   # C1 in the reference's exact order (CPython MT per window)
             run(w, np.full(64, 10_000, dtype=np.int64), 2, 2, 4096, 1, 50, order="exact")
+        elif w == "c2x":   # C2 in the reference's exact order (CPython MT, rank-deletion decode)
+            run(w, c2, 8, 8, 4096, 2, 3, warmup=1, order="exact")
         elif w == "c2v1x":
             run(w, c2, 8, 8, 4096, 1, 5, order="exact")
         elif w == "c2":
