@@ -32,7 +32,7 @@ namespace pss {
 
 namespace {
 constexpr int kTile = 4096;       // steps per LDS decode tile; also the largest pool2 window
-constexpr int kTileNT = 256;
+constexpr int kTileNT = 1024;   // 4 steps per thread: the searches are latency-bound, occupancy hides them
 
 struct V2xGeo {                   // one rank's stream, host-computed
     uint32_t P, T, S, B;          // pool1 size, main steps, pool2 windows, shuffle_buffer
@@ -157,33 +157,128 @@ __global__ __launch_bounds__(kTileNT) void k_v2x_tile(V2xGeo x, uint32_t per_ran
 }
 
 // ---- global levels of the pool1 decode: blocks of w steps -> 2w -----------------------------
-__global__ __launch_bounds__(256) void k_v2x_gmap(V2xGeo x, uint32_t nr, uint32_t w, uint32_t *__restrict__ V) {
+// Tiled like a GPU merge sort: a workgroup owns kGTile consecutive entries of one rank, finds
+// where its tile starts and ends in the sorted lists it reads (one binary search each, in
+// HBM), stages those sub-ranges in LDS with coalesced loads, works from LDS (kPer entries per
+// thread: one LDS search, then a sequential walk) and writes its tile back coalesced.
+constexpr uint32_t kGNT = 256, kPer = 8, kGTile = kGNT * kPer;   // w >= kTile is a multiple
+
+// Merge-path splits of every gmerge tile's first and end output, all at once (one thread per
+// tile boundary, so the binary searches' HBM latency overlaps).
+__global__ __launch_bounds__(256) void k_v2x_gsplit(V2xGeo x, uint32_t nr, uint32_t w,
+                                                    const uint32_t *__restrict__ V, uint32_t *__restrict__ SP) {
+    const uint32_t tpr = (x.ns + kGTile - 1) / kGTile;
+    const uint64_t gi = (uint64_t)blockIdx.x * 256 + threadIdx.x;   // (rank, tile, end?)
+    if (gi >= (uint64_t)nr * tpr * 2) return;
+    const uint32_t rl = (uint32_t)(gi / (2 * tpr)), tt = (uint32_t)(gi % (2 * tpr));
+    const uint32_t tile = tt >> 1, endp = tt & 1u;
+    const uint32_t *v = V + (size_t)rl * x.ns;
+    const uint32_t u0 = tile * kGTile, un = x.ns - u0 < kGTile ? x.ns - u0 : kGTile;
+    uint32_t r = 0;
+    {
+        const uint32_t a = (u0 / (2 * w)) * (2 * w), m = a + w;
+        if (m < x.ns) {
+            const uint32_t e = m + w < x.ns ? m + w : x.ns, nL = m - a, nR = e - m;
+            const uint32_t *L = v + a, *R = v + m;
+            const uint32_t d = u0 - a + (endp ? un : 0u);
+            uint32_t lo = d > nR ? d - nR : 0u, hi = d < nL ? d : nL;
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (L[mid] < R[d - mid - 1]) lo = mid + 1; else hi = mid;
+            }
+            r = lo;
+        }
+    }
+    SP[gi] = r;
+}
+
+// right blocks -> the left block's frame (in place)
+// Survivor tables: for the left block [a, m) of every pair, C[q] = #{i : D_i - i <= q} for
+// q < B_m (the alive count at m, <= P) -- the number of the left block's deletions at or
+// before its q-th survivor.  D_i - i is non-decreasing, so entry i owns C[q] for
+// q in [D_i - i, D_{i+1} - (i+1)): one thread per left-block entry, B_m writes per pair.
+__global__ __launch_bounds__(256) void k_v2x_ctab(V2xGeo x, uint32_t nr, uint32_t w,
+                                                  const uint32_t *__restrict__ V, uint32_t *__restrict__ C) {
+    const uint64_t gi = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    const uint32_t rl = (uint32_t)(gi / x.ns), u = (uint32_t)(gi % x.ns);
+    if (rl >= nr) return;
+    const uint32_t pair = u / (2 * w), a = pair * 2 * w, m = a + w;
+    if (u >= m || m >= x.ns) return;          // left-block entries of pairs with a right block
+    const uint32_t i = u - a, nL = w;
+    const uint32_t Bm = alive_at(x.P, x.T, m);
+    const uint32_t *DL = V + (size_t)rl * x.ns + a;
+    const uint32_t pairs = (x.ns + 2 * w - 1) / (2 * w);
+    uint32_t *c = C + ((size_t)rl * pairs + pair) * x.P;
+    const uint32_t e = DL[i] - i;
+    const uint32_t en = i + 1 < nL ? DL[i + 1] - (i + 1) : Bm;
+    const uint32_t hi = en < Bm ? en : Bm;
+    for (uint32_t q = e; q < hi; q++) c[q] = i + 1;
+    if (i == 0) {
+        const uint32_t z = e < Bm ? e : Bm;
+        for (uint32_t q = 0; q < z; q++) c[q] = 0;
+    }
+}
+
+// right blocks -> the left block's frame (in place): q < B_m is the q-th survivor of the
+// left block, q + C[q]; larger q are the right block's own insertions
+__global__ __launch_bounds__(256) void k_v2x_gmap(V2xGeo x, uint32_t nr, uint32_t w, uint32_t *__restrict__ V,
+                                                  const uint32_t *__restrict__ C) {
     const uint64_t gi = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     const uint32_t rl = (uint32_t)(gi / x.ns), u = (uint32_t)(gi % x.ns);
     if (rl >= nr) return;
     const uint32_t blk = u / w;
     if (!(blk & 1u)) return;
+    const uint32_t a = (blk - 1) * w, m = blk * w, pair = blk >> 1;
+    const uint32_t Ba = alive_at(x.P, x.T, a), Bm = alive_at(x.P, x.T, m), insL = ins_in(x.T, a, m);
+    const uint32_t pairs = (x.ns + 2 * w - 1) / (2 * w);
     uint32_t *v = V + (size_t)rl * x.ns;
-    const uint32_t a = (blk - 1) * w, m = blk * w;
-    v[u] = map_right(v + a, m - a, v[u], alive_at(x.P, x.T, a), alive_at(x.P, x.T, m), ins_in(x.T, a, m));
+    const uint32_t q = v[u];
+    v[u] = q < Bm ? q + C[((size_t)rl * pairs + pair) * x.P + q] : q - Bm + Ba + insL;
 }
 
-__global__ __launch_bounds__(256) void k_v2x_gmerge(V2xGeo x, uint32_t nr, uint32_t w, const uint32_t *__restrict__ V,
+// merge sibling blocks (sorted by position, carrying the step of each entry)
+__global__ __launch_bounds__(kGNT) void k_v2x_gmerge(V2xGeo x, uint32_t w, const uint32_t *__restrict__ V,
                                                     const uint32_t *__restrict__ O, uint32_t *__restrict__ Vd,
-                                                    uint32_t *__restrict__ Od) {
-    const uint64_t gi = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    const uint32_t rl = (uint32_t)(gi / x.ns), u = (uint32_t)(gi % x.ns);
-    if (rl >= nr) return;
+                                                    uint32_t *__restrict__ Od, const uint32_t *__restrict__ SP) {
+    __shared__ uint32_t sv[kGTile], so[kGTile], tv[kGTile], to[kGTile];
+    const uint32_t tpr = (x.ns + kGTile - 1) / kGTile;
+    const uint32_t rl = blockIdx.x / tpr, o0 = (blockIdx.x % tpr) * kGTile;
     const size_t base = (size_t)rl * x.ns;
-    const uint32_t *v = V + base;
-    const uint32_t a = (u / (2 * w)) * (2 * w), m = a + w;
-    uint32_t dst = u;
-    if (m < x.ns) {
-        const uint32_t e = m + w < x.ns ? m + w : x.ns;
-        dst = a + (u < m ? (u - a) + count_lt(v + m, e - m, v[u]) : (u - m) + count_lt(v + a, m - a, v[u]));
+    const uint32_t *v = V + base, *o = O + base;
+    uint32_t *vd = Vd + base, *od = Od + base;
+    const uint32_t on = x.ns - o0 < kGTile ? x.ns - o0 : kGTile;
+    const uint32_t a = (o0 / (2 * w)) * (2 * w), m = a + w;
+    if (m >= x.ns) {                           // lone left block: already merged
+        for (uint32_t u = threadIdx.x; u < on; u += kGNT) { vd[o0 + u] = v[o0 + u]; od[o0 + u] = o[o0 + u]; }
+        return;
     }
-    Vd[base + dst] = v[u];
-    Od[base + dst] = O[base + u];
+    const uint32_t e = m + w < x.ns ? m + w : x.ns, nL = m - a, nR = e - m;
+    const uint32_t *L = v + a, *R = v + m;
+    (void)nL; (void)nR;
+    const uint32_t i0 = SP[2 * blockIdx.x], i1 = SP[2 * blockIdx.x + 1], dA = o0 - a;   // merge-path splits
+    const uint32_t j0 = dA - i0, j1 = dA + on - i1;
+    const uint32_t sL = i1 - i0, sR = j1 - j0;   // sL + sR == on
+    for (uint32_t u = threadIdx.x; u < sL; u += kGNT) { sv[u] = L[i0 + u]; so[u] = o[a + i0 + u]; }
+    for (uint32_t u = threadIdx.x; u < sR; u += kGNT) { sv[sL + u] = R[j0 + u]; so[sL + u] = o[m + j0 + u]; }
+    __syncthreads();
+    const uint32_t p0 = threadIdx.x * kPer;
+    if (p0 < on) {
+        const uint32_t *lv = sv, *rv = sv + sL;
+        uint32_t lo = p0 > sR ? p0 - sR : 0u, hi = p0 < sL ? p0 : sL;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (lv[mid] < rv[p0 - mid - 1]) lo = mid + 1; else hi = mid;
+        }
+        uint32_t i = lo, j = p0 - lo;
+        const uint32_t pe = p0 + kPer < on ? p0 + kPer : on;
+        for (uint32_t p = p0; p < pe; p++) {
+            const bool takeL = j >= sR || (i < sL && lv[i] < rv[j]);
+            if (takeL) { tv[p] = lv[i]; to[p] = so[i]; i++; }
+            else { tv[p] = rv[j]; to[p] = so[sL + j]; j++; }
+        }
+    }
+    __syncthreads();
+    for (uint32_t u = threadIdx.x; u < on; u += kGNT) { vd[o0 + u] = tv[u]; od[o0 + u] = to[u]; }
 }
 
 // ---- ids of the decoded positions ------------------------------------------------------------
@@ -231,8 +326,11 @@ bool v2_exact_supported(const Geometry &g) {
 size_t v2_exact_ws_bytes(const Geometry &g, int32_t nr) {
     if (!v2_exact_supported(g)) return 0;
     const V2xGeo x = v2x_geo(g);
-    // K1, V, O, Vd, Od (ns each) + K2, Q2 (T each), per local rank
-    return (size_t)nr * ((size_t)5 * x.ns + (size_t)2 * x.T) * sizeof(uint32_t);
+    // K1, V, O, Vd, Od (ns each) + K2, Q2 (T each), per local rank; tile splits; survivor
+    // tables of the first global level (the most pairs)
+    const size_t pairs = (size_t)v2x_cdiv(x.ns, 2 * kTile);
+    return ((size_t)nr * ((size_t)5 * x.ns + (size_t)2 * x.T) +
+            (size_t)2 * nr * (size_t)v2x_cdiv(x.ns, kGTile) + 64 + (size_t)nr * pairs * x.P) * sizeof(uint32_t);
 }
 
 hipError_t launch_v2_exact(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, int32_t nr,
@@ -254,15 +352,22 @@ hipError_t launch_v2_exact(const Geometry &g, const RankDesc *ranks, int32_t ran
     const uint32_t per_rank = x.tiles1 + x.S;
     hipLaunchKernelGGL(k_v2x_tile, dim3(per_rank * (uint32_t)nr), dim3(kTileNT),
                        4 * kTile * sizeof(uint32_t), s, x, per_rank, K1, K2, V, O, Q2);
-    const dim3 grid((uint32_t)v2x_cdiv((int64_t)nsr, 256));   // one thread per (rank, step)
+    const dim3 grid1((uint32_t)v2x_cdiv((int64_t)nsr, 256));   // one thread per (rank, step)
+    // one workgroup per kGTile entries of a rank (the last tile of a rank may be short)
+    const int64_t tiles = (int64_t)nr * v2x_cdiv(x.ns, kGTile);
+    const dim3 gridt((uint32_t)tiles), grids((uint32_t)v2x_cdiv(2 * tiles, 256));
     const uint32_t nru = (uint32_t)nr;
+    uint32_t *SP = Q2 + tr;                    // 2 words per tile
+    uint32_t *C = SP + 2 * tiles + 64;         // survivor tables: pairs x P words per rank
     for (uint32_t w = kTile; w < x.ns; w <<= 1) {
-        hipLaunchKernelGGL(k_v2x_gmap, grid, dim3(256), 0, s, x, nru, w, V);
-        hipLaunchKernelGGL(k_v2x_gmerge, grid, dim3(256), 0, s, x, nru, w, V, O, Vd, Od);
+        hipLaunchKernelGGL(k_v2x_ctab, grid1, dim3(256), 0, s, x, nru, w, V, C);
+        hipLaunchKernelGGL(k_v2x_gmap, grid1, dim3(256), 0, s, x, nru, w, V, C);
+        hipLaunchKernelGGL(k_v2x_gsplit, grids, dim3(256), 0, s, x, nru, w, V, SP);
+        hipLaunchKernelGGL(k_v2x_gmerge, gridt, dim3(kGNT), 0, s, x, w, V, O, Vd, Od, SP);
         uint32_t *t = V; V = Vd; Vd = t;
         t = O; O = Od; Od = t;
     }
-    hipLaunchKernelGGL(k_v2x_out, grid, dim3(256), 0, s, g, x, nru, ranks, rank_lo, V, O, Q2,
+    hipLaunchKernelGGL(k_v2x_out, grid1, dim3(256), 0, s, g, x, nru, ranks, rank_lo, V, O, Q2,
                        pos_lo, count, out);
     return hipGetLastError();
 }
