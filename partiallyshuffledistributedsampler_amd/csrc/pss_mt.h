@@ -9,16 +9,6 @@ namespace pss {
 namespace {
 constexpr int kMtN = 624, kMtM = 397;
 
-struct MtInitTable { uint32_t v[kMtN]; };
-constexpr MtInitTable make_mt_init() {   // init_genrand(19650218), _randommodule.c
-    MtInitTable t{};
-    t.v[0] = 19650218u;
-    for (int i = 1; i < kMtN; i++) t.v[i] = 1812433253u * (t.v[i - 1] ^ (t.v[i - 1] >> 30)) + (uint32_t)i;
-    return t;
-}
-__constant__ MtInitTable kMtInit = make_mt_init();
-
-
 // Lanes of one wave hand values to each other through LDS here (the twist reads words other
 // lanes wrote one round earlier).  The hardware keeps a wave's LDS operations in order, but
 // the compiler reasons per thread and may hoist a load above a store it can prove is to a
@@ -46,11 +36,15 @@ __device__ __forceinline__ uint32_t mt_twist_word(uint32_t a, uint32_t b, uint32
 __device__ void mt_seed(uint32_t *mt, uint32_t key0, uint32_t key1, int klen) {
     const int lane = threadIdx.x & 63;
     // loop 1: i = 1..623, then the wrap (mt[0] = mt[623]) and one more step at i = 1
-    uint32_t prev = kMtInit.v[0];
+    // init_genrand(19650218)'s words are generated alongside (an independent scalar chain,
+    // cheaper than a scalar-cache load per step)
+    uint32_t g = 19650218u;
+    uint32_t prev = g;
     uint32_t first = 0;
     int j = 0;
     for (int i = 1; i < kMtN; i++) {
-        const uint32_t v = (kMtInit.v[i] ^ ((prev ^ (prev >> 30)) * 1664525u)) + (j ? key1 : key0) + (uint32_t)j;
+        g = 1812433253u * (g ^ (g >> 30)) + (uint32_t)i;
+        const uint32_t v = (g ^ ((prev ^ (prev >> 30)) * 1664525u)) + (j ? key1 : key0) + (uint32_t)j;
         if (lane == 0) mt[i] = v;
         if (i == 1) first = v;
         prev = v;

@@ -33,6 +33,7 @@ namespace pss {
 namespace {
 constexpr int kTile = 4096;       // steps per LDS decode tile; also the largest pool2 window
 constexpr int kTileNT = 1024;   // 4 steps per thread: the searches are latency-bound, occupancy hides them
+static_assert(kTileNT * 4 == kTile, "the tile merge gives each thread four outputs");
 
 struct V2xGeo {                   // one rank's stream, host-computed
     uint32_t P, T, S, B;          // pool1 size, main steps, pool2 windows, shuffle_buffer
@@ -52,15 +53,6 @@ __device__ __forceinline__ uint32_t count_e_le(const uint32_t *D, uint32_t n, ui
     while (lo < hi) {
         const uint32_t mid = (lo + hi) >> 1;
         if (D[mid] - mid <= q) lo = mid + 1; else hi = mid;
-    }
-    return lo;
-}
-// #{i < n : D[i] < y}
-__device__ __forceinline__ uint32_t count_lt(const uint32_t *D, uint32_t n, uint32_t y) {
-    uint32_t lo = 0, hi = n;
-    while (lo < hi) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (D[mid] < y) lo = mid + 1; else hi = mid;
     }
     return lo;
 }
@@ -134,14 +126,37 @@ __global__ __launch_bounds__(kTileNT) void k_v2x_tile(V2xGeo x, uint32_t per_ran
             }
         }
         __syncthreads();
-        for (uint32_t u = threadIdx.x; u < n; u += kTileNT) {     // merge sibling lists
-            const uint32_t a = (u / (2 * w)) * (2 * w), m = a + w;
-            if (m >= n) { vb[u] = va[u]; ob[u] = oa[u]; continue; }
-            const uint32_t e = m + w < n ? m + w : n;
-            const uint32_t pos = u < m ? (u - a) + count_lt(va + m, e - m, va[u])
-                                       : (u - m) + count_lt(va + a, m - a, va[u]);
-            vb[a + pos] = va[u];
-            ob[a + pos] = oa[u];
+        if (w == 1) {                                            // merge sibling lists
+            for (uint32_t u = threadIdx.x; u < n; u += kTileNT) {
+                const uint32_t a = u & ~1u, m = a + 1;
+                if (m >= n) { vb[u] = va[u]; ob[u] = oa[u]; continue; }
+                const uint32_t pos = u < m ? (va[u] > va[m] ? 1u : 0u) : (va[u] > va[a] ? 1u : 0u);
+                vb[a + pos] = va[u];
+                ob[a + pos] = oa[u];
+            }
+        } else {   // kTileNT * 4 == kTile: four consecutive outputs per thread, one merge-path search
+            const uint32_t p0 = threadIdx.x * 4u;
+            if (p0 < n) {
+                const uint32_t a = (p0 / (2 * w)) * (2 * w), m = a + w;
+                const uint32_t pe = p0 + 4u < n ? p0 + 4u : n;
+                if (m >= n) {
+                    for (uint32_t p = p0; p < pe; p++) { vb[p] = va[p]; ob[p] = oa[p]; }
+                } else {
+                    const uint32_t e = m + w < n ? m + w : n, nL = w, nR = e - m, d = p0 - a;
+                    const uint32_t *L = va + a, *R = va + m;
+                    uint32_t lo = d > nR ? d - nR : 0u, hi = d < nL ? d : nL;
+                    while (lo < hi) {
+                        const uint32_t mid = (lo + hi) >> 1;
+                        if (L[mid] < R[d - mid - 1]) lo = mid + 1; else hi = mid;
+                    }
+                    uint32_t i = lo, j = d - lo;
+                    for (uint32_t p = p0; p < pe; p++) {
+                        const bool takeL = j >= nR || (i < nL && L[i] < R[j]);
+                        if (takeL) { vb[p] = L[i]; ob[p] = oa[a + i]; i++; }
+                        else { vb[p] = R[j]; ob[p] = oa[m + j]; j++; }
+                    }
+                }
+            }
         }
         __syncthreads();
         uint32_t *t = va; va = vb; vb = t;
