@@ -111,9 +111,11 @@ int pss_emit_path(pss_sampler *h, int32_t *path);
  * the reference's in both modes):
  *   PSS_ORDER_COUNTER (0, default) -- the counter-based schedule (Philox / Feistel, DESIGN.md
  *       §3): per-sampler, independent of the process-global `random` state;
- *   PSS_ORDER_EXACT   (1) -- V1 only: each window is `seed(epoch + b*10000); shuffle(range(n))`
- *       with CPython's MT19937 exactly as V1:102,114-115,165-171 draws it, so the id stream is
- *       bit-identical to the reference's.  PSS_ENOTSUP for V2 and for shuffle_buffer > 8192.
+ *   PSS_ORDER_EXACT   (1) -- the reference's own draws with CPython's MT19937, so the id
+ *       stream is bit-identical to the reference's: V1 windows `seed(epoch + b*10000);
+ *       shuffle(range(n))` (V1:102,114-115,165-171, shuffle_buffer <= 8192); V2 get_index's
+ *       choice / remove / append with its per-window and per-tail-step reseeding (V2:96-116,
+ *       shuffle_buffer <= 4096, num_samples < 2^31).  PSS_ENOTSUP outside those bounds.
  * Replaces nothing in the reference: its order IS the exact one. */
 #define PSS_ORDER_COUNTER 0
 #define PSS_ORDER_EXACT 1
