@@ -138,8 +138,10 @@ size_t v1_workspace_bytes(const Geometry &g, int32_t nr, int64_t pos_lo, int64_t
 // to kV1ExactMaxB elements (LDS-resident draw and bucket arrays)
 constexpr int64_t kV1ExactMaxB = 8192;
 bool v1_exact_supported(const Geometry &g);
+size_t v1_exact_ws_bytes(const Geometry &g, int32_t nr, int64_t pos_lo, int64_t count);
 hipError_t launch_v1_exact(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, int32_t nr,
-                           int64_t pos_lo, int64_t count, int64_t epoch, int64_t *out, hipStream_t s);
+                           int64_t pos_lo, int64_t count, int64_t epoch, int64_t *out, uint16_t *ws,
+                           hipStream_t s);
 
 // V2 in the reference's exact order (pss_v2exact.hip): shuffle_buffer <= 4096, ns < 2^31
 bool v2_exact_supported(const Geometry &g);

@@ -31,10 +31,26 @@ namespace {
 constexpr int kExactNT = 256;
 }  // namespace
 
+// Phases 1-2 alone, one wave per window (2.5 KB of LDS, so a CU holds 32 of them): the draws
+// j_i of every window go to HBM (u16, B per window) for k_v1_exact's resolution.
+__global__ __launch_bounds__(64) void k_v1x_draws(Geometry g, int64_t w_lo, int64_t nw, int64_t epoch,
+                                                  uint16_t *__restrict__ J) {
+    __shared__ uint32_t mt[kMtN];
+    const int64_t w = w_lo + (int64_t)(blockIdx.x % nw);
+    const int64_t wb = w * g.B;
+    const int n = (int)(g.ns - wb < g.B ? g.ns - wb : g.B);
+    if (n <= 1) return;
+    uint16_t *jw = J + (size_t)blockIdx.x * (size_t)g.B;
+    mt_seed_int(mt, w == 0 ? epoch : epoch + w * 10000);
+    mt_draws(mt, (uint32_t)(n - 1), [&](uint32_t d) { return (uint32_t)n - d; },
+             [&](uint32_t d, uint32_t r) { jw[n - 1 - (int)d] = (uint16_t)r; });
+}
+
 // One workgroup per (local rank, window) of [w_lo, w_lo + nw).
 __global__ __launch_bounds__(kExactNT) void k_v1_exact(Geometry g, const RankDesc *__restrict__ ranks,
                                                        int32_t rank_lo, int64_t w_lo, int64_t nw,
                                                        int64_t pos_lo, int64_t count, int64_t epoch,
+                                                       const uint16_t *__restrict__ J,
                                                        int64_t *__restrict__ out) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     const int32_t rl = (int32_t)(blockIdx.x / nw);
@@ -50,7 +66,10 @@ __global__ __launch_bounds__(kExactNT) void k_v1_exact(Geometry g, const RankDes
     uint16_t *nxt = lst + n;                               // [n] parent -> root
     __shared__ uint32_t tot[kExactNT / 64];
 
-    if (wid == 0 && n > 1) {
+    if (J) {                 // draws already made by k_v1x_draws
+        const uint16_t *jw = J + (size_t)blockIdx.x * (size_t)g.B;
+        for (int i = tid; i < n; i += kExactNT) jv[i] = jw[i];
+    } else if (wid == 0 && n > 1) {
         // ---- 1. seed(a): key = 32-bit words of abs(a) (random_seed) ----
         mt_seed_int(mt, w == 0 ? epoch : epoch + w * 10000);
         // ---- 2. the draws of shuffle(range(n)): draw d is j_i = _randbelow(i + 1), i = n-1-d
@@ -125,8 +144,16 @@ size_t v1_exact_lds_bytes(int64_t n) {
 
 bool v1_exact_supported(const Geometry &g) { return g.B <= kV1ExactMaxB; }
 
+size_t v1_exact_ws_bytes(const Geometry &g, int32_t nr, int64_t pos_lo, int64_t count) {
+    const int64_t pos_hi = pos_lo + count < g.ns ? pos_lo + count : g.ns;
+    if (nr <= 0 || pos_hi <= pos_lo || !v1_exact_supported(g)) return 0;
+    const int64_t nw = (pos_hi - 1) / g.B - pos_lo / g.B + 1;
+    return (size_t)nr * (size_t)nw * (size_t)g.B * sizeof(uint16_t);
+}
+
 hipError_t launch_v1_exact(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, int32_t nr,
-                           int64_t pos_lo, int64_t count, int64_t epoch, int64_t *out, hipStream_t s) {
+                           int64_t pos_lo, int64_t count, int64_t epoch, int64_t *out, uint16_t *ws,
+                           hipStream_t s) {
     const int64_t pos_hi = pos_lo + count < g.ns ? pos_lo + count : g.ns;
     if (nr <= 0 || pos_hi <= pos_lo) return hipSuccess;
     if (!v1_exact_supported(g)) return hipErrorInvalidValue;
@@ -137,8 +164,12 @@ hipError_t launch_v1_exact(const Geometry &g, const RankDesc *ranks, int32_t ran
         (const void *)k_v1_exact, hipFuncAttributeMaxDynamicSharedMemorySize,
         (int)v1_exact_lds_bytes(kV1ExactMaxB));
     if (attr != hipSuccess) return attr;
-    hipLaunchKernelGGL(k_v1_exact, dim3((uint32_t)(nr * nw)), dim3(kExactNT), lds, s, g, ranks, rank_lo,
-                       w_lo, nw, pos_lo, count, epoch, out);
+    const dim3 grid((uint32_t)(nr * nw));
+    // with a workspace, the serial MT phases run one wave per window (many windows in flight)
+    // ahead of the resolution; without one, each workgroup's first wave does them in place
+    if (ws) hipLaunchKernelGGL(k_v1x_draws, grid, dim3(64), 0, s, g, w_lo, nw, epoch, ws);
+    hipLaunchKernelGGL(k_v1_exact, grid, dim3(kExactNT), lds, s, g, ranks, rank_lo, w_lo, nw, pos_lo,
+                       count, epoch, (const uint16_t *)ws, out);
     return hipGetLastError();
 }
 
