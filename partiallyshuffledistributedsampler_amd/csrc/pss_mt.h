@@ -3,6 +3,8 @@
 // speculative reader that turns the word stream into `_randbelow(n)` draws (random.py:239-249)
 // 64 words at a time.  Shared by pss_v1exact.hip and pss_v2exact.hip.
 #pragma once
+#include <type_traits>
+
 #include "pss_device.h"
 
 namespace pss {
@@ -33,25 +35,49 @@ __device__ __forceinline__ uint32_t mt_twist_word(uint32_t a, uint32_t b, uint32
 
 // init_by_array(key, klen) (random_seed -> init_by_array, _randommodule.c), klen <= 2.
 // Serial; run by one wave with uniform values.  mt[] is LDS.
+// lane L of v := s (a scalar): v_writelane_b32 (no clang builtin in this toolchain)
+template <int L>
+__device__ __forceinline__ uint32_t write_lane(uint32_t v, uint32_t s) {
+    __asm__ volatile("v_writelane_b32 %0, %1, %2" : "+v"(v) : "s"(s), "n"(L));
+    return v;
+}
+
+template <int L0, int Lend, class F>
+__device__ __forceinline__ void unroll_lanes(F &&f) {
+    if constexpr (L0 < Lend) {
+        f(std::integral_constant<int, L0>{});
+        unroll_lanes<L0 + 1, Lend>(f);
+    }
+}
+
 __device__ void mt_seed(uint32_t *mt, uint32_t key0, uint32_t key1, int klen) {
     const int lane = threadIdx.x & 63;
-    // loop 1: i = 1..623, then the wrap (mt[0] = mt[623]) and one more step at i = 1
-    // init_genrand(19650218)'s words are generated alongside (an independent scalar chain,
-    // cheaper than a scalar-cache load per step)
+    // Both chains run on scalar registers; each 64 results are collected into one VGPR with
+    // v_writelane (lane = step within the group) and stored with a single LDS write.
+    // loop 1: k = 0..622 at i = k + 1, then the wrap (mt[0] = mt[623]) and k = 623 at i = 1;
+    // step k adds key[k % klen] + k % klen.  init_genrand(19650218)'s words g are generated
+    // alongside (an independent chain, cheaper than a scalar-cache load per step).
+    const uint32_t add_even = key0, add_odd = klen == 2 ? key1 + 1u : key0;
     uint32_t g = 19650218u;
     uint32_t prev = g;
     uint32_t first = 0;
-    int j = 0;
-    for (int i = 1; i < kMtN; i++) {
-        g = 1812433253u * (g ^ (g >> 30)) + (uint32_t)i;
-        const uint32_t v = (g ^ ((prev ^ (prev >> 30)) * 1664525u)) + (j ? key1 : key0) + (uint32_t)j;
-        if (lane == 0) mt[i] = v;
-        if (i == 1) first = v;
-        prev = v;
-        if (++j >= klen) j = 0;
+    for (int i0 = 1; i0 < kMtN; i0 += 64) {
+        uint32_t vec = 0;
+        unroll_lanes<0, 64>([&](auto lc) {
+            constexpr int l = decltype(lc)::value;
+            const int i = i0 + l;
+            if (i < kMtN) {
+                g = 1812433253u * (g ^ (g >> 30)) + (uint32_t)i;
+                const uint32_t v = (g ^ ((prev ^ (prev >> 30)) * 1664525u)) + (((i - 1) & 1) ? add_odd : add_even);
+                vec = write_lane<l>(vec, v);
+                prev = v;
+            }
+        });
+        if (i0 == 1) first = (uint32_t)__builtin_amdgcn_readlane((int)vec, 0);
+        if (i0 + lane < kMtN) mt[i0 + lane] = vec;
     }
-    {   // k = 623: i = 1 again, prev = mt[0] = mt[623]
-        const uint32_t v = (first ^ ((prev ^ (prev >> 30)) * 1664525u)) + (j ? key1 : key0) + (uint32_t)j;
+    {   // k = 623: i = 1 again, prev = mt[0] = mt[623]; 623 is odd
+        const uint32_t v = (first ^ ((prev ^ (prev >> 30)) * 1664525u)) + add_odd;
         if (lane == 0) mt[1] = v;
         prev = v;
     }
@@ -59,16 +85,19 @@ __device__ void mt_seed(uint32_t *mt, uint32_t key0, uint32_t key1, int klen) {
     // loop 2: i = 2..623, wrap, i = 1; 623 steps.  mt[i] (loop-1 values) come from LDS in
     // 64-word vectors read ahead of the chain.
     for (int i0 = 2; i0 < kMtN; i0 += 64) {
-        const int cnt = kMtN - i0 < 64 ? kMtN - i0 : 64;
-        const uint32_t vec = (lane < cnt) ? mt[i0 + lane] : 0u;
-        uint32_t outv = 0;
-        for (int l = 0; l < cnt; l++) {
-            const uint32_t old = (uint32_t)__builtin_amdgcn_readlane((int)vec, l);
-            const uint32_t v = (old ^ ((prev ^ (prev >> 30)) * 1566083941u)) - (uint32_t)(i0 + l);
-            if (lane == l) outv = v;
-            prev = v;
-        }
-        if (lane < cnt) mt[i0 + lane] = outv;
+        const uint32_t vin = (i0 + lane < kMtN) ? mt[i0 + lane] : 0u;
+        uint32_t vec = 0;
+        unroll_lanes<0, 64>([&](auto lc) {
+            constexpr int l = decltype(lc)::value;
+            const int i = i0 + l;
+            if (i < kMtN) {
+                const uint32_t old = (uint32_t)__builtin_amdgcn_readlane((int)vin, l);
+                const uint32_t v = (old ^ ((prev ^ (prev >> 30)) * 1566083941u)) - (uint32_t)i;
+                vec = write_lane<l>(vec, v);
+                prev = v;
+            }
+        });
+        if (i0 + lane < kMtN) mt[i0 + lane] = vec;
         wave_lds_order();
     }
     {   // wrap: mt[0] = mt[623]; i = 1
