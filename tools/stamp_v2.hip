@@ -50,6 +50,19 @@ int main() {
     printf("lastocc: %d WGs G=%lld L=%lld: span %.1f us; start(us) p50 %.1f p90 %.1f max %.1f; end p10 %.1f p50 %.1f max %.1f; life p50 %.1f max %.1f\n",
            nwg, (long long)pl.G, (long long)pl.L, (r1 - r0) / 100.0, rs[nwg / 2], rs[nwg * 9 / 10], rs[nwg - 1],
            re[nwg / 10], re[nwg / 2], re[nwg - 1], life[nwg / 2], life[nwg - 1]);
+    {   // by XCC: mean end and life of the workgroups; and by tile position in the rank
+        double en[8] = {0}, lf[8] = {0}; int nx[8] = {0};
+        double enl = 0, enf = 0; int nl = 0, nf = 0;
+        for (int b = 0; b < nwg; b++) {
+            const uint64_t *x = &st[(size_t)b * 8];
+            const int xc = (int)(x[7] & 7);
+            en[xc] += (x[5] - r0) / 100.0; lf[xc] += (x[5] - x[4]) / 100.0; nx[xc]++;
+            if (b % pl.G == pl.G - 1) { enl += (x[5] - r0) / 100.0; nl++; } else { enf += (x[5] - r0) / 100.0; nf++; }
+        }
+        printf("by XCC (WGs, mean end us, mean life us):");
+        for (int k = 0; k < 8; k++) if (nx[k]) printf(" [%d: %d %.0f %.0f]", k, nx[k], en[k] / nx[k], lf[k] / nx[k]);
+        printf("\nlast tiles mean end %.1f us (%d), others %.1f us (%d)\n", enl / nl, nl, enf / nf, nf);
+    }
     printf("mean phase clk: prologue %.0f loop %.0f epilogue %.0f; CUs %zu, WGs per CU %d..%d\n",
            ph[0] / nwg, ph[1] / nwg, ph[2] / nwg, percu.size(), mn, mx);
     return 0;
