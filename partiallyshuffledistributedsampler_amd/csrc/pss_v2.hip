@@ -1086,7 +1086,7 @@ hipError_t launch_v2(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, 
                 const size_t lds = (size_t)pl.P1 * 4 + lds_keys;
                 static const int lo_nt = [] {   // A/B knob: threads per last-occurrence workgroup
                     const char *e = getenv("PSS_V2_LASTOCC_NT");
-                    return e ? atoi(e) : 512;   // 512: two rounds of workgroups even out the tail (0.065 -> 0.061 ms on C2)
+                    return e ? atoi(e) : 256;   // 512 shortens this pass (0.066 -> 0.060 ms) but the replay after it slows by as much (power-limited: interleaved A/B, tools/ab_lastocc_nt.sh)
                 }();
                 const bool pow2 = pl.P1 >= 2 && slot_paired((uint32_t)pl.P1);   // paired draws
                 const dim3 grid((uint32_t)(nr * g_need));
