@@ -286,12 +286,23 @@ template <bool NARROW>
 __global__ __launch_bounds__(64) void k_bk_emit(Geometry g, BigPlan p, int32_t rank_lo, BigWS w,
                                                 const RankDesc *__restrict__ ranks, uint32_t g_lo,
                                                 uint32_t ng, int64_t pos_lo, int64_t count,
-                                                int64_t *__restrict__ out) {
+                                                int64_t *__restrict__ out, int xcd_group) {
     __shared__ uint32_t buf[kChunk];
     __shared__ uint32_t rk[kRoundKeyWords * kMaxTileWindows];
     const uint32_t C = (uint32_t)p.C, P1 = (uint32_t)p.P1;
-    // block -> (rank r, emitted tile g_lo + tt, chunk c)
-    const uint32_t rtt = blockIdx.x / C, c = blockIdx.x - rtt * C;
+    // block -> (rank r, emitted tile g_lo + tt, chunk c).  Workgroups go to the 8 XCDs round
+    // robin by index; when the tiles divide evenly, every chunk of a tile is placed on the
+    // same XCD (tile rtt on XCD rtt % 8), so the ids the tile's 256 chunk waves scatter over
+    // its positions meet in one L2 and leave it as whole lines.
+    uint32_t rtt, c;
+    if (xcd_group && ((gridDim.x / C) & 7u) == 0) {
+        const uint32_t x = blockIdx.x & 7u, k = blockIdx.x >> 3;
+        rtt = (k / C) * 8u + x;
+        c = k - (k / C) * C;
+    } else {
+        rtt = blockIdx.x / C;
+        c = blockIdx.x - rtt * C;
+    }
     const uint32_t r = rtt / ng, tt = rtt - r * ng;
     const uint32_t rt = r * (uint32_t)p.G + g_lo + tt;
     const TileInfo ti = tile_info(p, rank_lo, rt);
@@ -376,12 +387,16 @@ hipError_t launch_v2_big(const Geometry &g, const RankDesc *ranks, int32_t rank_
             const bool narrow = g.N + g.ns < (int64_t)UINT32_MAX;
             const uint32_t ng = (uint32_t)(last_emit - g_lo + 1);
             const dim3 grid((uint32_t)nr * ng * (uint32_t)p.C);
+            static const int xcd_group = [] {   // A/B knob: 0 = chunks of a tile spread over XCDs
+                const char *e = getenv("PSS_V2BIG_XCD");
+                return e ? atoi(e) : 1;
+            }();
             if (narrow)
                 hipLaunchKernelGGL((k_bk_emit<true>), grid, dim3(64), 0, s, g, p, rank_lo, w, ranks,
-                                   (uint32_t)g_lo, ng, pos_lo, count, out);
+                                   (uint32_t)g_lo, ng, pos_lo, count, out, xcd_group);
             else
                 hipLaunchKernelGGL((k_bk_emit<false>), grid, dim3(64), 0, s, g, p, rank_lo, w, ranks,
-                                   (uint32_t)g_lo, ng, pos_lo, count, out);
+                                   (uint32_t)g_lo, ng, pos_lo, count, out, xcd_group);
         }
     }
     if (need_tail) {
