@@ -19,6 +19,7 @@
 //   k_v2_tail_f    (pss_v2.hip) the final pool from the VAL walk-back
 //
 // Same schedule as the LDS path: the output is bit-identical.
+#include <cstdio>
 #include <cstdlib>
 
 #include "pss_device.h"
@@ -69,6 +70,7 @@ struct BigWS {   // carved from one workspace; [rank][tile] blocks of fixed stri
     uint32_t *cst;    // [nr][G][C + 1]    start of each chunk's list inside the tile's list
     uint32_t *list;   // [nr][G][L]        tile-local step indices, grouped by chunk
     uint32_t *val;    // [nr][G][P1]       per-tile last inserted value per slot, or kNone
+    int32_t *err;     // device error flag (bounds guards; the handle's pss_check reports it)
 };
 
 size_t big_bytes(const BigPlan &p, int32_t nr) {
@@ -83,6 +85,7 @@ BigWS big_ws(void *base, const BigPlan &p, int32_t nr) {
     w.cst = w.cnt + t * p.nseg * p.C;
     w.list = w.cst + t * (p.C + 1);
     w.val = w.list + t * p.L;
+    w.err = nullptr;
     return w;
 }
 
@@ -194,7 +197,11 @@ __global__ __launch_bounds__(64) void k_bk_scatter(Geometry g, BigPlan p, int32_
 #pragma unroll
         for (int j = 0; j < 4; j++) {
             const uint32_t t = base + 64u * j + threadIdx.x;
-            if (t < hi) list[atomicAdd(&off[ch[j]], 1u)] = t;
+            if (t < hi) {
+                const uint32_t pos = atomicAdd(&off[ch[j]], 1u);
+                if (pos < ti.n) list[pos] = t;
+                else if (w.err) atomicOr(w.err, 16);   // counts and scatter disagree
+            }
         }
     }
 }
@@ -259,7 +266,11 @@ __global__ __launch_bounds__(64) void k_bk_lastocc(Geometry g, BigPlan p, int32_
     __syncthreads();
     const uint32_t *cst = w.cst + (size_t)rt * (C + 1);
     const uint32_t *list = w.list + (size_t)rt * p.L;
-    const uint32_t a = cst[c], b = cst[c + 1];
+    uint32_t a = cst[c], b = cst[c + 1];
+    if (a > b || b > ti.n) {                       // bounds guard: never walk outside the list
+        if (threadIdx.x == 0 && w.err) atomicOr(w.err, 32);
+        a = b = 0;
+    }
     // the list is in step order and one wave walks it in order: a later store wins (the
     // highest lane inside one store), so each slot ends with its last step
     for (uint32_t base = a; base < b; base += 256) {
@@ -282,11 +293,11 @@ __global__ __launch_bounds__(64) void k_bk_lastocc(Geometry g, BigPlan p, int32_
     }
 }
 
-template <bool NARROW>
+template <bool NARROW, bool XG>
 __global__ __launch_bounds__(64) void k_bk_emit(Geometry g, BigPlan p, int32_t rank_lo, BigWS w,
                                                 const RankDesc *__restrict__ ranks, uint32_t g_lo,
                                                 uint32_t ng, int64_t pos_lo, int64_t count,
-                                                int64_t *__restrict__ out, int xcd_group) {
+                                                int64_t *__restrict__ out) {
     __shared__ uint32_t buf[kChunk];
     __shared__ uint32_t rk[kRoundKeyWords * kMaxTileWindows];
     const uint32_t C = (uint32_t)p.C, P1 = (uint32_t)p.P1;
@@ -295,7 +306,7 @@ __global__ __launch_bounds__(64) void k_bk_emit(Geometry g, BigPlan p, int32_t r
     // same XCD (tile rtt on XCD rtt % 8), so the ids the tile's 256 chunk waves scatter over
     // its positions meet in one L2 and leave it as whole lines.
     uint32_t rtt, c;
-    if (xcd_group && ((gridDim.x / C) & 7u) == 0) {
+    if (XG) {   // host checked: nr * ng tiles divide by 8
         const uint32_t x = blockIdx.x & 7u, k = blockIdx.x >> 3;
         rtt = (k / C) * 8u + x;
         c = k - (k / C) * C;
@@ -327,7 +338,11 @@ __global__ __launch_bounds__(64) void k_bk_emit(Geometry g, BigPlan p, int32_t r
     int64_t *o = out + (int64_t)ti.rl * count + ((int64_t)ti.tlo - pos_lo);
     const uint32_t *cst = w.cst + (size_t)rt * (C + 1);
     const uint32_t *list = w.list + (size_t)rt * p.L;
-    const uint32_t a = cst[c], b = cst[c + 1];
+    uint32_t a = cst[c], b = cst[c + 1];
+    if (a > b || b > ti.n) {                       // bounds guard: never walk outside the list
+        if (threadIdx.x == 0 && w.err) atomicOr(w.err, 64);
+        a = b = 0;
+    }
     Pacer pace(b - a);
     for (uint32_t base = a; base < b; base += 256) {
         pace.step(base - a);
@@ -362,10 +377,19 @@ size_t v2_big_bytes(const Geometry &g, int32_t nr) {
 }
 
 hipError_t launch_v2_big(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, int32_t nr,
-                         int64_t pos_lo, int64_t count, int64_t *out, void *ws, hipStream_t s,
-                         const Marker &mk) {
+                         int64_t pos_lo, int64_t count, int64_t *out, void *ws, int32_t *err,
+                         hipStream_t s, const Marker &mk) {
     const BigPlan p = big_plan(g, nr);
-    const BigWS w = big_ws(ws, p, nr);
+    BigWS w = big_ws(ws, p, nr);
+    w.err = err;
+    static const bool dbg = getenv("PSS_DEBUG_SYNC") != nullptr;   // diagnostic: sync per kernel
+    auto chk = [&](const char *what) -> hipError_t {
+        if (!dbg) return hipSuccess;
+        const hipError_t e = hipStreamSynchronize(s);
+        fprintf(stderr, "[pss debug] %s: %s (P1 %lld L %lld G %lld C %lld)\n", what, hipGetErrorString(e),
+                (long long)p.P1, (long long)p.L, (long long)p.G, (long long)p.C);
+        return e;
+    };
     const int64_t pos_hi = pos_lo + count < g.ns ? pos_lo + count : g.ns;
     if (nr <= 0 || pos_hi <= pos_lo) return hipSuccess;
     const bool need_tail = pos_hi > p.T;
@@ -375,11 +399,17 @@ hipError_t launch_v2_big(const Geometry &g, const RankDesc *ranks, int32_t rank_
         const uint32_t rts = (uint32_t)(nr * p.G);
         const size_t lds_c = (size_t)p.C * 4;
         mk(K_V2_LASTOCC, s);
+        hipError_t e;
         hipLaunchKernelGGL(k_bk_count, dim3(rts * (uint32_t)p.nseg), dim3(64), lds_c, s, g, p, rank_lo, w);
+        if ((e = chk("k_bk_count")) != hipSuccess) return e;
         hipLaunchKernelGGL(k_bk_scan_seg, dim3(rts * (uint32_t)p.C), dim3(256), 0, s, p, w);
+        if ((e = chk("k_bk_scan_seg")) != hipSuccess) return e;
         hipLaunchKernelGGL(k_bk_scan_chunk, dim3(rts), dim3(1024), 0, s, p, w);
+        if ((e = chk("k_bk_scan_chunk")) != hipSuccess) return e;
         hipLaunchKernelGGL(k_bk_scatter, dim3(rts * (uint32_t)p.nseg), dim3(64), lds_c, s, g, p, rank_lo, w);
+        if ((e = chk("k_bk_scatter")) != hipSuccess) return e;
         hipLaunchKernelGGL(k_bk_lastocc, dim3(rts * (uint32_t)p.C), dim3(64), 0, s, g, p, rank_lo, w);
+        if ((e = chk("k_bk_lastocc")) != hipSuccess) return e;
         const int64_t last_emit = pos_lo < p.T ? ((pos_hi < p.T ? pos_hi : p.T) - 1) / p.L : -1;
         if (last_emit >= 0) {
             mk(K_V2_EMIT, s);
@@ -391,12 +421,15 @@ hipError_t launch_v2_big(const Geometry &g, const RankDesc *ranks, int32_t rank_
                 const char *e = getenv("PSS_V2BIG_XCD");
                 return e ? atoi(e) : 1;
             }();
-            if (narrow)
-                hipLaunchKernelGGL((k_bk_emit<true>), grid, dim3(64), 0, s, g, p, rank_lo, w, ranks,
-                                   (uint32_t)g_lo, ng, pos_lo, count, out, xcd_group);
-            else
-                hipLaunchKernelGGL((k_bk_emit<false>), grid, dim3(64), 0, s, g, p, rank_lo, w, ranks,
-                                   (uint32_t)g_lo, ng, pos_lo, count, out, xcd_group);
+            // the mapping is a template parameter chosen here: with the choice made inside the
+            // kernel (a runtime branch on gridDim), hipcc 7.2 reused a clobbered SGPR for the
+            // block index on the fallback path and the chunk index ran outside the tile
+            const bool xg = xcd_group && ((uint32_t)nr * ng) % 8u == 0;
+            auto kern = narrow ? (xg ? k_bk_emit<true, true> : k_bk_emit<true, false>)
+                               : (xg ? k_bk_emit<false, true> : k_bk_emit<false, false>);
+            hipLaunchKernelGGL(kern, grid, dim3(64), 0, s, g, p, rank_lo, w, ranks, (uint32_t)g_lo, ng,
+                               pos_lo, count, out);
+            if ((e = chk("k_bk_emit")) != hipSuccess) return e;
         }
     }
     if (need_tail) {
@@ -405,6 +438,7 @@ hipError_t launch_v2_big(const Geometry &g, const RankDesc *ranks, int32_t rank_
         vp.P1 = p.P1; vp.T = p.T; vp.L = p.L; vp.G = p.G; vp.global_buf = 1;
         hipError_t e = launch_v2_tail_vals(g, vp, ranks, rank_lo, nr, w.val, pos_lo, count, out, s, KeyTab{nullptr, 0});
         if (e != hipSuccess) return e;
+        if ((e = chk("k_v2_tail_f")) != hipSuccess) return e;
     }
     mk(-1, s);
     return hipGetLastError();

@@ -239,7 +239,8 @@ def test_v2_emit_paths_match_oracle(path, B, R, F, lo, hi):
 
 @pytest.mark.parametrize("path", ["xchg", "probe"])
 @pytest.mark.parametrize("B,R,F,lo,hi", [(20000, 3, 30, 5000, 20000), (65536, 2, 40, 10000, 30000),
-                                         (16385, 4, 20, 3000, 9000), (131072, 2, 12, 40000, 80000)])
+                                         (16385, 4, 20, 3000, 9000), (131072, 2, 12, 40000, 80000),
+                                         (20000, 8, 60, 19000, 21000)])   # 16 tiles: XCD-grouped replay
 def test_v2_large_pool_paths_match_oracle(path, B, R, F, lo, hi):
     # pools beyond the LDS slot table: slot-chunked replay ("xchg") and the HBM slot table
     # ("probe"), full epochs and ragged position ranges, against the oracle twin
