@@ -173,6 +173,8 @@ hipError_t launch_v2_tail_vals(const Geometry &g, const V2Plan &pl, const RankDe
 // pools beyond LDS (P1 in (16384, 2^22]): slot-chunked replay (pss_v2big.hip); workspace in
 // buf_ws (v2_buf_bytes covers it)
 bool v2_big_applicable(const Geometry &g);
+// launch_v2 splits into V2_STAGE_PRE / V2_STAGE_EMIT for this shape and emit path (EMIT_AUTO resolved)
+bool v2_stage_split(const Geometry &g, int32_t nr, int emit_path);
 size_t v2_big_bytes(const Geometry &g, int32_t nr);
 hipError_t launch_v2_big(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, int32_t nr,
                          int64_t pos_lo, int64_t count, int64_t *out, void *ws, int32_t *err,

@@ -276,6 +276,30 @@ struct pss_sampler {
     std::vector<Span> spans;
     int open_kind = -1;
     size_t open_ev = 0;
+    // V2 epoch lookahead: once generate() has been called with one shape for consecutive epochs,
+    // the last-occurrence pass (VAL tables + key table, which depend only on the epoch key and the
+    // shape) of epoch e+1 is queued on a low-priority side stream beside epoch e's replay, into the
+    // other of two VAL buffers.  generate(e+1) with the same shape then launches the replay only.
+    // PSS_V2_LOOKAHEAD=0 turns it off.
+    DevBuf<uint32_t> d_val2;
+    hipStream_t side = nullptr;
+    hipEvent_t ev_ahead = nullptr, ev_read[2] = {nullptr, nullptr};
+    struct Shape {
+        int64_t N, ns, B, pos_lo, count;
+        int32_t R, rank_lo, nr, path;
+        bool operator==(const Shape &o) const {
+            return N == o.N && ns == o.ns && B == o.B && pos_lo == o.pos_lo && count == o.count &&
+                   R == o.R && rank_lo == o.rank_lo && nr == o.nr && path == o.path;
+        }
+    };
+    bool ahead_valid = false;
+    Shape ahead_shape{};
+    uint32_t ahead_key0 = 0, ahead_key1 = 0;
+    int ahead_buf = 0;
+    bool last_valid = false;     // shape and epoch of the previous V2 generate
+    Shape last_shape{};
+    int64_t last_epoch = 0;
+    int val_next = 0;            // buffer a non-lookahead generate uses
 
     pss::Geometry geometry() const {
         pss::Geometry g{};
@@ -431,6 +455,10 @@ int pss_destroy(pss_sampler *h) {
         if (h->h_stage_ranks) (void)hipHostFree(h->h_stage_ranks);
         if (h->upload_done) (void)hipEventDestroy(h->upload_done);
         for (hipEvent_t e : h->ev_pool) (void)hipEventDestroy(e);
+        if (h->side) { (void)hipStreamSynchronize(h->side); (void)hipStreamDestroy(h->side); }
+        if (h->ev_ahead) (void)hipEventDestroy(h->ev_ahead);
+        for (hipEvent_t e : h->ev_read) if (e) (void)hipEventDestroy(e);
+        h->d_val2.release();
     }
     delete h;
     return PSS_OK;
@@ -504,6 +532,79 @@ int pss_prepare(pss_sampler *h, void *stream) {
     return prepare_prefix(h, (hipStream_t)stream);
 }
 
+namespace {
+
+bool lookahead_on() {
+    static const bool on = [] {
+        const char *e = getenv("PSS_V2_LOOKAHEAD");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
+// V2 counter order, splittable shape: the replay of this epoch on `s`, its last-occurrence pass
+// either taken from the lookahead queued by the previous call or run here; then, if the previous
+// call had this shape at epoch - 1, the pass of epoch + 1 on the side stream.
+int generate_v2_lookahead(pss_sampler *h, const pss::Geometry &g, int32_t rank_lo, int32_t nr,
+                          int64_t pos_lo, int64_t count, int64_t *out_dev, hipStream_t s,
+                          const pss::Marker &mk) {
+    const size_t words = (pss::v2_val_bytes(g, nr) + sizeof(uint32_t) - 1) / sizeof(uint32_t);
+    if (h->d_val.n < words || h->d_val2.n < words) {
+        if (h->side) PSS_HIP(hipStreamSynchronize(h->side));   // no pass may write a freed buffer
+        h->ahead_valid = false;
+        PSS_HIP(h->d_val.ensure(words));
+        PSS_HIP(h->d_val2.ensure(words));
+    }
+    if (!h->side) {
+        int least = 0, greatest = 0;
+        PSS_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
+        PSS_HIP(hipStreamCreateWithPriority(&h->side, hipStreamNonBlocking, least));
+        PSS_HIP(hipEventCreateWithFlags(&h->ev_ahead, hipEventDisableTiming));
+        for (hipEvent_t &e : h->ev_read) PSS_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
+    uint32_t *val[2] = {h->d_val.p, h->d_val2.p};
+    const pss_sampler::Shape shape{g.N, g.ns, g.B, pos_lo, count, g.R, rank_lo, nr, h->emit_path};
+    int buf;
+    if (h->ahead_valid && h->ahead_shape == shape && h->ahead_key0 == g.key0 && h->ahead_key1 == g.key1) {
+        buf = h->ahead_buf;
+        PSS_HIP(hipStreamWaitEvent(s, h->ev_ahead, 0));
+        PSS_HIP(pss::launch_v2(g, h->d_ranks.p, rank_lo, nr, pos_lo, count, out_dev, val[buf], nullptr,
+                               nullptr, h->d_err.p, s, mk, h->emit_path, pss::V2_STAGE_EMIT));
+    } else {
+        // a stale lookahead may still be writing its buffer: use the other one, after the last
+        // replay that read it
+        buf = h->ahead_valid ? 1 - h->ahead_buf : h->val_next;
+        PSS_HIP(hipStreamWaitEvent(s, h->ev_read[buf], 0));
+        PSS_HIP(hipStreamWaitEvent(s, h->ev_ahead, 0));   // an older lookahead may have written it
+        PSS_HIP(pss::launch_v2(g, h->d_ranks.p, rank_lo, nr, pos_lo, count, out_dev, val[buf], nullptr,
+                               nullptr, h->d_err.p, s, mk, h->emit_path, pss::V2_STAGE_ALL));
+    }
+    PSS_HIP(hipEventRecord(h->ev_read[buf], s));
+    h->val_next = 1 - buf;
+    const bool sequential = h->last_valid && h->last_shape == shape && h->last_epoch == h->epoch - 1;
+    h->last_valid = true;
+    h->last_shape = shape;
+    h->last_epoch = h->epoch;
+    h->ahead_valid = false;
+    if (sequential) {
+        pss::Geometry gn = g;
+        const uint64_t k = pss::epoch_key(h->seed, h->epoch + 1);
+        gn.key0 = (uint32_t)k; gn.key1 = (uint32_t)(k >> 32);
+        const int nb = 1 - buf;
+        PSS_HIP(hipStreamWaitEvent(h->side, h->ev_read[nb], 0));   // the replay that read it
+        PSS_HIP(pss::launch_v2(gn, h->d_ranks.p, rank_lo, nr, pos_lo, count, out_dev, val[nb], nullptr,
+                               nullptr, h->d_err.p, h->side, mk, h->emit_path, pss::V2_STAGE_PRE));
+        PSS_HIP(hipEventRecord(h->ev_ahead, h->side));
+        h->ahead_valid = true;
+        h->ahead_shape = shape;
+        h->ahead_key0 = gn.key0; h->ahead_key1 = gn.key1;
+        h->ahead_buf = nb;
+    }
+    return PSS_OK;
+}
+
+}  // namespace
+
 int pss_generate(pss_sampler *h, int32_t rank_lo, int32_t rank_hi, int64_t pos_lo,
                  int64_t count, int64_t *out_dev, void *stream) {
     if (!h) return fail(PSS_EINVAL, "NULL handle");
@@ -533,7 +634,11 @@ int pss_generate(pss_sampler *h, int32_t rank_lo, int32_t rank_hi, int64_t pos_l
         mk(pss::K_V2_EMIT, s);
         PSS_HIP(pss::launch_v2_exact(g, h->d_ranks.p, rank_lo, nr, pos_lo, count, h->epoch, out_dev,
                                      h->d_sort.p, s));
+    } else if (lookahead_on() && pss::v2_stage_split(g, nr, h->emit_path)) {
+        return generate_v2_lookahead(h, g, rank_lo, nr, pos_lo, count, out_dev, s, mk);
     } else {
+        h->ahead_valid = h->last_valid = false;
+        if (h->side) PSS_HIP(hipStreamSynchronize(h->side));   // a lookahead may still write VAL
         PSS_HIP(h->d_val.ensure(words(pss::v2_val_bytes(g, nr))));
         const size_t bb = pss::v2_buf_bytes(g, nr), sb = pss::v2_sort_bytes(g, nr);
         if (bb) PSS_HIP(h->d_buf.ensure(words(bb)));

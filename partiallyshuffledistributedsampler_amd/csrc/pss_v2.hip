@@ -1037,6 +1037,11 @@ hipError_t launch_v2_tail_vals(const Geometry &g, const V2Plan &pl, const RankDe
     return hipGetLastError();
 }
 
+bool v2_stage_split(const Geometry &g, int32_t nr, int emit_path) {
+    if (emit_path == EMIT_AUTO) emit_path = lds_xchg_ordered() ? EMIT_XCHG : EMIT_PROBE;
+    return emit_path == EMIT_XCHG && !v2_big_applicable(g) && !v2_plan(g, nr).global_buf;
+}
+
 hipError_t launch_v2(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, int32_t nr,
                      int64_t pos_lo, int64_t count, int64_t *out, uint32_t *VAL, uint32_t *gbuf,
                      uint32_t *sort_ws, int32_t *err, hipStream_t s, const Marker &mk,
@@ -1046,8 +1051,7 @@ hipError_t launch_v2(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, 
     // V2_STAGE_PRE (key table + last-occurrence pass, writes VAL) then V2_STAGE_EMIT (replay +
     // tail, reads VAL).  Only the LDS exchange path splits; everything else runs whole in the
     // PRE call and the EMIT call is a no-op.
-    const bool splittable = emit_path == EMIT_XCHG && !v2_big_applicable(g) && !v2_plan(g, nr).global_buf;
-    if (!splittable) {
+    if (!v2_stage_split(g, nr, emit_path)) {
         if (stage == V2_STAGE_EMIT) return hipSuccess;
         stage = V2_STAGE_ALL;
     }

@@ -85,6 +85,33 @@ def test_streams_match_oracle_twin(version, cfg):
         assert np.array_equal(allids, expect)
 
 
+@pytest.mark.parametrize("F,lo,hi,R,B", [(200, 50, 2000, 4, 4096), (64, 100, 300, 2, 64),
+                                        (30, 20000, 60000, 3, 1000)])
+def test_v2_epoch_lookahead_matches_oracle(F, lo, hi, R, B):
+    """Consecutive epochs of one shape take their last-occurrence pass from the lookahead queued
+    on the side stream by the previous generate; skipped / repeated epochs and shape changes in
+    between must fall back to the full launch.  Every stream == the oracle twin."""
+    rng = np.random.default_rng(F + B)
+    lengths = rng.integers(lo, hi, F)
+    N = int(lengths.sum())
+    eng = _engine(lengths, N, R, B, 2, seed=77)
+    ns = eng.num_samples
+    plan = [(0, 0, R), (1, 0, R), (2, 0, R), (3, 0, R), (5, 0, R), (6, 0, R), (6, 0, R),
+            (7, 1, R), (8, 0, R), (9, 0, R), (10, 0, R)]
+    outs = []
+    for epoch, r0, r1 in plan:
+        eng.init_iter(epoch)
+        old, new = eng.rank_starts()
+        outs.append((epoch, r0, r1, eng.generate(r0, r1), np.asarray(old).copy(), np.asarray(new).copy()))
+    torch.cuda.synchronize()
+    for epoch, r0, r1, out, old, new in outs:
+        out = out.cpu().numpy()
+        key = O.epoch_key(77, epoch)
+        for r in range(r0, r1):
+            ref = _oracle_stream(2, key, r, int(old[r]), int(new[r]), ns, B, N)
+            assert np.array_equal(out[r - r0], ref), (epoch, r)
+
+
 @pytest.mark.parametrize("version", [1, 2])
 def test_position_ranges_and_resume(version):
     rng = np.random.default_rng(5)
