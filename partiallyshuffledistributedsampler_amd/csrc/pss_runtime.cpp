@@ -558,7 +558,11 @@ int generate_v2_lookahead(pss_sampler *h, const pss::Geometry &g, int32_t rank_l
     if (!h->side) {
         int least = 0, greatest = 0;
         PSS_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
-        PSS_HIP(hipStreamCreateWithPriority(&h->side, hipStreamNonBlocking, least));
+        static const bool side_hi = [] {   // A/B knob: side stream at the greatest priority
+            const char *e = getenv("PSS_V2_LOOKAHEAD_PRIO");
+            return e && e[0] == 'h';
+        }();
+        PSS_HIP(hipStreamCreateWithPriority(&h->side, hipStreamNonBlocking, side_hi ? greatest : least));
         PSS_HIP(hipEventCreateWithFlags(&h->ev_ahead, hipEventDisableTiming));
         for (hipEvent_t &e : h->ev_read) PSS_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     }
