@@ -449,13 +449,14 @@ int pss_destroy(pss_sampler *h) {
     if (h->dev_init) {
         DeviceGuard dg(h->device);
         if (h->upload_pending) (void)hipEventSynchronize(h->upload_done);
+        if (h->side) (void)hipStreamSynchronize(h->side);   // a lookahead still writing VAL
         h->d_lens.release(); h->d_prefix.release(); h->d_order.release(); h->d_err.release();
         h->d_ranks.release(); h->d_val.release(); h->d_buf.release(); h->d_sort.release();
         if (h->h_stage_order) (void)hipHostFree(h->h_stage_order);
         if (h->h_stage_ranks) (void)hipHostFree(h->h_stage_ranks);
         if (h->upload_done) (void)hipEventDestroy(h->upload_done);
         for (hipEvent_t e : h->ev_pool) (void)hipEventDestroy(e);
-        if (h->side) { (void)hipStreamSynchronize(h->side); (void)hipStreamDestroy(h->side); }
+        if (h->side) (void)hipStreamDestroy(h->side);
         if (h->ev_ahead) (void)hipEventDestroy(h->ev_ahead);
         for (hipEvent_t e : h->ev_read) if (e) (void)hipEventDestroy(e);
         h->d_val2.release();
