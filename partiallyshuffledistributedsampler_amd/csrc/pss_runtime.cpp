@@ -650,6 +650,7 @@ int pss_generate(pss_sampler *h, int32_t rank_lo, int32_t rank_hi, int64_t pos_l
         if (sb) PSS_HIP(h->d_sort.ensure(words(sb)));
         PSS_HIP(pss::launch_v2(g, h->d_ranks.p, rank_lo, nr, pos_lo, count, out_dev, h->d_val.p,
                                h->d_buf.p, h->d_sort.p, h->d_err.p, s, mk, h->emit_path));
+        if (h->ev_read[0]) PSS_HIP(hipEventRecord(h->ev_read[0], s));   // last user of d_val
     }
     return PSS_OK;
 }

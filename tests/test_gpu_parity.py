@@ -96,10 +96,14 @@ def test_v2_epoch_lookahead_matches_oracle(F, lo, hi, R, B):
     N = int(lengths.sum())
     eng = _engine(lengths, N, R, B, 2, seed=77)
     ns = eng.num_samples
-    plan = [(0, 0, R), (1, 0, R), (2, 0, R), (3, 0, R), (5, 0, R), (6, 0, R), (6, 0, R),
-            (7, 1, R), (8, 0, R), (9, 0, R), (10, 0, R)]
+    # (epoch, ranks, emit path): "probe" calls take the unsplit path between lookaheads
+    plan = [(0, 0, R, "xchg"), (1, 0, R, "xchg"), (2, 0, R, "xchg"), (3, 0, R, "xchg"),
+            (5, 0, R, "xchg"), (6, 0, R, "xchg"), (6, 0, R, "xchg"), (7, 1, R, "xchg"),
+            (8, 0, R, "xchg"), (9, 0, R, "xchg"), (10, 0, R, "probe"), (11, 0, R, "xchg"),
+            (12, 0, R, "xchg"), (13, 0, R, "xchg")]
     outs = []
-    for epoch, r0, r1 in plan:
+    for epoch, r0, r1, path in plan:
+        eng.set_emit_path(path)
         eng.init_iter(epoch)
         old, new = eng.rank_starts()
         outs.append((epoch, r0, r1, eng.generate(r0, r1), np.asarray(old).copy(), np.asarray(new).copy()))
