@@ -219,9 +219,10 @@ def main():
         "vs_baseline": None,
         "dtype": "int64",
         "data": "synthetic",
-        "config": {"workload": "V2 two-pool sampler, %d files x %d samples, %d logical ranks "
-                               "per GPU, shuffle_buffer %d (BASELINE configs[1] per GPU)"
-                               % (F1, L, RG, B),
+        "config": {"workload": "%s, %d files x %d samples, %d logical ranks "
+                               "per GPU, shuffle_buffer %d (BASELINE configs[1] per GPU%s)"
+                               % ("V2 two-pool sampler" if ver == 2 else "V1 windowed sampler",
+                                  F1, L, RG, B, "" if ver == 2 else ", V1 variant"),
                    "version": ver, "files": F, "samples": N, "logical_ranks": R,
                    "shuffle_buffer": B, "ids_per_step": RG * ns * world,
                    "parallelism": "logical ranks sharded over %d GPU(s)" % world},
