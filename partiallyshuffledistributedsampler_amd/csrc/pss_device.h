@@ -70,8 +70,9 @@ __device__ __forceinline__ int64_t wrap_id(int64_t id, int64_t N) { return id >=
 // LDS pool permutation: perm = stable argsort of Philox keys (i>>2, c1, rank, dom)[i&3].
 // One 256-thread workgroup, n <= 256*EPT.  Keys stay in registers; LDS holds a 2^hb-bucket
 // histogram (hb = ceil(log2 n), i.e. the keys' top hb bits) and the n packed slots
-// (low 32-hb key bits << hb | i).  A bucket averages one element, so the in-bucket fix-up is
-// a short insertion sort.  Result: S[p] & (2^hb - 1) = index of the p-th smallest key.
+// (low 32-hb key bits << hb | i).  A bucket averages one element: each element's final slot is
+// its bucket start plus the count of smaller packed values in the bucket, then one in-place
+// write.  Result: S[p] & (2^hb - 1) = index of the p-th smallest key.
 // ------------------------------------------------------------------------------------------
 // Bucket arrays are padded by one word per 16 buckets: a thread that scans 16 consecutive
 // buckets then hits bank (17*t + i) mod 32 instead of a 32-way conflict on 16*t + i.
@@ -113,28 +114,48 @@ __device__ __forceinline__ int block_sort_keys(uint32_t k0, uint32_t k1, uint32_
     uint32_t run = block_excl_scan<NT>(s, tot, total);
     for (int b = blo; b < bhi; b++) { const uint32_t c = hist[bpad(b)]; hist[bpad(b)] = run; run += c; }
     __syncthreads();
+    // scatter by bucket (arbitrary order inside a bucket); each element keeps its packed value
+    // and bucket in registers
+    uint32_t bk[NQ][4];
 #pragma unroll
     for (int j = 0; j < NQ; j++)
 #pragma unroll
         for (int w = 0; w < 4; w++) {
             const int i = 4 * (tid + NT * j) + w;
+            const uint32_t k = key[j][w];
+            bk[j][w] = hb ? k >> sh : 0u;
+            key[j][w] = hb ? ((k << hb) | (uint32_t)i) : 0u;
             if (i < n) {
-                const uint32_t k = key[j][w];
-                const uint32_t pos = atomicAdd(&hist[bpad(hb ? k >> sh : 0)], 1u);
-                S[pos] = hb ? ((k << hb) | (uint32_t)i) : 0u;
+                const uint32_t pos = atomicAdd(&hist[bpad((int)bk[j][w])], 1u);
+                S[pos] = key[j][w];
             }
         }
     __syncthreads();
-    for (int b = tid; b < nb; b += NT) {  // hist[b] is now the END of bucket b
-        const int e = (int)hist[bpad(b)];
-        const int st = b ? (int)hist[bpad(b - 1)] : 0;
-        for (int x = st + 1; x < e; x++) {
-            const uint32_t v = S[x];
-            int y = x - 1;
-            while (y >= st && S[y] > v) { S[y + 1] = S[y]; y--; }
-            S[y + 1] = v;
+    // final slot of each element: bucket start + number of smaller packed values in its bucket
+    // (packed values are distinct; hist[b] is now the END of bucket b).  No divergent shifting.
+    int dst[NQ][4];
+#pragma unroll
+    for (int j = 0; j < NQ; j++)
+#pragma unroll
+        for (int w = 0; w < 4; w++) {
+            const int i = 4 * (tid + NT * j) + w;
+            dst[j][w] = -1;
+            if (i < n) {
+                const int b = (int)bk[j][w];
+                const int e = (int)hist[bpad(b)];
+                const int st = b ? (int)hist[bpad(b - 1)] : 0;
+                const uint32_t v = key[j][w];
+                int r = st;
+                for (int x = st; x < e; x++) r += S[x] < v ? 1 : 0;
+                dst[j][w] = r;
+            }
         }
-    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < NQ; j++)
+#pragma unroll
+        for (int w = 0; w < 4; w++)
+            if (dst[j][w] >= 0) S[dst[j][w]] = key[j][w];
     __syncthreads();
     return hb;
 }
