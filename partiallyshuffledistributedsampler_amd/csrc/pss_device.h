@@ -97,12 +97,17 @@ __device__ __forceinline__ int block_sort_keys(uint32_t k0, uint32_t k1, uint32_
     for (int i = tid; i < bpad_size(nb); i += NT) hist[i] = 0;
     __syncthreads();
     const int sh = 32 - hb;
+    // one returning LDS atomic per element: bucket count, and the element's ordinal in its bucket
+    uint32_t bk[NQ][4], od[NQ][4];
 #pragma unroll
     for (int j = 0; j < NQ; j++)
 #pragma unroll
         for (int w = 0; w < 4; w++) {
             const int i = 4 * (tid + NT * j) + w;
-            if (i < n) atomicAdd(&hist[bpad(hb ? key[j][w] >> sh : 0)], 1u);
+            const uint32_t k = key[j][w];
+            bk[j][w] = hb ? k >> sh : 0u;
+            key[j][w] = hb ? ((k << hb) | (uint32_t)i) : 0u;
+            od[j][w] = i < n ? atomicAdd(&hist[bpad((int)bk[j][w])], 1u) : 0u;
         }
     __syncthreads();
     const int per = nb >= NT ? nb / NT : 1;
@@ -113,26 +118,19 @@ __device__ __forceinline__ int block_sort_keys(uint32_t k0, uint32_t k1, uint32_
     uint32_t total;
     uint32_t run = block_excl_scan<NT>(s, tot, total);
     for (int b = blo; b < bhi; b++) { const uint32_t c = hist[bpad(b)]; hist[bpad(b)] = run; run += c; }
+    if (tid == 0) hist[bpad(nb)] = total;   // sentinel: end of the last bucket
     __syncthreads();
-    // scatter by bucket (arbitrary order inside a bucket); each element keeps its packed value
-    // and bucket in registers
-    uint32_t bk[NQ][4];
+    // scatter by bucket (ordinal order inside a bucket, arbitrary)
 #pragma unroll
     for (int j = 0; j < NQ; j++)
 #pragma unroll
         for (int w = 0; w < 4; w++) {
             const int i = 4 * (tid + NT * j) + w;
-            const uint32_t k = key[j][w];
-            bk[j][w] = hb ? k >> sh : 0u;
-            key[j][w] = hb ? ((k << hb) | (uint32_t)i) : 0u;
-            if (i < n) {
-                const uint32_t pos = atomicAdd(&hist[bpad((int)bk[j][w])], 1u);
-                S[pos] = key[j][w];
-            }
+            if (i < n) S[hist[bpad((int)bk[j][w])] + od[j][w]] = key[j][w];
         }
     __syncthreads();
     // final slot of each element: bucket start + number of smaller packed values in its bucket
-    // (packed values are distinct; hist[b] is now the END of bucket b).  No divergent shifting.
+    // (packed values are distinct; hist[b] is the START of bucket b).  No divergent shifting.
     int dst[NQ][4];
 #pragma unroll
     for (int j = 0; j < NQ; j++)
@@ -142,8 +140,8 @@ __device__ __forceinline__ int block_sort_keys(uint32_t k0, uint32_t k1, uint32_
             dst[j][w] = -1;
             if (i < n) {
                 const int b = (int)bk[j][w];
-                const int e = (int)hist[bpad(b)];
-                const int st = b ? (int)hist[bpad(b - 1)] : 0;
+                const int st = (int)hist[bpad(b)];
+                const int e = (int)hist[bpad(b + 1)];
                 const uint32_t v = key[j][w];
                 int r = st;
                 for (int x = st; x < e; x++) r += S[x] < v ? 1 : 0;
