@@ -178,7 +178,7 @@ bool v2_stage_split(const Geometry &g, int32_t nr, int emit_path);
 size_t v2_big_bytes(const Geometry &g, int32_t nr);
 hipError_t launch_v2_big(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, int32_t nr,
                          int64_t pos_lo, int64_t count, int64_t *out, void *ws, int32_t *err,
-                         hipStream_t s, const Marker &mk);
+                         hipStream_t s, const Marker &mk, int stage = V2_STAGE_ALL);
 hipError_t init_kernel_attributes_v2big();
 size_t v2_buf_bytes(const Geometry &g, int32_t nr);
 size_t v2_sort_bytes(const Geometry &g, int32_t nr);

@@ -277,11 +277,11 @@ struct pss_sampler {
     int open_kind = -1;
     size_t open_ev = 0;
     // V2 epoch lookahead: once generate() has been called with one shape for consecutive epochs,
-    // the last-occurrence pass (VAL tables + key table, which depend only on the epoch key and the
-    // shape) of epoch e+1 is queued on a low-priority side stream beside epoch e's replay, into the
+    // the last-occurrence pass (VAL tables + key table, or the pools-beyond-LDS bucketing
+    // workspace; all depend only on the epoch key and the shape) of epoch e+1 is queued on a low-priority side stream beside epoch e's replay, into the
     // other of two VAL buffers.  generate(e+1) with the same shape then launches the replay only.
     // PSS_V2_LOOKAHEAD=0 turns it off.
-    DevBuf<uint32_t> d_val2;
+    DevBuf<uint32_t> d_val2, d_buf2;
     hipStream_t side = nullptr;
     hipEvent_t ev_ahead = nullptr, ev_read[2] = {nullptr, nullptr};
     struct Shape {
@@ -459,7 +459,7 @@ int pss_destroy(pss_sampler *h) {
         if (h->side) (void)hipStreamDestroy(h->side);
         if (h->ev_ahead) (void)hipEventDestroy(h->ev_ahead);
         for (hipEvent_t e : h->ev_read) if (e) (void)hipEventDestroy(e);
-        h->d_val2.release();
+        h->d_val2.release(); h->d_buf2.release();
     }
     delete h;
     return PSS_OK;
@@ -550,11 +550,13 @@ int generate_v2_lookahead(pss_sampler *h, const pss::Geometry &g, int32_t rank_l
                           int64_t pos_lo, int64_t count, int64_t *out_dev, hipStream_t s,
                           const pss::Marker &mk) {
     const size_t words = (pss::v2_val_bytes(g, nr) + sizeof(uint32_t) - 1) / sizeof(uint32_t);
-    if (h->d_val.n < words || h->d_val2.n < words) {
+    const size_t bwords = (pss::v2_buf_bytes(g, nr) + sizeof(uint32_t) - 1) / sizeof(uint32_t);
+    if (h->d_val.n < words || h->d_val2.n < words || (bwords && (h->d_buf.n < bwords || h->d_buf2.n < bwords))) {
         if (h->side) PSS_HIP(hipStreamSynchronize(h->side));   // no pass may write a freed buffer
         h->ahead_valid = false;
         PSS_HIP(h->d_val.ensure(words));
         PSS_HIP(h->d_val2.ensure(words));
+        if (bwords) { PSS_HIP(h->d_buf.ensure(bwords)); PSS_HIP(h->d_buf2.ensure(bwords)); }
     }
     if (!h->side) {
         int least = 0, greatest = 0;
@@ -568,12 +570,13 @@ int generate_v2_lookahead(pss_sampler *h, const pss::Geometry &g, int32_t rank_l
         for (hipEvent_t &e : h->ev_read) PSS_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     }
     uint32_t *val[2] = {h->d_val.p, h->d_val2.p};
+    uint32_t *gbuf[2] = {bwords ? h->d_buf.p : nullptr, bwords ? h->d_buf2.p : nullptr};   // pools beyond LDS
     const pss_sampler::Shape shape{g.N, g.ns, g.B, pos_lo, count, g.R, rank_lo, nr, h->emit_path};
     int buf;
     if (h->ahead_valid && h->ahead_shape == shape && h->ahead_key0 == g.key0 && h->ahead_key1 == g.key1) {
         buf = h->ahead_buf;
         PSS_HIP(hipStreamWaitEvent(s, h->ev_ahead, 0));
-        PSS_HIP(pss::launch_v2(g, h->d_ranks.p, rank_lo, nr, pos_lo, count, out_dev, val[buf], nullptr,
+        PSS_HIP(pss::launch_v2(g, h->d_ranks.p, rank_lo, nr, pos_lo, count, out_dev, val[buf], gbuf[buf],
                                nullptr, h->d_err.p, s, mk, h->emit_path, pss::V2_STAGE_EMIT));
     } else {
         // a stale lookahead may still be writing its buffer: use the other one, after the last
@@ -581,7 +584,7 @@ int generate_v2_lookahead(pss_sampler *h, const pss::Geometry &g, int32_t rank_l
         buf = h->ahead_valid ? 1 - h->ahead_buf : h->val_next;
         PSS_HIP(hipStreamWaitEvent(s, h->ev_read[buf], 0));
         PSS_HIP(hipStreamWaitEvent(s, h->ev_ahead, 0));   // an older lookahead may have written it
-        PSS_HIP(pss::launch_v2(g, h->d_ranks.p, rank_lo, nr, pos_lo, count, out_dev, val[buf], nullptr,
+        PSS_HIP(pss::launch_v2(g, h->d_ranks.p, rank_lo, nr, pos_lo, count, out_dev, val[buf], gbuf[buf],
                                nullptr, h->d_err.p, s, mk, h->emit_path, pss::V2_STAGE_ALL));
     }
     PSS_HIP(hipEventRecord(h->ev_read[buf], s));
@@ -597,7 +600,7 @@ int generate_v2_lookahead(pss_sampler *h, const pss::Geometry &g, int32_t rank_l
         gn.key0 = (uint32_t)k; gn.key1 = (uint32_t)(k >> 32);
         const int nb = 1 - buf;
         PSS_HIP(hipStreamWaitEvent(h->side, h->ev_read[nb], 0));   // the replay that read it
-        PSS_HIP(pss::launch_v2(gn, h->d_ranks.p, rank_lo, nr, pos_lo, count, out_dev, val[nb], nullptr,
+        PSS_HIP(pss::launch_v2(gn, h->d_ranks.p, rank_lo, nr, pos_lo, count, out_dev, val[nb], gbuf[nb],
                                nullptr, h->d_err.p, h->side, mk, h->emit_path, pss::V2_STAGE_PRE));
         PSS_HIP(hipEventRecord(h->ev_ahead, h->side));
         h->ahead_valid = true;

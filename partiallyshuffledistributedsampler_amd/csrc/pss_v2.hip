@@ -1039,7 +1039,7 @@ hipError_t launch_v2_tail_vals(const Geometry &g, const V2Plan &pl, const RankDe
 
 bool v2_stage_split(const Geometry &g, int32_t nr, int emit_path) {
     if (emit_path == EMIT_AUTO) emit_path = lds_xchg_ordered() ? EMIT_XCHG : EMIT_PROBE;
-    return emit_path == EMIT_XCHG && !v2_big_applicable(g) && !v2_plan(g, nr).global_buf;
+    return emit_path == EMIT_XCHG && (v2_big_applicable(g) || !v2_plan(g, nr).global_buf);
 }
 
 hipError_t launch_v2(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, int32_t nr,
@@ -1057,7 +1057,7 @@ hipError_t launch_v2(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, 
     }
     const bool do_pre = stage != V2_STAGE_EMIT, do_emit = stage != V2_STAGE_PRE;
     if (emit_path == EMIT_XCHG && v2_big_applicable(g))   // pools beyond LDS: chunked replay
-        return launch_v2_big(g, ranks, rank_lo, nr, pos_lo, count, out, gbuf, err, s, mk);
+        return launch_v2_big(g, ranks, rank_lo, nr, pos_lo, count, out, gbuf, err, s, mk, stage);
     const V2Plan pl = v2_plan(g, nr);
     const int64_t pos_hi = pos_lo + count < g.ns ? pos_lo + count : g.ns;
     if (nr <= 0 || pos_hi <= pos_lo) return hipSuccess;

@@ -378,7 +378,10 @@ size_t v2_big_bytes(const Geometry &g, int32_t nr) {
 
 hipError_t launch_v2_big(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, int32_t nr,
                          int64_t pos_lo, int64_t count, int64_t *out, void *ws, int32_t *err,
-                         hipStream_t s, const Marker &mk) {
+                         hipStream_t s, const Marker &mk, int stage) {
+    // stage V2_STAGE_PRE: the bucketing + last-occurrence kernels (they read only the epoch key
+    // and write `ws`); V2_STAGE_EMIT: the replay and the tail, from that `ws`
+    const bool do_pre = stage != V2_STAGE_EMIT, do_emit = stage != V2_STAGE_PRE;
     const BigPlan p = big_plan(g, nr);
     BigWS w = big_ws(ws, p, nr);
     w.err = err;
@@ -398,8 +401,9 @@ hipError_t launch_v2_big(const Geometry &g, const RankDesc *ranks, int32_t rank_
         // emit runs over the tiles that hold requested positions
         const uint32_t rts = (uint32_t)(nr * p.G);
         const size_t lds_c = (size_t)p.C * 4;
-        mk(K_V2_LASTOCC, s);
         hipError_t e;
+        if (do_pre) {
+        mk(K_V2_LASTOCC, s);
         hipLaunchKernelGGL(k_bk_count, dim3(rts * (uint32_t)p.nseg), dim3(64), lds_c, s, g, p, rank_lo, w);
         if ((e = chk("k_bk_count")) != hipSuccess) return e;
         hipLaunchKernelGGL(k_bk_scan_seg, dim3(rts * (uint32_t)p.C), dim3(256), 0, s, p, w);
@@ -410,6 +414,8 @@ hipError_t launch_v2_big(const Geometry &g, const RankDesc *ranks, int32_t rank_
         if ((e = chk("k_bk_scatter")) != hipSuccess) return e;
         hipLaunchKernelGGL(k_bk_lastocc, dim3(rts * (uint32_t)p.C), dim3(64), 0, s, g, p, rank_lo, w);
         if ((e = chk("k_bk_lastocc")) != hipSuccess) return e;
+        }
+        if (!do_emit) { mk(-1, s); return hipGetLastError(); }
         const int64_t last_emit = pos_lo < p.T ? ((pos_hi < p.T ? pos_hi : p.T) - 1) / p.L : -1;
         if (last_emit >= 0) {
             mk(K_V2_EMIT, s);
@@ -432,6 +438,7 @@ hipError_t launch_v2_big(const Geometry &g, const RankDesc *ranks, int32_t rank_
             if ((e = chk("k_bk_emit")) != hipSuccess) return e;
         }
     }
+    if (!do_emit) return hipGetLastError();
     if (need_tail) {
         mk(K_V2_TAIL, s);
         V2Plan vp{};

@@ -86,7 +86,9 @@ def test_streams_match_oracle_twin(version, cfg):
 
 
 @pytest.mark.parametrize("F,lo,hi,R,B", [(200, 50, 2000, 4, 4096), (64, 100, 300, 2, 64),
-                                        (30, 20000, 60000, 3, 1000)])
+                                        (30, 20000, 60000, 3, 1000),
+                                        (20, 20000, 60000, 2, 20000),    # pools beyond LDS
+                                        (8, 100000, 200000, 2, 65536)])
 def test_v2_epoch_lookahead_matches_oracle(F, lo, hi, R, B):
     """Consecutive epochs of one shape take their last-occurrence pass from the lookahead queued
     on the side stream by the previous generate; skipped / repeated epochs and shape changes in
