@@ -281,9 +281,11 @@ struct pss_sampler {
     // workspace; all depend only on the epoch key and the shape) of epoch e+1 is queued on a low-priority side stream beside epoch e's replay, into the
     // other of two VAL buffers.  generate(e+1) with the same shape then launches the replay only.
     // PSS_V2_LOOKAHEAD=0 turns it off.
-    DevBuf<uint32_t> d_val2, d_buf2;
+    static constexpr int kLaBufs = 3;   // VAL (and big-pool workspace) ring: d_val/d_buf + 2
+    DevBuf<uint32_t> d_val2, d_buf2, d_val3, d_buf3;
     hipStream_t side = nullptr;
-    hipEvent_t ev_ahead = nullptr, ev_read[2] = {nullptr, nullptr};
+    hipEvent_t ev_read[kLaBufs] = {};   // per buffer: the last replay that read it
+    hipEvent_t ev_done[kLaBufs] = {};   // per buffer: the last lookahead pass that wrote it
     struct Shape {
         int64_t N, ns, B, pos_lo, count;
         int32_t R, rank_lo, nr, path;
@@ -292,14 +294,11 @@ struct pss_sampler {
                    R == o.R && rank_lo == o.rank_lo && nr == o.nr && path == o.path;
         }
     };
-    bool ahead_valid = false;
-    Shape ahead_shape{};
-    uint32_t ahead_key0 = 0, ahead_key1 = 0;
-    int ahead_buf = 0;
+    struct Pending { bool valid; Shape shape; uint32_t key0, key1; int buf; };
+    Pending pend[2] = {};        // queued lookahead passes (epochs e+1, e+2)
     bool last_valid = false;     // shape and epoch of the previous V2 generate
     Shape last_shape{};
     int64_t last_epoch = 0;
-    int val_next = 0;            // buffer a non-lookahead generate uses
 
     pss::Geometry geometry() const {
         pss::Geometry g{};
@@ -457,9 +456,9 @@ int pss_destroy(pss_sampler *h) {
         if (h->upload_done) (void)hipEventDestroy(h->upload_done);
         for (hipEvent_t e : h->ev_pool) (void)hipEventDestroy(e);
         if (h->side) (void)hipStreamDestroy(h->side);
-        if (h->ev_ahead) (void)hipEventDestroy(h->ev_ahead);
         for (hipEvent_t e : h->ev_read) if (e) (void)hipEventDestroy(e);
-        h->d_val2.release(); h->d_buf2.release();
+        for (hipEvent_t e : h->ev_done) if (e) (void)hipEventDestroy(e);
+        h->d_val2.release(); h->d_buf2.release(); h->d_val3.release(); h->d_buf3.release();
     }
     delete h;
     return PSS_OK;
@@ -549,14 +548,20 @@ bool lookahead_on() {
 int generate_v2_lookahead(pss_sampler *h, const pss::Geometry &g, int32_t rank_lo, int32_t nr,
                           int64_t pos_lo, int64_t count, int64_t *out_dev, hipStream_t s,
                           const pss::Marker &mk) {
+    constexpr int NB = pss_sampler::kLaBufs;
     const size_t words = (pss::v2_val_bytes(g, nr) + sizeof(uint32_t) - 1) / sizeof(uint32_t);
     const size_t bwords = (pss::v2_buf_bytes(g, nr) + sizeof(uint32_t) - 1) / sizeof(uint32_t);
-    if (h->d_val.n < words || h->d_val2.n < words || (bwords && (h->d_buf.n < bwords || h->d_buf2.n < bwords))) {
+    DevBuf<uint32_t> *V[NB] = {&h->d_val, &h->d_val2, &h->d_val3};
+    DevBuf<uint32_t> *W[NB] = {&h->d_buf, &h->d_buf2, &h->d_buf3};
+    bool grow = false;
+    for (int i = 0; i < NB; i++) grow |= V[i]->n < words || (bwords && W[i]->n < bwords);
+    if (grow) {
         if (h->side) PSS_HIP(hipStreamSynchronize(h->side));   // no pass may write a freed buffer
-        h->ahead_valid = false;
-        PSS_HIP(h->d_val.ensure(words));
-        PSS_HIP(h->d_val2.ensure(words));
-        if (bwords) { PSS_HIP(h->d_buf.ensure(bwords)); PSS_HIP(h->d_buf2.ensure(bwords)); }
+        for (auto &p : h->pend) p.valid = false;
+        for (int i = 0; i < NB; i++) {
+            PSS_HIP(V[i]->ensure(words));
+            if (bwords) PSS_HIP(W[i]->ensure(bwords));
+        }
     }
     if (!h->side) {
         int least = 0, greatest = 0;
@@ -566,47 +571,71 @@ int generate_v2_lookahead(pss_sampler *h, const pss::Geometry &g, int32_t rank_l
             return e && e[0] == 'h';
         }();
         PSS_HIP(hipStreamCreateWithPriority(&h->side, hipStreamNonBlocking, side_hi ? greatest : least));
-        PSS_HIP(hipEventCreateWithFlags(&h->ev_ahead, hipEventDisableTiming));
         for (hipEvent_t &e : h->ev_read) PSS_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        for (hipEvent_t &e : h->ev_done) PSS_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     }
-    uint32_t *val[2] = {h->d_val.p, h->d_val2.p};
-    uint32_t *gbuf[2] = {bwords ? h->d_buf.p : nullptr, bwords ? h->d_buf2.p : nullptr};   // pools beyond LDS
+    static const int depth = [] {   // epochs queued ahead: 2 (default) keeps the wait for a pass
+        const char *e = getenv("PSS_V2_LOOKAHEAD_DEPTH");   // off the replay's critical path
+        const int d = e ? atoi(e) : 2;
+        return d < 1 ? 1 : (d > 2 ? 2 : d);
+    }();
     const pss_sampler::Shape shape{g.N, g.ns, g.B, pos_lo, count, g.R, rank_lo, nr, h->emit_path};
-    int buf;
-    if (h->ahead_valid && h->ahead_shape == shape && h->ahead_key0 == g.key0 && h->ahead_key1 == g.key1) {
-        buf = h->ahead_buf;
-        PSS_HIP(hipStreamWaitEvent(s, h->ev_ahead, 0));
-        PSS_HIP(pss::launch_v2(g, h->d_ranks.p, rank_lo, nr, pos_lo, count, out_dev, val[buf], gbuf[buf],
-                               nullptr, h->d_err.p, s, mk, h->emit_path, pss::V2_STAGE_EMIT));
+    auto held = [&](int b) {
+        for (const auto &p : h->pend) if (p.valid && p.buf == b) return true;
+        return false;
+    };
+    int buf = -1;
+    for (auto &p : h->pend)
+        if (p.valid && p.shape == shape && p.key0 == g.key0 && p.key1 == g.key1) {
+            buf = p.buf;
+            p.valid = false;
+        }
+    if (buf >= 0) {
+        PSS_HIP(hipStreamWaitEvent(s, h->ev_done[buf], 0));
+        PSS_HIP(pss::launch_v2(g, h->d_ranks.p, rank_lo, nr, pos_lo, count, out_dev, V[buf]->p,
+                               bwords ? W[buf]->p : nullptr, nullptr, h->d_err.p, s, mk, h->emit_path,
+                               pss::V2_STAGE_EMIT));
     } else {
-        // a stale lookahead may still be writing its buffer: use the other one, after the last
-        // replay that read it
-        buf = h->ahead_valid ? 1 - h->ahead_buf : h->val_next;
+        // a buffer no queued lookahead holds, after its last reader and its last writer
+        for (int b = 0; b < NB && buf < 0; b++) if (!held(b)) buf = b;
         PSS_HIP(hipStreamWaitEvent(s, h->ev_read[buf], 0));
-        PSS_HIP(hipStreamWaitEvent(s, h->ev_ahead, 0));   // an older lookahead may have written it
-        PSS_HIP(pss::launch_v2(g, h->d_ranks.p, rank_lo, nr, pos_lo, count, out_dev, val[buf], gbuf[buf],
-                               nullptr, h->d_err.p, s, mk, h->emit_path, pss::V2_STAGE_ALL));
+        PSS_HIP(hipStreamWaitEvent(s, h->ev_done[buf], 0));
+        PSS_HIP(pss::launch_v2(g, h->d_ranks.p, rank_lo, nr, pos_lo, count, out_dev, V[buf]->p,
+                               bwords ? W[buf]->p : nullptr, nullptr, h->d_err.p, s, mk, h->emit_path,
+                               pss::V2_STAGE_ALL));
     }
     PSS_HIP(hipEventRecord(h->ev_read[buf], s));
-    h->val_next = 1 - buf;
     const bool sequential = h->last_valid && h->last_shape == shape && h->last_epoch == h->epoch - 1;
     h->last_valid = true;
     h->last_shape = shape;
     h->last_epoch = h->epoch;
-    h->ahead_valid = false;
-    if (sequential) {
+    uint32_t k0[3], k1[3];
+    for (int d = 1; d <= 2; d++) {
+        const uint64_t k = pss::epoch_key(h->seed, h->epoch + d);
+        k0[d] = (uint32_t)k; k1[d] = (uint32_t)(k >> 32);
+    }
+    for (auto &p : h->pend) {   // keep only passes of the coming epochs of this shape
+        const bool next = p.valid && p.shape == shape &&
+                          ((p.key0 == k0[1] && p.key1 == k1[1]) || (depth > 1 && p.key0 == k0[2] && p.key1 == k1[2]));
+        if (!next || !sequential) p.valid = false;
+    }
+    if (!sequential) return PSS_OK;
+    for (int d = 1; d <= depth; d++) {
+        bool queued = false;
+        for (const auto &p : h->pend) queued |= p.valid && p.key0 == k0[d] && p.key1 == k1[d];
+        if (queued) continue;
+        int nb = -1;
+        for (int b = 0; b < NB && nb < 0; b++) if (b != buf && !held(b)) nb = b;
+        if (nb < 0) break;
         pss::Geometry gn = g;
-        const uint64_t k = pss::epoch_key(h->seed, h->epoch + 1);
-        gn.key0 = (uint32_t)k; gn.key1 = (uint32_t)(k >> 32);
-        const int nb = 1 - buf;
+        gn.key0 = k0[d]; gn.key1 = k1[d];
         PSS_HIP(hipStreamWaitEvent(h->side, h->ev_read[nb], 0));   // the replay that read it
-        PSS_HIP(pss::launch_v2(gn, h->d_ranks.p, rank_lo, nr, pos_lo, count, out_dev, val[nb], gbuf[nb],
-                               nullptr, h->d_err.p, h->side, mk, h->emit_path, pss::V2_STAGE_PRE));
-        PSS_HIP(hipEventRecord(h->ev_ahead, h->side));
-        h->ahead_valid = true;
-        h->ahead_shape = shape;
-        h->ahead_key0 = gn.key0; h->ahead_key1 = gn.key1;
-        h->ahead_buf = nb;
+        PSS_HIP(pss::launch_v2(gn, h->d_ranks.p, rank_lo, nr, pos_lo, count, out_dev, V[nb]->p,
+                               bwords ? W[nb]->p : nullptr, nullptr, h->d_err.p, h->side, mk, h->emit_path,
+                               pss::V2_STAGE_PRE));
+        PSS_HIP(hipEventRecord(h->ev_done[nb], h->side));
+        for (auto &p : h->pend)
+            if (!p.valid) { p = {true, shape, k0[d], k1[d], nb}; break; }
     }
     return PSS_OK;
 }
@@ -645,7 +674,8 @@ int pss_generate(pss_sampler *h, int32_t rank_lo, int32_t rank_hi, int64_t pos_l
     } else if (lookahead_on() && pss::v2_stage_split(g, nr, h->emit_path)) {
         return generate_v2_lookahead(h, g, rank_lo, nr, pos_lo, count, out_dev, s, mk);
     } else {
-        h->ahead_valid = h->last_valid = false;
+        for (auto &p : h->pend) p.valid = false;
+        h->last_valid = false;
         if (h->side) PSS_HIP(hipStreamSynchronize(h->side));   // a lookahead may still write VAL
         PSS_HIP(h->d_val.ensure(words(pss::v2_val_bytes(g, nr))));
         const size_t bb = pss::v2_buf_bytes(g, nr), sb = pss::v2_sort_bytes(g, nr);
