@@ -102,7 +102,8 @@ def test_v2_epoch_lookahead_matches_oracle(F, lo, hi, R, B):
     plan = [(0, 0, R, "xchg"), (1, 0, R, "xchg"), (2, 0, R, "xchg"), (3, 0, R, "xchg"),
             (5, 0, R, "xchg"), (6, 0, R, "xchg"), (6, 0, R, "xchg"), (7, 1, R, "xchg"),
             (8, 0, R, "xchg"), (9, 0, R, "xchg"), (10, 0, R, "probe"), (11, 0, R, "xchg"),
-            (12, 0, R, "xchg"), (13, 0, R, "xchg")]
+            (12, 0, R, "xchg"), (13, 0, R, "xchg"), (14, 1, R, "xchg"), (15, 0, R, "xchg"),
+            (16, 1, R, "xchg")] + [(e, 0, R, "xchg") for e in range(17, 25)]
     outs = []
     for epoch, r0, r1, path in plan:
         eng.set_emit_path(path)
