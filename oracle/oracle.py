@@ -63,8 +63,6 @@ def lib():
         L.orc_epoch_key.restype = ctypes.c_uint64
         L.orc_feistel.argtypes = [ctypes.c_uint32, ctypes.c_uint32, U32P]
         L.orc_feistel.restype = ctypes.c_uint32
-        L.orc_sort_perm.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
-                                    ctypes.c_uint32, ctypes.c_int64, U32P]
         L.orc_v1_philox_stream.argtypes = [ctypes.c_uint64, ctypes.c_uint32] + [ctypes.c_int64] * 4 + \
             [ctypes.c_int, ctypes.c_int64, ctypes.c_int64, I64P]
         L.orc_v1_philox_stream.restype = ctypes.c_int64
@@ -204,12 +202,6 @@ def philox4x32(ctr, key64):
     o = np.zeros(4, dtype=np.uint32)
     lib().orc_philox4x32(_pu32(c), key64, _pu32(o))
     return o
-
-
-def sort_perm(key64, c1, rank, dom, n):
-    p = np.empty(max(n, 1), dtype=np.uint32)
-    lib().orc_sort_perm(key64, c1, rank, dom, n, _pu32(p))
-    return p[:n]
 
 
 def feistel(x, n, rk):

@@ -255,7 +255,7 @@ int64_t orc_v2_exact_prefix(int64_t epoch, int64_t old_start, int64_t new_start,
 #define PHILOX_M1 0xCD9E8D57U
 #define PHILOX_W0 0x9E3779B9U
 #define PHILOX_W1 0xBB67AE85U
-enum { DOM_V1_WIN = 1, DOM_V2_SLOT = 2, DOM_V2_INS = 3, DOM_V2_TAIL = 4 };
+enum { DOM_V1_WIN = 1, DOM_V2_SLOT = 2, DOM_V2_INS = 3, DOM_V2_TAIL = 4, DOM_V2_INIT = 5 };
 
 void orc_philox4x32(const uint32_t ctr_in[4], uint64_t key64, uint32_t out[4]) {
     uint32_t c0 = ctr_in[0], c1 = ctr_in[1], c2 = ctr_in[2], c3 = ctr_in[3];
@@ -282,8 +282,9 @@ uint64_t orc_epoch_key(uint64_t seed, int64_t epoch) {
     return orc_mix64(orc_mix64(seed) ^ (uint64_t)epoch);
 }
 
-/* keyed bijection of [0,n): 6-round balanced Feistel on 2h bits + cycle walking; round
- * function = top h bits of (R ^ rk[i]) * 0x9E3779B1 (multiplicative hashing) */
+/* keyed bijection of [0,n): 6-round balanced Feistel on 2h bits + cycle walking.  Round
+ * function: halves of h <= 8 bits -> top h bits of the low 16 bits of (R ^ k) * 0x9E37;
+ * wider halves -> top h bits of the low 32 bits of ((R ^ k) mod 2^24) * 0x9E3779. */
 uint32_t orc_feistel(uint32_t x, uint32_t n, const uint32_t rk[6]) {
     if (n <= 1) return 0;
     int bits = 0; while ((1ull << bits) < (uint64_t)n) bits++;
@@ -292,10 +293,8 @@ uint32_t orc_feistel(uint32_t x, uint32_t n, const uint32_t rk[6]) {
     do {
         uint32_t L = x >> h, R = x & mask;
         for (int i = 0; i < 6; i++) {
-            /* halves of <= 8 bits: 16-bit multiplicative hash (top h bits of the low 16 bits
-             * of (R ^ k) * 0x9E37); wider halves: top h bits of (R ^ k) * 0x9E3779B1 */
             uint32_t f = h <= 8 ? ((((R ^ rk[i]) * 0x9E37u) & 0xFFFFu) >> (16 - h))
-                                : (uint32_t)(((R ^ rk[i]) * 0x9E3779B1u) >> (32 - h));
+                                : ((((R ^ rk[i]) & 0xFFFFFFu) * 0x9E3779u) >> (32 - h));
             uint32_t t = L ^ f;
             L = R; R = t;
         }
@@ -304,49 +303,34 @@ uint32_t orc_feistel(uint32_t x, uint32_t n, const uint32_t rk[6]) {
     return x;
 }
 
-typedef struct { uint32_t key; uint32_t idx; } kv_t;
-static int kv_cmp(const void *a, const void *b) {
-    const kv_t *x = (const kv_t *)a, *y = (const kv_t *)b;
-    if (x->key != y->key) return x->key < y->key ? -1 : 1;
-    return x->idx < y->idx ? -1 : (x->idx > y->idx);
+/* 8 key words: Philox blocks (c0, 0, c2, dom) and (c0, 1, c2, dom) under key64 */
+static void orc_keys8(uint64_t key64, uint32_t c0, uint32_t c2, uint32_t dom, uint32_t k[8]) {
+    uint32_t a[4] = {c0, 0, c2, dom}, b[4] = {c0, 1, c2, dom};
+    orc_philox4x32(a, key64, k);
+    orc_philox4x32(b, key64, k + 4);
 }
 
-/* perm = stable argsort of Philox keys ctr=(i>>2, c1, rank, dom)[i&3], i<n */
-void orc_sort_perm(uint64_t key64, uint32_t c1, uint32_t rank, uint32_t dom, int64_t n,
-                   uint32_t *perm) {
-    kv_t *a = (kv_t *)malloc(sizeof(kv_t) * (size_t)(n > 0 ? n : 1));
-    for (int64_t q = 0; q * 4 < n; q++) {
-        uint32_t ctr[4] = {(uint32_t)q, c1, rank, dom}, o[4];
-        orc_philox4x32(ctr, key64, o);
-        for (int w = 0; w < 4 && q * 4 + w < n; w++) {
-            a[q * 4 + w].key = o[w];
-            a[q * 4 + w].idx = (uint32_t)(q * 4 + w);
-        }
-    }
-    qsort(a, (size_t)n, sizeof(kv_t), kv_cmp);
-    for (int64_t i = 0; i < n; i++) perm[i] = a[i].idx;
-    free(a);
-}
-
-/* V1 under the Philox schedule: window w of the rank block is ordered by perm_w = stable
- * argsort of Philox keys (i>>2, w, rank, DOM_V1_WIN); id = start + w*B + perm_w[p] (wrap at
- * N, V1:161-163).  Same multiset as orc_v1_exact_stream.  Positions [pos_lo, pos_lo+count). */
+/* V1 under the counter schedule: window w of the rank block is ordered by the keyed Feistel
+ * bijection of [0, len_w) with round keys orc_keys8(w, rank, DOM_V1_WIN); id = start + w*B +
+ * feistel_w(p) (wrap at N, V1:161-163).  Same multiset as orc_v1_exact_stream.  Positions
+ * [pos_lo, pos_lo+count). */
 int64_t orc_v1_philox_stream(uint64_t key64, uint32_t rank, int64_t start, int64_t ns,
                              int64_t B, int64_t N, int shuffle, int64_t pos_lo, int64_t count,
                              int64_t *out) {
     int64_t pos_hi = pos_lo + count; if (pos_hi > ns) pos_hi = ns;
     if (pos_lo >= pos_hi) return 0;
-    uint32_t *perm = (uint32_t *)malloc(sizeof(uint32_t) * (size_t)B);
     int64_t n_out = 0;
     for (int64_t w = pos_lo / B; w * B < pos_hi; w++) {
         int64_t len = ns - w * B; if (len > B) len = B;
-        if (shuffle) orc_sort_perm(key64, (uint32_t)w, rank, DOM_V1_WIN, len, perm);
-        else for (int64_t i = 0; i < len; i++) perm[i] = (uint32_t)i;
+        uint32_t rk[8];
+        if (shuffle) orc_keys8(key64, (uint32_t)w, rank, DOM_V1_WIN, rk);
         int64_t p0 = pos_lo > w * B ? pos_lo - w * B : 0;
         int64_t p1 = pos_hi - w * B < len ? pos_hi - w * B : len;
-        for (int64_t p = p0; p < p1; p++) out[n_out++] = wrap_id(start + w * B + perm[p], N);
+        for (int64_t p = p0; p < p1; p++) {
+            int64_t y = shuffle ? (int64_t)orc_feistel((uint32_t)p, (uint32_t)len, rk) : p;
+            out[n_out++] = wrap_id(start + w * B + y, N);
+        }
     }
-    free(perm);
     return n_out;
 }
 
@@ -387,43 +371,57 @@ static inline int64_t v2_vid_to_id(int64_t v, int64_t old_start, int64_t new_sta
     return wrap_id((v < 2 * B ? old_start : new_start) + v, N);
 }
 
-/* V2 under the Philox schedule (slot-replacement form of V2:96-116):
- *   P1 = min(B, ns) slots initialised with window 0 (v = s); T = ns - P1 steps;
- *   step t draws slot k_t (slot hash keyed by Philox DOM_V2_SLOT), emits buf[k_t] and stores the t-th inserted
- *   element there: window w = 1 + t/B, inserted in the order of the Feistel bijection keyed
- *   by Philox (w, 0|1, rank, DOM_V2_INS) (6 rounds);  then the final buffer is emitted in the
- *   order of the Feistel bijection of [0, P1) keyed by Philox (0, 0|1, rank, DOM_V2_TAIL).
+/* Pools beyond LDS (P1 > 16384): grouped draws.  G = ceil(P1 / 4096) groups of consecutive
+ * slots, q = P1 / G each plus one for the first P1 mod G; step t belongs to burst t / 16 and
+ * that burst to group (t / 16) mod G; the step draws uniformly inside its group. */
+#define ORC_LDS_SLOT_MAX 16384
+static inline uint32_t v2_slot_grouped(const uint32_t sk[4], int64_t t, uint32_t P1) {
+    uint32_t G = (P1 + 4095u) / 4096u, q = P1 / G, r = P1 % G;
+    uint32_t g = (uint32_t)(((uint64_t)t / 16u) % G);
+    uint32_t base = g * q + (g < r ? g : r), size = q + (g < r ? 1u : 0u);
+    uint32_t u = orc_slot_hash((uint32_t)t, sk[0], sk[1]);
+    return base + (uint32_t)(((uint64_t)u * size) >> 32);
+}
+
+/* V2 under the counter schedule (slot-replacement form of V2:96-116):
+ *   P1 = min(B, ns) slots initialised with window 0 -- slot s holds s, or for grouped pools
+ *   (P1 > 16384) the Feistel image of s keyed by orc_keys8(0, rank, DOM_V2_INIT); T = ns - P1
+ *   steps; step t draws slot k_t (slot hash keyed by Philox DOM_V2_SLOT, grouped for big
+ *   pools), emits buf[k_t] and stores the t-th inserted element there: window w = 1 + t/B,
+ *   inserted in the order of the Feistel bijection keyed by orc_keys8(w, rank, DOM_V2_INS);
+ *   then the final buffer is emitted in the order of the Feistel bijection of [0, P1) keyed by
+ *   orc_keys8(0, rank, DOM_V2_TAIL).
  * Writes all ns ids (rank order) to out; returns ns. */
 int64_t orc_v2_philox_stream(uint64_t key64, uint32_t rank, int64_t old_start,
                              int64_t new_start, int64_t ns, int64_t B, int64_t N, int64_t *out) {
     int64_t P1 = B < ns ? B : ns;
     int64_t T = ns - P1;
+    int grouped = P1 > ORC_LDS_SLOT_MAX;
     uint32_t *buf = (uint32_t *)malloc(sizeof(uint32_t) * (size_t)P1);
-    for (int64_t s = 0; s < P1; s++) buf[s] = (uint32_t)s;
+    if (grouped) {
+        uint32_t ik[8];
+        orc_keys8(key64, 0, rank, DOM_V2_INIT, ik);
+        for (int64_t s = 0; s < P1; s++) buf[s] = orc_feistel((uint32_t)s, (uint32_t)P1, ik);
+    } else {
+        for (int64_t s = 0; s < P1; s++) buf[s] = (uint32_t)s;
+    }
     int64_t cur_w = -1;
     uint32_t rk[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     uint32_t sk[4], skc[4] = {0, 0, rank, DOM_V2_SLOT};
     orc_philox4x32(skc, key64, sk);
     for (int64_t t = 0; t < T; t++) {
-        uint32_t k = v2_slot(sk, t, (uint32_t)P1);
+        uint32_t k = grouped ? v2_slot_grouped(sk, t, (uint32_t)P1) : v2_slot(sk, t, (uint32_t)P1);
         out[t] = v2_vid_to_id(buf[k], old_start, new_start, B, N);
         int64_t w = 1 + t / B, p = t % B;
-        if (w != cur_w) {   /* round keys: Philox blocks (w, 0|1, rank, DOM_V2_INS) */
-            uint32_t c0[4] = {(uint32_t)w, 0, rank, DOM_V2_INS};
-            uint32_t c1[4] = {(uint32_t)w, 1, rank, DOM_V2_INS};
-            orc_philox4x32(c0, key64, rk);
-            orc_philox4x32(c1, key64, rk + 4);
+        if (w != cur_w) {
+            orc_keys8(key64, (uint32_t)w, rank, DOM_V2_INS, rk);
             cur_w = w;
         }
         int64_t len = ns - w * B; if (len > B) len = B;
         buf[k] = (uint32_t)(w * B + orc_feistel((uint32_t)p, (uint32_t)len, rk));
     }
-    /* tail: the final buffer drained in the order of the Feistel bijection of [0, P1) keyed by
-     * Philox blocks (0, 0|1, rank, DOM_V2_TAIL) */
     uint32_t tk[8];
-    uint32_t t0[4] = {0, 0, rank, DOM_V2_TAIL}, t1[4] = {0, 1, rank, DOM_V2_TAIL};
-    orc_philox4x32(t0, key64, tk);
-    orc_philox4x32(t1, key64, tk + 4);
+    orc_keys8(key64, 0, rank, DOM_V2_TAIL, tk);
     for (int64_t j = 0; j < P1; j++)
         out[T + j] = v2_vid_to_id(buf[orc_feistel((uint32_t)j, (uint32_t)P1, tk)], old_start,
                                   new_start, B, N);

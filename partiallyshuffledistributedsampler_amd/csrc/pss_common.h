@@ -1,6 +1,7 @@
 // pss_common.h -- counter-based schedule primitives shared by the gfx950 kernels and the
-// host runtime (the Philox schedule of DESIGN.md §3).  oracle/pss_oracle.c restates the same
-// functions independently in C as the test checker; the two must agree bit-for-bit.
+// product's CPU mode (pss_cpu.cpp): the Philox schedule of DESIGN.md §3.  Both compile these
+// same definitions, so the CPU mode matches the GPU bit for bit by construction.
+// oracle/pss_oracle.c restates the schedule independently in C as the test checker.
 #pragma once
 #include <stdint.h>
 
@@ -13,7 +14,7 @@
 
 namespace pss {
 
-enum : uint32_t { DOM_V1_WIN = 1, DOM_V2_SLOT = 2, DOM_V2_INS = 3, DOM_V2_TAIL = 4 };
+enum : uint32_t { DOM_V1_WIN = 1, DOM_V2_SLOT = 2, DOM_V2_INS = 3, DOM_V2_TAIL = 4, DOM_V2_INIT = 5 };
 
 // Philox4x32-10 (Salmon et al., SC'11).  Each 64-bit product is one v_mad_u64_u32 on gfx950.
 PSS_HD void philox4x32_10(uint32_t &c0, uint32_t &c1, uint32_t &c2, uint32_t &c3,
@@ -65,9 +66,14 @@ constexpr int kFeistelRounds = 6;
 
 // Round function for halves of h <= 8 bits (windows up to 65536): the top h bits of the low
 // 16 bits of (R ^ k) * 0x9E37 -- a 16-bit multiplicative hash, so two chains fit one 32-bit
-// register and run on packed 16-bit ops (feistel2_pk16).  Wider halves: top h bits of the
-// 32-bit product (R ^ k) * 0x9E3779B1.
-constexpr uint32_t kFeistelM16 = 0x9E37u, kFeistelM32 = 0x9E3779B1u;
+// register and run on packed 16-bit ops (feistel2_pk16).  Wider halves (h in 9..16): the top h
+// bits of the low 32 bits of ((R ^ k) mod 2^24) * 0x9E3779 -- a 24 x 24-bit product, which is
+// one full-rate v_mul_u32_u24 on gfx950 (a 32-bit v_mul_lo_u32 issues at quarter rate).
+constexpr uint32_t kFeistelM16 = 0x9E37u, kFeistelM24 = 0x9E3779u;
+
+PSS_HD uint32_t feistel_f24(uint32_t r, uint32_t k, uint32_t sh) {
+    return (((r ^ k) & 0xFFFFFFu) * kFeistelM24) >> sh;
+}
 
 PSS_HD uint32_t feistel_pass(uint32_t x, uint32_t h, const uint32_t *k) {
     const uint32_t mask = (1u << h) - 1u;
@@ -84,7 +90,7 @@ PSS_HD uint32_t feistel_pass(uint32_t x, uint32_t h, const uint32_t *k) {
         const uint32_t sh = 32u - h;
 #pragma unroll
         for (int i = 0; i < kFeistelRounds; i++) {
-            const uint32_t t = L ^ (((R ^ k[i]) * kFeistelM32) >> sh);
+            const uint32_t t = L ^ feistel_f24(R, k[i], sh);
             L = R;
             R = t;
         }
@@ -153,6 +159,67 @@ PSS_HD uint32_t slot_draw(uint32_t t, uint32_t s0, uint32_t s1, uint32_t P1) {
         return u >> sh;
     }
     return scale32(slot_hash(t, s0, s1), P1);
+}
+
+// ------------------------------------------------------------------------------------------
+// V2 pools beyond LDS (P1 > kLdsSlotMax): grouped slot draws.  The P1 slots
+// are split into G = ceil(P1 / 4096) groups of q or q + 1 consecutive slots (the first r = P1
+// mod G groups have q + 1); steps come in bursts of 16, burst b = t / 16 belongs to group
+// b mod G and draws uniformly inside it.  Every group is then an independent slot machine of
+// <= 4096 slots fed by every G-th burst: one LDS-resident wave per (rank, group) replays it.
+// An element still leaves pool1 with probability ~1/P1 per step (1/S_g per step of its group,
+// one step in G), so the residence law of the reference's single pool is kept.
+// ------------------------------------------------------------------------------------------
+constexpr uint32_t kLdsSlotMax = 16384;   // largest V2 pool replayed as one LDS slot table
+constexpr uint32_t kGroupSlots = 4096;    // slots per group (at most)
+constexpr uint32_t kBurst = 16;           // consecutive steps of one group
+
+struct Groups {
+    uint32_t G, q, r;   // groups; q = P1 / G, r = P1 mod G (groups g < r have q + 1 slots)
+};
+
+PSS_HD Groups v2_groups(uint32_t P1) {
+    Groups gr;
+    gr.G = (P1 + kGroupSlots - 1) / kGroupSlots;
+    gr.q = P1 / gr.G;
+    gr.r = P1 % gr.G;
+    return gr;
+}
+PSS_HD uint32_t group_base(const Groups &gr, uint32_t g) { return g * gr.q + (g < gr.r ? g : gr.r); }
+PSS_HD uint32_t group_size(const Groups &gr, uint32_t g) { return gr.q + (g < gr.r ? 1u : 0u); }
+PSS_HD uint32_t group_of_step(const Groups &gr, uint32_t t) { return (t / kBurst) % gr.G; }
+
+// slot drawn at step t of a grouped pool
+PSS_HD uint32_t slot_draw_grouped(uint32_t t, uint32_t s0, uint32_t s1, const Groups &gr) {
+    const uint32_t g = group_of_step(gr, t);
+    return group_base(gr, g) + scale32(slot_hash(t, s0, s1), group_size(gr, g));
+}
+
+// global step of sub-step u of group g's stream (its bursts are b = m * G + g, m = u / 16)
+PSS_HD uint64_t group_step(const Groups &gr, uint32_t g, uint64_t u) {
+    return ((u / kBurst) * gr.G + g) * kBurst + (u % kBurst);
+}
+
+// number of the steps t < T that group g draws (its sub-stream length)
+PSS_HD uint64_t group_steps(const Groups &gr, uint32_t g, uint64_t T) {
+    const uint64_t full = T / kBurst, rem = T % kBurst;
+    uint64_t n = (full / gr.G + (g < full % gr.G ? 1u : 0u)) * kBurst;
+    if (rem && full % gr.G == g) n += rem;
+    return n;
+}
+
+// ------------------------------------------------------------------------------------------
+// Philox-derived keys (the counters of DESIGN.md §3's domain table), one definition for the
+// kernels and the CPU mode
+// ------------------------------------------------------------------------------------------
+// 8 words = Philox blocks (c0, 0, c2, dom) and (c0, 1, c2, dom); Feistel uses the first 6
+PSS_HD void round_keys8(uint32_t key0, uint32_t key1, uint32_t c0, uint32_t c2, uint32_t dom,
+                        uint32_t k[8]) {
+    for (uint32_t h = 0; h < 2; h++) {
+        uint32_t a = c0, b = h, c = c2, d = dom;
+        philox4x32_10_rolled(a, b, c, d, key0, key1);
+        k[4 * h] = a; k[4 * h + 1] = b; k[4 * h + 2] = c; k[4 * h + 3] = d;
+    }
 }
 
 }  // namespace pss

@@ -67,103 +67,6 @@ __device__ __forceinline__ T block_excl_scan(T x, T *tot, T &total) {
 __device__ __forceinline__ int64_t wrap_id(int64_t id, int64_t N) { return id >= N ? id - N : id; }
 
 // ------------------------------------------------------------------------------------------
-// LDS pool permutation: perm = stable argsort of Philox keys (i>>2, c1, rank, dom)[i&3].
-// One 256-thread workgroup, n <= 256*EPT.  Keys stay in registers; LDS holds a 2^hb-bucket
-// histogram (hb = ceil(log2 n), i.e. the keys' top hb bits) and the n packed slots
-// (low 32-hb key bits << hb | i).  A bucket averages one element: each element's final slot is
-// its bucket start plus the count of smaller packed values in the bucket, then one in-place
-// write.  Result: S[p] & (2^hb - 1) = index of the p-th smallest key.
-// ------------------------------------------------------------------------------------------
-// Bucket arrays are padded by one word per 16 buckets: a thread that scans 16 consecutive
-// buckets then hits bank (17*t + i) mod 32 instead of a 32-way conflict on 16*t + i.
-__device__ __forceinline__ int bpad(int b) { return b + (b >> 4); }
-__host__ __device__ constexpr int bpad_size(int nb) { return nb + nb / 16 + 1; }
-
-template <int EPT, int NT = 256>
-__device__ __forceinline__ int block_sort_keys(uint32_t k0, uint32_t k1, uint32_t c1,
-                                               uint32_t rank, uint32_t dom, int n,
-                                               uint32_t *S, uint32_t *hist, uint32_t *tot) {
-    constexpr int NQ = EPT / 4;
-    const int tid = threadIdx.x;
-    const int hb = n > 1 ? ceil_log2_u64((uint64_t)n) : 0;
-    const int nb = 1 << hb;
-    uint32_t key[NQ][4];
-#pragma unroll
-    for (int j = 0; j < NQ; j++) {
-        uint32_t c0 = (uint32_t)(tid + NT * j), cc1 = c1, c2 = rank, c3 = dom;
-        philox4x32_10(c0, cc1, c2, c3, k0, k1);
-        key[j][0] = c0; key[j][1] = cc1; key[j][2] = c2; key[j][3] = c3;
-    }
-    for (int i = tid; i < bpad_size(nb); i += NT) hist[i] = 0;
-    __syncthreads();
-    const int sh = 32 - hb;
-    // one returning LDS atomic per element: bucket count, and the element's ordinal in its bucket
-    uint32_t bk[NQ][4], od[NQ][4];
-#pragma unroll
-    for (int j = 0; j < NQ; j++)
-#pragma unroll
-        for (int w = 0; w < 4; w++) {
-            const int i = 4 * (tid + NT * j) + w;
-            const uint32_t k = key[j][w];
-            bk[j][w] = hb ? k >> sh : 0u;
-            key[j][w] = hb ? ((k << hb) | (uint32_t)i) : 0u;
-            od[j][w] = i < n ? atomicAdd(&hist[bpad((int)bk[j][w])], 1u) : 0u;
-        }
-    __syncthreads();
-    const int per = nb >= NT ? nb / NT : 1;
-    const int blo = tid * per < nb ? tid * per : nb;
-    const int bhi = blo + per < nb ? blo + per : nb;
-    uint32_t s = 0;
-    for (int b = blo; b < bhi; b++) s += hist[bpad(b)];
-    uint32_t total;
-    uint32_t run = block_excl_scan<NT>(s, tot, total);
-    for (int b = blo; b < bhi; b++) { const uint32_t c = hist[bpad(b)]; hist[bpad(b)] = run; run += c; }
-    if (tid == 0) hist[bpad(nb)] = total;   // sentinel: end of the last bucket
-    __syncthreads();
-    // scatter by bucket (ordinal order inside a bucket, arbitrary)
-#pragma unroll
-    for (int j = 0; j < NQ; j++)
-#pragma unroll
-        for (int w = 0; w < 4; w++) {
-            const int i = 4 * (tid + NT * j) + w;
-            if (i < n) S[hist[bpad((int)bk[j][w])] + od[j][w]] = key[j][w];
-        }
-    __syncthreads();
-    // final slot of each element: bucket start + number of smaller packed values in its bucket
-    // (packed values are distinct; hist[b] is the START of bucket b).  No divergent shifting.
-    int dst[NQ][4];
-#pragma unroll
-    for (int j = 0; j < NQ; j++)
-#pragma unroll
-        for (int w = 0; w < 4; w++) {
-            const int i = 4 * (tid + NT * j) + w;
-            dst[j][w] = -1;
-            if (i < n) {
-                const int b = (int)bk[j][w];
-                const int st = (int)hist[bpad(b)];
-                const int e = (int)hist[bpad(b + 1)];
-                const uint32_t v = key[j][w];
-                int r = st;
-                for (int x = st; x < e; x++) r += S[x] < v ? 1 : 0;
-                dst[j][w] = r;
-            }
-        }
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < NQ; j++)
-#pragma unroll
-        for (int w = 0; w < 4; w++)
-            if (dst[j][w] >= 0) S[dst[j][w]] = key[j][w];
-    __syncthreads();
-    return hb;
-}
-
-template <int EPT, int NT = 256>
-constexpr size_t sort_lds_bytes() {
-    return (size_t)(NT * EPT + bpad_size(NT * EPT) + 16) * sizeof(uint32_t);
-}
-
-// ------------------------------------------------------------------------------------------
 // V2 helpers
 // ------------------------------------------------------------------------------------------
 // slot draw of step t = sb*256 + j*64 + lane (super-batch sb, sub-batch j): slot_hash under

@@ -32,7 +32,6 @@ struct V2Plan {         // slot-machine tiling of one V2 stream (DESIGN.md §3.3
     int64_t T;          // replacement steps = ns - P1
     int64_t L;          // steps per tile
     int64_t G;          // tiles per rank = ceil(T / L)
-    int32_t global_buf; // 1: slot table lives in HBM scratch (P1 beyond the LDS budget)
     int32_t fold;       // 1: every virtual id < 2^24, probe byte folded into the slot word
     int64_t emit_lds;   // dynamic LDS of one k_v2_emit wave (padded to cap waves per CU)
     // 32-bit constants of the replay, computed on the host so that no kernel prologue runs a
@@ -53,54 +52,9 @@ struct Marker {
     void operator()(int kind, hipStream_t s) const { if (mark) mark(ctx, kind, s); }
 };
 
-constexpr int kLdsSortMax = 16384;  // largest pool sorted entirely in LDS
-constexpr int kLdsSlotMax = 16384;  // largest V2 slot table kept in LDS
 constexpr uint32_t kNone = 0xFFFFFFFFu;
 constexpr int kMarkBytes = 4096;    // V2 collision-probe bytes in LDS (slot & 4095)
 constexpr int kBucketCap = 8192;    // largest bucket the HBM multi-pass sort finishes in LDS
-
-// Pools too large for LDS (pss_bigsort.hip): a batch of independent permutation jobs.
-// Job j of the batch -> (rank, counter word c1, length n); all share the Philox domain.
-struct SortJobs {
-    int32_t kind;        // 0: V1 windows, j = rl*nw + (w - w_lo);  1: V2 tails, j = rl
-    int32_t rank_lo;
-    int64_t nw, w_lo;    // V1
-    int64_t B, ns, P1;
-    int64_t nmax;        // longest job
-    uint32_t dom;
-};
-
-__host__ __device__ inline void sort_job(const SortJobs &J, int64_t j, uint32_t &rank,
-                                         uint32_t &c1, int64_t &n) {
-    if (J.kind == 0) {
-        const int64_t rl = j / J.nw, w = J.w_lo + j % J.nw;
-        rank = (uint32_t)(J.rank_lo + rl);
-        c1 = (uint32_t)w;
-        const int64_t rem = J.ns - w * J.B;
-        n = rem < J.B ? rem : J.B;
-    } else {
-        rank = (uint32_t)(J.rank_lo + j);
-        c1 = 0;
-        n = J.P1;
-    }
-}
-
-struct BigSortWS {       // per batch of nj jobs, stride nmax (see big_sort_bytes)
-    uint32_t *start;     // [nj][nb + 1] bucket starts (exclusive scan), start[nb] = n
-    uint32_t *cur;       // [nj][nb]     scatter cursors
-    uint64_t *tmp;       // [nj][nmax]   (key << 32 | index) in bucket order
-    uint32_t *perm;      // [nj][nmax]   sorted indices
-    int64_t nb, nmax;
-    int32_t hb;          // bucket bits
-};
-size_t big_sort_bytes(int64_t nmax, int64_t nj);
-BigSortWS big_sort_ws(void *base, int64_t nmax, int64_t nj);
-// sorts jobs [job_lo, job_lo + nj) into ws.perm
-hipError_t launch_big_sort(const Geometry &g, const SortJobs &J, int64_t job_lo, int64_t nj,
-                           const BigSortWS &ws, int32_t *err, hipStream_t s);
-// jobs per batch so that one batch's workspace stays within `budget` bytes
-int64_t big_sort_batch(int64_t nmax, int64_t njobs, size_t budget);
-constexpr size_t kBigSortBudget = (size_t)2 << 30;
 
 // tiling of a launch over nr ranks: sized so that k_v2_emit fills every SIMD with two waves
 V2Plan v2_plan(const Geometry &g, int32_t nr);
@@ -128,10 +82,11 @@ hipError_t launch_map(const int64_t *prefix, int64_t F, const int64_t *ids, int6
 hipError_t launch_digest(const int64_t *ids, int64_t n, uint64_t *acc, hipStream_t s);
 hipError_t launch_digest_range(int64_t lo, int64_t hi, uint64_t *acc, hipStream_t s);
 
-// V1: ids of positions [pos_lo, pos_lo+count) of ranks [rank_lo, rank_lo+nr) -> out[r][count]
+// V1: ids of positions [pos_lo, pos_lo+count) of ranks [rank_lo, rank_lo+nr) -> out[r][count];
+// each window ordered by its keyed Feistel bijection (key table of the windows in key_ws)
 hipError_t launch_v1(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, int32_t nr,
-                     int64_t pos_lo, int64_t count, int64_t *out, uint32_t *sort_ws,
-                     int32_t *err, hipStream_t s, const Marker &mk = Marker());
+                     int64_t pos_lo, int64_t count, int64_t *out, uint32_t *key_ws,
+                     hipStream_t s, const Marker &mk = Marker());
 size_t v1_workspace_bytes(const Geometry &g, int32_t nr, int64_t pos_lo, int64_t count);
 
 // V1 in the reference's exact order (CPython MT19937 per window, pss_v1exact.hip): windows up
@@ -170,16 +125,19 @@ hipError_t launch_v2_tail_vals(const Geometry &g, const V2Plan &pl, const RankDe
                                int32_t rank_lo, int32_t nr, const uint32_t *VAL, int64_t pos_lo,
                                int64_t count, int64_t *out, hipStream_t s,
                                KeyTab kt);
-// pools beyond LDS (P1 in (16384, 2^22]): slot-chunked replay (pss_v2big.hip); workspace in
-// buf_ws (v2_buf_bytes covers it)
-bool v2_big_applicable(const Geometry &g);
+// pools beyond LDS (P1 > kLdsSlotMax): the grouped slot machine (pss_v2grp.hip); its key
+// table and per-tile tables live in val_ws (v2_val_bytes), the final tables in buf_ws
+// (v2_buf_bytes)
+bool v2_grouped(const Geometry &g);
+size_t v2_grp_val_bytes(const Geometry &g, int32_t nr);
+size_t v2_grp_fin_bytes(const Geometry &g, int32_t nr);
+hipError_t launch_v2_grp(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, int32_t nr,
+                         int64_t pos_lo, int64_t count, int64_t *out, uint32_t *val_ws,
+                         uint32_t *fin_ws, hipStream_t s, const Marker &mk, bool ordered,
+                         int stage);
+hipError_t init_kernel_attributes_v2grp();
 // launch_v2 splits into V2_STAGE_PRE / V2_STAGE_EMIT for this shape and emit path (EMIT_AUTO resolved)
 bool v2_stage_split(const Geometry &g, int32_t nr, int emit_path);
-size_t v2_big_bytes(const Geometry &g, int32_t nr);
-hipError_t launch_v2_big(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, int32_t nr,
-                         int64_t pos_lo, int64_t count, int64_t *out, void *ws, int32_t *err,
-                         hipStream_t s, const Marker &mk, int stage = V2_STAGE_ALL);
-hipError_t init_kernel_attributes_v2big();
 size_t v2_buf_bytes(const Geometry &g, int32_t nr);
 size_t v2_sort_bytes(const Geometry &g, int32_t nr);
 
@@ -188,7 +146,6 @@ hipError_t launch_debug_wave_scan(const uint64_t *in, uint64_t *out, int64_t n, 
 
 hipError_t init_kernel_attributes();
 hipError_t init_kernel_attributes_v2();
-hipError_t init_kernel_attributes_bigsort();
 
 
 

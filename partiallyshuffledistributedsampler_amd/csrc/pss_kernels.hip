@@ -1,15 +1,14 @@
 // pss_kernels.hip -- gfx950 (MI355X / CDNA4) kernels of the partial-shuffle sampler:
 // prologue (scan + partition), V1 generation, id -> (file, offset) map, coverage digest.
-// V2 lives in pss_v2.hip, pools beyond LDS in pss_bigsort.hip, primitives in pss_device.h.
+// V2 lives in pss_v2.hip (pools beyond LDS: pss_v2grp.hip), primitives in pss_device.h.
 //
 // The hot path of the reference (index generation, V1:157-172 / V2:96-116, and the id ->
 // (file, offset) scan, V1:181-221) is restated as integer, HBM-write-bound kernels:
 //
 //   k_scan_partial/_final  exclusive scan of files_len over the shuffled file order (wave64 DPP)
 //   k_part_*           balanced file -> rank partition (segments of each rank's id block)
-//   k_v1_lds<EPT>      V1: one workgroup per (rank, window); pool permutation = stable sort
-//                      of Philox keys in LDS (bucket pass on the top key bits + fix-up)
-//   k_v1_write_big     V1 windows > 16384: ids from the HBM multi-pass sort
+//   k_v1_feistel       V1: each window's permutation is a keyed Feistel bijection, evaluated
+//                      per position (random access, no sort; k_v1_keys: per-window round keys)
 //   k_map, k_digest    id -> (file position, offset); coverage digest for the RCCL check
 //
 // Schedule definitions: DESIGN.md §3, restated on the CPU in oracle/pss_oracle.c
@@ -224,51 +223,96 @@ __global__ void k_debug_wave_scan(const uint64_t *in, uint64_t *out, int64_t n) 
 }
 
 // ------------------------------------------------------------------------------------------
-// V1 (V1:157-172): window w of rank r -> ids start + w*B + perm_w[p], wrap at N
+// V1 (V1:157-172): window w of rank r -> ids start + w*B + perm_w[p], wrap at N, where perm_w
+// is the keyed Feistel bijection of [0, len_w) under round_keys8(w, rank, DOM_V1_WIN).  Random
+// access, no sort: every position is computed independently, so the kernel is a pure
+// compute + coalesced-store stream (the sort-based kernel it replaces spent its time in Philox
+// sort keys and LDS bucket passes).
 // ------------------------------------------------------------------------------------------
-template <int EPT, int NT>
-__global__ __launch_bounds__(NT) void k_v1_lds(Geometry g, const RankDesc *__restrict__ ranks,
-                                               int32_t rank_lo, int64_t w_lo, int64_t nw,
-                                               int64_t pos_lo, int64_t count,
-                                               int64_t *__restrict__ out) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-    uint32_t *S = smem, *hist = smem + NT * EPT, *tot = hist + bpad_size(NT * EPT);
-    const int32_t rl = (int32_t)(blockIdx.x / nw);
-    const int64_t w = w_lo + (int64_t)(blockIdx.x % nw);
-    const int32_t rank = rank_lo + rl;
-    const int64_t wb = w * g.B;
-    const int64_t n = g.ns - wb < g.B ? g.ns - wb : g.B;
-    const int64_t base = ranks[rank].new_start + wb;
-    int hb = 0;
-    if (g.shuffle) hb = block_sort_keys<EPT, NT>(g.key0, g.key1, (uint32_t)w, (uint32_t)rank, DOM_V1_WIN, (int)n, S, hist, tot);
-    const uint32_t mask = (1u << hb) - 1u;
-    int64_t *o = out + (int64_t)rl * count - pos_lo;
-    int64_t p0 = 0, p1 = n;
-    if (wb < pos_lo) p0 = pos_lo - wb;
-    if (wb + n > pos_lo + count) p1 = pos_lo + count - wb;
-    for (int64_t p = p0 + threadIdx.x; p < p1; p += NT) {
-        const uint32_t idx = g.shuffle ? (S[p] & mask) : (uint32_t)p;
-        o[wb + p] = wrap_id(base + idx, g.N);
-    }
+__global__ __launch_bounds__(256) void k_v1_keys(Geometry g, int32_t rank_lo, int64_t w_lo,
+                                                 int64_t nw, uint32_t *__restrict__ kt) {
+    const int32_t rl = (int32_t)blockIdx.y;
+    const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (j >= nw) return;
+    uint32_t k[kRoundKeyWords];
+    round_keys8(g.key0, g.key1, (uint32_t)(w_lo + j), (uint32_t)(rank_lo + rl), DOM_V1_WIN, k);
+    uint32_t *b = kt + ((int64_t)rl * nw + j) * kRoundKeyWords;
+#pragma unroll
+    for (int i = 0; i < kRoundKeyWords; i++) b[i] = k[i];
 }
 
-__global__ __launch_bounds__(256) void k_v1_write_big(Geometry g, const RankDesc *__restrict__ ranks,
-                                                     SortJobs J, int64_t job_lo, BigSortWS ws,
-                                                     int64_t pos_lo, int64_t count,
-                                                     int64_t *__restrict__ out) {
-    const int64_t jj = blockIdx.y;
-    uint32_t rank, w;
-    int64_t n;
-    sort_job(J, job_lo + jj, rank, w, n);
-    const int64_t rl = (int64_t)rank - J.rank_lo;
-    const int64_t wb = (int64_t)w * g.B;
-    const int64_t base = ranks[rank].new_start + wb;
-    const uint32_t *perm = ws.perm + jj * ws.nmax;
-    int64_t *o = out + rl * count - pos_lo;
-    const int64_t pos_hi = pos_lo + count;
-    for (int64_t p = (int64_t)blockIdx.x * 1024 + threadIdx.x; p < n && p < (int64_t)(blockIdx.x + 1) * 1024; p += 256) {
-        const int64_t pos = wb + p;
-        if (pos >= pos_lo && pos < pos_hi) o[pos] = wrap_id(base + perm[p], g.N);
+struct V1Plan {
+    int64_t sb_lo, nsb;        // 256-position super-blocks [sb_lo, sb_lo + nsb) of each rank
+    int64_t per_wave;          // super-blocks per wave
+    int64_t w_lo, nw;          // windows of the key table
+    uint32_t B, hB, walk_full, fast_ok;
+};
+
+// One wave per (rank, run of per_wave super-blocks).  Lane l computes positions p0 + 64 j + l,
+// j < 4, of each 256-position super-block p0.
+template <bool PACKED>
+__global__ __launch_bounds__(64) void k_v1_feistel(Geometry g, V1Plan vp, const RankDesc *__restrict__ ranks,
+                                                   int32_t rank_lo, const uint32_t *__restrict__ kt,
+                                                   int64_t pos_lo, int64_t count,
+                                                   int64_t *__restrict__ out) {
+    const int lane = threadIdx.x;
+    const int64_t waves_per_rank = (vp.nsb + vp.per_wave - 1) / vp.per_wave;
+    const int32_t rl = (int32_t)(blockIdx.x / waves_per_rank);
+    const int64_t sb0 = vp.sb_lo + (int64_t)(blockIdx.x % waves_per_rank) * vp.per_wave;
+    const int64_t sb1 = sb0 + vp.per_wave < vp.sb_lo + vp.nsb ? sb0 + vp.per_wave : vp.sb_lo + vp.nsb;
+    const int64_t start = ranks[rank_lo + rl].new_start;
+    const int64_t pos_hi = pos_lo + count < g.ns ? pos_lo + count : g.ns;
+    int64_t *o = out + (int64_t)rl * count - pos_lo;
+    const uint32_t *ktr = kt + (int64_t)rl * vp.nw * kRoundKeyWords;
+    const int64_t B = vp.B;
+    for (int64_t sb = sb0; sb < sb1; sb++) {
+        const int64_t p0 = sb * 256;
+        const int64_t w = p0 / B;                    // wave-uniform
+        const int64_t wB = w * B;
+        const bool fast = vp.fast_ok && p0 >= pos_lo && p0 + 256 <= pos_hi && wB + B <= g.ns &&
+                          p0 + 256 <= wB + B;
+        if (fast) {
+            // whole super-block inside one full window of 4^hB elements: no cycle walking
+            const uint32_t *kw = ktr + (w - vp.w_lo) * kRoundKeyWords;
+            const uint32_t x0 = (uint32_t)(p0 - wB);
+            const int64_t base = start + wB;
+            uint32_t y[4];
+            if constexpr (PACKED) {
+                uint32_t kp[kFeistelRounds];
+#pragma unroll
+                for (int i = 0; i < kFeistelRounds; i++)
+                    kp[i] = (__builtin_amdgcn_readfirstlane(kw[i]) & 0xFFFFu) * 0x10001u;
+                const uint32_t x[4] = {x0 + lane, x0 + 64u + lane, x0 + 128u + lane, x0 + 192u + lane};
+                feistel4_pk16(x, vp.hB, kp, y);
+            } else {
+                uint32_t kk[kFeistelRounds];
+#pragma unroll
+                for (int i = 0; i < kFeistelRounds; i++) kk[i] = __builtin_amdgcn_readfirstlane(kw[i]);
+#pragma unroll
+                for (int j = 0; j < 4; j++) y[j] = feistel_once(x0 + 64u * j + lane, vp.hB, kk);
+            }
+            int64_t *ob = o + p0;
+#pragma unroll
+            for (int j = 0; j < 4; j++) ob[64 * j + lane] = wrap_id(base + y[j], g.N);
+            continue;
+        }
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int64_t p = p0 + 64 * j + lane;
+            if (p < pos_lo || p >= pos_hi) continue;
+            int64_t y = p;
+            if (g.shuffle) {
+                const int64_t wp = p / B;
+                const int64_t len = g.ns - wp * B < B ? g.ns - wp * B : B;
+                const uint32_t *kw = ktr + (wp - vp.w_lo) * kRoundKeyWords;
+                uint32_t kk[kFeistelRounds];
+#pragma unroll
+                for (int i = 0; i < kFeistelRounds; i++) kk[i] = kw[i];
+                y = wp * B + feistel((uint32_t)(p - wp * B), (uint32_t)len,
+                                     feistel_half_bits((uint32_t)len), kk);
+            }
+            o[p] = wrap_id(start + y, g.N);
+        }
     }
 }
 
@@ -350,15 +394,6 @@ hipError_t launch_debug_wave_scan(const uint64_t *in, uint64_t *out, int64_t n, 
     return hipGetLastError();
 }
 
-template <int EPT, int NT = 256>
-static void launch_v1_ept(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, int32_t nr,
-                          int64_t w_lo, int64_t nw, int64_t pos_lo, int64_t count, int64_t *out,
-                          hipStream_t s) {
-    const size_t lds = g.shuffle ? sort_lds_bytes<EPT, NT>() : 16;
-    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_v1_lds<EPT, NT>), dim3((uint32_t)(nr * nw)), dim3(NT), lds, s,
-                       g, ranks, rank_lo, w_lo, nw, pos_lo, count, out);
-}
-
 static bool v1_window_range(const Geometry &g, int64_t pos_lo, int64_t count, int64_t &w_lo,
                             int64_t &nw) {
     const int64_t pos_hi = pos_lo + count < g.ns ? pos_lo + count : g.ns;
@@ -368,70 +403,49 @@ static bool v1_window_range(const Geometry &g, int64_t pos_lo, int64_t count, in
     return true;
 }
 
-static SortJobs v1_jobs(const Geometry &g, int32_t rank_lo, int64_t w_lo, int64_t nw) {
-    SortJobs J{};
-    J.kind = 0; J.rank_lo = rank_lo; J.nw = nw; J.w_lo = w_lo;
-    J.B = g.B; J.ns = g.ns; J.P1 = 0; J.dom = DOM_V1_WIN;
-    J.nmax = g.B < g.ns ? g.B : g.ns;
-    return J;
-}
-
+// key table: kRoundKeyWords words per (local rank, window of the position range)
 size_t v1_workspace_bytes(const Geometry &g, int32_t nr, int64_t pos_lo, int64_t count) {
     int64_t w_lo, nw;
-    const int64_t nmax = g.B < g.ns ? g.B : g.ns;
-    if (!g.shuffle || nmax <= kLdsSortMax || nr <= 0 || !v1_window_range(g, pos_lo, count, w_lo, nw))
-        return 0;
-    const int64_t jb = big_sort_batch(nmax, (int64_t)nr * nw, kBigSortBudget);
-    return big_sort_bytes(nmax, jb);
+    if (!g.shuffle || nr <= 0 || !v1_window_range(g, pos_lo, count, w_lo, nw)) return 0;
+    return (size_t)nr * (size_t)nw * kRoundKeyWords * sizeof(uint32_t);
 }
 
 hipError_t launch_v1(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, int32_t nr,
-                     int64_t pos_lo, int64_t count, int64_t *out, uint32_t *sort_ws,
-                     int32_t *err, hipStream_t s, const Marker &mk) {
+                     int64_t pos_lo, int64_t count, int64_t *out, uint32_t *key_ws,
+                     hipStream_t s, const Marker &mk) {
     int64_t w_lo, nw;
     if (nr <= 0 || !v1_window_range(g, pos_lo, count, w_lo, nw)) return hipSuccess;
-    const int64_t nmax = g.B < g.ns ? g.B : g.ns;
+    const int64_t pos_hi = pos_lo + count < g.ns ? pos_lo + count : g.ns;
     mk(K_V1, s);
-    static const int v1_nt = [] {   // experiment knob: threads per window workgroup
-        const char *e = getenv("PSS_V1_NT");   // 512 measured fastest at B = 4096 (C2 V1: 0.39 ms
-        return e ? atoi(e) : 512;              // vs 0.51 ms at 256 and 1024 threads)
-    }();
-    if (!g.shuffle || nmax <= 1024) launch_v1_ept<4>(g, ranks, rank_lo, nr, w_lo, nw, pos_lo, count, out, s);
-    else if (nmax <= 4096 && v1_nt == 1024) launch_v1_ept<4, 1024>(g, ranks, rank_lo, nr, w_lo, nw, pos_lo, count, out, s);
-    else if (nmax <= 4096 && v1_nt == 512) launch_v1_ept<8, 512>(g, ranks, rank_lo, nr, w_lo, nw, pos_lo, count, out, s);
-    else if (nmax <= 4096) launch_v1_ept<16>(g, ranks, rank_lo, nr, w_lo, nw, pos_lo, count, out, s);
-    else if (nmax <= 8192 && v1_nt == 512) launch_v1_ept<16, 512>(g, ranks, rank_lo, nr, w_lo, nw, pos_lo, count, out, s);
-    else if (nmax <= 8192) launch_v1_ept<32>(g, ranks, rank_lo, nr, w_lo, nw, pos_lo, count, out, s);
-    else if (nmax <= kLdsSortMax) launch_v1_ept<64>(g, ranks, rank_lo, nr, w_lo, nw, pos_lo, count, out, s);
-    else {
-        // pools beyond LDS: HBM multi-pass sort, batches of jobs bounded by kBigSortBudget
-        const SortJobs J = v1_jobs(g, rank_lo, w_lo, nw);
-        const int64_t njobs = (int64_t)nr * nw;
-        const int64_t jb = big_sort_batch(nmax, njobs, kBigSortBudget);
-        const BigSortWS ws = big_sort_ws(sort_ws, nmax, jb);
-        for (int64_t j0 = 0; j0 < njobs; j0 += jb) {
-            const int64_t nj = njobs - j0 < jb ? njobs - j0 : jb;
-            hipError_t e = launch_big_sort(g, J, j0, nj, ws, err, s);
-            if (e != hipSuccess) return e;
-            hipLaunchKernelGGL(k_v1_write_big, dim3((uint32_t)cdiv(nmax, 1024), (uint32_t)nj), dim3(256), 0, s,
-                               g, ranks, J, j0, ws, pos_lo, count, out);
-        }
-    }
+    if (g.shuffle)
+        hipLaunchKernelGGL(k_v1_keys, dim3((uint32_t)cdiv(nw, 256), (uint32_t)nr), dim3(256), 0, s,
+                           g, rank_lo, w_lo, nw, key_ws);
+    V1Plan vp{};
+    vp.sb_lo = pos_lo / 256;
+    vp.nsb = (pos_hi - 1) / 256 - vp.sb_lo + 1;
+    vp.w_lo = w_lo;
+    vp.nw = nw;
+    vp.B = (uint32_t)g.B;
+    vp.hB = feistel_half_bits(vp.B);
+    vp.walk_full = vp.B != (1u << (2 * vp.hB));
+    // fast super-blocks: inside one full window that needs no cycle walking
+    vp.fast_ok = g.shuffle && !vp.walk_full && (g.B % 256) == 0;
+    // ~16 super-blocks (4096 positions, 32 KB of output) per wave, at least 8 waves per CU
+    const int64_t total = (int64_t)nr * vp.nsb;
+    int64_t per = 16;
+    while (per > 1 && total / per < 8 * 256) per >>= 1;
+    vp.per_wave = per;
+    const int64_t waves = (int64_t)nr * cdiv(vp.nsb, per);
+    if (vp.hB <= 8)
+        hipLaunchKernelGGL((k_v1_feistel<true>), dim3((uint32_t)waves), dim3(64), 0, s, g, vp, ranks,
+                           rank_lo, (const uint32_t *)key_ws, pos_lo, count, out);
+    else
+        hipLaunchKernelGGL((k_v1_feistel<false>), dim3((uint32_t)waves), dim3(64), 0, s, g, vp, ranks,
+                           rank_lo, (const uint32_t *)key_ws, pos_lo, count, out);
     mk(-1, s);
     return hipGetLastError();
 }
 
-hipError_t init_kernel_attributes() {
-    const int big = 160 * 1024;
-    hipError_t e = hipSuccess;
-#define PSS_ATTR(fn) { hipError_t x = hipFuncSetAttribute((const void *)(fn), hipFuncAttributeMaxDynamicSharedMemorySize, big); if (x != hipSuccess) e = x; }
-    PSS_ATTR((k_v1_lds<32, 256>));
-    PSS_ATTR((k_v1_lds<64, 256>));
-    PSS_ATTR((k_v1_lds<16, 512>));
-#undef PSS_ATTR
-    hipError_t e2 = init_kernel_attributes_v2();
-    hipError_t e3 = init_kernel_attributes_bigsort();
-    return e != hipSuccess ? e : (e2 != hipSuccess ? e2 : e3);
-}
+hipError_t init_kernel_attributes() { return init_kernel_attributes_v2(); }
 
 }  // namespace pss

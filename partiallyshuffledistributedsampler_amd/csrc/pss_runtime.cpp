@@ -553,16 +553,19 @@ int generate_v2_lookahead(pss_sampler *h, const pss::Geometry &g, int32_t rank_l
     const size_t bwords = (pss::v2_buf_bytes(g, nr) + sizeof(uint32_t) - 1) / sizeof(uint32_t);
     DevBuf<uint32_t> *V[NB] = {&h->d_val, &h->d_val2, &h->d_val3};
     DevBuf<uint32_t> *W[NB] = {&h->d_buf, &h->d_buf2, &h->d_buf3};
-    bool grow = false;
-    for (int i = 0; i < NB; i++) grow |= V[i]->n < words || (bwords && W[i]->n < bwords);
-    if (grow) {
+    // buffers grow on first use: the one this call picks now, the other two only when a
+    // lookahead pass is actually queued into them (one-off calls never triple the workspace)
+    auto small = [&](int b) { return V[b]->n < words || (bwords && W[b]->n < bwords); };
+    auto grow = [&](int b) -> int {
+        if (!small(b)) return PSS_OK;
         if (h->side) PSS_HIP(hipStreamSynchronize(h->side));   // no pass may write a freed buffer
-        for (auto &p : h->pend) p.valid = false;
-        for (int i = 0; i < NB; i++) {
-            PSS_HIP(V[i]->ensure(words));
-            if (bwords) PSS_HIP(W[i]->ensure(bwords));
-        }
-    }
+        // a queued pass of another shape into this buffer is dropped with it
+        for (auto &p : h->pend) if (p.valid && p.buf == b) p.valid = false;
+        PSS_HIP(hipDeviceSynchronize());    // its last reader (a replay on any stream) is done
+        PSS_HIP(V[b]->ensure(words));
+        if (bwords) PSS_HIP(W[b]->ensure(bwords));
+        return PSS_OK;
+    };
     if (!h->side) {
         int least = 0, greatest = 0;
         PSS_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
@@ -590,6 +593,7 @@ int generate_v2_lookahead(pss_sampler *h, const pss::Geometry &g, int32_t rank_l
             buf = p.buf;
             p.valid = false;
         }
+    if (buf >= 0 && small(buf)) buf = -1;   // (cannot happen: queued passes had their size)
     if (buf >= 0) {
         PSS_HIP(hipStreamWaitEvent(s, h->ev_done[buf], 0));
         PSS_HIP(pss::launch_v2(g, h->d_ranks.p, rank_lo, nr, pos_lo, count, out_dev, V[buf]->p,
@@ -598,6 +602,7 @@ int generate_v2_lookahead(pss_sampler *h, const pss::Geometry &g, int32_t rank_l
     } else {
         // a buffer no queued lookahead holds, after its last reader and its last writer
         for (int b = 0; b < NB && buf < 0; b++) if (!held(b)) buf = b;
+        { const int rc = grow(buf); if (rc) return rc; }
         PSS_HIP(hipStreamWaitEvent(s, h->ev_read[buf], 0));
         PSS_HIP(hipStreamWaitEvent(s, h->ev_done[buf], 0));
         PSS_HIP(pss::launch_v2(g, h->d_ranks.p, rank_lo, nr, pos_lo, count, out_dev, V[buf]->p,
@@ -627,6 +632,7 @@ int generate_v2_lookahead(pss_sampler *h, const pss::Geometry &g, int32_t rank_l
         int nb = -1;
         for (int b = 0; b < NB && nb < 0; b++) if (b != buf && !held(b)) nb = b;
         if (nb < 0) break;
+        { const int rc = grow(nb); if (rc) return rc; }
         pss::Geometry gn = g;
         gn.key0 = k0[d]; gn.key1 = k1[d];
         PSS_HIP(hipStreamWaitEvent(h->side, h->ev_read[nb], 0));   // the replay that read it
@@ -665,7 +671,7 @@ int pss_generate(pss_sampler *h, int32_t rank_lo, int32_t rank_hi, int64_t pos_l
     } else if (h->version == 1) {
         const size_t sb = pss::v1_workspace_bytes(g, nr, pos_lo, count);
         if (sb) PSS_HIP(h->d_sort.ensure(words(sb)));
-        PSS_HIP(pss::launch_v1(g, h->d_ranks.p, rank_lo, nr, pos_lo, count, out_dev, h->d_sort.p, h->d_err.p, s, mk));
+        PSS_HIP(pss::launch_v1(g, h->d_ranks.p, rank_lo, nr, pos_lo, count, out_dev, h->d_sort.p, s, mk));
     } else if (h->order_mode == PSS_ORDER_EXACT) {
         PSS_HIP(h->d_sort.ensure(words(pss::v2_exact_ws_bytes(g, nr))));
         mk(pss::K_V2_EMIT, s);
@@ -677,6 +683,8 @@ int pss_generate(pss_sampler *h, int32_t rank_lo, int32_t rank_hi, int64_t pos_l
         for (auto &p : h->pend) p.valid = false;
         h->last_valid = false;
         if (h->side) PSS_HIP(hipStreamSynchronize(h->side));   // a lookahead may still write VAL
+        // d_val's last reader may be a replay on another stream (the lookahead path's buffer 0)
+        if (h->ev_read[0]) PSS_HIP(hipStreamWaitEvent(s, h->ev_read[0], 0));
         PSS_HIP(h->d_val.ensure(words(pss::v2_val_bytes(g, nr))));
         const size_t bb = pss::v2_buf_bytes(g, nr), sb = pss::v2_sort_bytes(g, nr);
         if (bb) PSS_HIP(h->d_buf.ensure(words(bb)));
@@ -803,6 +811,8 @@ int pss_check(pss_sampler *h, void *stream) {
     if (!h) return fail(PSS_EINVAL, "NULL handle");
     DeviceGuard dg(h->device);
     PSS_HIP(hipStreamSynchronize((hipStream_t)stream));
+    // lookahead passes on the side stream share the error word: let them land first
+    if (h->side) PSS_HIP(hipStreamSynchronize(h->side));
     PSS_HIP(hipGetLastError());
     if (!h->dev_init) return PSS_OK;
     int32_t err = 0;

@@ -3,18 +3,16 @@
 //
 //   k_v2_lastocc     pass A, slot table in LDS: per tile the last step that drew each slot
 //                    (order-independent ds_max) -> VAL[tile][s] = value inserted there
-//   k_v2_lastocc_g   pass A, slot table in HBM (pools > 16384): global atomicMax ...
-//   k_v2_convert_g   ... then last step -> inserted value, in place
-//   k_v2_init_g      HBM variant: slot table of each tile = state after the previous tile
-//   k_v2_emit<GBUF>  pass B: one wave replays a tile in step order, 64 steps per iteration;
+//   k_v2_emit        pass B: one wave replays a tile in step order, 64 steps per iteration;
 //                    each step exchanges its insertion into the drawn slot (ds_wrxchg_rtn /
 //                    global_atomic_swap) and emits what it held; lanes of one iteration that
 //                    drew the same slot are chained through ds_bpermute instead
 //   k_v2_emit_x      pass B on gfx950: one lane-ordered LDS exchange per step; the wave of a
 //                    rank's last tile also drains the final pool (the tail) from LDS
 //   k_v2_tail_f      the tail from the VAL tables, when the last tile is not replayed in the
-//                    same launch (or on the probe / HBM paths): final pool1 drained in the
-//                    order of a keyed Feistel bijection of [0, P1)
+//                    same launch (or on the probe path): final pool1 drained in the order of
+//                    a keyed Feistel bijection of [0, P1)
+// Pools beyond LDS (P1 > kLdsSlotMax) take the grouped schedule of pss_v2grp.hip.
 #include <cstdlib>
 #include <type_traits>
 
@@ -195,67 +193,6 @@ __global__ __launch_bounds__(NT) void k_v2_lastocc(Geometry g, V2Plan pl, int32_
 #endif
 }
 
-// ---- pass A, HBM ----------------------------------------------------------------------------
-constexpr int64_t kLastoccChunk = 65536;   // steps per workgroup
-
-__global__ __launch_bounds__(256) void k_v2_lastocc_g(Geometry g, V2Plan pl, int32_t rank_lo,
-                                                      int64_t ng, uint32_t *__restrict__ VAL) {
-    const int64_t tiles = blockIdx.y;
-    const int32_t rl = (int32_t)(tiles / ng);
-    const int64_t tile = tiles % ng;
-    const uint32_t rank = (uint32_t)(rank_lo + rl);
-    int64_t tlo, thi;
-    tile_bounds(pl, tile, tlo, thi);
-    const int64_t clo = tlo + (int64_t)blockIdx.x * kLastoccChunk;
-    if (clo >= thi) return;
-    const int64_t chi = clo + kLastoccChunk < thi ? clo + kLastoccChunk : thi;
-    uint32_t *V = VAL + ((int64_t)rl * pl.G + tile) * pl.P1;
-    const int64_t sb_lo = clo >> 8, sb_hi = (chi - 1) >> 8;
-    const int64_t ncnt = (sb_hi - sb_lo + 1) * 64;
-    const SlotKey sk = slot_key(g, rank);
-    for (int64_t ci = threadIdx.x; ci < ncnt; ci += 256) {
-        const int64_t sb = sb_lo + (ci >> 6);
-        const int lane = (int)(ci & 63);
-        uint32_t u[4];
-        slot_ks(sk, sb, lane, (uint32_t)pl.P1, u);
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const int64_t t = sb * 256 + j * 64 + lane;
-            if (t >= clo && t < chi) atomicMax(&V[u[j]], (uint32_t)(t - tlo + 1));
-        }
-    }
-}
-
-__global__ __launch_bounds__(256) void k_v2_convert_g(Geometry g, V2Plan pl, int32_t rank_lo,
-                                                      int64_t ng, uint32_t *__restrict__ VAL) {
-    const int64_t tiles = blockIdx.y;
-    const int32_t rl = (int32_t)(tiles / ng);
-    const int64_t tile = tiles % ng;
-    const uint32_t rank = (uint32_t)(rank_lo + rl);
-    const int64_t tlo = tile * pl.L;
-    uint32_t *V = VAL + ((int64_t)rl * pl.G + tile) * pl.P1;
-    for (int64_t s = (int64_t)blockIdx.x * 256 + threadIdx.x; s < pl.P1; s += (int64_t)gridDim.x * 256) {
-        const uint32_t lt = V[s];
-        if (!lt) { V[s] = kNone; continue; }
-        const int64_t t = tlo + (int64_t)lt - 1;
-        uint32_t k[kRoundKeyWords];
-        window_round_keys(g, rank, 1 + t / g.B, k);
-        V[s] = ins_value_k(g, t, k);
-    }
-}
-
-__global__ __launch_bounds__(256) void k_v2_init_g(V2Plan pl, int64_t g_lo, int64_t ng,
-                                                   const uint32_t *__restrict__ VAL,
-                                                   uint32_t *__restrict__ gbuf) {
-    const int64_t tiles = blockIdx.y;
-    const int32_t rl = (int32_t)(tiles / ng);
-    const int64_t tile = g_lo + tiles % ng;
-    const uint32_t *VALr = VAL + (int64_t)rl * pl.G * pl.P1;
-    uint32_t *b = gbuf + ((int64_t)rl * pl.G + tile) * pl.P1;
-    for (int64_t s = (int64_t)blockIdx.x * 256 + threadIdx.x; s < pl.P1; s += (int64_t)gridDim.x * 256)
-        b[s] = slot_value_after(VALr, pl.P1, tile - 1, s);
-}
-
 // ---- pass B -------------------------------------------------------------------------------
 // collision probe bytes live in LDS and are accessed volatile (the read-back must not be
 // forwarded from the store); the explicit address space keeps them ds_write_b8/ds_read_u8
@@ -398,12 +335,11 @@ struct EmitCtx {   // per-tile constants of k_v2_emit + the running pool2 positi
     }
 };
 
-template <bool GBUF, bool NARROW, bool FOLD>
+template <bool NARROW, bool FOLD>
 __global__ __launch_bounds__(64) void k_v2_emit(Geometry g, V2Plan pl,
                                                 const RankDesc *__restrict__ ranks,
                                                 int32_t rank_lo, int64_t g_lo, int64_t ng,
                                                 const uint32_t *__restrict__ VAL,
-                                                uint32_t *__restrict__ gbuf,
                                                 int64_t pos_lo, int64_t count,
                                                 int64_t *__restrict__ out) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
@@ -423,9 +359,7 @@ __global__ __launch_bounds__(64) void k_v2_emit(Geometry g, V2Plan pl,
     const int64_t w_lo = 1 + tlo / g.B;
     const int nwin = (int)(1 + (thi - 1) / g.B - w_lo + 1);
     uint32_t *buf;   // slot table: virtual ids held by the P1 slots at the tile's start
-    if (GBUF) {
-        buf = gbuf + ((int64_t)rl * pl.G + tile) * P1;      // filled by k_v2_init_g
-    } else {
+    {
         buf = (uint32_t *)(smem + kRoundKeyWords * nwin_max + mark_words);
         if (FOLD) mark = (lds_vu8 *)buf + 3;
         const uint32_t *VALr = VAL + (int64_t)rl * pl.G * P1;
@@ -946,8 +880,7 @@ V2Plan v2_plan(const Geometry &g, int32_t nr) {
     V2Plan p{};
     p.P1 = g.B < g.ns ? g.B : g.ns;
     p.T = g.ns - p.P1;
-    p.global_buf = p.P1 > kLdsSlotMax;
-    p.fold = !p.global_buf && g.ns <= (int64_t)1 << 24;
+    p.fold = g.ns <= (int64_t)1 << 24;
     static const int64_t mult_env = [] {
         const char *e = getenv("PSS_V2_TILE_MULT");   // tuning knob: tile = mult * P1 steps
         const long v = e ? atol(e) : 0;
@@ -960,7 +893,7 @@ V2Plan v2_plan(const Geometry &g, int32_t nr) {
     }();
     // emit wave LDS: Feistel keys of up to kMaxTileMult + 2 windows, the slot table, the probe
     const int64_t keys = (int64_t)kRoundKeyWords * 4 * (kMaxTileMult + 2);
-    const int64_t lds = keys + (p.global_buf ? 0 : p.P1 * 4) + (p.fold ? 0 : kMarkBytes);
+    const int64_t lds = keys + p.P1 * 4 + (p.fold ? 0 : kMarkBytes);
     // waves per CU the LDS admits, rounded down to whole SIMD quads (balanced SIMDs), <= 16;
     // the launch pads its LDS so that no CU takes more (dispatch would otherwise stack a 9th)
     int64_t wpc = kCuLdsBytes / lds;
@@ -977,8 +910,6 @@ V2Plan v2_plan(const Geometry &g, int32_t nr) {
     int64_t L;
     if (mult_env) {
         L = mult_env * p.P1;
-    } else if (p.global_buf) {
-        L = p.P1;
     } else {
         // one round of waves: tiles = waves per CU x CUs spread over the nr streams
         const int64_t waves = wpc * device_cus();
@@ -1011,17 +942,13 @@ static size_t keytab_words(const V2Plan &pl, const Geometry &g, int32_t nr) {
 }
 
 size_t v2_val_bytes(const Geometry &g, int32_t nr) {
+    if (v2_grouped(g)) return v2_grp_val_bytes(g, nr);
     const V2Plan p = v2_plan(g, nr);
     return ((size_t)nr * (size_t)p.G * (size_t)p.P1 + keytab_words(p, g, nr)) * sizeof(uint32_t);
 }
 
 size_t v2_buf_bytes(const Geometry &g, int32_t nr) {
-    const V2Plan p = v2_plan(g, nr);
-    if (!p.global_buf) return 0;
-    const size_t legacy = v2_val_bytes(g, nr);
-    if (!v2_big_applicable(g)) return legacy;
-    const size_t big = v2_big_bytes(g, nr);
-    return big > legacy ? big : legacy;
+    return v2_grouped(g) ? v2_grp_fin_bytes(g, nr) : 0;
 }
 
 size_t v2_sort_bytes(const Geometry &, int32_t) {
@@ -1039,7 +966,8 @@ hipError_t launch_v2_tail_vals(const Geometry &g, const V2Plan &pl, const RankDe
 
 bool v2_stage_split(const Geometry &g, int32_t nr, int emit_path) {
     if (emit_path == EMIT_AUTO) emit_path = lds_xchg_ordered() ? EMIT_XCHG : EMIT_PROBE;
-    return emit_path == EMIT_XCHG && (v2_big_applicable(g) || !v2_plan(g, nr).global_buf);
+    (void)nr;
+    return emit_path == EMIT_XCHG || v2_grouped(g);
 }
 
 hipError_t launch_v2(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, int32_t nr,
@@ -1056,8 +984,10 @@ hipError_t launch_v2(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, 
         stage = V2_STAGE_ALL;
     }
     const bool do_pre = stage != V2_STAGE_EMIT, do_emit = stage != V2_STAGE_PRE;
-    if (emit_path == EMIT_XCHG && v2_big_applicable(g))   // pools beyond LDS: chunked replay
-        return launch_v2_big(g, ranks, rank_lo, nr, pos_lo, count, out, gbuf, err, s, mk, stage);
+    if (v2_grouped(g))   // pools beyond LDS: the grouped slot machine (pss_v2grp.hip)
+        return launch_v2_grp(g, ranks, rank_lo, nr, pos_lo, count, out, VAL, gbuf, s, mk,
+                             emit_path == EMIT_XCHG, stage);
+    (void)err; (void)sort_ws;
     const V2Plan pl = v2_plan(g, nr);
     const int64_t pos_hi = pos_lo + count < g.ns ? pos_lo + count : g.ns;
     if (nr <= 0 || pos_hi <= pos_lo) return hipSuccess;
@@ -1082,7 +1012,7 @@ hipError_t launch_v2(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, 
         const int64_t g_need = need_tail ? pl.G : last_emit + 1;
         if (g_need > 0 && do_pre) {
             mk(K_V2_LASTOCC, s);
-            if (!pl.global_buf) {
+            {
                 static const int lo_mode = [] {   // A/B knob: "ordered" = one-wave plain-store kernel
                     const char *e = getenv("PSS_V2_LASTOCC");  // (measured 15% slower than ds_max on C2)
                     return e && e[0] == 'o' ? 1 : 0;
@@ -1101,13 +1031,6 @@ hipError_t launch_v2(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, 
                 else if (lo_nt == 512) PSS_LO(512, false);
                 else PSS_LO(256, false);
 #undef PSS_LO
-            } else {
-                hipError_t e = hipMemsetAsync(VAL, 0, (size_t)nr * (size_t)pl.G * (size_t)pl.P1 * sizeof(uint32_t), s);
-                if (e != hipSuccess) return e;
-                hipLaunchKernelGGL(k_v2_lastocc_g, dim3((uint32_t)cdiv(pl.L, kLastoccChunk), (uint32_t)(nr * g_need)),
-                                   dim3(256), 0, s, g, pl, rank_lo, g_need, VAL);
-                hipLaunchKernelGGL(k_v2_convert_g, dim3((uint32_t)cdiv(pl.P1, 256), (uint32_t)(nr * g_need)),
-                                   dim3(256), 0, s, g, pl, rank_lo, g_need, VAL);
             }
         }
         if (do_pre && !do_emit) mk(-1, s);
@@ -1117,7 +1040,7 @@ hipError_t launch_v2(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, 
             // 32-bit id arithmetic whenever every id (and id + ns before the wrap) fits
             const bool narrow = g.N + g.ns < (int64_t)UINT32_MAX;
             const dim3 grid((uint32_t)(nr * ng));
-            if (!pl.global_buf && emit_path == EMIT_XCHG) {
+            if (emit_path == EMIT_XCHG) {
                 mk(K_V2_EMIT, s);
                 const size_t need = lds_keys + (size_t)((pl.P1 + 3) & ~3) * 4;
                 const size_t lds = need > (size_t)pl.emit_lds ? need : (size_t)pl.emit_lds;
@@ -1131,28 +1054,17 @@ hipError_t launch_v2(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, 
                 else if (pow2) PSS_EX(false, true);
                 else PSS_EX(false, false);
 #undef PSS_EX
-            } else if (!pl.global_buf) {   // probe path (EMIT_PROBE)
+            } else {   // probe path (EMIT_PROBE)
                 mk(K_V2_EMIT, s);
                 const size_t need = lds_keys + (size_t)pl.P1 * 4 + (pl.fold ? 0 : kMarkBytes);
                 const size_t lds = need > (size_t)pl.emit_lds ? need : (size_t)pl.emit_lds;
-#define PSS_EMIT(N, F) hipLaunchKernelGGL((k_v2_emit<false, N, F>), grid, dim3(64), lds, s, g, pl, ranks, rank_lo, \
-                                          g_lo, ng, (const uint32_t *)VAL, (uint32_t *)nullptr, pos_lo, count, out)
+#define PSS_EMIT(N, F) hipLaunchKernelGGL((k_v2_emit<N, F>), grid, dim3(64), lds, s, g, pl, ranks, rank_lo, \
+                                          g_lo, ng, (const uint32_t *)VAL, pos_lo, count, out)
                 if (pl.fold && narrow) PSS_EMIT(true, true);
                 else if (pl.fold) PSS_EMIT(false, true);
                 else if (narrow) PSS_EMIT(true, false);
                 else PSS_EMIT(false, false);
 #undef PSS_EMIT
-            } else {
-                hipLaunchKernelGGL(k_v2_init_g, dim3((uint32_t)cdiv(pl.P1, 256), (uint32_t)(nr * ng)),
-                                   dim3(256), 0, s, pl, g_lo, ng, (const uint32_t *)VAL, gbuf);
-                mk(K_V2_EMIT, s);
-                const size_t lds = lds_keys + kMarkBytes;
-                if (narrow)
-                    hipLaunchKernelGGL((k_v2_emit<true, true, false>), grid, dim3(64), lds, s, g, pl, ranks, rank_lo,
-                                       g_lo, ng, (const uint32_t *)VAL, gbuf, pos_lo, count, out);
-                else
-                    hipLaunchKernelGGL((k_v2_emit<true, false, false>), grid, dim3(64), lds, s, g, pl, ranks, rank_lo,
-                                       g_lo, ng, (const uint32_t *)VAL, gbuf, pos_lo, count, out);
             }
         }
     }
@@ -1219,7 +1131,7 @@ bool lds_xchg_ordered() {
 hipError_t init_kernel_attributes_v2() {
     const int big = 160 * 1024;
     hipError_t e = check_lds_xchg_order();
-    if (e == hipSuccess) e = init_kernel_attributes_v2big();
+    if (e == hipSuccess) e = init_kernel_attributes_v2grp();
 #define PSS_ATTR(fn) { hipError_t x = hipFuncSetAttribute((const void *)(fn), hipFuncAttributeMaxDynamicSharedMemorySize, big); if (x != hipSuccess) e = x; }
     PSS_ATTR((k_v2_lastocc<64, true, true>));
     PSS_ATTR((k_v2_lastocc<64, true, false>));
@@ -1233,12 +1145,10 @@ hipError_t init_kernel_attributes_v2() {
     PSS_ATTR((k_v2_emit_x<true, false>));
     PSS_ATTR((k_v2_emit_x<false, true>));
     PSS_ATTR((k_v2_emit_x<false, false>));
-    PSS_ATTR((k_v2_emit<false, true, false>));
-    PSS_ATTR((k_v2_emit<false, false, false>));
-    PSS_ATTR((k_v2_emit<false, true, true>));
-    PSS_ATTR((k_v2_emit<false, false, true>));
-    PSS_ATTR((k_v2_emit<true, true, false>));
-    PSS_ATTR((k_v2_emit<true, false, false>));
+    PSS_ATTR((k_v2_emit<true, false>));
+    PSS_ATTR((k_v2_emit<false, false>));
+    PSS_ATTR((k_v2_emit<true, true>));
+    PSS_ATTR((k_v2_emit<false, true>));
 #undef PSS_ATTR
     return e;
 }

@@ -1,0 +1,158 @@
+"""GPU parity at the BASELINE.json shapes (workloads.py), through the C-ABI.
+
+Each configuration is checked at its real size:
+  * selected ranks' full epoch streams == the oracle's counter-schedule twin, bit for bit
+    (including the ranks whose blocks wrap at N, V1:161-163 / V2:113-114);
+  * exact coverage over ALL logical ranks by the commutative (count, digest) check of
+    SURVEY.md §8e: sum of splitmix64 over every emitted id == digest([0, N)) + digest([0, pad));
+  * the device error flag is read after every generate (eng.check()).
+Shapes: C2 (100M, R=8), C3 (1B, R=1024), C4 (Zipf N=2.59e9 > 2^31, R=4096: the pinned-staging
+rank upload and ids above 2^31), a wide case (N + ns >= 2^32: the 64-bit id paths) and C5
+(B = 2^20: pools beyond LDS) over consecutive epochs (the lookahead ring).
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as O
+import workloads as W
+
+pytestmark = pytest.mark.gpu
+
+pss = pytest.importorskip("partiallyshuffledistributedsampler_amd.engine")
+
+
+def _engine(lengths, N, R, B, version, seed=0):
+    return pss.IndexEngine(lengths, N, R, B, version, shuffle=True, seed=seed, device=0)
+
+
+def _gen(eng, lo, hi, **kw):
+    out = eng.generate(lo, hi, **kw)
+    eng.check()
+    return out
+
+
+def _twin(version, key, r, old, new, ns, B, N):
+    if version == 1:
+        return O.v1_philox_stream(key, r, int(new[r]), ns, B, N)
+    return O.v2_philox_stream(key, r, int(old[r]), int(new[r]), ns, B, N)
+
+
+def _coverage(eng, N, R, chunk):
+    """(count, digest) over every logical rank, generated `chunk` ranks at a time."""
+    acc = torch.zeros(1, dtype=torch.int64, device="cuda")
+    count = 0
+    for lo in range(0, R, chunk):
+        hi = min(R, lo + chunk)
+        out = _gen(eng, lo, hi)
+        pss.digest(out.view(-1), acc)
+        count += out.numel()
+        del out
+    eng.check()
+    ns = eng.num_samples
+    pad = ns * R - N
+    want = (O.digest_range(0, N) + O.digest_range(0, pad)) & 0xFFFFFFFFFFFFFFFF
+    return count == ns * R and pss.as_u64(acc) == want
+
+
+def _wrapping_ranks(new, ns, N):
+    return [r for r in range(len(new)) if int(new[r]) + ns > N]
+
+
+@pytest.mark.parametrize("version", [2, 1])
+def test_c2_all_ranks_match_twin(version):
+    lengths, N, R, B, _ = W.shape("c2")
+    eng = _engine(lengths, N, R, B, version, seed=0)
+    ns = eng.num_samples
+    for epoch in (0, 1):     # consecutive epochs: the second takes the queued lookahead pass
+        eng.init_iter(epoch)
+        old, new = eng.rank_starts()
+        out = _gen(eng, 0, R).cpu().numpy()
+        key = O.epoch_key(0, epoch)
+        for r in range(R):
+            assert np.array_equal(out[r], _twin(version, key, r, old, new, ns, B, N)), (epoch, r)
+        assert _coverage(eng, N, R, R)                   # N = ns * R: no pad
+    eng.close()
+
+
+def test_c3_coverage_and_ranks_match_twin():
+    lengths, N, R, B, ver = W.shape("c3")
+    eng = _engine(lengths, N, R, B, ver, seed=0)
+    ns = eng.num_samples
+    eng.init_iter(3)
+    old, new = eng.rank_starts()
+    assert _coverage(eng, N, R, 256)
+    key = O.epoch_key(0, 3)
+    picks = sorted({0, 1, 127, 128, 511, 1023} | set(_wrapping_ranks(new, ns, N)))
+    for r in picks:
+        got = _gen(eng, r, r + 1).cpu().numpy()[0]
+        assert np.array_equal(got, _twin(ver, key, r, old, new, ns, B, N)), r
+    # one GPU's block of 128 logical ranks at 8 GPUs, against the same ranks generated alone
+    blk = _gen(eng, 128, 256).cpu().numpy()
+    assert np.array_equal(blk[0], _twin(ver, key, 128, old, new, ns, B, N))
+    assert np.array_equal(blk[127], _gen(eng, 255, 256).cpu().numpy()[0])
+    eng.close()
+
+
+def test_c4_zipf_4096_ranks():
+    lengths, N, R, B, ver = W.shape("c4")
+    assert N == 2_594_705_250 and R > 1024      # ids above 2^31; staging upload of R > 1024
+    eng = _engine(lengths, N, R, B, ver, seed=0)
+    ns = eng.num_samples
+    assert ns == 633_473
+    for epoch in (0, 1):
+        eng.init_iter(epoch)
+        old, new = eng.rank_starts()
+        key = O.epoch_key(0, epoch)
+        wrap = _wrapping_ranks(new, ns, N) + [r for r in range(R) if int(old[r]) + 2 * B > N]
+        hi_ids = [r for r in range(R) if int(new[r]) > 2 ** 31][:2]
+        picks = sorted(set([0, 1, 1024, 2047, 4095] + wrap + hi_ids))
+        for r in picks:
+            got = _gen(eng, r, r + 1).cpu().numpy()[0]
+            assert np.array_equal(got, _twin(ver, key, r, old, new, ns, B, N)), (epoch, r)
+        assert int(_gen(eng, hi_ids[0], hi_ids[0] + 1).max()) > 2 ** 31
+        assert _coverage(eng, N, R, 512)
+    eng.close()
+
+
+@pytest.mark.parametrize("version", [2, 1])
+def test_wide_ids_beyond_2_32(version):
+    """N + ns >= 2^32: the kernels' 64-bit id instantiations (every id of the 32-bit fast
+    paths fits below 2^32 only when N + ns < 2^32)."""
+    F, L, R, B = 2000, 2_200_000, 4096, 4096
+    lengths = np.full(F, L, dtype=np.int64)
+    N = F * L
+    assert N > 2 ** 32
+    eng = _engine(lengths, N, R, B, version, seed=11)
+    ns = eng.num_samples
+    eng.init_iter(2)
+    old, new = eng.rank_starts()
+    key = O.epoch_key(11, 2)
+    top = [r for r in range(R) if int(new[r]) > 2 ** 32][:2]
+    picks = sorted(set([0, 7] + top + _wrapping_ranks(new, ns, N)))
+    for r in picks:
+        got = _gen(eng, r, r + 1).cpu().numpy()[0]
+        assert np.array_equal(got, _twin(version, key, r, old, new, ns, B, N)), r
+    assert int(_gen(eng, top[0], top[0] + 1).max()) > 2 ** 32
+    assert _coverage(eng, N, R, 512)
+    eng.close()
+
+
+def test_c5_big_pool_consecutive_epochs():
+    lengths, N, R, B, ver = W.shape("c5")
+    eng = _engine(lengths, N, R, B, ver, seed=0)
+    ns = eng.num_samples
+    outs = []
+    for epoch in range(4):   # sequential epochs cycle the lookahead buffers
+        eng.init_iter(epoch)
+        old, new = eng.rank_starts()
+        outs.append((epoch, old.copy(), new.copy(), _gen(eng, 0, R)))
+    for epoch, old, new, out in outs:
+        key = O.epoch_key(0, epoch)
+        o = out.cpu().numpy()
+        for r in sorted({epoch % R, R - 1}):
+            assert np.array_equal(o[r], _twin(ver, key, r, old, new, ns, B, N)), (epoch, r)
+    del outs
+    eng.init_iter(9)
+    assert _coverage(eng, N, R, R)
+    eng.close()

@@ -18,8 +18,22 @@ pytestmark = pytest.mark.gpu
 pss = pytest.importorskip("partiallyshuffledistributedsampler_amd.engine")
 
 
-def _engine(lengths, N, R, B, version, shuffle=True, seed=0):
-    return pss.IndexEngine(lengths, N, R, B, version, shuffle=shuffle, seed=seed, device=0)
+class _Checked(pss.IndexEngine):
+    """IndexEngine whose every generate / map is followed by pss_check (device error flag)."""
+
+    def generate(self, *a, **kw):
+        out = super().generate(*a, **kw)
+        self.check(kw.get("stream"))
+        return out
+
+    def map(self, *a, **kw):
+        r = super().map(*a, **kw)
+        self.check(kw.get("stream"))
+        return r
+
+
+def _engine(lengths, N, R, B, version, shuffle=True, seed=0, order="counter"):
+    return _Checked(lengths, N, R, B, version, shuffle=shuffle, seed=seed, device=0, order=order)
 
 
 def _oracle_stream(version, key, rank, old, new, ns, B, N, shuffle=True):
@@ -307,7 +321,7 @@ def test_v1_exact_order_matches_reference_streams(name):
     fx = load(name)
     files, lengths, fl, N, R, B, bs, shuffle = fixture_params(fx)
     lens = [fl.get(p, lengths[p]) if fl else lengths[p] for p in files]
-    eng = pss.IndexEngine(lens, N, R, B, 1, shuffle=shuffle, seed=0, device=0, order="exact")
+    eng = _engine(lens, N, R, B, 1, shuffle=shuffle, seed=0, order="exact")
     assert eng.order_mode() == "exact"
     for ep_i, er0 in enumerate(fx["ranks"][0]["epochs"]):
         eng.init_iter(er0["epoch"])
@@ -336,7 +350,7 @@ def test_v1_exact_order_matches_exact_oracle(F, lo, hi, R, B, epochs):
     rng = np.random.default_rng(F + B)
     lengths = rng.integers(lo, hi, F)
     N = int(lengths.sum())
-    eng = pss.IndexEngine(lengths, N, R, B, 1, seed=7, device=0, order="exact")
+    eng = _engine(lengths, N, R, B, 1, seed=7, order="exact")
     ns = eng.num_samples
     for epoch in epochs:
         eng.init_iter(epoch)
@@ -367,7 +381,7 @@ def test_v2_exact_order_matches_reference_streams(name):
     fx = load(name)
     files, lengths, fl, N, R, B, bs, shuffle = fixture_params(fx)
     lens = [fl.get(p, lengths[p]) if fl else lengths[p] for p in files]
-    eng = pss.IndexEngine(lens, N, R, B, 2, seed=0, device=0, order="exact")
+    eng = _engine(lens, N, R, B, 2, seed=0, order="exact")
     for ep_i, er0 in enumerate(fx["ranks"][0]["epochs"]):
         eng.init_iter(er0["epoch"])
         out = eng.generate(0, R).cpu().numpy()
@@ -394,7 +408,7 @@ def test_v2_exact_order_matches_exact_oracle(F, lo, hi, R, B, epochs):
     rng = np.random.default_rng(F * 7 + B)
     lengths = rng.integers(lo, hi, F)
     N = int(lengths.sum())
-    eng = pss.IndexEngine(lengths, N, R, B, 2, seed=7, device=0, order="exact")
+    eng = _engine(lengths, N, R, B, 2, seed=7, order="exact")
     ns = eng.num_samples
     for epoch in epochs:
         eng.init_iter(epoch)

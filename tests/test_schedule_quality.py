@@ -62,3 +62,20 @@ def test_v1_window_permutation_is_uniform(B, ns):
     d = (np.arange(full)[None, :] % B) - rel.reshape(x.shape[0], -1)
     assert np.abs(d).max() < B
     assert abs(d.mean()) < 0.02 * B
+
+
+@pytest.mark.parametrize("B,ns", [(20000, 160000)])
+def test_v2_grouped_pool_law_matches_reference(B, ns):
+    # pools beyond LDS (P1 > 16384) draw in bursts of 16 inside G = ceil(P1 / 4096) slot groups
+    # (DESIGN.md §3.2.1); the displacement law must still be the reference's single-pool law
+    N = 10**12
+    ex = [O.v2_exact_stream(e, 0, 0, ns, B, N) for e in range(3)]
+    ph = [O.v2_philox_stream(O.epoch_key(s, e), r, 0, 0, ns, B, N)
+          for s in (0, 3) for e in range(2) for r in range(2)]
+    dx, upx, lagx = _stats(ex, B)
+    dp, upp, lagp = _stats(ph, B)
+    assert dp.min() >= -2.0 and dx.min() >= -2.0
+    np.testing.assert_allclose(np.quantile(dp, QS), np.quantile(dx, QS), atol=0.02)
+    assert abs(dp.std() / dx.std() - 1) < 0.01
+    assert abs(upp - upx) < 0.005
+    assert abs(lagp - lagx) < 0.005
