@@ -373,14 +373,47 @@ static inline int64_t v2_vid_to_id(int64_t v, int64_t old_start, int64_t new_sta
 
 /* Pools beyond LDS (P1 > 16384): grouped draws.  G = ceil(P1 / 4096) groups of consecutive
  * slots, q = P1 / G each plus one for the first P1 mod G; step t belongs to burst t / 16 and
- * that burst to group (t / 16) mod G; the step draws uniformly inside its group. */
+ * that burst to group (t / 16) mod G; u = the step's index inside its group's own stream.
+ * The step draws uniformly inside its group: power-of-two groups pair sub-steps u and u + 64
+ * (u mod 128 < 64) on one hash of the lower one's step (high / low half-word), other sizes
+ * hash every step. */
 #define ORC_LDS_SLOT_MAX 16384
+typedef struct { uint32_t G, q, r; } orc_groups;
+static orc_groups orc_groups_of(uint32_t P1) {
+    orc_groups gr; gr.G = (P1 + 4095u) / 4096u; gr.q = P1 / gr.G; gr.r = P1 % gr.G; return gr;
+}
+static uint32_t orc_gbase(orc_groups gr, uint32_t g) { return g * gr.q + (g < gr.r ? g : gr.r); }
+static uint32_t orc_gsize(orc_groups gr, uint32_t g) { return gr.q + (g < gr.r ? 1u : 0u); }
+static uint64_t orc_gstep(orc_groups gr, uint32_t g, uint64_t u) {
+    return ((u / 16u) * gr.G + g) * 16u + u % 16u;
+}
 static inline uint32_t v2_slot_grouped(const uint32_t sk[4], int64_t t, uint32_t P1) {
-    uint32_t G = (P1 + 4095u) / 4096u, q = P1 / G, r = P1 % G;
-    uint32_t g = (uint32_t)(((uint64_t)t / 16u) % G);
-    uint32_t base = g * q + (g < r ? g : r), size = q + (g < r ? 1u : 0u);
-    uint32_t u = orc_slot_hash((uint32_t)t, sk[0], sk[1]);
-    return base + (uint32_t)(((uint64_t)u * size) >> 32);
+    orc_groups gr = orc_groups_of(P1);
+    uint32_t g = (uint32_t)(((uint64_t)t / 16u) % gr.G);
+    uint32_t size = orc_gsize(gr, g);
+    uint64_t u = ((uint64_t)t / 16u / gr.G) * 16u + (uint64_t)t % 16u;
+    uint32_t local;
+    if ((size & (size - 1u)) == 0u) {
+        int b = 0; while ((1u << b) < size) b++;
+        if (b == 0) local = 0;
+        else if (u & 64u)
+            local = (orc_slot_hash((uint32_t)orc_gstep(gr, g, u - 64u), sk[0], sk[1]) << 16) >> (32 - b);
+        else
+            local = orc_slot_hash((uint32_t)t, sk[0], sk[1]) >> (32 - b);
+    } else {
+        local = (uint32_t)(((uint64_t)orc_slot_hash((uint32_t)t, sk[0], sk[1]) * size) >> 32);
+    }
+    return orc_gbase(gr, g) + local;
+}
+
+/* Grouped tail: rounds in which every group emits its next (up to) 16 elements, groups in
+ * order; group g's e-th element is slot orc_feistel(e, S_g, keys8(g, rank, DOM_V2_TAIL)) of
+ * the group. */
+static uint32_t orc_gtail_pos(orc_groups gr, uint32_t g, uint32_t e) {
+    uint32_t full = gr.q / 16u;
+    if (e < full * 16u) return (e / 16u) * 16u * gr.G + g * 16u + e % 16u;
+    uint32_t c = gr.q % 16u;
+    return full * 16u * gr.G + g * c + (g < gr.r ? g : gr.r) + (e - full * 16u);
 }
 
 /* V2 under the counter schedule (slot-replacement form of V2:96-116):
@@ -390,7 +423,7 @@ static inline uint32_t v2_slot_grouped(const uint32_t sk[4], int64_t t, uint32_t
  *   pools), emits buf[k_t] and stores the t-th inserted element there: window w = 1 + t/B,
  *   inserted in the order of the Feistel bijection keyed by orc_keys8(w, rank, DOM_V2_INS);
  *   then the final buffer is emitted in the order of the Feistel bijection of [0, P1) keyed by
- *   orc_keys8(0, rank, DOM_V2_TAIL).
+ *   orc_keys8(0, rank, DOM_V2_TAIL) (grouped pools: the round-robin group drain above).
  * Writes all ns ids (rank order) to out; returns ns. */
 int64_t orc_v2_philox_stream(uint64_t key64, uint32_t rank, int64_t old_start,
                              int64_t new_start, int64_t ns, int64_t B, int64_t N, int64_t *out) {
@@ -421,10 +454,21 @@ int64_t orc_v2_philox_stream(uint64_t key64, uint32_t rank, int64_t old_start,
         buf[k] = (uint32_t)(w * B + orc_feistel((uint32_t)p, (uint32_t)len, rk));
     }
     uint32_t tk[8];
-    orc_keys8(key64, 0, rank, DOM_V2_TAIL, tk);
-    for (int64_t j = 0; j < P1; j++)
-        out[T + j] = v2_vid_to_id(buf[orc_feistel((uint32_t)j, (uint32_t)P1, tk)], old_start,
-                                  new_start, B, N);
+    if (grouped) {
+        orc_groups gr = orc_groups_of((uint32_t)P1);
+        for (uint32_t g = 0; g < gr.G; g++) {
+            uint32_t S = orc_gsize(gr, g), base = orc_gbase(gr, g);
+            orc_keys8(key64, g, rank, DOM_V2_TAIL, tk);
+            for (uint32_t e = 0; e < S; e++)
+                out[T + orc_gtail_pos(gr, g, e)] =
+                    v2_vid_to_id(buf[base + orc_feistel(e, S, tk)], old_start, new_start, B, N);
+        }
+    } else {
+        orc_keys8(key64, 0, rank, DOM_V2_TAIL, tk);
+        for (int64_t j = 0; j < P1; j++)
+            out[T + j] = v2_vid_to_id(buf[orc_feistel((uint32_t)j, (uint32_t)P1, tk)], old_start,
+                                      new_start, B, N);
+    }
     free(buf);
     return ns;
 }

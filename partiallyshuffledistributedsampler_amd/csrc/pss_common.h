@@ -189,15 +189,48 @@ PSS_HD uint32_t group_base(const Groups &gr, uint32_t g) { return g * gr.q + (g 
 PSS_HD uint32_t group_size(const Groups &gr, uint32_t g) { return gr.q + (g < gr.r ? 1u : 0u); }
 PSS_HD uint32_t group_of_step(const Groups &gr, uint32_t t) { return (t / kBurst) % gr.G; }
 
-// slot drawn at step t of a grouped pool
-PSS_HD uint32_t slot_draw_grouped(uint32_t t, uint32_t s0, uint32_t s1, const Groups &gr) {
-    const uint32_t g = group_of_step(gr, t);
-    return group_base(gr, g) + scale32(slot_hash(t, s0, s1), group_size(gr, g));
-}
-
 // global step of sub-step u of group g's stream (its bursts are b = m * G + g, m = u / 16)
 PSS_HD uint64_t group_step(const Groups &gr, uint32_t g, uint64_t u) {
     return ((u / kBurst) * gr.G + g) * kBurst + (u % kBurst);
+}
+
+// sub-step of step t inside its group's stream
+PSS_HD uint64_t group_substep(const Groups &gr, uint64_t t) {
+    return (t / kBurst / gr.G) * kBurst + t % kBurst;
+}
+
+// Slot, inside group g of size S, drawn by sub-step u (global step t).  Groups of 2^b slots
+// pair sub-steps u and u + 64 (u mod 128 < 64): one hash of the lower one's step serves both,
+// the lower takes the top b bits of its high half-word, the upper those of the low half-word
+// (both exactly uniform).  Other sizes hash every step and scale it to [0, S).
+PSS_HD uint32_t group_slot(const Groups &gr, uint32_t g, uint32_t S, uint64_t u, uint32_t t,
+                           uint32_t s0, uint32_t s1) {
+    if ((S & (S - 1u)) == 0u) {
+        if (S == 1u) return 0u;
+        const uint32_t sh = 32u - (uint32_t)ceil_log2_u64(S);
+        if (u & 64u) return (slot_hash((uint32_t)group_step(gr, g, u - 64u), s0, s1) << 16) >> sh;
+        return slot_hash(t, s0, s1) >> sh;
+    }
+    return scale32(slot_hash(t, s0, s1), S);
+}
+
+// slot (global index) drawn at step t of a grouped pool
+PSS_HD uint32_t slot_draw_grouped(uint32_t t, uint32_t s0, uint32_t s1, const Groups &gr) {
+    const uint32_t g = group_of_step(gr, t);
+    const uint32_t S = group_size(gr, g);
+    return group_base(gr, g) + group_slot(gr, g, S, group_substep(gr, t), t, s0, s1);
+}
+
+// Tail of a grouped pool: the final pool is drained in rounds; in each round every group emits
+// its next (up to) 16 elements, groups in order.  Group g emits its S_g elements in the order
+// of its own Feistel bijection of [0, S_g) (keys round_keys8(g, rank, DOM_V2_TAIL)).  Position
+// (after T) of group g's e-th element: full rounds while every group still has 16 left, then
+// one last round of the q mod 16 (+1 for g < r) leftovers.
+PSS_HD uint32_t group_tail_pos(const Groups &gr, uint32_t g, uint32_t e) {
+    const uint32_t full = gr.q / kBurst;
+    if (e < full * kBurst) return (e / kBurst) * kBurst * gr.G + g * kBurst + e % kBurst;
+    const uint32_t c = gr.q % kBurst;
+    return full * kBurst * gr.G + g * c + (g < gr.r ? g : gr.r) + (e - full * kBurst);
 }
 
 // number of the steps t < T that group g draws (its sub-stream length)

@@ -126,15 +126,12 @@ hipError_t launch_v2_tail_vals(const Geometry &g, const V2Plan &pl, const RankDe
                                int64_t count, int64_t *out, hipStream_t s,
                                KeyTab kt);
 // pools beyond LDS (P1 > kLdsSlotMax): the grouped slot machine (pss_v2grp.hip); its key
-// table and per-tile tables live in val_ws (v2_val_bytes), the final tables in buf_ws
-// (v2_buf_bytes)
+// table and per-tile tables live in val_ws (v2_val_bytes)
 bool v2_grouped(const Geometry &g);
 size_t v2_grp_val_bytes(const Geometry &g, int32_t nr);
-size_t v2_grp_fin_bytes(const Geometry &g, int32_t nr);
 hipError_t launch_v2_grp(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, int32_t nr,
                          int64_t pos_lo, int64_t count, int64_t *out, uint32_t *val_ws,
-                         uint32_t *fin_ws, hipStream_t s, const Marker &mk, bool ordered,
-                         int stage);
+                         hipStream_t s, const Marker &mk, bool ordered, int stage);
 hipError_t init_kernel_attributes_v2grp();
 // launch_v2 splits into V2_STAGE_PRE / V2_STAGE_EMIT for this shape and emit path (EMIT_AUTO resolved)
 bool v2_stage_split(const Geometry &g, int32_t nr, int emit_path);

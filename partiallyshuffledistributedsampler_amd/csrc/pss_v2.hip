@@ -947,8 +947,8 @@ size_t v2_val_bytes(const Geometry &g, int32_t nr) {
     return ((size_t)nr * (size_t)p.G * (size_t)p.P1 + keytab_words(p, g, nr)) * sizeof(uint32_t);
 }
 
-size_t v2_buf_bytes(const Geometry &g, int32_t nr) {
-    return v2_grouped(g) ? v2_grp_fin_bytes(g, nr) : 0;
+size_t v2_buf_bytes(const Geometry &, int32_t) {
+    return 0;   // no HBM slot tables: small pools replay in LDS, big ones in LDS groups
 }
 
 size_t v2_sort_bytes(const Geometry &, int32_t) {
@@ -985,9 +985,9 @@ hipError_t launch_v2(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, 
     }
     const bool do_pre = stage != V2_STAGE_EMIT, do_emit = stage != V2_STAGE_PRE;
     if (v2_grouped(g))   // pools beyond LDS: the grouped slot machine (pss_v2grp.hip)
-        return launch_v2_grp(g, ranks, rank_lo, nr, pos_lo, count, out, VAL, gbuf, s, mk,
+        return launch_v2_grp(g, ranks, rank_lo, nr, pos_lo, count, out, VAL, s, mk,
                              emit_path == EMIT_XCHG, stage);
-    (void)err; (void)sort_ws;
+    (void)err; (void)sort_ws; (void)gbuf;
     const V2Plan pl = v2_plan(g, nr);
     const int64_t pos_hi = pos_lo + count < g.ns ? pos_lo + count : g.ns;
     if (nr <= 0 || pos_hi <= pos_lo) return hipSuccess;

@@ -13,9 +13,8 @@
 //                last step that drew each slot -> VAL = the value it inserted, or kNone
 //   k_g_emit     per (rank, group, tile), one wave: slot table at the tile's start (initial
 //                Feistel-permuted window 0, or the VAL walk-back), then the replay, 256 steps
-//                per iteration; the last tile of a group stores its final table in FIN
-//   k_g_tail     final pool drained in the order of the tail Feistel bijection of [0, P1),
-//                gathered from FIN
+//                per iteration; the wave of a group's last tile then drains the group's final
+//                table from LDS into its tail positions (pss_common.h group_tail_pos)
 #include <type_traits>
 
 #include "pss_device.h"
@@ -24,9 +23,9 @@ namespace pss {
 
 static inline int64_t gdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
-// key table layout per local rank (words): [0, 2) slot key, [8, 16) tail keys,
-// [16, 24) init keys, [24 + 8 (w - 1), + 8) round keys of pool2 window w = 1 .. W
-constexpr int64_t kGKeySlot = 0, kGKeyTail = 8, kGKeyInit = 16, kGKeyWin = 24;
+// key table layout per local rank (words): [0, 2) slot key, [8, 16) init keys,
+// [16 + 8 (w - 1), + 8) round keys of pool2 window w = 1 .. W
+constexpr int64_t kGKeySlot = 0, kGKeyInit = 8, kGKeyWin = 16;
 
 struct GPlan {
     int64_t P1, T, W;        // slots, steps, pool2 windows
@@ -88,10 +87,9 @@ __global__ __launch_bounds__(256) void k_g_keys(Geometry g, int32_t rank_lo, int
         return;
     }
     int64_t off;
-    if (item == 1) { round_keys8(g.key0, g.key1, 0, rank, DOM_V2_TAIL, k); off = kGKeyTail; }
-    else if (item == 2) { round_keys8(g.key0, g.key1, 0, rank, DOM_V2_INIT, k); off = kGKeyInit; }
-    else if (item < W + 3) {
-        const int64_t w = item - 2;
+    if (item == 1) { round_keys8(g.key0, g.key1, 0, rank, DOM_V2_INIT, k); off = kGKeyInit; }
+    else if (item < W + 2) {
+        const int64_t w = item - 1;
         round_keys8(g.key0, g.key1, (uint32_t)w, rank, DOM_V2_INS, k);
         off = kGKeyWin + kRoundKeyWords * (w - 1);
     } else {
@@ -132,7 +130,7 @@ __global__ __launch_bounds__(256) void k_g_lastocc(Geometry g, GPlan pl, int32_t
     __syncthreads();
     for (uint32_t u = ulo + threadIdx.x; u < uhi; u += 256) {
         const uint32_t t = (uint32_t)group_step(pl.gr, grp, u);
-        atomicMax(&lastT[scale32(slot_hash(t, s0, s1), S)], u - ulo + 1);
+        atomicMax(&lastT[group_slot(pl.gr, grp, S, u, t, s0, s1)], u - ulo + 1);
     }
     __syncthreads();
     uint32_t *V = VAL + ((int64_t)sg * nt + tile) * pl.Smax;
@@ -187,11 +185,39 @@ __device__ __forceinline__ uint32_t xchg_unordered(uint32_t *buf, g_lds_vu8 *mar
     return (valid && !lower) ? atomicExch(&buf[k], ins_last) : ins_prev;
 }
 
+// Four one-pass Feistel chains under wave-uniform round keys K (a full window of 4^h elements).
+// h <= 8: packed 16-bit pairs (feistel4_pk16).  h > 8: the keyed-carry form of feistel_pass --
+// with A_i = R_i ^ K_i, A_{i+1} = A_{i-1} ^ F(A_i) ^ (K_{i-1} ^ K_{i+1}) (one 3-input xor per
+// round, F = one full-rate 24-bit multiply + shift); output L = A_5 ^ K_5, R = A_4 ^ F(A_5) ^ K_4.
+// Same values as feistel_once on each chain.
+__device__ __forceinline__ void feistel4_uniform(const uint32_t x[4], uint32_t h, const uint32_t K[6],
+                                                 uint32_t y[4]) {
+    if (h <= 8) {
+        uint32_t kp[kFeistelRounds];
+#pragma unroll
+        for (int i = 0; i < kFeistelRounds; i++) kp[i] = (K[i] & 0xFFFFu) * 0x10001u;
+        feistel4_pk16(x, h, kp, y);
+        return;
+    }
+    const uint32_t mask = (1u << h) - 1u, sh = 32u - h;
+    const uint32_t K02 = K[0] ^ K[2], K13 = K[1] ^ K[3], K24 = K[2] ^ K[4], K35 = K[3] ^ K[5];
+    auto F = [&](uint32_t a) -> uint32_t { return ((a & 0xFFFFFFu) * kFeistelM24) >> sh; };
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+        const uint32_t A0 = (x[c] & mask) ^ K[0];
+        const uint32_t A1 = (x[c] >> h) ^ F(A0) ^ K[1];
+        const uint32_t A2 = A0 ^ F(A1) ^ K02;
+        const uint32_t A3 = A1 ^ F(A2) ^ K13;
+        const uint32_t A4 = A2 ^ F(A3) ^ K24;
+        const uint32_t A5 = A3 ^ F(A4) ^ K35;
+        y[c] = ((A5 ^ K[5]) << h) | (A4 ^ F(A5) ^ K[4]);
+    }
+}
+
 template <bool ORDERED, bool NARROW>
 __global__ __launch_bounds__(64) void k_g_emit(Geometry g, GPlan pl, const RankDesc *__restrict__ ranks,
                                                int32_t rank_lo, const uint32_t *__restrict__ KT,
-                                               const uint32_t *__restrict__ VAL,
-                                               uint32_t *__restrict__ FIN, int do_fin,
+                                               const uint32_t *__restrict__ VAL, int do_tail,
                                                int64_t pos_lo, int64_t count,
                                                int64_t *__restrict__ out) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
@@ -210,14 +236,15 @@ __global__ __launch_bounds__(64) void k_g_emit(Geometry g, GPlan pl, const RankD
     const uint32_t ulo = tile * (uint32_t)pl.L < Tg ? tile * (uint32_t)pl.L : Tg;
     const uint32_t uhi = Tg - ulo < (uint32_t)pl.L ? Tg : ulo + (uint32_t)pl.L;
     const int64_t pos_hi = pos_lo + count;
-    const bool last = tile == ntl - 1;
-    bool emits = false;
+    const bool drain = tile == ntl - 1 && do_tail;
+    bool emits = false, full_emit = false;
     if (ulo < uhi) {
         const int64_t tf = (int64_t)group_step(pl.gr, grp, ulo);
         const int64_t tl = (int64_t)group_step(pl.gr, grp, uhi - 1);
         emits = tl >= pos_lo && tf < pos_hi;
+        full_emit = tf >= pos_lo && tl < pos_hi;
     }
-    if (!emits && !(last && do_fin)) return;
+    if (!emits && !drain) return;
     const RankDesc rd = ranks[rank];
     GIds<NARROW> ids;
     ids.twoB = pl.twoB;
@@ -242,110 +269,93 @@ __global__ __launch_bounds__(64) void k_g_emit(Geometry g, GPlan pl, const RankD
     const uint32_t s0 = ktr[kGKeySlot], s1 = ktr[kGKeySlot + 1];
     int64_t *o = out + (int64_t)rl * count - pos_lo;
     const uint32_t G = pl.gr.G, B = pl.B32;
+    const uint32_t G64 = 64u * G;
     const bool pow2 = (S & (S - 1u)) == 0u;
     const uint32_t shS = 32u - (uint32_t)ceil_log2_u64(S);
-    const bool full_emit = emits && (int64_t)group_step(pl.gr, grp, ulo) >= pos_lo &&
-                           (int64_t)group_step(pl.gr, grp, uhi - 1) < pos_hi;
-    // per lane and sub-batch j: the step t_j of sub-step u0 + 64 j + lane and its pool2
-    // position (w_j, p_j), advanced by 256 G steps per iteration without division
-    uint32_t tj[4], wj[4], pj[4];
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-        tj[j] = (uint32_t)group_step(pl.gr, grp, (uint64_t)ulo + 64u * j + lane);
-        wj[j] = 1 + tj[j] / B;
-        pj[j] = tj[j] - (wj[j] - 1) * B;
-    }
-    const uint32_t dT = 256u * G;
-    const bool win_fast = !pl.walk_full;
+    // lane l serves sub-steps u0 + 64 j + l: step t_first + c_lane + j * 64 G, where t_first is
+    // the iteration's first step (wave-uniform, advanced by 256 G per iteration without
+    // division, together with its pool2 window wa and offset pa)
+    const uint32_t c_lane = ((uint32_t)lane >> 4) * 16u * G + ((uint32_t)lane & 15u);
+    const uint32_t span = 240u * G + 15u;            // last step of an iteration - first step
+    uint32_t t_first = (uint32_t)group_step(pl.gr, grp, ulo);
+    uint32_t wa = 1 + t_first / B;
+    uint32_t pa = t_first - (wa - 1) * B;
     for (uint32_t u0 = ulo; u0 < uhi; u0 += 256) {
-        // wave-uniform window of the iteration's first step; the iteration spans < B steps,
-        // so every lane is in window wa or wa + 1
-        const uint32_t wa = (uint32_t)__builtin_amdgcn_readfirstlane((int)wj[0]);
-        const uint32_t *ka = ktr + kGKeyWin + kRoundKeyWords * (wa - 1);
-        uint32_t KA[kFeistelRounds], KB[kFeistelRounds];
+        const uint32_t *kw = ktr + kGKeyWin + kRoundKeyWords * (wa - 1);
+        const bool uni = full_emit && u0 + 256 <= uhi && !pl.walk_full && wa < pl.w_last && pa + span < B;
+        if (uni) {
+            // every step of the iteration is valid, emitted, and inserts from the full window
+            // wa: round keys in SGPRs, no per-lane window bookkeeping
+            uint32_t K[kFeistelRounds];
 #pragma unroll
-        for (int i = 0; i < kFeistelRounds; i++) KA[i] = ka[i];
-        const bool two = wa < pl.w_last;   // window wa + 1 exists
-#pragma unroll
-        for (int i = 0; i < kFeistelRounds; i++) KB[i] = two ? ka[kRoundKeyWords + i] : 0u;
-        const bool fast = win_fast && wa + 1 < pl.w_last && u0 + 256 <= uhi && full_emit;
-        uint32_t k[4], ins[4];
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const uint32_t hsh = slot_hash(tj[j], s0, s1);
-            k[j] = pow2 ? hsh >> shS : scale32(hsh, S);
-            const bool b = wj[j] != wa;
-            uint32_t kk[kFeistelRounds];
-#pragma unroll
-            for (int i = 0; i < kFeistelRounds; i++) kk[i] = b ? KB[i] : KA[i];
-            if (fast) {
-                ins[j] = wj[j] * B + feistel_once(pj[j], pl.hB, kk);
+            for (int i = 0; i < kFeistelRounds; i++) K[i] = __builtin_amdgcn_readfirstlane(kw[i]);
+            const uint32_t tb = t_first + c_lane, xb = pa + c_lane;
+            uint32_t k[4];
+            if (pow2) {      // paired draws: sub-steps u, u + 64 share the hash of the lower step
+                const uint32_t h0 = slot_hash(tb, s0, s1), h2 = slot_hash(tb + 2u * G64, s0, s1);
+                k[0] = h0 >> shS; k[1] = (h0 << 16) >> shS;
+                k[2] = h2 >> shS; k[3] = (h2 << 16) >> shS;
             } else {
-                const bool lastw = wj[j] == pl.w_last;
-                const bool valid = u0 + 64u * j + lane < uhi;
-                ins[j] = valid ? wj[j] * B + feistel(pj[j], lastw ? pl.len_last : B,
-                                                     lastw ? pl.h_last : pl.hB, kk)
-                               : 0u;
+#pragma unroll
+                for (int j = 0; j < 4; j++) k[j] = scale32(slot_hash(tb + j * G64, s0, s1), S);
             }
-        }
-        uint32_t v[4];
-        if constexpr (ORDERED) {
+            const uint32_t x[4] = {xb, xb + G64, xb + 2u * G64, xb + 3u * G64};
+            uint32_t y[4];
+            feistel4_uniform(x, pl.hB, K, y);
+            // ids of the window's values wa B + y: one add when the window maps contiguously
+            const uint32_t wB = wa * B;
+            uint32_t ins[4];
+            const uint32_t id_first = ids.to_slot(wB), id_last = ids.to_slot(wB + B - 1u);
+            const bool contig = NARROW && id_last - id_first == B - 1u && ((wB < pl.twoB) == (wB + B - 1u < pl.twoB));
+#pragma unroll
+            for (int j = 0; j < 4; j++) ins[j] = contig ? id_first + y[j] : ids.to_slot(wB + y[j]);
+            uint32_t v[4];
 #pragma unroll
             for (int j = 0; j < 4; j++) {
-                const bool valid = fast || u0 + 64u * j + lane < uhi;
-                v[j] = valid ? atomicExch(&buf[k[j]], ids.to_slot(ins[j])) : 0u;
+                if constexpr (ORDERED) v[j] = atomicExch(&buf[k[j]], ins[j]);
+                else v[j] = xchg_unordered(buf, mark, k[j], ins[j], true, lane);
             }
+            int64_t *ob = o + tb;
+#pragma unroll
+            for (int j = 0; j < 4; j++) ob[(int64_t)j * G64] = ids.from_slot(v[j]);
         } else {
 #pragma unroll
             for (int j = 0; j < 4; j++) {
-                const bool valid = fast || u0 + 64u * j + lane < uhi;
-                v[j] = xchg_unordered(buf, mark, k[j], ids.to_slot(ins[j]), valid, lane);
+                const uint32_t u = u0 + 64u * j + (uint32_t)lane;
+                const bool valid = u < uhi;
+                const uint32_t t = t_first + c_lane + j * G64;
+                uint32_t p = pa + c_lane + j * G64, w = wa;
+                while (p >= B) { p -= B; w++; }
+                uint32_t kk = 0u, in = 0u;
+                if (valid) {
+                    kk = group_slot(pl.gr, grp, S, u, t, s0, s1);
+                    const uint32_t *kwl = ktr + kGKeyWin + kRoundKeyWords * (w - 1);
+                    uint32_t K[kFeistelRounds];
+#pragma unroll
+                    for (int i = 0; i < kFeistelRounds; i++) K[i] = kwl[i];
+                    const bool lastw = w == pl.w_last;
+                    in = ids.to_slot(w * B + feistel(p, lastw ? pl.len_last : B, lastw ? pl.h_last : pl.hB, K));
+                }
+                uint32_t vv;
+                if constexpr (ORDERED) vv = valid ? atomicExch(&buf[kk], in) : 0u;
+                else vv = xchg_unordered(buf, mark, kk, in, valid, lane);
+                if (valid && (int64_t)t >= pos_lo && (int64_t)t < pos_hi) o[t] = ids.from_slot(vv);
             }
         }
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const bool valid = fast || u0 + 64u * j + lane < uhi;
-            if (valid && (fast || ((int64_t)tj[j] >= pos_lo && (int64_t)tj[j] < pos_hi)))
-                o[tj[j]] = ids.from_slot(v[j]);
-            tj[j] += dT;
-            pj[j] += dT;
-            if (pj[j] >= B) { pj[j] -= B; wj[j]++; }
-        }
+        t_first += 256u * G;
+        pa += 256u * G;
+        if (pa >= B) { pa -= B; wa++; }
     }
-    if (last && do_fin) {
+    if (drain) {
+        // the group's final table is this wave's LDS: drain it in its tail order
         __syncthreads();
-        uint32_t *F = FIN + (int64_t)rl * pl.P1 + base;
-        for (uint32_t s = lane; s < S; s += 64) F[s] = buf[s];
-    }
-}
-
-// ---- tail ---------------------------------------------------------------------------------
-template <bool NARROW>
-__global__ __launch_bounds__(256) void k_g_tail(Geometry g, GPlan pl, const RankDesc *__restrict__ ranks,
-                                                int32_t rank_lo, const uint32_t *__restrict__ KT,
-                                                const uint32_t *__restrict__ FIN,
-                                                int64_t pos_lo, int64_t count,
-                                                int64_t *__restrict__ out) {
-    const int32_t rl = (int32_t)blockIdx.y;
-    const RankDesc rd = ranks[rank_lo + rl];
-    GIds<NARROW> ids;
-    ids.twoB = pl.twoB;
-    ids.old32 = (uint32_t)rd.old_start; ids.new32 = (uint32_t)rd.new_start;
-    ids.N32 = (uint32_t)g.N;
-    ids.rd = rd;
-    ids.g = g;
-    const uint32_t *tk = KT + rl * pl.kt_stride + kGKeyTail;
-    uint32_t kk[kFeistelRounds];
-#pragma unroll
-    for (int i = 0; i < kFeistelRounds; i++) kk[i] = tk[i];
-    const uint32_t P1 = (uint32_t)pl.P1;
-    const uint32_t *F = FIN + (int64_t)rl * pl.P1;
-    int64_t *o = out + (int64_t)rl * count - pos_lo;
-    const int64_t pos_hi = pos_lo + count;
-    for (uint32_t j = blockIdx.x * 256u + threadIdx.x; j < P1; j += gridDim.x * 256u) {
-        const int64_t pos = pl.T + j;
-        if (pos < pos_lo || pos >= pos_hi) continue;
-        o[pos] = ids.from_slot(F[feistel(j, P1, pl.hP, kk)]);
+        uint32_t tk[kRoundKeyWords];
+        round_keys8(g.key0, g.key1, grp, rank, DOM_V2_TAIL, tk);
+        const uint32_t hS = feistel_half_bits(S);
+        for (uint32_t e = lane; e < S; e += 64) {
+            const int64_t pos = pl.T + group_tail_pos(pl.gr, grp, e);
+            if (pos >= pos_lo && pos < pos_hi) o[pos] = ids.from_slot(buf[feistel(e, S, hS, tk)]);
+        }
     }
 }
 
@@ -362,15 +372,9 @@ size_t v2_grp_val_bytes(const Geometry &g, int32_t nr) {
     return words * sizeof(uint32_t);
 }
 
-// FIN: the final slot table of every rank (read by the tail)
-size_t v2_grp_fin_bytes(const Geometry &g, int32_t nr) {
-    const int64_t P1 = g.B < g.ns ? g.B : g.ns;
-    return (size_t)nr * (size_t)P1 * sizeof(uint32_t);
-}
-
 hipError_t launch_v2_grp(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, int32_t nr,
                          int64_t pos_lo, int64_t count, int64_t *out, uint32_t *VALws,
-                         uint32_t *FIN, hipStream_t s, const Marker &mk, bool ordered, int stage) {
+                         hipStream_t s, const Marker &mk, bool ordered, int stage) {
     const int64_t pos_hi = pos_lo + count < g.ns ? pos_lo + count : g.ns;
     if (nr <= 0 || pos_hi <= pos_lo) return hipSuccess;
     const GPlan pl = gplan(g, nr, gcus());
@@ -379,7 +383,7 @@ hipError_t launch_v2_grp(const Geometry &g, const RankDesc *ranks, int32_t rank_
     uint32_t *VAL = VALws + (size_t)nr * (size_t)pl.kt_stride;
     if (do_pre) {
         mk(K_V2_LASTOCC, s);
-        const int64_t items = pl.W + 3;
+        const int64_t items = pl.W + 2;
         hipLaunchKernelGGL(k_g_keys, dim3((uint32_t)gdiv(items, 256), (uint32_t)nr), dim3(256), 0, s,
                            g, rank_lo, pl.W, pl.kt_stride, KT);
         if (pl.tiles > 1)
@@ -390,43 +394,19 @@ hipError_t launch_v2_grp(const Geometry &g, const RankDesc *ranks, int32_t rank_
     if (!do_emit) return hipGetLastError();
     const bool need_tail = pos_hi > pl.T;
     const bool narrow = g.N + g.ns < (int64_t)UINT32_MAX;
-    const int do_fin = need_tail ? 1 : 0;
-    if (pl.T > 0) {
-        mk(K_V2_EMIT, s);
-        const dim3 grid((uint32_t)((int64_t)nr * pl.gr.G * pl.tiles));
-        // LDS padded so that a CU takes exactly 8 waves (2 per SIMD, balanced) instead of 9
-        size_t lds = (size_t)pl.Smax * 4 + (ordered ? 0 : (size_t)pl.Smax) + 16;
-        if (lds * 9 <= 160 * 1024) lds = 160 * 1024 / 9 + 16;
+    mk(K_V2_EMIT, s);
+    const dim3 grid((uint32_t)((int64_t)nr * pl.gr.G * pl.tiles));
+    // LDS padded so that a CU takes exactly 8 waves (2 per SIMD, balanced) instead of 9
+    size_t lds = (size_t)pl.Smax * 4 + (ordered ? 0 : (size_t)pl.Smax) + 16;
+    if (lds * 9 <= 160 * 1024) lds = 160 * 1024 / 9 + 16;
+    const int dt = need_tail ? 1 : 0;
 #define PSS_GE(O, N) hipLaunchKernelGGL((k_g_emit<O, N>), grid, dim3(64), lds, s, g, pl, ranks, rank_lo, \
-                                        (const uint32_t *)KT, (const uint32_t *)VAL, FIN, do_fin, pos_lo, count, out)
-        if (ordered && narrow) PSS_GE(true, true);
-        else if (ordered) PSS_GE(true, false);
-        else if (narrow) PSS_GE(false, true);
-        else PSS_GE(false, false);
+                                        (const uint32_t *)KT, (const uint32_t *)VAL, dt, pos_lo, count, out)
+    if (ordered && narrow) PSS_GE(true, true);
+    else if (ordered) PSS_GE(true, false);
+    else if (narrow) PSS_GE(false, true);
+    else PSS_GE(false, false);
 #undef PSS_GE
-    }
-    if (need_tail) {
-        mk(K_V2_TAIL, s);
-        if (pl.T == 0) {
-            // no steps: the final table is the initial one -- written by a one-tile emit of
-            // the empty stream (each group wave stores its initial table)
-            const dim3 grid((uint32_t)((int64_t)nr * pl.gr.G * pl.tiles));
-            const size_t lds = (size_t)pl.Smax * 4 + (ordered ? 0 : (size_t)pl.Smax) + 16;
-            if (narrow)
-                hipLaunchKernelGGL((k_g_emit<true, true>), grid, dim3(64), lds, s, g, pl, ranks, rank_lo,
-                                   (const uint32_t *)KT, (const uint32_t *)VAL, FIN, 1, pos_lo, count, out);
-            else
-                hipLaunchKernelGGL((k_g_emit<true, false>), grid, dim3(64), lds, s, g, pl, ranks, rank_lo,
-                                   (const uint32_t *)KT, (const uint32_t *)VAL, FIN, 1, pos_lo, count, out);
-        }
-        const dim3 grid((uint32_t)gdiv(pl.P1 < 262144 ? pl.P1 : 262144, 256), (uint32_t)nr);
-        if (narrow)
-            hipLaunchKernelGGL((k_g_tail<true>), grid, dim3(256), 0, s, g, pl, ranks, rank_lo,
-                               (const uint32_t *)KT, (const uint32_t *)FIN, pos_lo, count, out);
-        else
-            hipLaunchKernelGGL((k_g_tail<false>), grid, dim3(256), 0, s, g, pl, ranks, rank_lo,
-                               (const uint32_t *)KT, (const uint32_t *)FIN, pos_lo, count, out);
-    }
     mk(-1, s);
     return hipGetLastError();
 }
