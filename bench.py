@@ -1,18 +1,23 @@
 #!/usr/bin/env python
 """Benchmark of the MI355X partial-shuffle sampler's hot path (BASELINE.json metric).
 
-Workload (BASELINE.json configs[1]): V2 two-pool sampler, 10,000 files x
-10,000 samples = 100M samples, 8 logical ranks, shuffle_buffer 4096 -- per GPU.  One step =
+Default workload (BASELINE.json configs[1]): V2 two-pool sampler, 10,000 files
+x 10,000 samples = 100M samples, 8 logical ranks, shuffle_buffer 4096 -- per GPU.  One step =
 one epoch: set_epoch + init_iter (host CPython-MT file/block history, epoch upload) +
-generation of every id of the GPU's 8 logical ranks into HBM (the id -> file prefix scan is
-run by the first map after an epoch change, not by generation).  With --gpus N
-(torchrun, one process per GPU) GPU g owns logical ranks [8g, 8g+8) of an 8N-rank sampler over
-N x 100M samples (weak scaling, no data-path collective); after the timed loop the ranks
-all-gather (count, coverage digest) over RCCL and rank 0 checks exact coverage.
+generation of every id of the GPU's logical ranks into HBM.  With --gpus N (torchrun, one
+process per GPU) GPU g owns logical ranks [8g, 8g+8) of an 8N-rank sampler over N x 100M samples
+(weak scaling, no data-path collective); after the timed loop the ranks all-gather
+(count, coverage digest) over RCCL and rank 0 checks exact coverage.
+Other workloads (--workload): c2v1 (V1 on C2's files), c5 (B = 2^20 pools beyond LDS, weak),
+c3 (1B samples / 100K files / R = 1024 sharded over the N GPUs: strong scaling, the total work
+of BASELINE configs[2] is fixed).
 
-Prints ONE JSON line (rank 0).  Also reported: the dominant kernel's HBM roofline (live HIP
-event timing on the launch stream), the CPU oracle port of the reference algorithm on a
-bounded sample (cpu_baseline), and set_epoch -> first batch latency at 1B samples.
+Prints ONE JSON line (rank 0).  `value` is the whole-job throughput (all GPUs' ids / the
+slowest rank's time), `per_gpu` = value / N is the metric's per-GPU figure.  Also reported:
+the dominant kernel's HBM roofline (live HIP-event timing on the launch stream), the CPU
+baseline (the reference algorithm restated, on this box's host cores, bounded samples;
+cpu_baseline), set_epoch -> first batch latency at 1B samples through the drop-in sampler
+class, and the sampler's full per-epoch data path (generate + map + pinned D2H).
 """
 import argparse
 import json
@@ -27,6 +32,7 @@ import torch.distributed as dist
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+import workloads as W  # noqa: E402
 from partiallyshuffledistributedsampler_amd.distributed import (  # noqa: E402
     coverage_ok, expected_digest_gpu, gather_pairs, shard)
 from partiallyshuffledistributedsampler_amd.engine import IndexEngine, as_u64, digest  # noqa: E402
@@ -35,10 +41,13 @@ HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 BYTES_PER_ID = 8               # one int64 id written per emitted index
 METRIC = "shuffled indices/sec per GPU (G idx/s) + % HBM roofline; set_epoch latency @1B"
 
+# name: (workloads.py config, scaling) -- weak: per-GPU files and ranks fixed, strong: the
+# configuration's total fixed and its logical ranks sharded over the GPUs
 WORKLOADS = {
-    # name: (files per GPU, samples per file, logical ranks per GPU, shuffle_buffer, version)
-    "c2": (10_000, 10_000, 8, 4096, 2),
-    "c2v1": (10_000, 10_000, 8, 4096, 1),
+    "c2": ("c2", "weak"),
+    "c2v1": ("c2", "weak"),
+    "c5": ("c5", "weak"),
+    "c3": ("c3", "strong"),
 }
 
 
@@ -59,42 +68,180 @@ def _pmc_traffic(symbols):
     return None
 
 
-def cpu_baseline(seconds_budget=12.0):
-    """The oracle's C port of the reference V2 algorithm (CPython MT + list.remove pools,
-    V2:96-116) on rank streams of the same workload, single core, bounded sample."""
+# ---- CPU baseline --------------------------------------------------------------------------------
+def _host():
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"cores": len(os.sched_getaffinity(0)), "cpu_model": model}
+
+
+def cpu_baseline(seconds_budget=10.0):
+    """The reference algorithm on this box's host cores (the reference is not on the GPU box:
+    its restatements in oracle/, pinned by the goldens), bounded samples, one core each:
+      value       -- V2 (the bench workload C2): oracle's C port of get_index (CPython MT19937 +
+                     list.remove pools, V2:96-116) over whole rank streams, G idx/s;
+      c1_v1       -- C1 (BASELINE configs[0]): oracle/pyref.py's Python V1 __next__ loop
+                     (V1:151-259) with its per-batch gc.collect() on and off, 64 batches,
+                     extrapolated to the epoch;
+      c3_v2/c5_v2 -- Python get_index at B = 4096 / 2^20 (C3 / C5), a prefix, extrapolated;
+      c3_v2_set_epoch_to_first_batch_ms -- Python init_iter (100K-file shuffle, 1024 blocks) +
+                     the first 1024 get_index draws at C3.
+    """
+    import gc
+    import random
     from oracle import oracle as O
-    F, L, R, B, _ = WORKLOADS["c2"]
-    N = F * L
+    from oracle.pyref import V1Loop, V2Draws
+    lengths, N, R, B, _ = W.shape("c2")
     ns = O.num_samples(N, R)
-    h = O.RefHistory(2, F, R, 0, N)
-    h.init_iter(0)
     total, t0, r = 0, time.perf_counter(), 0
     while r < R and time.perf_counter() - t0 < seconds_budget:
-        hr = O.RefHistory(2, F, R, r, N)
+        hr = O.RefHistory(2, len(lengths), R, r, N)
         hr.init_iter(0)
         total += len(O.v2_exact_stream(0, hr.old_start, hr.start, ns, B, N))
         r += 1
     dt = time.perf_counter() - t0
-    return {"value": total / dt / 1e9, "unit": "G idx/s", "cores": 1, "kind": "port",
-            "sample": "reference V2 algorithm (oracle C port: CPython MT19937 + list.remove "
-                      "pools) over the full epoch streams of logical ranks 0..%d of the c2 "
-                      "workload (%d ids, %.1f s, 1 thread)" % (r - 1, total, dt)}
+    out = {"value": total / dt / 1e9, "unit": "G idx/s", "cores": 1, "kind": "port",
+           "sample": "reference V2 algorithm (oracle C port: CPython MT19937 + list.remove "
+                     "pools, V2:96-116) over the full epoch streams of logical ranks 0..%d of "
+                     "the c2 workload (%d ids, %.1f s, 1 thread)" % (r - 1, total, dt),
+           "host": _host()}
+    # C1, Python V1 loop, gc on / off
+    l1, N1, R1, B1, _ = W.shape("c1")
+    ns1 = O.num_samples(N1, R1)
+    arr = np.arange(int(l1.max()), dtype=np.int64)
+    c1 = {}
+    for use_gc in (True, False):
+        loop = V1Loop(0, ns1, B1, N1, l1.tolist(), lambda f: {"x": arr[:l1[f]]}, bs=1024,
+                      use_gc=use_gc)
+        nb, t0 = 0, time.perf_counter()
+        while nb < 64 and loop.next_batch() is not None:
+            nb += 1
+        dt = time.perf_counter() - t0
+        per_batch = dt / nb
+        c1["gc_on" if use_gc else "gc_off"] = {
+            "idx_per_s": nb * 1024 / dt,
+            "epoch_s_extrapolated": per_batch * (-(-ns1 // 1024)) * R1,
+            "sample": "%d batches of 1024 of rank 0, extrapolated to both ranks' epoch" % nb}
+    out["c1_v1"] = c1
+    # C3 / C5 get_index prefixes
+    for name, draws in (("c3", 65536), ("c5", 256)):
+        ln, Nn, Rn, Bn, _ = W.shape(name)
+        nsn = O.num_samples(Nn, Rn)
+        d = V2Draws(0, 0, nsn, Bn)
+        gc.disable()
+        t0 = time.perf_counter()
+        for _ in range(draws):
+            d.get_index()
+        dt = time.perf_counter() - t0
+        gc.enable()
+        out["%s_v2" % name] = {
+            "idx_per_s": draws / dt,
+            "epoch_s_extrapolated_one_rank": dt / draws * nsn,
+            "sample": "%d get_index draws of one rank (B=%d), extrapolated (label: extrapolated)"
+                      % (draws, Bn)}
+    # C3 set_epoch -> first batch, Python: init_iter's shuffles (V2:142-152) + 1024 draws
+    ln, Nn, Rn, Bn, _ = W.shape("c3")
+    nsn = O.num_samples(Nn, Rn)
+    files = list(range(len(ln)))
+    times = []
+    for e in range(3):
+        t0 = time.perf_counter()
+        random.seed(e)
+        fid = list(range(len(files)))
+        random.shuffle(fid)
+        files = [files[i] for i in fid]
+        blocks = list(range(Rn))
+        random.seed(e + 1)
+        random.shuffle(blocks)
+        d = V2Draws(0, nsn * blocks[0], nsn, Bn, epoch=e)
+        for _ in range(1024):
+            d.get_index()
+        times.append((time.perf_counter() - t0) * 1e3)
+    out["c3_v2_set_epoch_to_first_batch_ms"] = float(np.median(times))
+    return out
 
 
-def latency_1b(device, reps=5):
-    """set_epoch -> first batch at 1B samples / 100K files / R=1024:
-    host init_iter + epoch upload + device scan + generation of the rank's whole epoch +
-    id->(file, offset) map + pinned D2H of the first batch of 1024."""
-    F, L, R, B = 100_000, 10_000, 1024, 4096
-    lengths = np.full(F, L, dtype=np.int64)
-    eng = IndexEngine(lengths, F * L, R, B, 2, seed=0, device=device)
+def cpu_mode_figure(seconds_budget=8.0):
+    """The product's own CPU mode (libpss PSS_DEVICE_CPU, the GPU's schedule on host threads)
+    on the c2 workload: G idx/s and the threads it used."""
+    lengths, N, R, B, ver = W.shape("c2")
+    env = os.environ.get("PSS_CPU_THREADS")
+    threads = int(env) if env and int(env) > 0 else len(os.sched_getaffinity(0))
+    eng = IndexEngine(lengths, N, R, B, ver, seed=0, device="cpu")
+    out = torch.empty((R, eng.num_samples), dtype=torch.int64)
+    steps, t0 = 0, time.perf_counter()
+    while steps < 3 and time.perf_counter() - t0 < seconds_budget:
+        eng.init_iter(steps)
+        eng.generate(0, R, out=out)
+        steps += 1
+    dt = time.perf_counter() - t0
+    eng.close()
+    return {"value": R * eng.num_samples * steps / dt / 1e9, "unit": "G idx/s",
+            "threads": threads, "sample": "%d epochs of c2 (all 8 ranks)" % steps}
+
+
+# ---- latency and the drop-in data path ---------------------------------------------------------
+class _DS:
+    def __init__(self, files):
+        self.files = files
+
+    def reset(self):
+        pass
+
+
+def _reader_for(fl, width):
+    arr = np.arange(width, dtype=np.int64)
+
+    def reader(path, get_data=False):
+        n = fl[path]
+        return n if not get_data else ({"x": arr[:n]}, n)
+    return reader
+
+
+def latency_dropin(device, reps=5):
+    """set_epoch(e); next(iter(sampler)) at 1B samples / 100K files / R = 1024 (C3) through the
+    drop-in DistributedSamplerViaLocallyShuffleV2 class with an in-memory reader: host
+    init_iter + epoch upload + generation of the rank's epoch + prefix scan + id -> (file,
+    offset) map + pinned D2H + the first batch's grouping and file read.  Also the 128 logical
+    ranks one of 8 GPUs owns (ranks=(0, 128)), and the engine-level figure."""
+    from partiallyshuffledistributedsampler_amd.DistributedSamplerViaLocallyShuffleV2 import \
+        DistributedSamplerViaLocallyShuffle as V2
+    lengths, N, R, B, _ = W.shape("c3")
+    files = ["c3/%06d.npz" % i for i in range(len(lengths))]
+    fl = dict(zip(files, lengths.tolist()))
+    reader = _reader_for(fl, int(lengths.max()))
+    res = {}
+    for key, kw in (("set_epoch_to_first_batch_ms", {}),
+                    ("set_epoch_to_first_batch_128_ranks_ms", {"ranks": (0, 128)})):
+        s = V2(_DS(files), reader, num_replicas=R, rank=0, shuffle_buffer=B, total_size=1,
+               batch_size=1024, files_len=fl, device=device, **kw)
+        times = []
+        for e in range(reps + 1):
+            torch.cuda.synchronize(device)
+            t0 = time.perf_counter()
+            s.set_epoch(e)
+            b = next(iter(s))
+            t1 = time.perf_counter()
+            assert sum(len(d["x"]) for d in b[0]) == 1024
+            if e:
+                times.append((t1 - t0) * 1e3)
+        res[key] = float(np.median(times))
+    # engine only: init_iter + generate + map + D2H of the first batch
+    eng = IndexEngine(lengths, N, R, B, 2, seed=0, device=device)
     ns = eng.num_samples
     ids = torch.empty((1, ns), dtype=torch.int64, device=device)
     fpos = torch.empty(ns, dtype=torch.int32, device=device)
     off = torch.empty(ns, dtype=torch.int64, device=device)
     h_f = torch.empty(1024, dtype=torch.int32, pin_memory=True)
     h_o = torch.empty(1024, dtype=torch.int64, pin_memory=True)
-    times, times_gpu = [], []
+    times = []
     for e in range(reps + 1):
         torch.cuda.synchronize(device)
         t0 = time.perf_counter()
@@ -104,23 +251,45 @@ def latency_1b(device, reps=5):
         h_f.copy_(fpos[:1024], non_blocking=True)
         h_o.copy_(off[:1024], non_blocking=True)
         torch.cuda.synchronize(device)
-        t1 = time.perf_counter()
-        # all 128 logical ranks one GPU owns at 8 GPUs
-        eng.init_iter(e + 1000)
-        big = eng.generate(0, 128)
+        if e:
+            times.append((time.perf_counter() - t0) * 1e3)
+    eng.close()
+    res["engine_set_epoch_to_first_batch_ms"] = float(np.median(times))
+    res["config"] = ("V2, 100K files / 1B samples, R=1024, B=4096, batch 1024, in-memory "
+                     "reader; through DistributedSamplerViaLocallyShuffleV2 (one rank, and "
+                     "ranks=(0, 128): one of 8 GPUs' block)")
+    return res
+
+
+def sampler_data_path(device, reps=3):
+    """The drop-in's per-epoch device path at C2 for one rank (12.5M ids): set_epoch + iter ->
+    generation + prefix scan + id -> (file, offset) map + pinned D2H of every (file, offset)
+    pair; ms until all of it is on the host."""
+    from partiallyshuffledistributedsampler_amd.DistributedSamplerViaLocallyShuffleV2 import \
+        DistributedSamplerViaLocallyShuffle as V2
+    lengths, N, R, B, _ = W.shape("c2")
+    files = ["c2/%05d.npz" % i for i in range(len(lengths))]
+    fl = dict(zip(files, lengths.tolist()))
+    s = V2(_DS(files), _reader_for(fl, int(lengths.max())), num_replicas=R, rank=0,
+           shuffle_buffer=B, total_size=1, batch_size=1024, files_len=fl, device=device)
+    times = []
+    for e in range(reps + 1):
         torch.cuda.synchronize(device)
-        t2 = time.perf_counter()
-        del big
+        t0 = time.perf_counter()
+        s.set_epoch(e)
+        iter(s)
+        s._wait_host(s.num_samples)
+        t1 = time.perf_counter()
         if e:
             times.append((t1 - t0) * 1e3)
-            times_gpu.append((t2 - t1) * 1e3)
-    eng.close()
-    return {"set_epoch_to_first_batch_ms": float(np.median(times)),
-            "set_epoch_all_128_ranks_of_one_gpu_ms": float(np.median(times_gpu)),
-            "config": "V2, 100K files / 1B samples, R=1024, B=4096 (one sampler rank; and the "
-                      "128 logical ranks one of 8 GPUs generates)"}
+    ms = float(np.median(times))
+    return {"epoch_ms": ms, "ids": s.num_samples, "G_idx_per_s": s.num_samples / ms / 1e6,
+            "host_bytes": s.num_samples * 12,
+            "config": "C2, one rank (12.5M ids): generate + map + pinned D2H of (int32 file, "
+                      "int64 offset) per id"}
 
 
+# ---- main ------------------------------------------------------------------------------------
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -150,13 +319,19 @@ def main():
         else:
             dist.init_process_group("nccl", device_id=dev)
 
-    F1, L, RG, B, ver = WORKLOADS[args.workload]
-    F, R = F1 * world, RG * world
-    N = F * L
-    lengths = np.full(F, L, dtype=np.int64)
+    cfg_name, scaling = WORKLOADS[args.workload]
+    ver = 1 if args.workload == "c2v1" else W.CONFIGS[cfg_name][5]
+    l1, _, R1, B, _ = W.shape(cfg_name)
+    if scaling == "weak":        # the configuration per GPU: N x its files and ranks
+        lengths = np.tile(l1, world)
+        R = R1 * world
+    else:                        # the configuration in total, its ranks sharded over the GPUs
+        lengths, R = l1, R1
+    N = int(lengths.sum())
     eng = IndexEngine(lengths, N, R, B, ver, shuffle=True, seed=0, device=local)
     ns = eng.num_samples
     r_lo, r_hi = shard(R, world, rank)
+    RG = r_hi - r_lo
     out = torch.empty((RG, ns), dtype=torch.int64, device=dev)
     stream = torch.cuda.current_stream(dev)
 
@@ -167,6 +342,7 @@ def main():
     for e in range(args.warmup):
         step(e)
     torch.cuda.synchronize(dev)
+    eng.check()
     if world > 1:
         dist.barrier()
     eng.profile(not args.no_kernel_timing)
@@ -183,6 +359,7 @@ def main():
         dt = float(t.item())
     prof = eng.profile_read()
     eng.profile(False)
+    eng.check()
 
     # coverage of the last epoch across all GPUs: (count, digest) all-gather over RCCL
     pairs = gather_pairs(out.numel(), as_u64(digest(out.view(-1))), device=cdev)
@@ -190,22 +367,24 @@ def main():
     if rank == 0:
         coverage = coverage_ok(pairs, ns, R, expected_digest_gpu(N, ns, R, dev))
 
-    ids_total = RG * ns * world * args.steps
+    ids_total = sum(c for c, _ in pairs) * args.steps
     value = ids_total / dt / 1e9
     kname = "v2_emit" if ver == 2 else "v1_window"
     k_ms, k_n = prof.get(kname, (0.0, 0))
     per_launch_ms = k_ms / max(k_n, 1)
-    if ver == 2:
-        P1 = min(B, ns)
-        units = RG * (ns - P1)      # ids one v2_emit launch writes
+    P1 = min(B, ns)
+    if ver == 2 and P1 <= 16384:
+        units = RG * (ns - P1)      # ids one v2_emit launch writes (the tail rides along)
+        syms = ["k_v2_emit_x"] if eng.emit_path() == "xchg" else ["k_v2_emit"]
+    elif ver == 2:
+        units = RG * ns             # grouped pools: the emit kernel also drains the tail
+        syms = ["k_g_emit"]
     else:
         units = RG * ns
+        syms = ["k_v1_feistel"]
     achieved = units * BYTES_PER_ID / (per_launch_ms * 1e-3) / 1e9 if per_launch_ms > 0 else 0.0
-    if ver == 2:
-        syms = ["k_v2_emit_x"] if eng.emit_path() == "xchg" else ["k_v2_emit"]
-    else:
-        syms = ["k_v1_lds"]
     traffic = _pmc_traffic(syms)
+    desc = W.CONFIGS[cfg_name][0] + (" (V1 variant)" if args.workload == "c2v1" else "")
     line = {
         "metric": METRIC,
         "value": value,
@@ -215,31 +394,35 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": dt / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": scaling,
         "vs_baseline": None,
         "dtype": "int64",
         "data": "synthetic",
-        "config": {"workload": "%s, %d files x %d samples, %d logical ranks "
-                               "per GPU, shuffle_buffer %d (BASELINE configs[1] per GPU%s)"
-                               % ("V2 two-pool sampler" if ver == 2 else "V1 windowed sampler",
-                                  F1, L, RG, B, "" if ver == 2 else ", V1 variant"),
-                   "version": ver, "files": F, "samples": N, "logical_ranks": R,
-                   "shuffle_buffer": B, "ids_per_step": RG * ns * world,
+        "per_gpu": value / world,
+        "aggregate": value,
+        "config": {"workload": ("%s; %s" % (desc, "per GPU" if scaling == "weak"
+                                            else "sharded over the GPUs")),
+                   "name": args.workload, "version": ver, "files": len(lengths), "samples": N,
+                   "logical_ranks": R, "ranks_per_gpu": RG, "shuffle_buffer": B,
+                   "ids_per_step": ids_total // args.steps,
                    "parallelism": "logical ranks sharded over %d GPU(s)" % world},
-        "roofline": {"bound": "hbm", "kernel": kname, "achieved": achieved,
+        "roofline": {"bound": "hbm", "kernel": kname, "symbols": syms, "achieved": achieved,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                      "traffic": traffic, "launch_ms": per_launch_ms,
                      "algorithmic_bytes_per_launch": units * BYTES_PER_ID},
         "kernels_ms_per_step": {k: v[0] / max(1, args.steps) for k, v in prof.items()},
         "coverage_ok": coverage,
     }
+    eng.close()
+    del out
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline()
+        line["cpu_mode"] = cpu_mode_figure()
     if rank == 0 and not args.no_latency:
-        line["latency"] = latency_1b(local)
+        line["latency"] = latency_dropin(local)
+        line["sampler_data_path"] = sampler_data_path(local)
     if rank == 0:
         print(json.dumps(line), flush=True)
-    eng.close()
     if world > 1:
         dist.destroy_process_group()
 

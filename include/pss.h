@@ -14,6 +14,10 @@
  *     hipStream_t (NULL = default stream).  Device work is stream-ordered and asynchronous;
  *     nothing on the per-epoch path allocates once workspaces have grown to their size.
  *   - a handle is not thread-safe; distinct handles share no state.
+ *   - CPU mode: a handle created with device = PSS_DEVICE_CPU runs the same schedule on host
+ *     threads (bit-identical to the GPU); every `*_dev` pointer is then a HOST pointer, `stream`
+ *     is ignored and calls return when their work is done.  No HIP call is made, so it also
+ *     runs on a machine without a GPU (BASELINE configs[0]).
  */
 #ifndef PSS_H
 #define PSS_H
@@ -32,6 +36,8 @@ typedef struct pss_sampler pss_sampler;
 #define PSS_ESTATE 4    /* call out of order (e.g. generate before init_iter) */
 #define PSS_EDEVICE 5   /* a kernel reported a device-side error flag */
 
+#define PSS_DEVICE_CPU (-1)   /* pss_create device: the CPU mode */
+
 const char *pss_last_error(void);
 int pss_abi_version(void);
 
@@ -42,7 +48,8 @@ int pss_abi_version(void);
  *   num_samples   =  int(math.ceil(total_size * 1.0 / num_replicas)) (V1:42)
  *   version       -- 1 (one pool) or 2 (two pools, TF-like); shuffle is ignored by V2.
  *   seed          -- Philox key of the pool permutations (extension; the reference has none)
- *   device        -- HIP device ordinal used for every device call of this handle.
+ *   device        -- HIP device ordinal used for every device call of this handle, or
+ *                    PSS_DEVICE_CPU for the CPU mode.
  * No device memory is touched until the first device call. */
 int pss_create(const int64_t *files_len, int64_t num_files, int64_t total_size,
                int32_t num_replicas, int64_t shuffle_buffer, int32_t version, int32_t shuffle,
@@ -89,6 +96,12 @@ int pss_partition(pss_sampler *h, int32_t rank_lo, int32_t rank_hi, int64_t *seg
  * sensitive).  pss_digest_range digests the ids lo..hi-1. */
 int pss_digest(const int64_t *ids_dev, int64_t n, uint64_t *acc_dev, void *stream);
 int pss_digest_range(int64_t lo, int64_t hi, uint64_t *acc_dev, void *stream);
+/* the same on host memory (CPU mode, or any host id array) */
+int pss_digest_host(const int64_t *ids, int64_t n, uint64_t *acc);
+int pss_digest_range_host(int64_t lo, int64_t hi, uint64_t *acc);
+
+/* device ordinal of the handle, or PSS_DEVICE_CPU */
+int pss_device(const pss_sampler *h, int32_t *device);
 
 /* Kernel timing: while enabled, every launch of this handle is bracketed by HIP events on
  * its stream.  pss_profile_read synchronises on them and returns, per kernel kind
@@ -99,6 +112,18 @@ int pss_profile_read(pss_sampler *h, double *total_ms, int64_t *launches, int32_
 
 /* Synchronise `stream` and report any device-side error flag of the handle. */
 int pss_check(pss_sampler *h, void *stream);
+
+/* Asynchronous form: enqueue on `stream` a copy of the device error word into *dst (pinned
+ * host memory); nonzero once the stream has reached it means a kernel of this handle flagged
+ * an error (a queued lookahead pass of a later epoch reports in a later snapshot).  The word is
+ * sticky until pss_check clears it.  CPU mode: *dst = 0 at once. */
+int pss_error_snapshot(pss_sampler *h, int32_t *dst, void *stream);
+
+/* id -> (file position, offset) on the host against a caller-owned exclusive prefix of
+ * `nfiles` files (prefix[0..nfiles]); same reflection rule and flags as pss_map.  Used by the
+ * facade when file lengths are probed lazily in scan order (V1:181-190). */
+int pss_map_prefix_host(const int64_t *prefix, int64_t nfiles, const int64_t *ids, int64_t n,
+                        int32_t *file_pos, int64_t *offset);
 
 /* V2 replay kernel selection (no effect on results, which are identical on every path):
  * 0 = auto (one LDS exchange per step when the device passed the start-up lane-order check,

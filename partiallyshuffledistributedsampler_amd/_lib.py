@@ -1,7 +1,8 @@
 """ctypes binding of libpss.so (include/pss.h).
 
 The library is built in-tree by ``__graft_entry__.build()`` (hipcc, gfx950).  There is no
-fallback: if the library is missing or a call fails, an exception is raised.
+fallback: if the library is missing or a call fails, an exception is raised.  (The CPU mode,
+device="cpu", is part of the same library: PSS_DEVICE_CPU handles.)
 """
 import ctypes
 import os
@@ -10,6 +11,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libpss.so")
 
 PSS_OK = 0
+PSS_DEVICE_CPU = -1
 _c_i64p = ctypes.POINTER(ctypes.c_int64)
 _c_i32p = ctypes.POINTER(ctypes.c_int32)
 _vp = ctypes.c_void_p
@@ -41,6 +43,11 @@ SIGNATURES = {
     "pss_order_mode": ([_vp, _c_i32p], ctypes.c_int),
     "pss_profile_read": ([_vp, ctypes.POINTER(ctypes.c_double), _c_i64p, _i32], ctypes.c_int),
     "pss_debug_wave_scan": ([_vp, _vp, _i64, _vp], ctypes.c_int),
+    "pss_digest_host": ([_vp, _i64, _vp], ctypes.c_int),
+    "pss_digest_range_host": ([_i64, _i64, _vp], ctypes.c_int),
+    "pss_device": ([_vp, _c_i32p], ctypes.c_int),
+    "pss_error_snapshot": ([_vp, _vp, _vp], ctypes.c_int),
+    "pss_map_prefix_host": ([_vp, _i64, _vp, _i64, _vp, _vp], ctypes.c_int),
 }
 
 _lib = None
@@ -58,7 +65,7 @@ def load():
     if not os.path.exists(LIB_PATH):
         raise ImportError(
             "libpss.so is not built (%s). Build it with "
-            "`python -c 'import __graft_entry__ as g; g.build()'` -- there is no CPU fallback."
+            "`python -c 'import __graft_entry__ as g; g.build()'` -- there is no fallback."
             % LIB_PATH)
     lib = ctypes.CDLL(LIB_PATH)
     for name, (argt, rest) in SIGNATURES.items():

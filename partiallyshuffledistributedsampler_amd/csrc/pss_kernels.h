@@ -129,6 +129,7 @@ hipError_t launch_v2_tail_vals(const Geometry &g, const V2Plan &pl, const RankDe
 // table and per-tile tables live in val_ws (v2_val_bytes)
 bool v2_grouped(const Geometry &g);
 size_t v2_grp_val_bytes(const Geometry &g, int32_t nr);
+int64_t v2_grp_tiles(const Geometry &g, int32_t nr);   // tiles per (rank, group) stream
 hipError_t launch_v2_grp(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, int32_t nr,
                          int64_t pos_lo, int64_t count, int64_t *out, uint32_t *val_ws,
                          hipStream_t s, const Marker &mk, bool ordered, int stage);

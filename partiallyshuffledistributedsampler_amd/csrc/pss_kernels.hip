@@ -17,6 +17,7 @@
 #include <cstdlib>
 
 #include "pss_device.h"
+#include "pss_map.h"
 
 namespace pss {
 
@@ -74,46 +75,6 @@ __global__ __launch_bounds__(256) void k_scan_final(const int64_t *__restrict__ 
         carry += total;
     }
     if (c == gridDim.x - 1 && threadIdx.x == 0) prefix[F] = (int64_t)carry;
-}
-
-// largest f in [0, F) with prefix[f] <= id  (the file holding id; empty files are skipped
-// because an empty file shares its prefix with the next one)
-__device__ __forceinline__ int64_t file_of(const int64_t *prefix, int64_t F, int64_t id) {
-    int64_t lo = 0, hi = F;
-    while (hi - lo > 1) {
-        const int64_t mid = (lo + hi) >> 1;
-        if (prefix[mid] <= id) lo = mid; else hi = mid;
-    }
-    return lo;
-}
-
-// The id ranges a rank reads in one epoch, in stream order, wrapped at N and clipped to the
-// scanned total T = prefix[F] (ids >= T are reflected, V1:191-196).
-struct Ranges { int64_t lo[4], hi[4]; int n; };
-
-__device__ void rank_ranges(const Geometry &g, const RankDesc &rd, int64_t T, Ranges &r) {
-    int64_t plo[2], plen[2];
-    int np = 0;
-    if (g.version == 1) {
-        plo[0] = rd.new_start; plen[0] = g.ns; np = 1;
-    } else {
-        const int64_t a = 2 * g.B < g.ns ? 2 * g.B : g.ns;
-        plo[0] = rd.old_start; plen[0] = a; np = 1;
-        if (g.ns > a) { plo[1] = rd.new_start + a; plen[1] = g.ns - a; np = 2; }
-    }
-    r.n = 0;
-    for (int i = 0; i < np; i++) {
-        int64_t lo = plo[i] % g.N, len = plen[i];
-        while (len > 0) {
-            const int64_t take = (g.N - lo) < len ? (g.N - lo) : len;
-            int64_t h = lo + take;
-            const int64_t l = lo;
-            if (h > T) h = T;
-            if (l < h) { r.lo[r.n] = l; r.hi[r.n] = h; r.n++; }
-            len -= take;
-            lo = 0;
-        }
-    }
 }
 
 __global__ void k_part_count(Geometry g, const RankDesc *ranks, int32_t rank_lo, int32_t nr,
@@ -179,21 +140,9 @@ __global__ void k_part_emit(Geometry g, const RankDesc *ranks, int32_t rank_lo, 
 __global__ void k_map(const int64_t *__restrict__ prefix, int64_t F,
                       const int64_t *__restrict__ ids, int64_t n, int32_t *__restrict__ fpos,
                       int64_t *__restrict__ off) {
-    const int64_t T = prefix[F];
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
-         i += (int64_t)gridDim.x * blockDim.x) {
-        int64_t id = ids[i];
-        bool refl = false;
-        if (id >= T) {
-            id = 2 * T - id;
-            if (id == T) id = T - 1;
-            refl = true;
-        }
-        if (id < 0) { fpos[i] = INT32_MIN; off[i] = ids[i]; continue; }
-        const int64_t f = file_of(prefix, F, id);
-        fpos[i] = refl ? (int32_t)(-1 - f) : (int32_t)f;
-        off[i] = id - prefix[f];
-    }
+         i += (int64_t)gridDim.x * blockDim.x)
+        map_one(prefix, F, ids[i], fpos[i], off[i]);
 }
 
 __global__ void k_digest(const int64_t *__restrict__ ids, int64_t n, uint64_t *acc) {

@@ -5,6 +5,7 @@
 // MT19937, the device buffers of the current epoch, and the kernel launches.
 #include <hip/hip_runtime.h>
 
+#include <chrono>
 #include <cmath>
 #include <condition_variable>
 #include <cstdio>
@@ -19,6 +20,10 @@
 #include "../../include/pss.h"
 #include "pss_common.h"
 #include "pss_kernels.h"
+#include "pss_host_mt.h"
+#include "pss_cpu.h"
+
+using pss::CPythonMT;
 
 namespace {
 
@@ -36,94 +41,6 @@ int fail(int code, const std::string &msg) {
             return fail(e_ == hipErrorNotSupported ? PSS_ENOTSUP : PSS_EHIP,              \
                         std::string(#call) + ": " + hipGetErrorString(e_));               \
     } while (0)
-
-// ------------------------------------------------------------------------------------------
-// CPython 3.10 `random` (MT19937): seed(int) = init_by_array over the 32-bit words of
-// abs(seed); shuffle = Fisher-Yates with _randbelow_with_getrandbits (random.py:239-249,
-// 380-396).  The file-order and block permutations pin the file->rank assignment, so they
-// must match the reference exactly.
-// ------------------------------------------------------------------------------------------
-class CPythonMT {
-  public:
-    void seed(int64_t a) {
-        uint64_t m = a < 0 ? (uint64_t)(-(a + 1)) + 1u : (uint64_t)a;
-        uint32_t key[2] = {(uint32_t)m, (uint32_t)(m >> 32)};
-        init_by_array(key, key[1] ? 2 : 1);
-    }
-    uint32_t next() {
-        if (__builtin_expect(mti_ >= kN, 0)) twist();
-        return out_[mti_++];
-    }
-    // random.py:239-249 (_randbelow_with_getrandbits): k = n.bit_length(), draw getrandbits(k)
-    // (the top k bits of one 32-bit output) until below n
-    uint32_t randbelow(uint32_t n) {  // n < 2^32
-        if (n == 0) return 0;
-        const int sh = __builtin_clz(n);                 // 32 - k
-        uint32_t r;
-        do { r = next() >> sh; } while (r >= n);
-        return r;
-    }
-    template <typename T>
-    void shuffle(T *x, int64_t n) {   // random.py:380-396
-        for (int64_t i = n - 1; i >= 1; i--) {
-            const int64_t j = randbelow((uint32_t)(i + 1));
-            const T t = x[i]; x[i] = x[j]; x[j] = t;
-        }
-    }
-
-  private:
-    static constexpr int kN = 624, kM = 397;
-    uint32_t mt_[kN];
-    uint32_t out_[kN];   // tempered outputs of the current block
-    int mti_ = kN + 1;
-
-    void init_genrand(uint32_t s) {
-        mt_[0] = s;
-        for (int i = 1; i < kN; i++) mt_[i] = 1812433253u * (mt_[i - 1] ^ (mt_[i - 1] >> 30)) + (uint32_t)i;
-        mti_ = kN;
-    }
-    void init_by_array(const uint32_t *key, int klen) {
-        init_genrand(19650218u);
-        int i = 1, j = 0;
-        for (int k = kN > klen ? kN : klen; k; k--) {
-            mt_[i] = (mt_[i] ^ ((mt_[i - 1] ^ (mt_[i - 1] >> 30)) * 1664525u)) + key[j] + (uint32_t)j;
-            i++; j++;
-            if (i >= kN) { mt_[0] = mt_[kN - 1]; i = 1; }
-            if (j >= klen) j = 0;
-        }
-        for (int k = kN - 1; k; k--) {
-            mt_[i] = (mt_[i] ^ ((mt_[i - 1] ^ (mt_[i - 1] >> 30)) * 1566083941u)) - (uint32_t)i;
-            i++;
-            if (i >= kN) { mt_[0] = mt_[kN - 1]; i = 1; }
-        }
-        mt_[0] = 0x80000000u;
-        mti_ = kN;
-    }
-    void twist() {
-        static const uint32_t mag01[2] = {0u, 0x9908b0dfu};
-        int kk = 0;
-        uint32_t y;
-        for (; kk < kN - kM; kk++) {
-            y = (mt_[kk] & 0x80000000u) | (mt_[kk + 1] & 0x7fffffffu);
-            mt_[kk] = mt_[kk + kM] ^ (y >> 1) ^ mag01[y & 1u];
-        }
-        for (; kk < kN - 1; kk++) {
-            y = (mt_[kk] & 0x80000000u) | (mt_[kk + 1] & 0x7fffffffu);
-            mt_[kk] = mt_[kk + (kM - kN)] ^ (y >> 1) ^ mag01[y & 1u];
-        }
-        y = (mt_[kN - 1] & 0x80000000u) | (mt_[0] & 0x7fffffffu);
-        mt_[kN - 1] = mt_[kM - 1] ^ (y >> 1) ^ mag01[y & 1u];
-        for (int i = 0; i < kN; i++) {   // temper the whole block at once (vectorises)
-            uint32_t t = mt_[i];
-            t ^= t >> 11;
-            t ^= (t << 7) & 0x9d2c5680u;
-            t ^= (t << 15) & 0xefc60000u;
-            t ^= t >> 18;
-            out_[i] = t;
-        }
-        mti_ = 0;
-    }
-};
 
 // The file-order permutation of an epoch (V1:114-117 seed(e + 1), V2:143-144 seed(e)):
 // MT19937 Fisher-Yates of range(F).  A pure function of (version, epoch, F), so it can be
@@ -245,6 +162,10 @@ struct pss_sampler {
     std::vector<int64_t> files_len;
     int64_t F = 0, N = 0, ns = 0, B = 0;
     int32_t R = 0, version = 1, shuffle = 1, device = 0;
+    bool cpu = false;             // PSS_DEVICE_CPU: host threads, host pointers, no HIP call
+    std::vector<int64_t> h_prefix;   // CPU mode: prefix over the epoch's file order
+    double cpu_ms[pss::K_NUM_KINDS] = {};
+    int64_t cpu_calls[pss::K_NUM_KINDS] = {};
     int32_t emit_path = 0;        // pss::EmitPath
     int32_t order_mode = 0;       // PSS_ORDER_COUNTER / PSS_ORDER_EXACT
     std::unique_ptr<PermPrefetcher> perms;   // file permutations of the coming epochs
@@ -398,12 +319,33 @@ int prepare_prefix(pss_sampler *h, hipStream_t s) {
     return PSS_OK;
 }
 
+// CPU mode: the exclusive prefix over the epoch's file order, computed on first use
+int cpu_prefix(pss_sampler *h) {
+    if (!h->iterated) return fail(PSS_ESTATE, "pss_init_iter must be called before generation");
+    if (!h->prefix_dirty && (int64_t)h->h_prefix.size() == h->F + 1) return PSS_OK;
+    h->h_prefix.resize((size_t)h->F + 1);
+    pss::cpu::scan_prefix(h->files_len.data(), h->order.data(), h->F, h->h_prefix.data());
+    h->prefix_dirty = false;
+    return PSS_OK;
+}
+
+struct CpuTimer {   // pss_profile in CPU mode: wall milliseconds per kernel kind
+    pss_sampler *h;
+    int kind;
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+    ~CpuTimer() {
+        if (!h->profiling) return;
+        h->cpu_ms[kind] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        h->cpu_calls[kind] += 1;
+    }
+};
+
 }  // namespace
 
 extern "C" {
 
 const char *pss_last_error(void) { return g_err.c_str(); }
-int pss_abi_version(void) { return 1; }
+int pss_abi_version(void) { return 2; }
 
 int pss_create(const int64_t *files_len, int64_t num_files, int64_t total_size,
                int32_t num_replicas, int64_t shuffle_buffer, int32_t version, int32_t shuffle,
@@ -428,6 +370,7 @@ int pss_create(const int64_t *files_len, int64_t num_files, int64_t total_size,
     h->shuffle = shuffle ? 1 : 0;
     h->seed = seed;
     h->device = device;
+    h->cpu = device == PSS_DEVICE_CPU;
     h->ns = (int64_t)std::ceil((double)total_size / (double)num_replicas);  // V1:42 (float ceil)
     if (h->ns >= (int64_t)UINT32_MAX) { delete h; return fail(PSS_ENOTSUP, "num_samples >= 2^32 per rank"); }
     h->order.resize(num_files);
@@ -445,7 +388,7 @@ int pss_create(const int64_t *files_len, int64_t num_files, int64_t total_size,
 
 int pss_destroy(pss_sampler *h) {
     if (!h) return PSS_OK;
-    if (h->dev_init) {
+    if (h->dev_init && !h->cpu) {
         DeviceGuard dg(h->device);
         if (h->upload_pending) (void)hipEventSynchronize(h->upload_done);
         if (h->side) (void)hipStreamSynchronize(h->side);   // a lookahead still writing VAL
@@ -528,6 +471,7 @@ int pss_rank_starts(const pss_sampler *h, int64_t *old_start, int64_t *new_start
 
 int pss_prepare(pss_sampler *h, void *stream) {
     if (!h) return fail(PSS_EINVAL, "NULL handle");
+    if (h->cpu) return cpu_prefix(h);
     DeviceGuard dg(h->device);
     return prepare_prefix(h, (hipStream_t)stream);
 }
@@ -654,6 +598,14 @@ int pss_generate(pss_sampler *h, int32_t rank_lo, int32_t rank_hi, int64_t pos_l
     if (rank_lo < 0 || rank_hi > h->R || rank_lo > rank_hi) return fail(PSS_EINVAL, "bad rank range");
     if (pos_lo < 0 || count < 0) return fail(PSS_EINVAL, "bad position range");
     if (count > 0 && rank_hi > rank_lo && !out_dev) return fail(PSS_EINVAL, "out_dev is NULL");
+    if (h->cpu) {
+        if (!h->iterated) return fail(PSS_ESTATE, "pss_init_iter must be called before generation");
+        if (rank_hi == rank_lo || count == 0 || pos_lo >= h->ns) return PSS_OK;
+        CpuTimer tm{h, h->version == 1 ? pss::K_V1 : pss::K_V2_EMIT};
+        pss::cpu::generate(h->geometry(), h->ranks.data(), rank_lo, rank_hi - rank_lo, pos_lo, count,
+                           h->epoch, h->order_mode == PSS_ORDER_EXACT, out_dev);
+        return PSS_OK;
+    }
     DeviceGuard dg(h->device);
     hipStream_t s = (hipStream_t)stream;
     int rc = prepare(h, s);
@@ -699,7 +651,7 @@ int pss_generate(pss_sampler *h, int32_t rank_lo, int32_t rank_hi, int64_t pos_l
 int pss_set_emit_path(pss_sampler *h, int32_t path) {
     if (!h) return fail(PSS_EINVAL, "NULL handle");
     if (path < pss::EMIT_AUTO || path > pss::EMIT_PROBE) return fail(PSS_EINVAL, "bad emit path");
-    if (path == pss::EMIT_XCHG) {
+    if (path == pss::EMIT_XCHG && !h->cpu) {
         DeviceGuard dg(h->device);
         int rc = ensure_device(h);
         if (rc) return rc;
@@ -713,7 +665,7 @@ int pss_set_emit_path(pss_sampler *h, int32_t path) {
 int pss_set_order_mode(pss_sampler *h, int32_t mode) {
     if (!h) return fail(PSS_EINVAL, "NULL handle");
     if (mode != PSS_ORDER_COUNTER && mode != PSS_ORDER_EXACT) return fail(PSS_EINVAL, "bad order mode");
-    if (mode == PSS_ORDER_EXACT) {
+    if (mode == PSS_ORDER_EXACT && !h->cpu) {   // the CPU mode has no LDS bounds
         if (h->version == 1 && !pss::v1_exact_supported(h->geometry()))
             return fail(PSS_ENOTSUP, "V1 exact order needs shuffle_buffer <= 8192");
         if (h->version == 2 && !pss::v2_exact_supported(h->geometry()))
@@ -731,6 +683,7 @@ int pss_order_mode(const pss_sampler *h, int32_t *mode) {
 
 int pss_emit_path(pss_sampler *h, int32_t *path) {
     if (!h || !path) return fail(PSS_EINVAL, "NULL argument");
+    if (h->cpu) { *path = 0; return PSS_OK; }   // no replay kernel in CPU mode
     if (h->emit_path != pss::EMIT_AUTO) { *path = h->emit_path; return PSS_OK; }
     DeviceGuard dg(h->device);
     int rc = ensure_device(h);
@@ -750,8 +703,17 @@ int pss_profile(pss_sampler *h, int32_t enable) {
 
 int pss_profile_read(pss_sampler *h, double *total_ms, int64_t *launches, int32_t nkinds) {
     if (!h || !total_ms || !launches) return fail(PSS_EINVAL, "NULL argument");
-    DeviceGuard dg(h->device);
     for (int32_t k = 0; k < nkinds; k++) { total_ms[k] = 0; launches[k] = 0; }
+    if (h->cpu) {
+        for (int32_t k = 0; k < nkinds && k < pss::K_NUM_KINDS; k++) {
+            total_ms[k] = h->cpu_ms[k];
+            launches[k] = h->cpu_calls[k];
+            h->cpu_ms[k] = 0;
+            h->cpu_calls[k] = 0;
+        }
+        return PSS_OK;
+    }
+    DeviceGuard dg(h->device);
     for (const auto &sp : h->spans) {
         PSS_HIP(hipEventSynchronize(h->ev_pool[sp.b]));
         float ms = 0.f;
@@ -769,6 +731,13 @@ int pss_map(pss_sampler *h, const int64_t *ids_dev, int64_t n, int32_t *file_pos
     if (!h) return fail(PSS_EINVAL, "NULL handle");
     if (n < 0 || (n > 0 && (!ids_dev || !file_pos_dev || !offset_dev))) return fail(PSS_EINVAL, "bad arguments");
     if (h->F == 0) return fail(PSS_ESTATE, "no files to map into");
+    if (h->cpu) {
+        const int rc = cpu_prefix(h);
+        if (rc) return rc;
+        CpuTimer tm{h, pss::K_MAP};
+        pss::cpu::map(h->h_prefix.data(), h->F, ids_dev, n, file_pos_dev, offset_dev);
+        return PSS_OK;
+    }
     DeviceGuard dg(h->device);
     hipStream_t s = (hipStream_t)stream;
     int rc = prepare_prefix(h, s);
@@ -785,6 +754,14 @@ int pss_partition(pss_sampler *h, int32_t rank_lo, int32_t rank_hi, int64_t *seg
     if (!seg_off_dev) return fail(PSS_EINVAL, "seg_off_dev is NULL");
     if (seg_cap > 0 && (!seg_file_dev || !seg_lo_dev || !seg_hi_dev)) return fail(PSS_EINVAL, "NULL segment arrays");
     if (h->F == 0) return fail(PSS_ESTATE, "no files to partition");
+    if (h->cpu) {
+        const int rc = cpu_prefix(h);
+        if (rc) return rc;
+        if (!pss::cpu::partition(h->geometry(), h->ranks.data(), rank_lo, rank_hi - rank_lo, h->h_prefix.data(),
+                                 h->F, seg_off_dev, seg_file_dev, seg_lo_dev, seg_hi_dev, seg_cap))
+            return fail(PSS_EDEVICE, "partition capacity exceeded");
+        return PSS_OK;
+    }
     DeviceGuard dg(h->device);
     hipStream_t s = (hipStream_t)stream;
     int rc = prepare_prefix(h, s);
@@ -809,6 +786,7 @@ int pss_digest_range(int64_t lo, int64_t hi, uint64_t *acc_dev, void *stream) {
 
 int pss_check(pss_sampler *h, void *stream) {
     if (!h) return fail(PSS_EINVAL, "NULL handle");
+    if (h->cpu) return PSS_OK;   // CPU mode reports errors by return code
     DeviceGuard dg(h->device);
     PSS_HIP(hipStreamSynchronize((hipStream_t)stream));
     // lookahead passes on the side stream share the error word: let them land first
@@ -822,6 +800,43 @@ int pss_check(pss_sampler *h, void *stream) {
         return fail(PSS_EDEVICE, "device error flag " + std::to_string(err) +
                                      " (1: partition capacity exceeded, 2: sort bucket overflow)");
     }
+    return PSS_OK;
+}
+
+int pss_error_snapshot(pss_sampler *h, int32_t *dst, void *stream) {
+    if (!h || !dst) return fail(PSS_EINVAL, "NULL argument");
+    if (h->cpu || !h->dev_init) { *dst = 0; return PSS_OK; }
+    DeviceGuard dg(h->device);
+    // not ordered after queued lookahead passes (that would hold the caller's stream behind
+    // the next epochs' work): a flag they raise shows in a later snapshot or in pss_check
+    PSS_HIP(hipMemcpyAsync(dst, h->d_err.p, sizeof(int32_t), hipMemcpyDeviceToHost, (hipStream_t)stream));
+    return PSS_OK;
+}
+
+int pss_map_prefix_host(const int64_t *prefix, int64_t nfiles, const int64_t *ids, int64_t n,
+                        int32_t *file_pos, int64_t *offset) {
+    if (nfiles < 0 || n < 0 || !prefix || (n > 0 && (!ids || !file_pos || !offset)))
+        return fail(PSS_EINVAL, "bad arguments");
+    if (nfiles == 0) return fail(PSS_ESTATE, "no files to map into");
+    pss::cpu::map(prefix, nfiles, ids, n, file_pos, offset);
+    return PSS_OK;
+}
+
+int pss_digest_host(const int64_t *ids, int64_t n, uint64_t *acc) {
+    if (n < 0 || !acc || (n > 0 && !ids)) return fail(PSS_EINVAL, "bad arguments");
+    *acc += pss::cpu::digest(ids, n);
+    return PSS_OK;
+}
+
+int pss_digest_range_host(int64_t lo, int64_t hi, uint64_t *acc) {
+    if (!acc) return fail(PSS_EINVAL, "acc is NULL");
+    *acc += pss::cpu::digest_range(lo, hi);
+    return PSS_OK;
+}
+
+int pss_device(const pss_sampler *h, int32_t *device) {
+    if (!h || !device) return fail(PSS_EINVAL, "NULL argument");
+    *device = h->cpu ? PSS_DEVICE_CPU : h->device;
     return PSS_OK;
 }
 

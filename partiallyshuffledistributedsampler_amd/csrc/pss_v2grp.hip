@@ -364,6 +364,8 @@ __global__ __launch_bounds__(64) void k_g_emit(Geometry g, GPlan pl, const RankD
 // ------------------------------------------------------------------------------------------
 bool v2_grouped(const Geometry &g) { return (g.B < g.ns ? g.B : g.ns) > (int64_t)kLdsSlotMax; }
 
+int64_t v2_grp_tiles(const Geometry &g, int32_t nr) { return gplan(g, nr, gcus()).tiles; }
+
 // VAL ring buffer: key table (nr * kt_stride) then the per-tile last-occurrence tables
 size_t v2_grp_val_bytes(const Geometry &g, int32_t nr) {
     const GPlan p = gplan(g, nr, gcus());

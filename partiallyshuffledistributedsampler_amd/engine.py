@@ -1,9 +1,10 @@
 """IndexEngine: one libpss sampler handle plus the torch plumbing around it.
 
-torch is used only for device memory and streams; every index is produced by the HIP
-kernels behind include/pss.h.  Construction needs no GPU (the handle's host-side history,
-pss_init_iter, is pure host code); every device method requires a ROCm GPU and raises
-otherwise -- there is no CPU fallback.
+torch is used only for device memory and streams; every index is produced by libpss.so
+(include/pss.h): the HIP kernels on a GPU handle, or the library's CPU mode when the engine
+is created with device="cpu" (the same counter schedule on host threads, bit-identical to the
+GPU; BASELINE configs[0] runs there without a GPU).  A GPU engine never falls back to the CPU:
+its device methods raise without a ROCm GPU.
 """
 import ctypes
 
@@ -17,9 +18,15 @@ _i32p = ctypes.POINTER(ctypes.c_int32)
 
 
 def _stream_ptr(stream, device):
+    if device.type == "cpu":
+        return ctypes.c_void_p(0)
     if stream is None:
         stream = torch.cuda.current_stream(device)
     return ctypes.c_void_p(stream.cuda_stream)
+
+
+def is_cpu(device):
+    return device == "cpu" or (isinstance(device, torch.device) and device.type == "cpu")
 
 
 def require_gpu():
@@ -33,6 +40,8 @@ class IndexEngine:
 
     def __init__(self, files_len, total_size, num_replicas, shuffle_buffer, version,
                  shuffle=True, seed=0, device=0, order="counter"):
+        """device: a HIP device ordinal (or torch.device("cuda", i)), or "cpu" for the CPU
+        mode of the same schedule."""
         lib = _lib.load()
         fl = np.ascontiguousarray(files_len, dtype=np.int64)
         self.num_files = len(fl)
@@ -40,7 +49,10 @@ class IndexEngine:
         self.num_replicas = int(num_replicas)
         self.shuffle_buffer = int(shuffle_buffer)
         self.version = int(version)
-        self.device = int(device)
+        self.cpu = is_cpu(device)
+        if isinstance(device, torch.device) and not self.cpu:
+            device = device.index if device.index is not None else 0
+        self.device = -1 if self.cpu else int(device)
         h = ctypes.c_void_p()
         _lib.check(lib.pss_create(fl.ctypes.data_as(_i64p), len(fl), self.total_size,
                                   self.num_replicas, self.shuffle_buffer, self.version,
@@ -88,6 +100,8 @@ class IndexEngine:
 
     # ---- device --------------------------------------------------------------------------
     def _dev(self):
+        if self.cpu:
+            return torch.device("cpu")
         require_gpu()
         return torch.device("cuda", self.device)
 
@@ -155,7 +169,7 @@ class IndexEngine:
     def emit_path(self):
         v = ctypes.c_int32()
         _lib.call("pss_emit_path", self._h, ctypes.byref(v))
-        return {1: "xchg", 2: "probe"}[v.value]
+        return {0: "cpu", 1: "xchg", 2: "probe"}[v.value]
 
     ORDER_MODES = {"counter": 0, "exact": 1}
 
@@ -187,17 +201,29 @@ class IndexEngine:
 
 
 def digest(ids, acc=None, stream=None):
-    """acc (int64 device tensor holding a uint64 bit pattern) += sum(splitmix64(ids))."""
-    require_gpu()
+    """acc (1-element int64 tensor holding a uint64 bit pattern, on ids' device) +=
+    sum(splitmix64(ids)).  Device ids: one kernel; host ids: the library's host loop."""
     d = ids.device
+    ids = ids.contiguous()
     if acc is None:
         acc = torch.zeros(1, dtype=torch.int64, device=d)
+    if d.type == "cpu":
+        _lib.call("pss_digest_host", ctypes.c_void_p(ids.data_ptr()), ids.numel(),
+                  ctypes.c_void_p(acc.data_ptr()))
+        return acc
+    require_gpu()
     _lib.call("pss_digest", ctypes.c_void_p(ids.data_ptr()), ids.numel(),
               ctypes.c_void_p(acc.data_ptr()), _stream_ptr(stream, d))
     return acc
 
 
 def digest_range(lo, hi, device, acc=None, stream=None):
+    """acc += sum(splitmix64(i)) for i in [lo, hi); device: a GPU ordinal / device or "cpu"."""
+    if is_cpu(device):
+        if acc is None:
+            acc = torch.zeros(1, dtype=torch.int64)
+        _lib.call("pss_digest_range_host", int(lo), int(hi), ctypes.c_void_p(acc.data_ptr()))
+        return acc
     require_gpu()
     d = torch.device("cuda", device) if isinstance(device, int) else device
     if acc is None:

@@ -31,7 +31,7 @@ def test_library_exports_every_declared_symbol():
     lib = _lib.load()
     for name in _declared():
         assert hasattr(lib, name), name
-    assert lib.pss_abi_version() == 1
+    assert lib.pss_abi_version() == 2
 
 
 def test_create_validates_arguments():

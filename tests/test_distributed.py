@@ -1,6 +1,8 @@
 """Multi-process (gloo, world_size 2, CPU) coverage of the N>1 path: logical-rank sharding,
-the (count, digest) all-gather and the coverage check.  Ids come from the oracle's Philox
-twin here (the GPU produces the same ids bit for bit, see test_gpu_parity.py)."""
+the (count, digest) all-gather and the coverage check.  Each process drives the product's
+IndexEngine in the library's CPU mode (the same schedule the GPU runs, bit for bit -- see
+test_cpu_mode.py / test_gpu_parity.py) and digests its shard with the library's host digest;
+the coverage target comes from the oracle."""
 import os
 import socket
 
@@ -23,31 +25,25 @@ def _free_port():
 def _worker(rank, world, port, version, corrupt, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
+    os.environ.setdefault("PSS_CPU_THREADS", "2")
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from oracle import oracle as O
+    from partiallyshuffledistributedsampler_amd.engine import IndexEngine, as_u64, digest
     rng = np.random.default_rng(2)
     lengths = rng.integers(100, 900, 50)
     N, R, B, seed, epoch = int(lengths.sum()), 7, 128, 11, 4
-    ns = O.num_samples(N, R)
-    key = O.epoch_key(seed, epoch)
+    eng = IndexEngine(lengths, N, R, B, version, seed=seed, device="cpu")
+    ns = eng.num_samples
+    eng.init_iter(epoch)
     lo, hi = shard(R, world, rank)
-    cnt, dig = 0, 0
-    for r in range(lo, hi):
-        h = O.RefHistory(version, len(lengths), R, r, N)
-        h.init_iter(epoch)
-        if version == 1:
-            ids = O.v1_philox_stream(key, r, h.start, ns, B, N)
-        else:
-            ids = O.v2_philox_stream(key, r, h.old_start, h.start, ns, B, N)
-        if corrupt and rank == 1 and r == hi - 1:
-            ids = ids.copy()
-            ids[0] = ids[1]           # a duplicate + a drop: the digest must notice
-        cnt += len(ids)
-        dig = (dig + O.digest(ids)) & ((1 << 64) - 1)
-    pairs = gather_pairs(cnt, dig)
+    ids = eng.generate(lo, hi)                     # [hi - lo, ns] host tensor
+    if corrupt and rank == 1:
+        ids[-1, 0] = ids[-1, 1]                    # a duplicate + a drop: the digest must notice
+    pairs = gather_pairs(ids.numel(), as_u64(digest(ids.view(-1))))
     pad = ns * R - N
     expect = (O.digest_range(0, N) + O.digest_range(0, pad)) & ((1 << 64) - 1)
     q.put((rank, coverage_ok(pairs, ns, R, expect), len(pairs)))
+    eng.close()
     dist.destroy_process_group()
 
 

@@ -421,3 +421,22 @@ def test_v2_exact_order_matches_exact_oracle(F, lo, hi, R, B, epochs):
             lo_p, cnt = ns // 3, ns // 2
             part = eng.generate(1, R, lo_p, cnt).cpu().numpy()
             assert np.array_equal(part, out[1:, lo_p:lo_p + cnt])
+
+
+@pytest.mark.parametrize("version", [1, 2])
+@pytest.mark.parametrize("cfg", CONFIGS + [(10_000, (10_000, 10_001), 8, 1 << 20)])
+def test_gpu_equals_cpu_mode(version, cfg):
+    """north_star: the internal CPU mode of the counter schedule matches the GPU bit for bit
+    (same engine API, device="cpu" vs the HIP kernels), including the C5 pool (B = 2^20)."""
+    F, (lo, hi), R, B = cfg
+    rng = np.random.default_rng(F * 1000 + R + 1)
+    lengths = rng.integers(lo, hi, F)
+    N = int(lengths.sum())
+    gpu = _engine(lengths, N, R, B, version, seed=99)
+    cpu = pss.IndexEngine(lengths, N, R, B, version, seed=99, device="cpu")
+    for epoch in (1, 2):
+        gpu.init_iter(epoch)
+        cpu.init_iter(epoch)
+        a = gpu.generate(0, R).cpu().numpy()
+        b = cpu.generate(0, R).numpy()
+        assert np.array_equal(a, b), (cfg, version, epoch)

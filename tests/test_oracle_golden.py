@@ -116,3 +116,36 @@ def test_v2_multiset_old_new_split():
             ref = np.where(v < 2 * B, old + v, new + v) % N
             assert len(s) == ns
             assert np.array_equal(np.sort(s), np.sort(ref))
+
+
+def test_pyref_loops_reproduce_reference_streams():
+    """oracle/pyref.py (bench.py's cpu_baseline restatement of the reference loops) draws the
+    reference's own id streams (tests/golden raw batches, captured at V1:178 / V2:181)."""
+    import numpy as np
+    from oracle.pyref import V1Loop, V2Draws
+    for name in ("v1_small", "v1_c1_small", "v1_zipf"):
+        fx = load(name)
+        files, lengths, fl, N, R, B, bs, shuffle = fixture_params(fx)
+        rrec = fx["ranks"][0]
+        ns = rrec["num_samples"]
+        for er in rrec["epochs"]:
+            if er.get("resume_step") is not None:
+                continue
+            lens = [fl.get(p, lengths[p]) for p in er["files"]]
+            loop = V1Loop(er["start_num"], ns, B, N, lens,
+                          lambda f: {"x": np.arange(lens[f])}, epoch=er["epoch"], bs=bs, use_gc=False)
+            got = []
+            while loop.next_batch() is not None:
+                got.append(loop.last_indices)
+            assert got[:len(er["batches"])] == er["batches"], (name, er["epoch"])
+    for name in ("v2_small", "v2_zipf"):
+        fx = load(name)
+        files, lengths, fl, N, R, B, bs, shuffle = fixture_params(fx)
+        for rrec in fx["ranks"]:
+            ns = rrec["num_samples"]
+            er = rrec["epochs"][0]
+            d = V2Draws(er["old_start"], er["start_num"], ns, B, epoch=er["epoch"])
+            want = [x for b in er["batches"] for x in b]
+            got = [d.get_index() for _ in range(len(want))]
+            got = [x - N if x >= N else x for x in got]
+            assert got == want, (name, rrec["rank"])
