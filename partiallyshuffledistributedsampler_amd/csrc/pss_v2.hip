@@ -966,9 +966,10 @@ hipError_t launch_v2_tail_vals(const Geometry &g, const V2Plan &pl, const RankDe
 
 bool v2_stage_split(const Geometry &g, int32_t nr, int emit_path) {
     if (emit_path == EMIT_AUTO) emit_path = lds_xchg_ordered() ? EMIT_XCHG : EMIT_PROBE;
-    // grouped pools split only when their streams are tiled: with one tile per stream the
-    // pre-pass is a tiny key-table kernel, cheaper in line than behind a cross-stream wait
-    if (v2_grouped(g)) return v2_grp_tiles(g, nr) > 1;
+    // grouped pools always split: their pre-pass (key table, last occurrences of tiled
+    // streams) runs a step ahead on the side stream; in line it cost the replay ~40 us per
+    // epoch at C5 (profiles/r02/c5_split_ab.txt)
+    if (v2_grouped(g)) return true;
     return emit_path == EMIT_XCHG;
 }
 

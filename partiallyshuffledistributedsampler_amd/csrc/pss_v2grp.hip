@@ -190,31 +190,58 @@ __device__ __forceinline__ uint32_t xchg_unordered(uint32_t *buf, g_lds_vu8 *mar
 // with A_i = R_i ^ K_i, A_{i+1} = A_{i-1} ^ F(A_i) ^ (K_{i-1} ^ K_{i+1}) (one 3-input xor per
 // round, F = one full-rate 24-bit multiply + shift); output L = A_5 ^ K_5, R = A_4 ^ F(A_5) ^ K_4.
 // Same values as feistel_once on each chain.
+template <bool PACKED>
 __device__ __forceinline__ void feistel4_uniform(const uint32_t x[4], uint32_t h, const uint32_t K[6],
                                                  uint32_t y[4]) {
-    if (h <= 8) {
+    if constexpr (PACKED) {
         uint32_t kp[kFeistelRounds];
 #pragma unroll
         for (int i = 0; i < kFeistelRounds; i++) kp[i] = (K[i] & 0xFFFFu) * 0x10001u;
         feistel4_pk16(x, h, kp, y);
-        return;
-    }
-    const uint32_t mask = (1u << h) - 1u, sh = 32u - h;
-    const uint32_t K02 = K[0] ^ K[2], K13 = K[1] ^ K[3], K24 = K[2] ^ K[4], K35 = K[3] ^ K[5];
-    auto F = [&](uint32_t a) -> uint32_t { return ((a & 0xFFFFFFu) * kFeistelM24) >> sh; };
+    } else {
+        const uint32_t mask = (1u << h) - 1u, sh = 32u - h;
+        const uint32_t K02 = K[0] ^ K[2], K13 = K[1] ^ K[3], K24 = K[2] ^ K[4], K35 = K[3] ^ K[5];
+        auto F = [&](uint32_t a) -> uint32_t { return ((a & 0xFFFFFFu) * kFeistelM24) >> sh; };
 #pragma unroll
-    for (int c = 0; c < 4; c++) {
-        const uint32_t A0 = (x[c] & mask) ^ K[0];
-        const uint32_t A1 = (x[c] >> h) ^ F(A0) ^ K[1];
-        const uint32_t A2 = A0 ^ F(A1) ^ K02;
-        const uint32_t A3 = A1 ^ F(A2) ^ K13;
-        const uint32_t A4 = A2 ^ F(A3) ^ K24;
-        const uint32_t A5 = A3 ^ F(A4) ^ K35;
-        y[c] = ((A5 ^ K[5]) << h) | (A4 ^ F(A5) ^ K[4]);
+        for (int c = 0; c < 4; c++) {
+            const uint32_t A0 = (x[c] & mask) ^ K[0];
+            const uint32_t A1 = (x[c] >> h) ^ F(A0) ^ K[1];
+            const uint32_t A2 = A0 ^ F(A1) ^ K02;
+            const uint32_t A3 = A1 ^ F(A2) ^ K13;
+            const uint32_t A4 = A2 ^ F(A3) ^ K24;
+            const uint32_t A5 = A3 ^ F(A4) ^ K35;
+            y[c] = ((A5 ^ K[5]) << h) | (A4 ^ F(A5) ^ K[4]);
+        }
     }
 }
 
-template <bool ORDERED, bool NARROW>
+// Table-wide Feistel pass of a wave: out[s] = f(feistel(off + s, n, h, K)) for s < cnt, four
+// chains per lane; the one-pass forms when n = 4^h (no cycle walking), else the walking one.
+template <class Put>
+__device__ __forceinline__ void feistel_table(uint32_t off, uint32_t cnt, uint32_t n, uint32_t h,
+                                              const uint32_t *Kg, int lane, Put put) {
+    uint32_t K[kFeistelRounds];
+#pragma unroll
+    for (int i = 0; i < kFeistelRounds; i++) K[i] = __builtin_amdgcn_readfirstlane(Kg[i]);
+    if (n == (1u << (2 * h))) {
+        for (uint32_t s0 = 0; s0 < cnt; s0 += 256) {
+            uint32_t x[4], y[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) x[j] = off + s0 + 64u * j + (uint32_t)lane;
+            if (h <= 8) feistel4_uniform<true>(x, h, K, y);
+            else feistel4_uniform<false>(x, h, K, y);
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const uint32_t s = s0 + 64u * j + (uint32_t)lane;
+                if (s < cnt) put(s, y[j]);
+            }
+        }
+    } else {
+        for (uint32_t s = lane; s < cnt; s += 64) put(s, feistel(off + s, n, h, K));
+    }
+}
+
+template <bool ORDERED, bool NARROW, bool PACKED, bool POW2>
 __global__ __launch_bounds__(64) void k_g_emit(Geometry g, GPlan pl, const RankDesc *__restrict__ ranks,
                                                int32_t rank_lo, const uint32_t *__restrict__ KT,
                                                const uint32_t *__restrict__ VAL, int do_tail,
@@ -254,7 +281,10 @@ __global__ __launch_bounds__(64) void k_g_emit(Geometry g, GPlan pl, const RankD
     ids.g = g;
     // slot table at the tile's start: the last value an earlier tile inserted into each slot,
     // else the initial content -- window 0 permuted by the init Feistel bijection of [0, P1)
-    {
+    if (tile == 0) {
+        feistel_table(base, S, (uint32_t)pl.P1, pl.hP, ktr + kGKeyInit, lane,
+                      [&](uint32_t s, uint32_t v) { buf[s] = ids.to_slot(v); });
+    } else {
         const uint32_t *ik = ktr + kGKeyInit;
         const int64_t ntv = pl.tiles - 1;
         const uint32_t *Vg = VAL + (int64_t)sg * ntv * pl.Smax;
@@ -269,9 +299,9 @@ __global__ __launch_bounds__(64) void k_g_emit(Geometry g, GPlan pl, const RankD
     const uint32_t s0 = ktr[kGKeySlot], s1 = ktr[kGKeySlot + 1];
     int64_t *o = out + (int64_t)rl * count - pos_lo;
     const uint32_t G = pl.gr.G, B = pl.B32;
-    const uint32_t G64 = 64u * G;
-    const bool pow2 = (S & (S - 1u)) == 0u;
+    const uint32_t G64 = 64u * G, G256 = 256u * G;
     const uint32_t shS = 32u - (uint32_t)ceil_log2_u64(S);
+    const bool gpow2 = (S & (S - 1u)) == 0u;         // this group pairs its draws
     // lane l serves sub-steps u0 + 64 j + l: step t_first + c_lane + j * 64 G, where t_first is
     // the iteration's first step (wave-uniform, advanced by 256 G per iteration without
     // division, together with its pool2 window wa and offset pa)
@@ -280,71 +310,93 @@ __global__ __launch_bounds__(64) void k_g_emit(Geometry g, GPlan pl, const RankD
     uint32_t t_first = (uint32_t)group_step(pl.gr, grp, ulo);
     uint32_t wa = 1 + t_first / B;
     uint32_t pa = t_first - (wa - 1) * B;
-    for (uint32_t u0 = ulo; u0 < uhi; u0 += 256) {
-        const uint32_t *kw = ktr + kGKeyWin + kRoundKeyWords * (wa - 1);
-        const bool uni = full_emit && u0 + 256 <= uhi && !pl.walk_full && wa < pl.w_last && pa + span < B;
-        if (uni) {
-            // every step of the iteration is valid, emitted, and inserts from the full window
-            // wa: round keys in SGPRs, no per-lane window bookkeeping
+    const bool runs_ok = full_emit && !pl.walk_full;
+    uint32_t u0 = ulo;
+    while (u0 < uhi) {
+        // a run of whole iterations inside the full window wa: keys in SGPRs, no bookkeeping
+        uint32_t n = 0;
+        if (runs_ok && wa < pl.w_last && pa + span < B && uhi - u0 >= 256u) {
+            const uint32_t by_win = (B - 1u - span - pa) / G256 + 1u;
+            const uint32_t by_end = (uhi - u0) / 256u;
+            n = by_win < by_end ? by_win : by_end;
+        }
+        if (n) {
+            const uint32_t *kw = ktr + kGKeyWin + kRoundKeyWords * (wa - 1);
             uint32_t K[kFeistelRounds];
 #pragma unroll
             for (int i = 0; i < kFeistelRounds; i++) K[i] = __builtin_amdgcn_readfirstlane(kw[i]);
-            const uint32_t tb = t_first + c_lane, xb = pa + c_lane;
-            uint32_t k[4];
-            if (pow2) {      // paired draws: sub-steps u, u + 64 share the hash of the lower step
-                const uint32_t h0 = slot_hash(tb, s0, s1), h2 = slot_hash(tb + 2u * G64, s0, s1);
-                k[0] = h0 >> shS; k[1] = (h0 << 16) >> shS;
-                k[2] = h2 >> shS; k[3] = (h2 << 16) >> shS;
-            } else {
-#pragma unroll
-                for (int j = 0; j < 4; j++) k[j] = scale32(slot_hash(tb + j * G64, s0, s1), S);
-            }
-            const uint32_t x[4] = {xb, xb + G64, xb + 2u * G64, xb + 3u * G64};
-            uint32_t y[4];
-            feistel4_uniform(x, pl.hB, K, y);
             // ids of the window's values wa B + y: one add when the window maps contiguously
             const uint32_t wB = wa * B;
-            uint32_t ins[4];
             const uint32_t id_first = ids.to_slot(wB), id_last = ids.to_slot(wB + B - 1u);
-            const bool contig = NARROW && id_last - id_first == B - 1u && ((wB < pl.twoB) == (wB + B - 1u < pl.twoB));
+            const bool contig = NARROW && id_last - id_first == B - 1u &&
+                                ((wB < pl.twoB) == (wB + B - 1u < pl.twoB));
+            uint32_t tb = t_first + c_lane, xb = pa + c_lane;
+            int64_t *ob = o + t_first;                                // wave-uniform base
+            const uint32_t boff = c_lane * 8u;                        // per-lane byte offsets
+            auto body = [&](auto ctg) {
+                for (uint32_t it = 0; it < n; it++) {
+                    uint32_t k[4];
+                    if (POW2 || gpow2) {    // paired draws: sub-steps u, u + 64 share one hash
+                        const uint32_t h0 = slot_hash(tb, s0, s1), h2 = slot_hash(tb + 2u * G64, s0, s1);
+                        k[0] = h0 >> shS; k[1] = (h0 << 16) >> shS;
+                        k[2] = h2 >> shS; k[3] = (h2 << 16) >> shS;
+                    } else {
 #pragma unroll
-            for (int j = 0; j < 4; j++) ins[j] = contig ? id_first + y[j] : ids.to_slot(wB + y[j]);
-            uint32_t v[4];
+                        for (int j = 0; j < 4; j++) k[j] = scale32(slot_hash(tb + j * G64, s0, s1), S);
+                    }
+                    const uint32_t x[4] = {xb, xb + G64, xb + 2u * G64, xb + 3u * G64};
+                    uint32_t y[4], v[4];
+                    feistel4_uniform<PACKED>(x, pl.hB, K, y);
 #pragma unroll
-            for (int j = 0; j < 4; j++) {
-                if constexpr (ORDERED) v[j] = atomicExch(&buf[k[j]], ins[j]);
-                else v[j] = xchg_unordered(buf, mark, k[j], ins[j], true, lane);
-            }
-            int64_t *ob = o + tb;
+                    for (int j = 0; j < 4; j++) {
+                        const uint32_t in = decltype(ctg)::value ? id_first + y[j] : ids.to_slot(wB + y[j]);
+                        if constexpr (ORDERED) v[j] = atomicExch(&buf[k[j]], in);
+                        else v[j] = xchg_unordered(buf, mark, k[j], in, true, lane);
+                    }
 #pragma unroll
-            for (int j = 0; j < 4; j++) ob[(int64_t)j * G64] = ids.from_slot(v[j]);
-        } else {
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                const uint32_t u = u0 + 64u * j + (uint32_t)lane;
-                const bool valid = u < uhi;
-                const uint32_t t = t_first + c_lane + j * G64;
-                uint32_t p = pa + c_lane + j * G64, w = wa;
-                while (p >= B) { p -= B; w++; }
-                uint32_t kk = 0u, in = 0u;
-                if (valid) {
-                    kk = group_slot(pl.gr, grp, S, u, t, s0, s1);
-                    const uint32_t *kwl = ktr + kGKeyWin + kRoundKeyWords * (w - 1);
-                    uint32_t K[kFeistelRounds];
-#pragma unroll
-                    for (int i = 0; i < kFeistelRounds; i++) K[i] = kwl[i];
-                    const bool lastw = w == pl.w_last;
-                    in = ids.to_slot(w * B + feistel(p, lastw ? pl.len_last : B, lastw ? pl.h_last : pl.hB, K));
+                    for (int j = 0; j < 4; j++)
+                        *(int64_t *)((char *)ob + (boff + 8u * (uint32_t)j * G64)) = ids.from_slot(v[j]);
+                    tb += G256;
+                    xb += G256;
+                    ob += G256;
                 }
-                uint32_t vv;
-                if constexpr (ORDERED) vv = valid ? atomicExch(&buf[kk], in) : 0u;
-                else vv = xchg_unordered(buf, mark, kk, in, valid, lane);
-                if (valid && (int64_t)t >= pos_lo && (int64_t)t < pos_hi) o[t] = ids.from_slot(vv);
-            }
+            };
+            if (contig) body(std::true_type{});
+            else body(std::false_type{});
+            t_first += n * G256;
+            pa += n * G256;
+            u0 += 256u * n;
+            continue;
         }
-        t_first += 256u * G;
-        pa += 256u * G;
-        if (pa >= B) { pa -= B; wa++; }
+        // one iteration across a window boundary, partly valid or partly emitted
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const uint32_t u = u0 + 64u * j + (uint32_t)lane;
+            const bool valid = u < uhi;
+            const uint32_t t = t_first + c_lane + j * G64;
+            uint32_t p = pa + c_lane + j * G64, w = wa;
+            while (p >= B) { p -= B; w++; }
+            uint32_t kk = 0u, in = 0u;
+            if (valid) {
+                kk = group_slot(pl.gr, grp, S, u, t, s0, s1);
+                const uint32_t *kwl = ktr + kGKeyWin + kRoundKeyWords * (w - 1);
+                uint32_t K[kFeistelRounds];
+#pragma unroll
+                for (int i = 0; i < kFeistelRounds; i++) K[i] = kwl[i];
+                const bool lastw = w == pl.w_last;
+                in = ids.to_slot(w * B + (lastw || pl.walk_full
+                                              ? feistel(p, lastw ? pl.len_last : B, lastw ? pl.h_last : pl.hB, K)
+                                              : feistel_once(p, pl.hB, K)));
+            }
+            uint32_t vv;
+            if constexpr (ORDERED) vv = valid ? atomicExch(&buf[kk], in) : 0u;
+            else vv = xchg_unordered(buf, mark, kk, in, valid, lane);
+            if (valid && (int64_t)t >= pos_lo && (int64_t)t < pos_hi) o[t] = ids.from_slot(vv);
+        }
+        t_first += G256;
+        pa += G256;
+        while (pa >= B) { pa -= B; wa++; }
+        u0 += 256u;
     }
     if (drain) {
         // the group's final table is this wave's LDS: drain it in its tail order
@@ -352,10 +404,10 @@ __global__ __launch_bounds__(64) void k_g_emit(Geometry g, GPlan pl, const RankD
         uint32_t tk[kRoundKeyWords];
         round_keys8(g.key0, g.key1, grp, rank, DOM_V2_TAIL, tk);
         const uint32_t hS = feistel_half_bits(S);
-        for (uint32_t e = lane; e < S; e += 64) {
+        feistel_table(0u, S, S, hS, tk, lane, [&](uint32_t e, uint32_t s) {
             const int64_t pos = pl.T + group_tail_pos(pl.gr, grp, e);
-            if (pos >= pos_lo && pos < pos_hi) o[pos] = ids.from_slot(buf[feistel(e, S, hS, tk)]);
-        }
+            if (pos >= pos_lo && pos < pos_hi) o[pos] = ids.from_slot(buf[s]);
+        });
     }
 }
 
@@ -402,12 +454,17 @@ hipError_t launch_v2_grp(const Geometry &g, const RankDesc *ranks, int32_t rank_
     size_t lds = (size_t)pl.Smax * 4 + (ordered ? 0 : (size_t)pl.Smax) + 16;
     if (lds * 9 <= 160 * 1024) lds = 160 * 1024 / 9 + 16;
     const int dt = need_tail ? 1 : 0;
-#define PSS_GE(O, N) hipLaunchKernelGGL((k_g_emit<O, N>), grid, dim3(64), lds, s, g, pl, ranks, rank_lo, \
-                                        (const uint32_t *)KT, (const uint32_t *)VAL, dt, pos_lo, count, out)
-    if (ordered && narrow) PSS_GE(true, true);
-    else if (ordered) PSS_GE(true, false);
-    else if (narrow) PSS_GE(false, true);
-    else PSS_GE(false, false);
+    const bool packed = pl.hB <= 8;
+    const bool pow2 = pl.gr.r == 0 && (pl.gr.q & (pl.gr.q - 1u)) == 0u;   // every group 2^b slots
+#define PSS_GE(O, N, PK, P2) hipLaunchKernelGGL((k_g_emit<O, N, PK, P2>), grid, dim3(64), lds, s, g, pl, ranks, \
+                                                rank_lo, (const uint32_t *)KT, (const uint32_t *)VAL, dt, pos_lo, count, out)
+#define PSS_GE2(O, N) do { if (packed && pow2) PSS_GE(O, N, true, true); else if (packed) PSS_GE(O, N, true, false); \
+                           else if (pow2) PSS_GE(O, N, false, true); else PSS_GE(O, N, false, false); } while (0)
+    if (ordered && narrow) PSS_GE2(true, true);
+    else if (ordered) PSS_GE2(true, false);
+    else if (narrow) PSS_GE2(false, true);
+    else PSS_GE2(false, false);
+#undef PSS_GE2
 #undef PSS_GE
     mk(-1, s);
     return hipGetLastError();
@@ -417,10 +474,22 @@ hipError_t init_kernel_attributes_v2grp() {
     const int big = 160 * 1024;
     hipError_t e = hipSuccess;
 #define PSS_ATTR(fn) { hipError_t x = hipFuncSetAttribute((const void *)(fn), hipFuncAttributeMaxDynamicSharedMemorySize, big); if (x != hipSuccess) e = x; }
-    PSS_ATTR((k_g_emit<true, true>));
-    PSS_ATTR((k_g_emit<true, false>));
-    PSS_ATTR((k_g_emit<false, true>));
-    PSS_ATTR((k_g_emit<false, false>));
+    PSS_ATTR((k_g_emit<true, true, true, true>));
+    PSS_ATTR((k_g_emit<true, true, true, false>));
+    PSS_ATTR((k_g_emit<true, true, false, true>));
+    PSS_ATTR((k_g_emit<true, true, false, false>));
+    PSS_ATTR((k_g_emit<true, false, true, true>));
+    PSS_ATTR((k_g_emit<true, false, true, false>));
+    PSS_ATTR((k_g_emit<true, false, false, true>));
+    PSS_ATTR((k_g_emit<true, false, false, false>));
+    PSS_ATTR((k_g_emit<false, true, true, true>));
+    PSS_ATTR((k_g_emit<false, true, true, false>));
+    PSS_ATTR((k_g_emit<false, true, false, true>));
+    PSS_ATTR((k_g_emit<false, true, false, false>));
+    PSS_ATTR((k_g_emit<false, false, true, true>));
+    PSS_ATTR((k_g_emit<false, false, true, false>));
+    PSS_ATTR((k_g_emit<false, false, false, true>));
+    PSS_ATTR((k_g_emit<false, false, false, false>));
     PSS_ATTR(k_g_lastocc);
 #undef PSS_ATTR
     return e;

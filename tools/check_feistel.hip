@@ -11,7 +11,7 @@ __global__ void k_check(uint32_t h, uint32_t seed, uint32_t *bad) {
     const uint32_t base = (blockIdx.x * 64u + threadIdx.x) * 4u;
     uint32_t x[4], y[4];
     for (int c = 0; c < 4; c++) x[c] = (base + c) & (n - 1u);
-    feistel4_uniform(x, h, K, y);
+    if (h <= 8) feistel4_uniform<true>(x, h, K, y); else feistel4_uniform<false>(x, h, K, y);
     for (int c = 0; c < 4; c++) {
         const uint32_t z = feistel_once(x[c], h, K);
         if (y[c] != z) {
