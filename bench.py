@@ -51,10 +51,10 @@ WORKLOADS = {
 }
 
 
-def _pmc_traffic(symbols):
-    """HBM bytes per launch of the first kernel symbol found in profiles/pmc_traffic.json
-    (written by tools/pmc_summary.py from separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE
-    passes over this same bench), or None."""
+def _pmc_traffic(workload, symbols):
+    """HBM bytes per launch of the first kernel symbol found for this workload in
+    profiles/pmc_traffic.json (written by tools/pmc_summary.py from separate rocprofv3 --pmc
+    FETCH_SIZE / WRITE_SIZE passes over this same bench at N=1), or None."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(p) as f:
@@ -62,7 +62,7 @@ def _pmc_traffic(symbols):
     except (OSError, ValueError):
         return None
     for sym in symbols:
-        v = d.get(sym, {}).get("hbm_bytes_per_launch")
+        v = d.get(workload, {}).get(sym, {}).get("hbm_bytes_per_launch")
         if v is not None:
             return v
     return None
@@ -383,7 +383,7 @@ def main():
         units = RG * ns
         syms = ["k_v1_feistel"]
     achieved = units * BYTES_PER_ID / (per_launch_ms * 1e-3) / 1e9 if per_launch_ms > 0 else 0.0
-    traffic = _pmc_traffic(syms)
+    traffic = _pmc_traffic(args.workload, syms) if world == 1 else None
     desc = W.CONFIGS[cfg_name][0] + (" (V1 variant)" if args.workload == "c2v1" else "")
     line = {
         "metric": METRIC,

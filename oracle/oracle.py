@@ -68,6 +68,7 @@ def lib():
         L.orc_v1_philox_stream.restype = ctypes.c_int64
         L.orc_v2_philox_stream.argtypes = [ctypes.c_uint64, ctypes.c_uint32] + [ctypes.c_int64] * 5 + [I64P]
         L.orc_v2_philox_stream.restype = ctypes.c_int64
+        L.orc_v2_slots.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int64, ctypes.c_int64, U32P]
         L.orc_map.argtypes = [I64P, ctypes.c_int64, I64P, ctypes.c_int64, I32P, I64P]
         L.orc_digest.argtypes = [I64P, ctypes.c_int64]
         L.orc_digest.restype = ctypes.c_uint64
@@ -222,6 +223,12 @@ def v2_philox_stream(key64, rank, old_start, new_start, ns, B, N):
     out = np.empty(ns, dtype=np.int64)
     lib().orc_v2_philox_stream(key64, rank, old_start, new_start, ns, B, N, _p64(out))
     return out
+
+
+def v2_slots(key64, rank, P1, T):
+    out = np.empty(max(T, 1), dtype=np.uint32)
+    lib().orc_v2_slots(key64, rank, P1, T, _pu32(out))
+    return out[:T]
 
 
 def map_ids(prefix, ids):

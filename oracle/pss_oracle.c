@@ -284,7 +284,7 @@ uint64_t orc_epoch_key(uint64_t seed, int64_t epoch) {
 
 /* keyed bijection of [0,n): 6-round balanced Feistel on 2h bits + cycle walking.  Round
  * function: halves of h <= 8 bits -> top h bits of the low 16 bits of (R ^ k) * 0x9E37;
- * wider halves -> top h bits of the low 32 bits of ((R ^ k) mod 2^24) * 0x9E3779. */
+ * wider halves -> bits [24 - h, 24) of ((R ^ k) mod 2^24) * 0x9E3779. */
 uint32_t orc_feistel(uint32_t x, uint32_t n, const uint32_t rk[6]) {
     if (n <= 1) return 0;
     int bits = 0; while ((1ull << bits) < (uint64_t)n) bits++;
@@ -294,7 +294,7 @@ uint32_t orc_feistel(uint32_t x, uint32_t n, const uint32_t rk[6]) {
         uint32_t L = x >> h, R = x & mask;
         for (int i = 0; i < 6; i++) {
             uint32_t f = h <= 8 ? ((((R ^ rk[i]) * 0x9E37u) & 0xFFFFu) >> (16 - h))
-                                : ((((R ^ rk[i]) & 0xFFFFFFu) * 0x9E3779u) >> (32 - h));
+                                : (((((R ^ rk[i]) & 0xFFFFFFu) * 0x9E3779u) >> (24 - h)) & mask);
             uint32_t t = L ^ f;
             L = R; R = t;
         }
@@ -471,6 +471,15 @@ int64_t orc_v2_philox_stream(uint64_t key64, uint32_t rank, int64_t old_start,
     }
     free(buf);
     return ns;
+}
+
+/* the slot drawn at each step t < T of one rank's V2 stream (schedule-quality tests) */
+void orc_v2_slots(uint64_t key64, uint32_t rank, int64_t P1, int64_t T, uint32_t *out) {
+    uint32_t sk[4], skc[4] = {0, 0, rank, DOM_V2_SLOT};
+    orc_philox4x32(skc, key64, sk);
+    int grouped = P1 > ORC_LDS_SLOT_MAX;
+    for (int64_t t = 0; t < T; t++)
+        out[t] = grouped ? v2_slot_grouped(sk, t, (uint32_t)P1) : v2_slot(sk, t, (uint32_t)P1);
 }
 
 /* ------------------------------------------------------------------------------------ */

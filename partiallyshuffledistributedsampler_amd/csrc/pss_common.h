@@ -66,13 +66,17 @@ constexpr int kFeistelRounds = 6;
 
 // Round function for halves of h <= 8 bits (windows up to 65536): the top h bits of the low
 // 16 bits of (R ^ k) * 0x9E37 -- a 16-bit multiplicative hash, so two chains fit one 32-bit
-// register and run on packed 16-bit ops (feistel2_pk16).  Wider halves (h in 9..16): the top h
-// bits of the low 32 bits of ((R ^ k) mod 2^24) * 0x9E3779 -- a 24 x 24-bit product, which is
-// one full-rate v_mul_u32_u24 on gfx950 (a 32-bit v_mul_lo_u32 issues at quarter rate).
+// register and run on packed 16-bit ops (feistel2_pk16).  Wider halves (h in 9..16): bits
+// [24 - h, 24) of ((R ^ k) mod 2^24) * 0x9E3779 -- a 24 x 24-bit product (one full-rate
+// v_mul_u32_u24 on gfx950; a 32-bit v_mul_lo_u32 issues at quarter rate) and one v_bfe_u32.
+// The bits just below 2^24 are taken because there one input step moves the output by
+// 0x9E3779 / 2^(24-h), i.e. the golden-ratio fraction of the output range -- the top bits of
+// the 32-bit product would move by only ~2.5 at h = 10, and neighbouring positions then map
+// to neighbouring values (tests/test_schedule_quality.py measures both).
 constexpr uint32_t kFeistelM16 = 0x9E37u, kFeistelM24 = 0x9E3779u;
 
-PSS_HD uint32_t feistel_f24(uint32_t r, uint32_t k, uint32_t sh) {
-    return (((r ^ k) & 0xFFFFFFu) * kFeistelM24) >> sh;
+PSS_HD uint32_t feistel_f24(uint32_t r, uint32_t k, uint32_t h) {
+    return ((((r ^ k) & 0xFFFFFFu) * kFeistelM24) >> (24u - h)) & ((1u << h) - 1u);
 }
 
 PSS_HD uint32_t feistel_pass(uint32_t x, uint32_t h, const uint32_t *k) {
@@ -87,10 +91,9 @@ PSS_HD uint32_t feistel_pass(uint32_t x, uint32_t h, const uint32_t *k) {
             R = t;
         }
     } else {
-        const uint32_t sh = 32u - h;
 #pragma unroll
         for (int i = 0; i < kFeistelRounds; i++) {
-            const uint32_t t = L ^ feistel_f24(R, k[i], sh);
+            const uint32_t t = L ^ feistel_f24(R, k[i], h);
             L = R;
             R = t;
         }

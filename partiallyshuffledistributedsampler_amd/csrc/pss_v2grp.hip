@@ -188,7 +188,7 @@ __device__ __forceinline__ uint32_t xchg_unordered(uint32_t *buf, g_lds_vu8 *mar
 // Four one-pass Feistel chains under wave-uniform round keys K (a full window of 4^h elements).
 // h <= 8: packed 16-bit pairs (feistel4_pk16).  h > 8: the keyed-carry form of feistel_pass --
 // with A_i = R_i ^ K_i, A_{i+1} = A_{i-1} ^ F(A_i) ^ (K_{i-1} ^ K_{i+1}) (one 3-input xor per
-// round, F = one full-rate 24-bit multiply + shift); output L = A_5 ^ K_5, R = A_4 ^ F(A_5) ^ K_4.
+// round, F = one full-rate 24-bit multiply + bit-field extract); output L = A_5 ^ K_5, R = A_4 ^ F(A_5) ^ K_4.
 // Same values as feistel_once on each chain.
 template <bool PACKED>
 __device__ __forceinline__ void feistel4_uniform(const uint32_t x[4], uint32_t h, const uint32_t K[6],
@@ -199,9 +199,9 @@ __device__ __forceinline__ void feistel4_uniform(const uint32_t x[4], uint32_t h
         for (int i = 0; i < kFeistelRounds; i++) kp[i] = (K[i] & 0xFFFFu) * 0x10001u;
         feistel4_pk16(x, h, kp, y);
     } else {
-        const uint32_t mask = (1u << h) - 1u, sh = 32u - h;
+        const uint32_t mask = (1u << h) - 1u, sh = 24u - h;
         const uint32_t K02 = K[0] ^ K[2], K13 = K[1] ^ K[3], K24 = K[2] ^ K[4], K35 = K[3] ^ K[5];
-        auto F = [&](uint32_t a) -> uint32_t { return ((a & 0xFFFFFFu) * kFeistelM24) >> sh; };
+        auto F = [&](uint32_t a) -> uint32_t { return (((a & 0xFFFFFFu) * kFeistelM24) >> sh) & mask; };
 #pragma unroll
         for (int c = 0; c < 4; c++) {
             const uint32_t A0 = (x[c] & mask) ^ K[0];

@@ -235,3 +235,33 @@ def test_lazy_length_probes_follow_reference_scan(ver, order, device):
                 assert calls == er["probes"], (sc["name"], rrec["rank"], er["epoch"])
                 if order == "exact":
                     assert got == er["read_files"], (sc["name"], rrec["rank"], er["epoch"])
+
+
+@pytest.mark.gpu
+def test_device_error_flag_reaches_the_sampler():
+    """A kernel that flags the device error word (here: the partition kernel given too little
+    segment capacity) makes the drop-in raise at the next batch instead of serving ids from an
+    incomplete epoch (pss_error_snapshot), and pss_check reports it by code."""
+    import ctypes
+    import torch
+    from partiallyshuffledistributedsampler_amd import _lib
+    fx = load("v2_small")
+    s = make(fx, 0, 0)
+    s.set_epoch(0)
+    it = iter(s)
+    next(it)
+    eng = s._engine
+    seg_off = torch.zeros(eng.num_replicas + 1, dtype=torch.int64, device="cuda")
+    one = torch.zeros(1, dtype=torch.int64, device="cuda")
+    one32 = torch.zeros(1, dtype=torch.int32, device="cuda")
+    stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    _lib.call("pss_partition", eng._h, 0, eng.num_replicas, ctypes.c_void_p(seg_off.data_ptr()),
+              ctypes.c_void_p(one32.data_ptr()), ctypes.c_void_p(one.data_ptr()),
+              ctypes.c_void_p(one.data_ptr()), 1, stream)      # capacity 1: the flag is set
+    s.set_epoch(1)
+    it = iter(s)
+    with pytest.raises(RuntimeError, match="device error"):
+        next(it)
+    with pytest.raises(_lib.PSSError):
+        eng.check()
+    eng.check()                                   # pss_check cleared the word

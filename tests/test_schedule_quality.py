@@ -79,3 +79,78 @@ def test_v2_grouped_pool_law_matches_reference(B, ns):
     assert abs(dp.std() / dx.std() - 1) < 0.01
     assert abs(upp - upx) < 0.005
     assert abs(lagp - lagx) < 0.005
+
+
+# ---- randomness of the counter schedule's primitives ------------------------------------------
+def _chi2(counts):
+    counts = np.asarray(counts, dtype=np.float64).ravel()
+    exp = counts.sum() / counts.size
+    return ((counts - exp) ** 2 / exp).sum(), counts.size - 1
+
+
+def _chi2_ok(counts, z=5.0):
+    # chi-square with k dof against its normal approximation: mean k, sd sqrt(2k)
+    x, k = _chi2(counts)
+    return abs(x - k) < z * np.sqrt(2 * k), (x, k)
+
+
+@pytest.mark.parametrize("P1", [256, 4096, 100, 3000, 20000, 65536])
+def test_slot_draws_are_uniform_per_slot(P1):
+    """Every slot is drawn equally often (chi-square over the P1 slots), for paired power-of-two
+    pools, multiply-shift pools and both kinds of grouped pools (P1 > 16384)."""
+    T = 200 * P1 if P1 <= 4096 else 60 * P1
+    k = O.v2_slots(O.epoch_key(5, 1), 3, P1, T)
+    ok, stat = _chi2_ok(np.bincount(k, minlength=P1))
+    assert ok, stat
+
+
+@pytest.mark.parametrize("P1", [256, 4096, 65536])
+def test_paired_draws_are_independent(P1):
+    """Paired draws share one 32-bit hash (steps t and t + 64 in small pools, sub-steps u and
+    u + 64 of a group in grouped ones): the joint distribution of the two slots' top 4 bits is
+    uniform over the 256 cells, and so is that of consecutive steps."""
+    T = 4_000_000
+    k = O.v2_slots(O.epoch_key(9, 2), 0, P1, T).astype(np.int64)
+    hb = int(np.log2(P1 if P1 <= 16384 else 4096))
+    top = (k % (1 << hb)) >> (hb - 4)                    # slot inside the group, top 4 bits
+    if P1 <= 16384:
+        t = np.arange(T)
+        lo = t[(t % 128) < 64]
+        pairs = (lo, lo + 64)
+    else:
+        G = P1 // 4096
+        t = np.arange(T)
+        g, u = (t // 16) % G, (t // 16 // G) * 16 + t % 16
+        sel = (u % 128) < 64
+        partner = ((u + 64) // 16 * G + g) * 16 + (u + 64) % 16
+        ok_ = sel & (partner < T)
+        pairs = (t[ok_], partner[ok_])
+    for a, b in (pairs, (np.arange(T - 1), np.arange(1, T))):
+        joint = np.bincount(top[a] * 16 + top[b], minlength=256)
+        ok, stat = _chi2_ok(joint)
+        assert ok, stat
+
+
+@pytest.mark.parametrize("n", [1024, 4096, 65536, 1 << 20, 5000, 3 << 20])
+def test_feistel_insertion_order_is_uniform(n):
+    """The keyed Feistel bijections (16-bit round function for halves <= 8 bits, 24-bit one
+    above; cycle walking when n is not a power of 4): over many keys, the images of the first
+    positions are uniform over [0, n) (chi-square on 32 bins) and the images of two neighbours
+    are independent (chi-square on 8 x 8 bins).  (Below 1024 elements, halves of <= 5 bits,
+    the 16-bit rounds leave a small neighbour dependence: z ~ 3-6 at n = 256)"""
+    rng = np.random.default_rng(n)
+    keys = rng.integers(0, 2 ** 32, (4000, 6), dtype=np.uint64).astype(np.uint32)
+    y0 = np.array([O.feistel(0, n, k) for k in keys], dtype=np.int64)
+    y1 = np.array([O.feistel(1, n, k) for k in keys], dtype=np.int64)
+    y7 = np.array([O.feistel(7, n, k) for k in keys], dtype=np.int64)
+    for y in (y0, y1, y7):
+        ok, stat = _chi2_ok(np.bincount(y * 32 // n, minlength=32))
+        assert ok, stat
+    ok, stat = _chi2_ok(np.bincount((y0 * 8 // n) * 8 + y1 * 8 // n, minlength=64))
+    assert ok, stat
+    # one key: a permutation of [0, n) whose neighbouring images are uncorrelated
+    if n <= 65536:
+        perm = np.array([O.feistel(i, n, keys[0]) for i in range(n)], dtype=np.int64)
+        assert np.array_equal(np.sort(perm), np.arange(n))
+        assert abs(np.corrcoef(perm[:-1], perm[1:])[0, 1]) < 0.05
+        assert abs(np.corrcoef(np.arange(n), perm)[0, 1]) < 0.05

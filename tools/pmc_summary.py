@@ -1,7 +1,8 @@
 #!/usr/bin/env python
 """Summarise rocprofv3 --pmc passes into profiles/pmc_traffic.json (read by bench.py).
 
-Usage: python tools/pmc_summary.py OUT.json PASS_DIR [PASS_DIR ...]
+Usage: python tools/pmc_summary.py OUT.json WORKLOAD PASS_DIR [PASS_DIR ...]
+(merges the workload's entry into OUT.json: {workload: {kernel: ...}}, the bench.py workload names)
 
 Each PASS_DIR holds one rocprofv3 counter-collection run (csv output).  Per kernel we average
 the counters over its dispatches and convert them to HBM bytes per launch the way
@@ -38,7 +39,7 @@ def load(pass_dir):
 
 
 def main():
-    out, dirs = sys.argv[1], sys.argv[2:]
+    out, workload, dirs = sys.argv[1], sys.argv[2], sys.argv[3:]
     merged = defaultdict(dict)
     for d in dirs:
         for k, ctrs in load(d).items():
@@ -53,8 +54,14 @@ def main():
         res[k] = {"counters_per_launch": c, "hbm_bytes_per_launch": hbm,
                   "write_bytes_per_launch": ws * 1024.0 if ws is not None else None,
                   "fetch_bytes_per_launch_corrected": 2.0 * fs * 1024.0 if fs is not None else None}
+    try:
+        with open(out) as f:
+            allres = json.load(f)
+    except (OSError, ValueError):
+        allres = {}
+    allres[workload] = {k: v for k, v in res.items() if k.startswith("k_")}
     with open(out, "w") as f:
-        json.dump(res, f, indent=1, sort_keys=True)
+        json.dump(allres, f, indent=1, sort_keys=True)
     for k, v in sorted(res.items()):
         print(k, v["hbm_bytes_per_launch"], v["counters_per_launch"])
 
