@@ -289,6 +289,40 @@ def sampler_data_path(device, reps=3):
                       "int64 offset) per id"}
 
 
+def handoff_figures(device, reps=5):
+    """The fused hand-off at C2 (all 8 logical ranks, 100M positions): pss_generate_mapped ->
+    (int32 file, int32 offset) per position in HBM -- V1 fused into the generation kernel, V2
+    generation + bucket-indexed map; and the standalone map of 100M int64 ids."""
+    lengths, N, R, B, _ = W.shape("c2")
+    out = {}
+    for ver in (1, 2):
+        eng = IndexEngine(lengths, N, R, B, ver, seed=0, device=device)
+        eng.init_iter(0)
+        eng.generate_mapped(0, R)
+        torch.cuda.synchronize(device)
+        t0 = time.perf_counter()
+        for e in range(reps):
+            eng.init_iter(1 + e)
+            eng.generate_mapped(0, R)
+        torch.cuda.synchronize(device)
+        ms = (time.perf_counter() - t0) / reps * 1e3
+        out["v%d_mapped" % ver] = {"ms_per_epoch": ms, "G_pos_per_s": R * eng.num_samples / ms / 1e6}
+        if ver == 2:
+            ids = eng.generate(0, R)
+            fp, off = eng.map(ids.view(-1))
+            torch.cuda.synchronize(device)
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                eng.map(ids.view(-1), fp, off)
+            torch.cuda.synchronize(device)
+            ms = (time.perf_counter() - t0) / reps * 1e3
+            out["map_100M_ids_ms"] = ms
+            del ids, fp, off
+        eng.close()
+    out["config"] = "C2, 8 logical ranks x 12.5M positions -> (int32 file_pos, int32 offset)"
+    return out
+
+
 # ---- main ------------------------------------------------------------------------------------
 def main():
     ap = argparse.ArgumentParser()
@@ -421,6 +455,7 @@ def main():
     if rank == 0 and not args.no_latency:
         line["latency"] = latency_dropin(local)
         line["sampler_data_path"] = sampler_data_path(local)
+        line["handoff"] = handoff_figures(local)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -85,6 +85,23 @@ int pss_generate(pss_sampler *h, int32_t rank_lo, int32_t rank_hi, int64_t pos_l
 int pss_map(pss_sampler *h, const int64_t *ids_dev, int64_t n, int32_t *file_pos_dev,
             int64_t *offset_dev, void *stream);
 
+/* Fused hand-off: the positions of pss_generate delivered directly as
+ * (int32 file position in the shuffled order, int32 offset) -- 8 bytes per id, the form the
+ * reader and an on-GPU gather consume (V1:181-221).  Same layout as pss_generate
+ * ([r - rank_lo][pos - pos_lo]) and the same reflection flag as pss_map.  V1 (counter order):
+ * one kernel, each id mapped where it is computed; V2: generation into handle scratch, then
+ * the bucket-indexed map.  PSS_ENOTSUP if a file holds 2^31 samples or more. */
+int pss_generate_mapped(pss_sampler *h, int32_t rank_lo, int32_t rank_hi, int64_t pos_lo,
+                        int64_t count, int32_t *file_pos_dev, int32_t *offset_dev, void *stream);
+
+/* On-GPU gather of rows of device-resident files (V1:243-248): out_dev[i] = the row_bytes-byte
+ * row base_rows_dev[f] + offset_dev[i] of data_dev, f = the dataset-order index of shuffled file
+ * position file_pos_dev[i] (reflected ids, file_pos < 0, read file -1 - file_pos).  base_rows_dev
+ * has one entry per dataset file: its first row in data_dev.  Uses the current epoch's order. */
+int pss_gather(pss_sampler *h, const void *data_dev, int64_t row_bytes, const int64_t *base_rows_dev,
+               const int32_t *file_pos_dev, const int32_t *offset_dev, int64_t n, void *out_dev,
+               void *stream);
+
 /* File -> rank partition: for ranks [rank_lo, rank_hi), the (file position, lo, hi) segments
  * their epoch reads, in stream order of the id ranges.  seg_off_dev[0..n] is always written
  * (exclusive offsets); segments only when seg_cap >= seg_off_dev[n]. */

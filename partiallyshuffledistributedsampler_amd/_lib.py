@@ -48,6 +48,8 @@ SIGNATURES = {
     "pss_device": ([_vp, _c_i32p], ctypes.c_int),
     "pss_error_snapshot": ([_vp, _vp, _vp], ctypes.c_int),
     "pss_map_prefix_host": ([_vp, _i64, _vp, _i64, _vp, _vp], ctypes.c_int),
+    "pss_generate_mapped": ([_vp, _i32, _i32, _i64, _i64, _vp, _vp, _vp], ctypes.c_int),
+    "pss_gather": ([_vp, _vp, _i64, _vp, _vp, _vp, _i64, _vp, _vp], ctypes.c_int),
 }
 
 _lib = None

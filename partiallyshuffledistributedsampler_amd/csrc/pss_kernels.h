@@ -76,17 +76,36 @@ hipError_t launch_partition(const Geometry &g, const RankDesc *ranks, int32_t ra
                             int32_t *seg_file, int64_t *seg_lo, int64_t *seg_hi,
                             int64_t seg_cap, int32_t *err, hipStream_t s);
 
-hipError_t launch_map(const int64_t *prefix, int64_t F, const int64_t *ids, int64_t n,
-                      int32_t *fpos, int64_t *off, hipStream_t s);
+// bucket index of the prefix (pss_map.h map_one_bucketed), then the map itself: int64 offsets
+// into `off`, or int32 ones into `off32` when that is non-null
+hipError_t launch_bucket_index(const int64_t *prefix, int64_t F, int32_t kb, int64_t nb, int32_t *BT,
+                               hipStream_t s);
+hipError_t launch_map(const int64_t *prefix, int64_t F, const int32_t *BT, int32_t kb, int64_t nb,
+                      const int64_t *ids, int64_t n, int32_t *fpos, int64_t *off, int32_t *off32,
+                      hipStream_t s);
+// rows of device-resident files: out[i] = data row base[order[|f_i|]] + off_i
+hipError_t launch_gather(const void *data, int64_t row_bytes, const int64_t *base, const int32_t *order,
+                         const int32_t *fpos, const int32_t *off, int64_t n, void *out, hipStream_t s);
 
 hipError_t launch_digest(const int64_t *ids, int64_t n, uint64_t *acc, hipStream_t s);
 hipError_t launch_digest_range(int64_t lo, int64_t hi, uint64_t *acc, hipStream_t s);
 
+// the epoch's prefix + bucket index, and (int32 file, int32 offset) outputs of a mapped launch
+struct MapArgs {
+    const int64_t *prefix;
+    int64_t F;
+    const int32_t *BT;
+    int32_t kb;
+    int64_t nb;
+    int32_t *fpos, *off;
+};
+
 // V1: ids of positions [pos_lo, pos_lo+count) of ranks [rank_lo, rank_lo+nr) -> out[r][count];
-// each window ordered by its keyed Feistel bijection (key table of the windows in key_ws)
+// each window ordered by its keyed Feistel bijection (key table of the windows in key_ws).
+// mapped != nullptr: (file position, offset) into mapped->fpos / off instead (out unused)
 hipError_t launch_v1(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, int32_t nr,
                      int64_t pos_lo, int64_t count, int64_t *out, uint32_t *key_ws,
-                     hipStream_t s, const Marker &mk = Marker());
+                     hipStream_t s, const Marker &mk = Marker(), const MapArgs *mapped = nullptr);
 size_t v1_workspace_bytes(const Geometry &g, int32_t nr, int64_t pos_lo, int64_t count);
 
 // V1 in the reference's exact order (CPython MT19937 per window, pss_v1exact.hip): windows up

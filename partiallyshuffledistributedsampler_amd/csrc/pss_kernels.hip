@@ -137,12 +137,43 @@ __global__ void k_part_emit(Geometry g, const RankDesc *ranks, int32_t rank_lo, 
 // id -> (file position, offset) over the shuffled order (V1:181-221).  Ids at or past the
 // scanned total are reflected exactly as V1:191-196 does; the host moves those to the end of
 // their batch (they are flagged by a negative file position: fpos = -1 - f).
-__global__ void k_map(const int64_t *__restrict__ prefix, int64_t F,
-                      const int64_t *__restrict__ ids, int64_t n, int32_t *__restrict__ fpos,
-                      int64_t *__restrict__ off) {
+__global__ void k_bucket_index(const int64_t *__restrict__ prefix, int64_t F, int32_t kb, int64_t nb,
+                               int32_t *__restrict__ BT) {
+    for (int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; b < nb;
+         b += (int64_t)gridDim.x * blockDim.x)
+        BT[b] = (int32_t)file_of(prefix, F, b << kb);
+}
+
+template <typename OFF>
+__global__ void k_map(const int64_t *__restrict__ prefix, int64_t F, const int32_t *__restrict__ BT,
+                      int32_t kb, int64_t nb, const int64_t *__restrict__ ids, int64_t n,
+                      int32_t *__restrict__ fpos, OFF *__restrict__ off) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
-         i += (int64_t)gridDim.x * blockDim.x)
-        map_one(prefix, F, ids[i], fpos[i], off[i]);
+         i += (int64_t)gridDim.x * blockDim.x) {
+        int32_t f;
+        int64_t o;
+        map_one_bucketed(prefix, F, BT, kb, nb, ids[i], f, o);
+        fpos[i] = f;
+        off[i] = (OFF)o;
+    }
+}
+
+// Rows of device-resident files: out[i] = data[base[order[f_i]] + off_i] (row_bytes each), the
+// on-GPU form of the reference's per-file fancy-index gather (V1:243-248).  `base` gives each
+// file's first row in the data tensor, files in dataset order; reflected ids (f < 0) read
+// file -1 - f.  One 16-, 4- or 1-byte word per thread.
+template <typename W>
+__global__ void k_gather(const W *__restrict__ data, int64_t row_words, const int64_t *__restrict__ base,
+                         const int32_t *__restrict__ order, const int32_t *__restrict__ fpos,
+                         const int32_t *__restrict__ off, int64_t n, W *__restrict__ out) {
+    const int64_t total = n * row_words;
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < total;
+         k += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t i = k / row_words, w = k - i * row_words;
+        const int32_t f = fpos[i] < 0 ? -1 - fpos[i] : fpos[i];
+        const int64_t row = base[order[f]] + off[i];
+        out[k] = data[row * row_words + w];
+    }
 }
 
 __global__ void k_digest(const int64_t *__restrict__ ids, int64_t n, uint64_t *acc) {
@@ -198,12 +229,14 @@ struct V1Plan {
 };
 
 // One wave per (rank, run of per_wave super-blocks).  Lane l computes positions p0 + 64 j + l,
-// j < 4, of each 256-position super-block p0.
-template <bool PACKED>
+// j < 4, of each 256-position super-block p0.  MAPPED: instead of the int64 id, the id's
+// (int32 file position, int32 offset) through the epoch's bucket index (MapArgs) -- the fused
+// form of pss_map, same 8 bytes per position.
+template <bool PACKED, bool MAPPED>
 __global__ __launch_bounds__(64) void k_v1_feistel(Geometry g, V1Plan vp, const RankDesc *__restrict__ ranks,
                                                    int32_t rank_lo, const uint32_t *__restrict__ kt,
                                                    int64_t pos_lo, int64_t count,
-                                                   int64_t *__restrict__ out) {
+                                                   int64_t *__restrict__ out, MapArgs ma) {
     const int lane = threadIdx.x;
     const int64_t waves_per_rank = (vp.nsb + vp.per_wave - 1) / vp.per_wave;
     const int32_t rl = (int32_t)(blockIdx.x / waves_per_rank);
@@ -212,6 +245,19 @@ __global__ __launch_bounds__(64) void k_v1_feistel(Geometry g, V1Plan vp, const 
     const int64_t start = ranks[rank_lo + rl].new_start;
     const int64_t pos_hi = pos_lo + count < g.ns ? pos_lo + count : g.ns;
     int64_t *o = out + (int64_t)rl * count - pos_lo;
+    int32_t *ofp = ma.fpos + (int64_t)rl * count - pos_lo;
+    int32_t *ooff = ma.off + (int64_t)rl * count - pos_lo;
+    auto put = [&](int64_t p, int64_t id) {
+        if constexpr (MAPPED) {
+            int32_t f;
+            int64_t of;
+            map_one_bucketed(ma.prefix, ma.F, ma.BT, ma.kb, ma.nb, id, f, of);
+            ofp[p] = f;
+            ooff[p] = (int32_t)of;
+        } else {
+            o[p] = id;
+        }
+    };
     const uint32_t *ktr = kt + (int64_t)rl * vp.nw * kRoundKeyWords;
     const int64_t B = vp.B;
     for (int64_t sb = sb0; sb < sb1; sb++) {
@@ -240,9 +286,8 @@ __global__ __launch_bounds__(64) void k_v1_feistel(Geometry g, V1Plan vp, const 
 #pragma unroll
                 for (int j = 0; j < 4; j++) y[j] = feistel_once(x0 + 64u * j + lane, vp.hB, kk);
             }
-            int64_t *ob = o + p0;
 #pragma unroll
-            for (int j = 0; j < 4; j++) ob[64 * j + lane] = wrap_id(base + y[j], g.N);
+            for (int j = 0; j < 4; j++) put(p0 + 64 * j + lane, wrap_id(base + y[j], g.N));
             continue;
         }
 #pragma unroll
@@ -260,7 +305,7 @@ __global__ __launch_bounds__(64) void k_v1_feistel(Geometry g, V1Plan vp, const 
                 y = wp * B + feistel((uint32_t)(p - wp * B), (uint32_t)len,
                                      feistel_half_bits((uint32_t)len), kk);
             }
-            o[p] = wrap_id(start + y, g.N);
+            put(p, wrap_id(start + y, g.N));
         }
     }
 }
@@ -319,10 +364,39 @@ static inline int grid_for(int64_t n, int bs) {
     return (int)b;
 }
 
-hipError_t launch_map(const int64_t *prefix, int64_t F, const int64_t *ids, int64_t n,
-                      int32_t *fpos, int64_t *off, hipStream_t s) {
+hipError_t launch_bucket_index(const int64_t *prefix, int64_t F, int32_t kb, int64_t nb, int32_t *BT,
+                               hipStream_t s) {
+    hipLaunchKernelGGL(k_bucket_index, dim3(grid_for(nb, 256)), dim3(256), 0, s, prefix, F, kb, nb, BT);
+    return hipGetLastError();
+}
+
+hipError_t launch_map(const int64_t *prefix, int64_t F, const int32_t *BT, int32_t kb, int64_t nb,
+                      const int64_t *ids, int64_t n, int32_t *fpos, int64_t *off, int32_t *off32,
+                      hipStream_t s) {
     if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_map, dim3(grid_for(n, 256)), dim3(256), 0, s, prefix, F, ids, n, fpos, off);
+    if (off32)
+        hipLaunchKernelGGL(k_map<int32_t>, dim3(grid_for(n, 256)), dim3(256), 0, s, prefix, F, BT, kb, nb,
+                           ids, n, fpos, off32);
+    else
+        hipLaunchKernelGGL(k_map<int64_t>, dim3(grid_for(n, 256)), dim3(256), 0, s, prefix, F, BT, kb, nb,
+                           ids, n, fpos, off);
+    return hipGetLastError();
+}
+
+hipError_t launch_gather(const void *data, int64_t row_bytes, const int64_t *base, const int32_t *order,
+                         const int32_t *fpos, const int32_t *off, int64_t n, void *out, hipStream_t s) {
+    if (n <= 0 || row_bytes <= 0) return hipSuccess;
+    const bool a16 = row_bytes % 16 == 0 && ((uintptr_t)data % 16) == 0 && ((uintptr_t)out % 16) == 0;
+    const bool a4 = row_bytes % 4 == 0 && ((uintptr_t)data % 4) == 0 && ((uintptr_t)out % 4) == 0;
+    if (a16)
+        hipLaunchKernelGGL(k_gather<uint4>, dim3(grid_for(n * (row_bytes / 16), 256)), dim3(256), 0, s,
+                           (const uint4 *)data, row_bytes / 16, base, order, fpos, off, n, (uint4 *)out);
+    else if (a4)
+        hipLaunchKernelGGL(k_gather<uint32_t>, dim3(grid_for(n * (row_bytes / 4), 256)), dim3(256), 0, s,
+                           (const uint32_t *)data, row_bytes / 4, base, order, fpos, off, n, (uint32_t *)out);
+    else
+        hipLaunchKernelGGL(k_gather<uint8_t>, dim3(grid_for(n * row_bytes, 256)), dim3(256), 0, s,
+                           (const uint8_t *)data, row_bytes, base, order, fpos, off, n, (uint8_t *)out);
     return hipGetLastError();
 }
 
@@ -361,7 +435,7 @@ size_t v1_workspace_bytes(const Geometry &g, int32_t nr, int64_t pos_lo, int64_t
 
 hipError_t launch_v1(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, int32_t nr,
                      int64_t pos_lo, int64_t count, int64_t *out, uint32_t *key_ws,
-                     hipStream_t s, const Marker &mk) {
+                     hipStream_t s, const Marker &mk, const MapArgs *mapped) {
     int64_t w_lo, nw;
     if (nr <= 0 || !v1_window_range(g, pos_lo, count, w_lo, nw)) return hipSuccess;
     const int64_t pos_hi = pos_lo + count < g.ns ? pos_lo + count : g.ns;
@@ -385,12 +459,14 @@ hipError_t launch_v1(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, 
     while (per > 1 && total / per < 8 * 256) per >>= 1;
     vp.per_wave = per;
     const int64_t waves = (int64_t)nr * cdiv(vp.nsb, per);
-    if (vp.hB <= 8)
-        hipLaunchKernelGGL((k_v1_feistel<true>), dim3((uint32_t)waves), dim3(64), 0, s, g, vp, ranks,
-                           rank_lo, (const uint32_t *)key_ws, pos_lo, count, out);
-    else
-        hipLaunchKernelGGL((k_v1_feistel<false>), dim3((uint32_t)waves), dim3(64), 0, s, g, vp, ranks,
-                           rank_lo, (const uint32_t *)key_ws, pos_lo, count, out);
+    const MapArgs ma = mapped ? *mapped : MapArgs{};
+#define PSS_V1(PK, MP) hipLaunchKernelGGL((k_v1_feistel<PK, MP>), dim3((uint32_t)waves), dim3(64), 0, s, g, vp, \
+                                          ranks, rank_lo, (const uint32_t *)key_ws, pos_lo, count, out, ma)
+    if (vp.hB <= 8 && mapped) PSS_V1(true, true);
+    else if (vp.hB <= 8) PSS_V1(true, false);
+    else if (mapped) PSS_V1(false, true);
+    else PSS_V1(false, false);
+#undef PSS_V1
     mk(-1, s);
     return hipGetLastError();
 }

@@ -63,4 +63,37 @@ PSS_HD void map_one(const int64_t *prefix, int64_t F, int64_t id0, int32_t &fpos
     off = id - prefix[f];
 }
 
+// Bucket index of the epoch's prefix (pss_kernels.hip k_bucket_index): BT[b] = file_of(b << kb),
+// one bucket per ~average file length, so an id's file is found between BT[b] and BT[b + 1]
+// -- usually one or two probes instead of a binary search over all F files.
+PSS_HD int32_t bucket_shift(int64_t total, int64_t F) {
+    int64_t avg = F > 0 ? total / F : 1;
+    int32_t kb = 0;
+    while (((int64_t)2 << kb) <= avg && kb < 40) kb++;
+    return kb;
+}
+PSS_HD int64_t bucket_count(int64_t total, int32_t kb) { return (total >> kb) + 2; }
+
+PSS_HD void map_one_bucketed(const int64_t *prefix, int64_t F, const int32_t *BT, int32_t kb,
+                             int64_t nb, int64_t id0, int32_t &fpos, int64_t &off) {
+    const int64_t T = prefix[F];
+    int64_t id = id0;
+    bool refl = false;
+    if (id >= T) {
+        id = 2 * T - id;
+        if (id == T) id = T - 1;
+        refl = true;
+    }
+    if (id < 0) { fpos = INT32_MIN; off = id0; return; }
+    const int64_t b = id >> kb;
+    int64_t lo = BT[b];
+    int64_t hi = b + 1 < nb ? (int64_t)BT[b + 1] : F - 1;   // answer in [lo, hi]
+    while (hi > lo) {                                        // largest f with prefix[f] <= id
+        const int64_t mid = (lo + hi + 1) >> 1;
+        if (prefix[mid] <= id) lo = mid; else hi = mid - 1;
+    }
+    fpos = refl ? (int32_t)(-1 - lo) : (int32_t)lo;
+    off = id - prefix[lo];
+}
+
 }  // namespace pss

@@ -22,6 +22,7 @@
 #include "pss_kernels.h"
 #include "pss_host_mt.h"
 #include "pss_cpu.h"
+#include "pss_map.h"
 
 using pss::CPythonMT;
 
@@ -181,7 +182,11 @@ struct pss_sampler {
     bool dirty = true;            // rank descriptors of the epoch not on the device yet
     bool order_dirty = true;      // file order not uploaded (only map / partition need it)
     bool prefix_dirty = true;     // prefix scan owed (run lazily by map / partition)
-    DevBuf<int64_t> d_lens, d_prefix;
+    DevBuf<int64_t> d_lens, d_prefix, d_ids;   // d_ids: scratch ids of pss_generate_mapped
+    DevBuf<int32_t> d_bucket;     // bucket index of the prefix (pss_map.h), kb / nb below
+    int32_t kb = 0;
+    int64_t nb = 0, max_len = 0;
+    hipEvent_t ids_free = nullptr;   // last reader of d_ids
     DevBuf<int32_t> d_order, d_err;
     DevBuf<pss::RankDesc> d_ranks;
     DevBuf<uint32_t> d_val, d_buf, d_sort;
@@ -262,6 +267,7 @@ int ensure_device(pss_sampler *h) {
     PSS_HIP(h->d_prefix.ensure((size_t)h->F + 1 + pss::scan_scratch_words(h->F)));
     PSS_HIP(h->d_ranks.ensure((size_t)h->R));
     PSS_HIP(h->d_err.ensure(1));
+    PSS_HIP(h->d_bucket.ensure((size_t)h->nb));
     PSS_HIP(hipMemset(h->d_err.p, 0, sizeof(int32_t)));
     if (h->F) PSS_HIP(hipMemcpy(h->d_lens.p, h->files_len.data(), sizeof(int64_t) * h->F, hipMemcpyHostToDevice));
     PSS_HIP(hipHostMalloc((void **)&h->h_stage_order, sizeof(int32_t) * (h->F ? h->F : 1)));
@@ -314,6 +320,7 @@ int prepare_prefix(pss_sampler *h, hipStream_t s) {
     mk(pss::K_SCAN, s);
     PSS_HIP(pss::launch_scan_prefix(h->d_lens.p, h->d_order.p, h->F, h->d_prefix.p,
                                     (uint64_t *)(h->d_prefix.p + h->F + 1), s));
+    PSS_HIP(pss::launch_bucket_index(h->d_prefix.p, h->F, h->kb, h->nb, h->d_bucket.p, s));
     mk(-1, s);
     h->prefix_dirty = false;
     return PSS_OK;
@@ -360,8 +367,14 @@ int pss_create(const int64_t *files_len, int64_t num_files, int64_t total_size,
     if (total_size <= 0) return fail(PSS_EINVAL, "total_size must be positive");
     pss_sampler *h = new pss_sampler();
     h->files_len.assign(files_len, files_len + num_files);
-    for (int64_t v : h->files_len)
+    int64_t scanned = 0;
+    for (int64_t v : h->files_len) {
         if (v < 0) { delete h; return fail(PSS_EINVAL, "negative file length"); }
+        scanned += v;
+        if (v > h->max_len) h->max_len = v;
+    }
+    h->kb = pss::bucket_shift(scanned, num_files);
+    h->nb = pss::bucket_count(scanned, h->kb);
     h->F = num_files;
     h->N = total_size;
     h->R = num_replicas;
@@ -394,6 +407,8 @@ int pss_destroy(pss_sampler *h) {
         if (h->side) (void)hipStreamSynchronize(h->side);   // a lookahead still writing VAL
         h->d_lens.release(); h->d_prefix.release(); h->d_order.release(); h->d_err.release();
         h->d_ranks.release(); h->d_val.release(); h->d_buf.release(); h->d_sort.release();
+        h->d_bucket.release(); h->d_ids.release();
+        if (h->ids_free) (void)hipEventDestroy(h->ids_free);
         if (h->h_stage_order) (void)hipHostFree(h->h_stage_order);
         if (h->h_stage_ranks) (void)hipHostFree(h->h_stage_ranks);
         if (h->upload_done) (void)hipEventDestroy(h->upload_done);
@@ -742,7 +757,96 @@ int pss_map(pss_sampler *h, const int64_t *ids_dev, int64_t n, int32_t *file_pos
     hipStream_t s = (hipStream_t)stream;
     int rc = prepare_prefix(h, s);
     if (rc) return rc;
-    PSS_HIP(pss::launch_map(h->d_prefix.p, h->F, ids_dev, n, file_pos_dev, offset_dev, s));
+    PSS_HIP(pss::launch_map(h->d_prefix.p, h->F, h->d_bucket.p, h->kb, h->nb, ids_dev, n, file_pos_dev,
+                            offset_dev, nullptr, s));
+    return PSS_OK;
+}
+
+int pss_generate_mapped(pss_sampler *h, int32_t rank_lo, int32_t rank_hi, int64_t pos_lo,
+                        int64_t count, int32_t *file_pos_dev, int32_t *offset_dev, void *stream) {
+    if (!h) return fail(PSS_EINVAL, "NULL handle");
+    if (rank_lo < 0 || rank_hi > h->R || rank_lo > rank_hi) return fail(PSS_EINVAL, "bad rank range");
+    if (pos_lo < 0 || count < 0) return fail(PSS_EINVAL, "bad position range");
+    if (count > 0 && rank_hi > rank_lo && (!file_pos_dev || !offset_dev)) return fail(PSS_EINVAL, "NULL output");
+    if (h->F == 0) return fail(PSS_ESTATE, "no files to map into");
+    if (h->max_len > (int64_t)INT32_MAX) return fail(PSS_ENOTSUP, "a file longer than 2^31-1 samples (int32 offsets)");
+    const int32_t nr = rank_hi - rank_lo;
+    if (nr == 0 || count == 0 || pos_lo >= h->ns) return PSS_OK;
+    const size_t n = (size_t)nr * (size_t)count;
+    if (h->cpu) {
+        const int rc = cpu_prefix(h);
+        if (rc) return rc;
+        std::vector<int64_t> ids(n, 0), off(n);
+        int rc2 = pss_generate(h, rank_lo, rank_hi, pos_lo, count, ids.data(), nullptr);
+        if (rc2) return rc2;
+        const int64_t valid = std::min(count, h->ns - pos_lo);
+        CpuTimer tm{h, pss::K_MAP};
+        for (int32_t r = 0; r < nr; r++) {
+            const size_t o = (size_t)r * count;
+            pss::cpu::map(h->h_prefix.data(), h->F, ids.data() + o, valid, file_pos_dev + o, off.data() + o);
+            for (int64_t i = 0; i < valid; i++) offset_dev[o + i] = (int32_t)off[o + i];
+        }
+        return PSS_OK;
+    }
+    DeviceGuard dg(h->device);
+    hipStream_t s = (hipStream_t)stream;
+    int rc = prepare_prefix(h, s);
+    if (rc) return rc;
+    const pss::Geometry g = h->geometry();
+    const pss::Marker mk = marker_of(h);
+    if (h->version == 1 && h->order_mode == PSS_ORDER_COUNTER) {
+        // fused: the V1 kernel maps each id as it computes it
+        auto words = [](size_t bytes) { return (bytes + sizeof(uint32_t) - 1) / sizeof(uint32_t); };
+        const size_t sb = pss::v1_workspace_bytes(g, nr, pos_lo, count);
+        if (sb) PSS_HIP(h->d_sort.ensure(words(sb)));
+        pss::MapArgs ma{h->d_prefix.p, h->F, h->d_bucket.p, h->kb, h->nb, file_pos_dev, offset_dev};
+        PSS_HIP(pss::launch_v1(g, h->d_ranks.p, rank_lo, nr, pos_lo, count, nullptr, h->d_sort.p, s, mk, &ma));
+        return PSS_OK;
+    }
+    // V2 (and the exact orders): ids into the handle's scratch, then the bucket map
+    if (!h->ids_free) PSS_HIP(hipEventCreateWithFlags(&h->ids_free, hipEventDisableTiming));
+    if (h->d_ids.n < n) {
+        PSS_HIP(hipEventSynchronize(h->ids_free));
+        PSS_HIP(h->d_ids.ensure(n));
+    }
+    PSS_HIP(hipStreamWaitEvent(s, h->ids_free, 0));
+    rc = pss_generate(h, rank_lo, rank_hi, pos_lo, count, h->d_ids.p, stream);
+    if (rc) return rc;
+    const int64_t valid = std::min(count, h->ns - pos_lo);
+    mk(pss::K_MAP, s);
+    for (int32_t r = 0; r < nr; r++) {
+        const size_t o = (size_t)r * count;
+        PSS_HIP(pss::launch_map(h->d_prefix.p, h->F, h->d_bucket.p, h->kb, h->nb, h->d_ids.p + o, valid,
+                                file_pos_dev + o, nullptr, offset_dev + o, s));
+    }
+    mk(-1, s);
+    PSS_HIP(hipEventRecord(h->ids_free, s));
+    return PSS_OK;
+}
+
+int pss_gather(pss_sampler *h, const void *data_dev, int64_t row_bytes, const int64_t *base_rows_dev,
+               const int32_t *file_pos_dev, const int32_t *offset_dev, int64_t n, void *out_dev,
+               void *stream) {
+    if (!h) return fail(PSS_EINVAL, "NULL handle");
+    if (n < 0 || row_bytes < 0 || (n > 0 && (!data_dev || !base_rows_dev || !file_pos_dev || !offset_dev || !out_dev)))
+        return fail(PSS_EINVAL, "bad arguments");
+    if (n == 0 || row_bytes == 0) return PSS_OK;
+    if (h->cpu) {
+        const char *d = (const char *)data_dev;
+        char *o = (char *)out_dev;
+        for (int64_t i = 0; i < n; i++) {
+            const int32_t f = file_pos_dev[i] < 0 ? -1 - file_pos_dev[i] : file_pos_dev[i];
+            const int64_t row = base_rows_dev[h->order[f]] + offset_dev[i];
+            std::memcpy(o + i * row_bytes, d + row * row_bytes, (size_t)row_bytes);
+        }
+        return PSS_OK;
+    }
+    DeviceGuard dg(h->device);
+    hipStream_t s = (hipStream_t)stream;
+    const int rc = prepare_order(h, s);
+    if (rc) return rc;
+    PSS_HIP(pss::launch_gather(data_dev, row_bytes, base_rows_dev, h->d_order.p, file_pos_dev, offset_dev, n,
+                               out_dev, s));
     return PSS_OK;
 }
 

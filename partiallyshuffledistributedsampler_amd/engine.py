@@ -136,6 +136,40 @@ class IndexEngine:
                   _stream_ptr(stream, d))
         return fpos, off
 
+    def generate_mapped(self, rank_lo, rank_hi, pos_lo=0, count=None, stream=None):
+        """(file_pos, offset) int32 tensors [ranks, count] of positions [pos_lo, pos_lo+count):
+        the fused hand-off (pss_generate_mapped) -- 8 bytes per id, no int64 id pass."""
+        d = self._dev()
+        if count is None:
+            count = self.num_samples - pos_lo
+        count = max(0, int(count))
+        nr = rank_hi - rank_lo
+        fpos = torch.empty((nr, count), dtype=torch.int32, device=d)
+        off = torch.empty((nr, count), dtype=torch.int32, device=d)
+        _lib.call("pss_generate_mapped", self._h, int(rank_lo), int(rank_hi), int(pos_lo), count,
+                  ctypes.c_void_p(fpos.data_ptr()), ctypes.c_void_p(off.data_ptr()),
+                  _stream_ptr(stream, d))
+        return fpos, off
+
+    def gather(self, data, base_rows, fpos, off, out=None, stream=None):
+        """Rows of device-resident files (pss_gather): data [rows, ...] holds every dataset file's
+        samples, file f starting at row base_rows[f] (dataset order); returns data rows of the
+        (file_pos, offset) pairs, in their order (the on-GPU form of V1:243-248)."""
+        d = self._dev()
+        fpos = fpos.reshape(-1).contiguous()
+        off = off.reshape(-1).to(torch.int32).contiguous()
+        base_rows = base_rows.to(device=d, dtype=torch.int64).contiguous()
+        assert data.device == d and data.is_contiguous() and fpos.device == d
+        n = fpos.numel()
+        row_bytes = data[0].numel() * data.element_size() if data.dim() > 0 and data.shape[0] else 0
+        if out is None:
+            out = torch.empty((n,) + tuple(data.shape[1:]), dtype=data.dtype, device=d)
+        _lib.call("pss_gather", self._h, ctypes.c_void_p(data.data_ptr()), row_bytes,
+                  ctypes.c_void_p(base_rows.data_ptr()), ctypes.c_void_p(fpos.data_ptr()),
+                  ctypes.c_void_p(off.data_ptr()), n, ctypes.c_void_p(out.data_ptr()),
+                  _stream_ptr(stream, d))
+        return out
+
     def partition(self, rank_lo, rank_hi, stream=None):
         """Host arrays (seg_off[n+1], seg_file, seg_lo, seg_hi) of the ranks' file segments."""
         d = self._dev()

@@ -294,6 +294,22 @@ class _PartialShuffleSampler(Sampler):
             return (self._block[self.rank - self.ranks[0]], None, None)
         return self._dev
 
+    def device_batches(self, data, base_rows):
+        """This rank's remaining batches of the epoch gathered on the device: yields
+        (rows, file_pos, offset) with rows = data[base_rows[file] + offset] for the batch's ids
+        in stream order (pss_gather) -- no host round trip.  `data` holds every dataset file's
+        samples on the sampler's device, file f (dataset order) starting at row base_rows[f]."""
+        if self._dev is None:
+            raise RuntimeError("device_batches needs iter(sampler) first and every file length "
+                               "in files_len")
+        eng = self._engine
+        _, fpos, off = self._dev
+        while self._pos < self._end:
+            lo, hi = self._pos, min(self._pos + self.batch_size, self._end)
+            self._pos = hi
+            self.count_batches += 1
+            yield eng.gather(data, base_rows, fpos[lo:hi], off[lo:hi]), fpos[lo:hi], off[lo:hi]
+
     def block_indices(self):
         """[hi - lo, num_samples] ids of every logical rank of the block ranks=(lo, hi)."""
         if self._block is None:

@@ -265,3 +265,54 @@ def test_device_error_flag_reaches_the_sampler():
     with pytest.raises(_lib.PSSError):
         eng.check()
     eng.check()                                   # pss_check cleared the word
+
+
+@pytest.mark.parametrize("device", DEVICES)
+def test_fused_mapping_and_device_gather(device):
+    """pss_generate_mapped (V1: fused into the generation kernel; V2: generate + bucket map)
+    equals generate + map, and pss_gather returns the rows the host reader would gather
+    (V1:243-248), for the rank's whole epoch."""
+    import torch
+    from partiallyshuffledistributedsampler_amd.engine import IndexEngine
+    rng = np.random.default_rng(31)
+    lens = rng.integers(0, 700, 90)           # empty files included
+    N, R = int(lens.sum()), 5
+    dev = torch.device("cpu") if device == "cpu" else torch.device("cuda", 0)
+    for ver, B in ((1, 256), (2, 256), (2, 20000), (1, 70000)):
+        eng = IndexEngine(lens, N, R, B, ver, seed=4, device=device)
+        eng.init_iter(3)
+        ids = eng.generate(0, R)
+        fpos, off = eng.map(ids.reshape(-1))
+        f2, o2 = eng.generate_mapped(1, R, 7, 1000)
+        ns = eng.num_samples
+        c = min(1000, ns - 7)
+        want_f = fpos.reshape(R, -1)[1:, 7:7 + c]
+        want_o = off.reshape(R, -1)[1:, 7:7 + c]
+        assert torch.equal(f2[:, :c].cpu(), want_f.cpu()) and torch.equal(o2[:, :c].long().cpu(), want_o.cpu())
+        # device-resident rows: file f's sample j is the row (f, j); files stored in dataset order
+        base = np.concatenate([[0], np.cumsum(lens)[:-1]])
+        data = torch.stack([torch.from_numpy(np.repeat(np.arange(len(lens)), lens)),
+                            torch.from_numpy(np.concatenate([np.arange(n) for n in lens]))], 1).to(dev)
+        rows = eng.gather(data, torch.from_numpy(base), fpos, off)
+        order = eng.file_order()
+        fp = fpos.cpu().numpy()
+        f_abs = np.where(fp < 0, -1 - fp, fp)
+        assert np.array_equal(rows[:, 0].cpu().numpy(), order[f_abs])
+        assert np.array_equal(rows[:, 1].cpu().numpy(), off.cpu().numpy())
+        eng.close()
+    # through the sampler: batches gathered on the device == the host reader's batches
+    fx = load("v2_small")
+    files, lengths, fl, N, R, B, bs, shuffle = fixture_params(fx)
+    s = make(fx, 0, device)
+    s.set_epoch(0)
+    host = batches_of(iter(s))
+    s = make(fx, 0, device)            # a fresh sampler: init_iter's history is cumulative
+    s.set_epoch(0)
+    iter(s)
+    lens2 = np.array([lengths[p] for p in files])
+    base2 = torch.from_numpy(np.concatenate([[0], np.cumsum(lens2)[:-1]]))
+    data2 = torch.from_numpy(np.concatenate([np.arange(n) for n in lens2])).to(dev)
+    dev_batches = list(s.device_batches(data2, base2))
+    assert len(dev_batches) >= len(host)
+    for (tg, _, rf), (rows, f, o) in zip(host, dev_batches):
+        assert sorted(np.concatenate([d["off"] for d in tg]).tolist()) == sorted(rows.cpu().tolist())
