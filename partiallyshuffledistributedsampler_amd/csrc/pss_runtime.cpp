@@ -210,6 +210,7 @@ struct pss_sampler {
     static constexpr int kLaBufs = 3;   // VAL (and big-pool workspace) ring: d_val/d_buf + 2
     DevBuf<uint32_t> d_val2, d_buf2, d_val3, d_buf3;
     hipStream_t side = nullptr;
+    hipEvent_t ev_side = nullptr;       // the last pass launched on the side stream
     hipEvent_t ev_read[kLaBufs] = {};   // per buffer: the last replay that read it
     hipEvent_t ev_done[kLaBufs] = {};   // per buffer: the last lookahead pass that wrote it
     struct Shape {
@@ -414,6 +415,7 @@ int pss_destroy(pss_sampler *h) {
         if (h->upload_done) (void)hipEventDestroy(h->upload_done);
         for (hipEvent_t e : h->ev_pool) (void)hipEventDestroy(e);
         if (h->side) (void)hipStreamDestroy(h->side);
+        if (h->ev_side) (void)hipEventDestroy(h->ev_side);
         for (hipEvent_t e : h->ev_read) if (e) (void)hipEventDestroy(e);
         for (hipEvent_t e : h->ev_done) if (e) (void)hipEventDestroy(e);
         h->d_val2.release(); h->d_buf2.release(); h->d_val3.release(); h->d_buf3.release();
@@ -535,6 +537,7 @@ int generate_v2_lookahead(pss_sampler *h, const pss::Geometry &g, int32_t rank_l
         PSS_HIP(hipStreamCreateWithPriority(&h->side, hipStreamNonBlocking, side_hi ? greatest : least));
         for (hipEvent_t &e : h->ev_read) PSS_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         for (hipEvent_t &e : h->ev_done) PSS_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        PSS_HIP(hipEventCreateWithFlags(&h->ev_side, hipEventDisableTiming));
     }
     static const int depth = [] {   // epochs queued ahead: 2 (default) keeps the wait for a pass
         const char *e = getenv("PSS_V2_LOOKAHEAD_DEPTH");   // off the replay's critical path
@@ -599,6 +602,7 @@ int generate_v2_lookahead(pss_sampler *h, const pss::Geometry &g, int32_t rank_l
                                bwords ? W[nb]->p : nullptr, nullptr, h->d_err.p, h->side, mk, h->emit_path,
                                pss::V2_STAGE_PRE));
         PSS_HIP(hipEventRecord(h->ev_done[nb], h->side));
+        PSS_HIP(hipEventRecord(h->ev_side, h->side));
         for (auto &p : h->pend)
             if (!p.valid) { p = {true, shape, k0[d], k1[d], nb}; break; }
     }
@@ -649,8 +653,9 @@ int pss_generate(pss_sampler *h, int32_t rank_lo, int32_t rank_hi, int64_t pos_l
     } else {
         for (auto &p : h->pend) p.valid = false;
         h->last_valid = false;
-        if (h->side) PSS_HIP(hipStreamSynchronize(h->side));   // a lookahead may still write VAL
-        // d_val's last reader may be a replay on another stream (the lookahead path's buffer 0)
+        // a lookahead pass may still write a VAL buffer, and d_val's last reader may be a replay
+        // on another stream: order this launch after both on the device (no host round trip)
+        if (h->side) PSS_HIP(hipStreamWaitEvent(s, h->ev_side, 0));
         if (h->ev_read[0]) PSS_HIP(hipStreamWaitEvent(s, h->ev_read[0], 0));
         PSS_HIP(h->d_val.ensure(words(pss::v2_val_bytes(g, nr))));
         const size_t bb = pss::v2_buf_bytes(g, nr), sb = pss::v2_sort_bytes(g, nr);

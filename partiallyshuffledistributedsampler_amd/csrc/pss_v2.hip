@@ -967,9 +967,15 @@ hipError_t launch_v2_tail_vals(const Geometry &g, const V2Plan &pl, const RankDe
 bool v2_stage_split(const Geometry &g, int32_t nr, int emit_path) {
     if (emit_path == EMIT_AUTO) emit_path = lds_xchg_ordered() ? EMIT_XCHG : EMIT_PROBE;
     // grouped pools always split: their pre-pass (key table, last occurrences of tiled
-    // streams) runs a step ahead on the side stream; in line it cost the replay ~40 us per
-    // epoch at C5 (profiles/r02/c5_split_ab.txt)
-    if (v2_grouped(g)) return true;
+    // streams) runs a step ahead on the side stream; in line (A/B knob PSS_V2_GRP_SPLIT=0) the
+    // C5 step is 0.264 ms against 0.233 ms split (profiles/r02/c5_split_ab.txt)
+    if (v2_grouped(g)) {
+        static const bool inline_pre = [] {
+            const char *e = getenv("PSS_V2_GRP_SPLIT");
+            return e && e[0] == '0';
+        }();
+        return !inline_pre;
+    }
     return emit_path == EMIT_XCHG;
 }
 
