@@ -144,17 +144,28 @@ __global__ void k_bucket_index(const int64_t *__restrict__ prefix, int64_t F, in
         BT[b] = (int32_t)file_of(prefix, F, b << kb);
 }
 
+constexpr int kMapIlp = 4;
+
 template <typename OFF>
-__global__ void k_map(const int64_t *__restrict__ prefix, int64_t F, const int32_t *__restrict__ BT,
-                      int32_t kb, int64_t nb, const int64_t *__restrict__ ids, int64_t n,
-                      int32_t *__restrict__ fpos, OFF *__restrict__ off) {
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
-         i += (int64_t)gridDim.x * blockDim.x) {
-        int32_t f;
-        int64_t o;
-        map_one_bucketed(prefix, F, BT, kb, nb, ids[i], f, o);
-        fpos[i] = f;
-        off[i] = (OFF)o;
+__global__ __launch_bounds__(256) void k_map(const int64_t *__restrict__ prefix, int64_t F,
+                                             const int32_t *__restrict__ BT, int32_t kb, int64_t nb,
+                                             const int64_t *__restrict__ ids, int64_t n,
+                                             int32_t *__restrict__ fpos, OFF *__restrict__ off) {
+    // each id is a chain of dependent L2 reads (bucket bounds, then the prefix): a thread runs
+    // kMapIlp ids a grid-stride apart, coalesced and with their chains interleaved
+    const int64_t T = prefix[F];
+    const int64_t S = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i0 < n; i0 += kMapIlp * S) {
+        int64_t id[kMapIlp];
+#pragma unroll
+        for (int k = 0; k < kMapIlp; k++) id[k] = i0 + k * S < n ? ids[i0 + k * S] : 0;
+        int32_t f[kMapIlp];
+        int64_t o[kMapIlp];
+#pragma unroll
+        for (int k = 0; k < kMapIlp; k++) map_one_bucketed_t(prefix, F, T, BT, kb, nb, id[k], f[k], o[k]);
+#pragma unroll
+        for (int k = 0; k < kMapIlp; k++)
+            if (i0 + k * S < n) { fpos[i0 + k * S] = f[k]; off[i0 + k * S] = (OFF)o[k]; }
     }
 }
 
@@ -374,12 +385,11 @@ hipError_t launch_map(const int64_t *prefix, int64_t F, const int32_t *BT, int32
                       const int64_t *ids, int64_t n, int32_t *fpos, int64_t *off, int32_t *off32,
                       hipStream_t s) {
     if (n <= 0) return hipSuccess;
+    const dim3 grid(grid_for(cdiv(n, kMapIlp), 256));
     if (off32)
-        hipLaunchKernelGGL(k_map<int32_t>, dim3(grid_for(n, 256)), dim3(256), 0, s, prefix, F, BT, kb, nb,
-                           ids, n, fpos, off32);
+        hipLaunchKernelGGL(k_map<int32_t>, grid, dim3(256), 0, s, prefix, F, BT, kb, nb, ids, n, fpos, off32);
     else
-        hipLaunchKernelGGL(k_map<int64_t>, dim3(grid_for(n, 256)), dim3(256), 0, s, prefix, F, BT, kb, nb,
-                           ids, n, fpos, off);
+        hipLaunchKernelGGL(k_map<int64_t>, grid, dim3(256), 0, s, prefix, F, BT, kb, nb, ids, n, fpos, off);
     return hipGetLastError();
 }
 

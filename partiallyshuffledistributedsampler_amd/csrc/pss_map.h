@@ -74,9 +74,9 @@ PSS_HD int32_t bucket_shift(int64_t total, int64_t F) {
 }
 PSS_HD int64_t bucket_count(int64_t total, int32_t kb) { return (total >> kb) + 2; }
 
-PSS_HD void map_one_bucketed(const int64_t *prefix, int64_t F, const int32_t *BT, int32_t kb,
-                             int64_t nb, int64_t id0, int32_t &fpos, int64_t &off) {
-    const int64_t T = prefix[F];
+// T = prefix[F] (the scanned total), hoisted by callers that map many ids
+PSS_HD void map_one_bucketed_t(const int64_t *prefix, int64_t F, int64_t T, const int32_t *BT,
+                               int32_t kb, int64_t nb, int64_t id0, int32_t &fpos, int64_t &off) {
     int64_t id = id0;
     bool refl = false;
     if (id >= T) {
@@ -94,6 +94,11 @@ PSS_HD void map_one_bucketed(const int64_t *prefix, int64_t F, const int32_t *BT
     }
     fpos = refl ? (int32_t)(-1 - lo) : (int32_t)lo;
     off = id - prefix[lo];
+}
+
+PSS_HD void map_one_bucketed(const int64_t *prefix, int64_t F, const int32_t *BT, int32_t kb,
+                             int64_t nb, int64_t id0, int32_t &fpos, int64_t &off) {
+    map_one_bucketed_t(prefix, F, prefix[F], BT, kb, nb, id0, fpos, off);
 }
 
 }  // namespace pss
