@@ -142,6 +142,7 @@ __global__ __launch_bounds__(256) void k_g_lastocc(Geometry g, GPlan pl, int32_t
 
 // ---- pass B: replay ---------------------------------------------------------------------------
 typedef __attribute__((address_space(3))) volatile uint8_t g_lds_vu8;
+typedef unsigned int g_u32x2 __attribute__((ext_vector_type(2)));
 
 template <bool NARROW>
 struct GIds {   // virtual index <-> slot word <-> emitted id
@@ -190,6 +191,14 @@ __device__ __forceinline__ uint32_t xchg_unordered(uint32_t *buf, g_lds_vu8 *mar
 // with A_i = R_i ^ K_i, A_{i+1} = A_{i-1} ^ F(A_i) ^ (K_{i-1} ^ K_{i+1}) (one 3-input xor per
 // round, F = one full-rate 24-bit multiply + bit-field extract); output L = A_5 ^ K_5, R = A_4 ^ F(A_5) ^ K_4.
 // Same values as feistel_once on each chain.
+// a ^ b ^ k in one v_bitop3_b32 (truth table 0x96) with the wave-uniform k read from an SGPR;
+// hipcc fuses only some 3-input xors itself
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t k) {
+    uint32_t r;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "s"(k));
+    return r;
+}
+
 template <bool PACKED>
 __device__ __forceinline__ void feistel4_uniform(const uint32_t x[4], uint32_t h, const uint32_t K[6],
                                                  uint32_t y[4]) {
@@ -201,17 +210,43 @@ __device__ __forceinline__ void feistel4_uniform(const uint32_t x[4], uint32_t h
     } else {
         const uint32_t mask = (1u << h) - 1u, sh = 24u - h;
         const uint32_t K02 = K[0] ^ K[2], K13 = K[1] ^ K[3], K24 = K[2] ^ K[4], K35 = K[3] ^ K[5];
-        auto F = [&](uint32_t a) -> uint32_t { return (((a & 0xFFFFFFu) * kFeistelM24) >> sh) & mask; };
+        // F = bits [24 - h, 24) of the 24-bit product: one v_mul_u32_u24 and one v_bfe_u32, so
+        // that each round is mul, bfe and a single 3-input xor (v_bitop3)
+        auto F = [&](uint32_t a) -> uint32_t {
+            return __builtin_amdgcn_ubfe((a & 0xFFFFFFu) * kFeistelM24, sh, h);
+        };
 #pragma unroll
         for (int c = 0; c < 4; c++) {
             const uint32_t A0 = (x[c] & mask) ^ K[0];
-            const uint32_t A1 = (x[c] >> h) ^ F(A0) ^ K[1];
-            const uint32_t A2 = A0 ^ F(A1) ^ K02;
-            const uint32_t A3 = A1 ^ F(A2) ^ K13;
-            const uint32_t A4 = A2 ^ F(A3) ^ K24;
-            const uint32_t A5 = A3 ^ F(A4) ^ K35;
-            y[c] = ((A5 ^ K[5]) << h) | (A4 ^ F(A5) ^ K[4]);
+            const uint32_t A1 = xor3(x[c] >> h, F(A0), K[1]);
+            const uint32_t A2 = xor3(A0, F(A1), K02);
+            const uint32_t A3 = xor3(A1, F(A2), K13);
+            const uint32_t A4 = xor3(A2, F(A3), K24);
+            const uint32_t A5 = xor3(A3, F(A4), K35);
+            y[c] = ((A5 ^ K[5]) << h) | xor3(A4, F(A5), K[4]);
         }
+    }
+}
+
+// feistel4_uniform<false> when the four inputs xb + c 64 G (c < 4) share their low h bits and the
+// run advances them by multiples of 2^h (64 G % 2^h == 0): A0 = (xb & mask) ^ K0 and
+// C1 = F(A0) ^ K1 are then constants of the run, and chain c's left half is lb + c g64h with
+// lb = xb >> h.  Same values, four instructions fewer per chain.
+__device__ __forceinline__ void feistel4_rinv(uint32_t lb, uint32_t g64h, uint32_t A0, uint32_t C1,
+                                              uint32_t h, const uint32_t K[6], uint32_t y[4]) {
+    const uint32_t sh = 24u - h;
+    const uint32_t K02 = K[0] ^ K[2], K13 = K[1] ^ K[3], K24 = K[2] ^ K[4], K35 = K[3] ^ K[5];
+    auto F = [&](uint32_t a) -> uint32_t {
+        return __builtin_amdgcn_ubfe((a & 0xFFFFFFu) * kFeistelM24, sh, h);
+    };
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+        const uint32_t A1 = (lb + (uint32_t)c * g64h) ^ C1;
+        const uint32_t A2 = xor3(A0, F(A1), K02);
+        const uint32_t A3 = xor3(A1, F(A2), K13);
+        const uint32_t A4 = xor3(A2, F(A3), K24);
+        const uint32_t A5 = xor3(A3, F(A4), K35);
+        y[c] = ((A5 ^ K[5]) << h) | xor3(A4, F(A5), K[4]);
     }
 }
 
@@ -331,9 +366,25 @@ __global__ __launch_bounds__(64) void k_g_emit(Geometry g, GPlan pl, const RankD
             const bool contig = NARROW && id_last - id_first == B - 1u &&
                                 ((wB < pl.twoB) == (wB + B - 1u < pl.twoB));
             uint32_t tb = t_first + c_lane, xb = pa + c_lane;
-            int64_t *ob = o + t_first;                                // wave-uniform base
-            const uint32_t boff = c_lane * 8u;                        // per-lane byte offsets
-            auto body = [&](auto ctg) {
+            // the run's stores through a buffer descriptor on its wave-uniform base: 32-bit
+            // per-lane offsets, no 64-bit address registers rewritten under in-flight stores
+            // (with those, hipcc drained vmcnt(0) every iteration)
+            const uint64_t obase = (uint64_t)(uintptr_t)(o + t_first);
+            const uint32_t ob_lo = __builtin_amdgcn_readfirstlane((uint32_t)obase);
+            const uint32_t ob_hi = __builtin_amdgcn_readfirstlane((uint32_t)(obase >> 32));
+            const __amdgpu_buffer_rsrc_t orsrc = __builtin_amdgcn_make_buffer_rsrc(
+                (void *)(((uint64_t)ob_hi << 32) | ob_lo), 0, (int)(n * G256 * 8u), 0x00020000);
+            uint32_t voff = c_lane * 8u;                              // per-lane byte offsets
+            const uint32_t hmask = (1u << pl.hB) - 1u;
+            auto body = [&](auto ctg, auto rinv) {
+                constexpr bool RINV = decltype(rinv)::value;
+                uint32_t A0 = 0u, C1 = 0u, lb = 0u;
+                const uint32_t g64h = G64 >> pl.hB, g256h = G256 >> pl.hB;
+                if constexpr (RINV) {
+                    A0 = (xb & hmask) ^ K[0];
+                    C1 = __builtin_amdgcn_ubfe((A0 & 0xFFFFFFu) * kFeistelM24, 24u - pl.hB, pl.hB) ^ K[1];
+                    lb = xb >> pl.hB;
+                }
                 for (uint32_t it = 0; it < n; it++) {
                     uint32_t k[4];
                     if (POW2 || gpow2) {    // paired draws: sub-steps u, u + 64 share one hash
@@ -344,9 +395,14 @@ __global__ __launch_bounds__(64) void k_g_emit(Geometry g, GPlan pl, const RankD
 #pragma unroll
                         for (int j = 0; j < 4; j++) k[j] = scale32(slot_hash(tb + j * G64, s0, s1), S);
                     }
-                    const uint32_t x[4] = {xb, xb + G64, xb + 2u * G64, xb + 3u * G64};
                     uint32_t y[4], v[4];
-                    feistel4_uniform<PACKED>(x, pl.hB, K, y);
+                    if constexpr (RINV) {
+                        feistel4_rinv(lb, g64h, A0, C1, pl.hB, K, y);
+                        lb += g256h;
+                    } else {
+                        const uint32_t x[4] = {xb, xb + G64, xb + 2u * G64, xb + 3u * G64};
+                        feistel4_uniform<PACKED>(x, pl.hB, K, y);
+                    }
 #pragma unroll
                     for (int j = 0; j < 4; j++) {
                         const uint32_t in = decltype(ctg)::value ? id_first + y[j] : ids.to_slot(wB + y[j]);
@@ -354,15 +410,28 @@ __global__ __launch_bounds__(64) void k_g_emit(Geometry g, GPlan pl, const RankD
                         else v[j] = xchg_unordered(buf, mark, k[j], in, true, lane);
                     }
 #pragma unroll
-                    for (int j = 0; j < 4; j++)
-                        *(int64_t *)((char *)ob + (boff + 8u * (uint32_t)j * G64)) = ids.from_slot(v[j]);
+                    for (int j = 0; j < 4; j++) {
+                        const uint64_t id = (uint64_t)ids.from_slot(v[j]);
+                        const g_u32x2 d = {(uint32_t)id, (uint32_t)(id >> 32)};
+                        __builtin_amdgcn_raw_buffer_store_b64(d, orsrc, (int)voff, (int)(8u * (uint32_t)j * G64), 0);
+                    }
                     tb += G256;
                     xb += G256;
-                    ob += G256;
+                    voff += 8u * G256;
                 }
             };
-            if (contig) body(std::true_type{});
-            else body(std::false_type{});
+            if constexpr (!PACKED) {
+                if ((G64 & hmask) == 0u) {   // run-invariant right halves (feistel4_rinv)
+                    if (contig) body(std::true_type{}, std::true_type{});
+                    else body(std::false_type{}, std::true_type{});
+                } else {
+                    if (contig) body(std::true_type{}, std::false_type{});
+                    else body(std::false_type{}, std::false_type{});
+                }
+            } else {
+                if (contig) body(std::true_type{}, std::false_type{});
+                else body(std::false_type{}, std::false_type{});
+            }
             t_first += n * G256;
             pa += n * G256;
             u0 += 256u * n;
