@@ -8,7 +8,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libpss.so")
+# PSS_LIB: another build of the library (same-box A/B of kernel variants); default the in-tree one
+LIB_PATH = os.environ.get("PSS_LIB") or os.path.join(_HERE, "libpss.so")
 
 PSS_OK = 0
 PSS_DEVICE_CPU = -1

@@ -37,6 +37,7 @@ struct GPlan {
     uint32_t B32, hB, walk_full, w_last, len_last, h_last, hP, twoB;
 };
 
+
 static GPlan gplan(const Geometry &g, int32_t nr, int cus) {
     GPlan p{};
     p.P1 = g.B < g.ns ? g.B : g.ns;
@@ -347,6 +348,21 @@ __global__ __launch_bounds__(64) void k_g_emit(Geometry g, GPlan pl, const RankD
     uint32_t pa = t_first - (wa - 1) * B;
     const bool runs_ok = full_emit && !pl.walk_full;
     uint32_t u0 = ulo;
+    // round keys of window wk (Kc) and of wk + 1 (Kn, issued a run ahead of its first use)
+    const int32_t W = (int32_t)pl.W;
+    auto win_keys = [&](uint32_t w, uint32_t Kx[kFeistelRounds]) {
+        if (w >= 1u && (int32_t)w <= W) {
+            const uint32_t *kw = ktr + kGKeyWin + kRoundKeyWords * (w - 1);
+#pragma unroll
+            for (int i = 0; i < kFeistelRounds; i++) Kx[i] = __builtin_amdgcn_readfirstlane(kw[i]);
+        } else {
+#pragma unroll
+            for (int i = 0; i < kFeistelRounds; i++) Kx[i] = 0u;
+        }
+    };
+    uint32_t wk = wa, Kc[kFeistelRounds], Kn[kFeistelRounds];
+    win_keys(wk, Kc);
+    win_keys(wk + 1u, Kn);
     while (u0 < uhi) {
         // a run of whole iterations inside the full window wa: keys in SGPRs, no bookkeeping
         uint32_t n = 0;
@@ -356,10 +372,19 @@ __global__ __launch_bounds__(64) void k_g_emit(Geometry g, GPlan pl, const RankD
             n = by_win < by_end ? by_win : by_end;
         }
         if (n) {
-            const uint32_t *kw = ktr + kGKeyWin + kRoundKeyWords * (wa - 1);
+            if (wa != wk) {
+                if (wa == wk + 1u) {
+#pragma unroll
+                    for (int i = 0; i < kFeistelRounds; i++) Kc[i] = Kn[i];
+                } else {
+                    win_keys(wa, Kc);
+                }
+                wk = wa;
+                win_keys(wk + 1u, Kn);
+            }
             uint32_t K[kFeistelRounds];
 #pragma unroll
-            for (int i = 0; i < kFeistelRounds; i++) K[i] = __builtin_amdgcn_readfirstlane(kw[i]);
+            for (int i = 0; i < kFeistelRounds; i++) K[i] = Kc[i];
             // ids of the window's values wa B + y: one add when the window maps contiguously
             const uint32_t wB = wa * B;
             const uint32_t id_first = ids.to_slot(wB), id_last = ids.to_slot(wB + B - 1u);
