@@ -2,6 +2,7 @@
 #pragma once
 #include "pss_common.h"
 #include "pss_kernels.h"
+#include "pss_map.h"
 
 namespace pss {
 
@@ -294,6 +295,131 @@ __device__ __forceinline__ int64_t emit_id(uint32_t v, uint32_t twoB, uint32_t o
         return (int64_t)(id < N32 ? id : idw);
     }
     return v2_id(v, rd, g);
+}
+
+// ---- fused (file, offset) output of the V2 replay kernels (pss_generate_mapped) ------------------
+// A replay wave's ids come, with overwhelming probability, from one interval of ids: the pool2
+// windows of its tile and the kSegBackWin before it (a value survives a window of steps in a pool
+// of <= B slots with probability <= e^-1).  The wave cuts that interval into kSegBuckets equal
+// buckets and keeps, per bucket, its first file, the bucket's one file boundary (if any) and
+// the first file's start -- three parallel LDS arrays, one independent read each per id.
+// Buckets holding two or more boundaries, ids outside the interval and ids past the scanned
+// total (reflected) take the global bucketed map (map_one_bucketed_t): results equal pss_map's.
+constexpr uint32_t kSegBuckets = 256, kSegBackWin = 40;
+constexpr uint32_t kSegLdsWords = 3 * kSegBuckets;
+constexpr uint32_t kSegMulti = 0xFFFFu;    // bucket with >= 2 boundaries: global path
+
+// the global map for the rare ids the LDS buckets miss
+__device__ __forceinline__ void seg_global_map(const MapArgs &ma, int64_t T, int64_t id,
+                                               int32_t &f, int32_t &off) {
+    int64_t o;
+    map_one_bucketed_t(ma.prefix, ma.F, T, ma.BT, ma.kb, ma.nb, id, f, o);
+    off = (int32_t)o;
+}
+
+struct SegMap {
+    MapArgs ma;
+    int64_t T;          // prefix[F]
+    int64_t id_lo;      // [id_lo, id_lo + len) maps through LDS
+    uint32_t len, kbm;
+    int32_t f0;
+    const uint32_t *fw;  // LDS: file of the bucket's start (relative to f0) | files to the one after its boundary << 16
+    const int32_t *sw;   // LDS: the boundary (relative id), or INT32_MAX
+    const int32_t *bw;   // LDS: start of the bucket's first file (relative id, may be < 0)
+
+    // one wave (the whole workgroup) builds it; lds: kSegLdsWords words
+    __device__ __forceinline__ void build(const MapArgs &m, int64_t lo, int64_t hi, uint32_t *lds,
+                                          int lane) {
+        ma = m;
+        T = m.prefix[m.F];
+        id_lo = lo;
+        len = 0;
+        kbm = 0;
+        f0 = 0;
+        uint32_t *fww = lds;
+        int32_t *sww = (int32_t *)(lds + kSegBuckets), *bww = (int32_t *)(lds + 2 * kSegBuckets);
+        fw = fww; sw = sww; bw = bww;
+        if (hi > T) hi = T;                       // past the total: reflected ids, global path
+        if (hi <= lo || hi - lo >= ((int64_t)1 << 30)) return;
+        int32_t fa;
+        int64_t o;
+        map_one_bucketed_t(m.prefix, m.F, T, m.BT, m.kb, m.nb, lo, fa, o);
+        if (fa < 0) return;
+        const uint32_t L = (uint32_t)(hi - lo);
+        uint32_t k = 0;
+        while (((L - 1u) >> k) >= kSegBuckets) k++;
+        // four buckets per lane, their global lookups interleaved
+#pragma unroll
+        for (int q = 0; q < (int)(kSegBuckets / 64); q++) {
+            const uint32_t b = (uint32_t)lane + 64u * q;
+            const int64_t r0 = (int64_t)b << k, r1 = (r0 + ((int64_t)1 << k)) < (int64_t)L ? r0 + ((int64_t)1 << k) : L;
+            uint32_t word = kSegMulti << 16;
+            int32_t split = INT32_MAX, base = 0;
+            if (r0 < (int64_t)L) {
+                int32_t f;
+                map_one_bucketed_t(m.prefix, m.F, T, m.BT, m.kb, m.nb, lo + r0, f, o);
+                const int64_t pa = m.prefix[f] - lo;                 // start of the bucket's first file
+                const int64_t pb = f + 1 < m.F ? m.prefix[f + 1] - lo : (int64_t)L;   // its end
+                uint32_t df = 0;
+                if (pb < r1) {                                       // a boundary inside the bucket
+                    int32_t fb;
+                    map_one_bucketed_t(m.prefix, m.F, T, m.BT, m.kb, m.nb, lo + pb, fb, o);  // skips empty files
+                    const int64_t pc = fb + 1 < m.F ? m.prefix[fb + 1] - lo : (int64_t)L;
+                    df = pc < r1 ? kSegMulti : (uint32_t)(fb - f);
+                    split = (int32_t)pb;
+                }
+                if (f - fa >= 0xFFFF || df > 0xFFFEu) df = kSegMulti;
+                word = (uint32_t)(f - fa) | (df << 16);
+                base = (int32_t)pa;
+            }
+            fww[b] = word;
+            sww[b] = split;
+            bww[b] = base;
+        }
+        __syncthreads();
+        f0 = fa;
+        kbm = k;
+        len = L;
+    }
+
+    __device__ __forceinline__ void map(int64_t id, int32_t &f, int32_t &off) const {
+        const uint64_t rel = (uint64_t)(id - id_lo);
+        bool hit = false;
+        if (rel < (uint64_t)len) {
+            const int32_t r = (int32_t)rel;
+            const uint32_t b = (uint32_t)r >> kbm;
+            const uint32_t w = fw[b];
+            const int32_t split = sw[b], base = bw[b];
+            const uint32_t df = w >> 16;
+            if (df != kSegMulti) {
+                const bool up = r >= split;
+                f = f0 + (int32_t)(w & 0xFFFFu) + (up ? (int32_t)df : 0);
+                off = r - (up ? split : base);
+                hit = true;
+            }
+        }
+        if (!hit) seg_global_map(ma, T, id, f, off);
+    }
+};
+
+// The id interval staged for virtual values [v_lo, v_hi) of one rank: ids are base + v (base =
+// old start below twoB, new start above) wrapped modulo N, so the values may map to two or three
+// id intervals; the one holding the value v_pref (the tile's own first window) is staged.
+__device__ __forceinline__ void seg_interval(uint32_t v_lo, uint32_t v_hi, uint32_t v_pref,
+                                             uint32_t twoB, const RankDesc &rd, const Geometry &g,
+                                             int64_t &lo, int64_t &hi) {
+    lo = hi = 0;
+    if (v_hi <= v_lo) return;
+    if (v_lo < twoB && v_hi > twoB) {
+        if (v_pref < twoB) v_hi = twoB;
+        else v_lo = twoB;
+    }
+    const int64_t base = v_lo < twoB ? rd.old_start : rd.new_start;
+    const int64_t a = base + v_lo, b = base + v_hi, p = base + v_pref;
+    if (b <= g.N) { lo = a; hi = b; }
+    else if (a >= g.N) { lo = a - g.N; hi = b - g.N; }
+    else if (p >= g.N) { lo = 0; hi = b - g.N; }
+    else { lo = a; hi = g.N; }
 }
 
 }  // namespace pss

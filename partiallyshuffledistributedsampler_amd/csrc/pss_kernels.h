@@ -137,13 +137,15 @@ hipError_t launch_v2(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, 
                      int64_t pos_lo, int64_t count, int64_t *out, uint32_t *val_ws,
                      uint32_t *buf_ws, uint32_t *sort_ws, int32_t *err, hipStream_t s,
                      const Marker &mk = Marker(), int emit_path = EMIT_AUTO,
-                     int stage = V2_STAGE_ALL);
+                     int stage = V2_STAGE_ALL, const MapArgs *mapped = nullptr);
+// mapped != nullptr (v2_mapped_fused shapes only): (file, offset) instead of ids
+bool v2_mapped_fused(const Geometry &g, int emit_path);
 size_t v2_val_bytes(const Geometry &g, int32_t nr);
 // V2 tail from per-tile VAL tables (walk-back), positions [pos_lo, pos_lo+count) past T
 hipError_t launch_v2_tail_vals(const Geometry &g, const V2Plan &pl, const RankDesc *ranks,
                                int32_t rank_lo, int32_t nr, const uint32_t *VAL, int64_t pos_lo,
                                int64_t count, int64_t *out, hipStream_t s,
-                               KeyTab kt);
+                               KeyTab kt, const MapArgs *mapped = nullptr);
 // pools beyond LDS (P1 > kLdsSlotMax): the grouped slot machine (pss_v2grp.hip); its key
 // table and per-tile tables live in val_ws (v2_val_bytes)
 bool v2_grouped(const Geometry &g);

@@ -508,7 +508,7 @@ bool lookahead_on() {
 // call had this shape at epoch - 1, the pass of epoch + 1 on the side stream.
 int generate_v2_lookahead(pss_sampler *h, const pss::Geometry &g, int32_t rank_lo, int32_t nr,
                           int64_t pos_lo, int64_t count, int64_t *out_dev, hipStream_t s,
-                          const pss::Marker &mk) {
+                          const pss::Marker &mk, const pss::MapArgs *ma) {
     constexpr int NB = pss_sampler::kLaBufs;
     const size_t words = (pss::v2_val_bytes(g, nr) + sizeof(uint32_t) - 1) / sizeof(uint32_t);
     const size_t bwords = (pss::v2_buf_bytes(g, nr) + sizeof(uint32_t) - 1) / sizeof(uint32_t);
@@ -560,7 +560,7 @@ int generate_v2_lookahead(pss_sampler *h, const pss::Geometry &g, int32_t rank_l
         PSS_HIP(hipStreamWaitEvent(s, h->ev_done[buf], 0));
         PSS_HIP(pss::launch_v2(g, h->d_ranks.p, rank_lo, nr, pos_lo, count, out_dev, V[buf]->p,
                                bwords ? W[buf]->p : nullptr, nullptr, h->d_err.p, s, mk, h->emit_path,
-                               pss::V2_STAGE_EMIT));
+                               pss::V2_STAGE_EMIT, ma));
     } else {
         // a buffer no queued lookahead holds, after its last reader and its last writer
         for (int b = 0; b < NB && buf < 0; b++) if (!held(b)) buf = b;
@@ -569,7 +569,7 @@ int generate_v2_lookahead(pss_sampler *h, const pss::Geometry &g, int32_t rank_l
         PSS_HIP(hipStreamWaitEvent(s, h->ev_done[buf], 0));
         PSS_HIP(pss::launch_v2(g, h->d_ranks.p, rank_lo, nr, pos_lo, count, out_dev, V[buf]->p,
                                bwords ? W[buf]->p : nullptr, nullptr, h->d_err.p, s, mk, h->emit_path,
-                               pss::V2_STAGE_ALL));
+                               pss::V2_STAGE_ALL, ma));
     }
     PSS_HIP(hipEventRecord(h->ev_read[buf], s));
     const bool sequential = h->last_valid && h->last_shape == shape && h->last_epoch == h->epoch - 1;
@@ -609,6 +609,11 @@ int generate_v2_lookahead(pss_sampler *h, const pss::Geometry &g, int32_t rank_l
     return PSS_OK;
 }
 
+// pss_generate's device path; ma != nullptr (V2 counter order, v2_mapped_fused shapes): the
+// replay writes (file, offset) into ma's arrays instead of ids into out_dev
+int generate_impl(pss_sampler *h, int32_t rank_lo, int32_t rank_hi, int64_t pos_lo, int64_t count,
+                  int64_t *out_dev, void *stream, const pss::MapArgs *ma);
+
 }  // namespace
 
 int pss_generate(pss_sampler *h, int32_t rank_lo, int32_t rank_hi, int64_t pos_lo,
@@ -617,6 +622,13 @@ int pss_generate(pss_sampler *h, int32_t rank_lo, int32_t rank_hi, int64_t pos_l
     if (rank_lo < 0 || rank_hi > h->R || rank_lo > rank_hi) return fail(PSS_EINVAL, "bad rank range");
     if (pos_lo < 0 || count < 0) return fail(PSS_EINVAL, "bad position range");
     if (count > 0 && rank_hi > rank_lo && !out_dev) return fail(PSS_EINVAL, "out_dev is NULL");
+    return generate_impl(h, rank_lo, rank_hi, pos_lo, count, out_dev, stream, nullptr);
+}
+
+namespace {
+
+int generate_impl(pss_sampler *h, int32_t rank_lo, int32_t rank_hi, int64_t pos_lo, int64_t count,
+                  int64_t *out_dev, void *stream, const pss::MapArgs *ma) {
     if (h->cpu) {
         if (!h->iterated) return fail(PSS_ESTATE, "pss_init_iter must be called before generation");
         if (rank_hi == rank_lo || count == 0 || pos_lo >= h->ns) return PSS_OK;
@@ -649,7 +661,7 @@ int pss_generate(pss_sampler *h, int32_t rank_lo, int32_t rank_hi, int64_t pos_l
         PSS_HIP(pss::launch_v2_exact(g, h->d_ranks.p, rank_lo, nr, pos_lo, count, h->epoch, out_dev,
                                      h->d_sort.p, s));
     } else if (lookahead_on() && pss::v2_stage_split(g, nr, h->emit_path)) {
-        return generate_v2_lookahead(h, g, rank_lo, nr, pos_lo, count, out_dev, s, mk);
+        return generate_v2_lookahead(h, g, rank_lo, nr, pos_lo, count, out_dev, s, mk, ma);
     } else {
         for (auto &p : h->pend) p.valid = false;
         h->last_valid = false;
@@ -662,11 +674,14 @@ int pss_generate(pss_sampler *h, int32_t rank_lo, int32_t rank_hi, int64_t pos_l
         if (bb) PSS_HIP(h->d_buf.ensure(words(bb)));
         if (sb) PSS_HIP(h->d_sort.ensure(words(sb)));
         PSS_HIP(pss::launch_v2(g, h->d_ranks.p, rank_lo, nr, pos_lo, count, out_dev, h->d_val.p,
-                               h->d_buf.p, h->d_sort.p, h->d_err.p, s, mk, h->emit_path));
+                               h->d_buf.p, h->d_sort.p, h->d_err.p, s, mk, h->emit_path,
+                               pss::V2_STAGE_ALL, ma));
         if (h->ev_read[0]) PSS_HIP(hipEventRecord(h->ev_read[0], s));   // last user of d_val
     }
     return PSS_OK;
 }
+
+}  // namespace
 
 int pss_set_emit_path(pss_sampler *h, int32_t path) {
     if (!h) return fail(PSS_EINVAL, "NULL handle");
@@ -808,7 +823,12 @@ int pss_generate_mapped(pss_sampler *h, int32_t rank_lo, int32_t rank_hi, int64_
         PSS_HIP(pss::launch_v1(g, h->d_ranks.p, rank_lo, nr, pos_lo, count, nullptr, h->d_sort.p, s, mk, &ma));
         return PSS_OK;
     }
-    // V2 (and the exact orders): ids into the handle's scratch, then the bucket map
+    if (h->version == 2 && h->order_mode == PSS_ORDER_COUNTER && pss::v2_mapped_fused(g, h->emit_path)) {
+        // fused: the replay maps each id as it emits it (LDS segment map per tile)
+        pss::MapArgs ma{h->d_prefix.p, h->F, h->d_bucket.p, h->kb, h->nb, file_pos_dev, offset_dev};
+        return generate_impl(h, rank_lo, rank_hi, pos_lo, count, nullptr, stream, &ma);
+    }
+    // V2 grouped pools (and the exact orders): ids into the handle's scratch, then the bucket map
     if (!h->ids_free) PSS_HIP(hipEventCreateWithFlags(&h->ids_free, hipEventDisableTiming));
     if (h->d_ids.n < n) {
         PSS_HIP(hipEventSynchronize(h->ids_free));

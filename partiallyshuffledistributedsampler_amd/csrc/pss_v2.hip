@@ -454,13 +454,15 @@ __global__ __launch_bounds__(64) void k_v2_emit(Geometry g, V2Plan pl,
 // highest lane's insertion.  That is exactly the sequential replay of 64 consecutive steps, so
 // each step is ONE exchange -- no probe, no ballot, no per-clash fix-up -- and the four
 // exchanges of a super-batch issue back to back behind a single wait.
-template <bool NARROW, bool POW2>
+// MAPPED: (int32 file position, int32 offset) into ma.fpos / ma.off instead of int64 ids into
+// out, through the wave's LDS segment map (SegMap, pss_device.h)
+template <bool NARROW, bool POW2, bool MAPPED>
 __global__ __launch_bounds__(64) void k_v2_emit_x(Geometry g, V2Plan pl,
                                                   const RankDesc *__restrict__ ranks,
                                                   int32_t rank_lo, int64_t g_lo, int64_t ng,
                                                   const uint32_t *__restrict__ VAL,
                                                   int64_t pos_lo, int64_t count, int do_tail,
-                                                  int64_t *__restrict__ out, KeyTab kt) {
+                                                  int64_t *__restrict__ out, KeyTab kt, MapArgs ma) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
 #ifdef PSS_STAMPS
     if (threadIdx.x == 0 && blockIdx.x < (1u << 16)) pss_stamps[blockIdx.x][2] = __builtin_amdgcn_s_memrealtime();
@@ -469,10 +471,9 @@ __global__ __launch_bounds__(64) void k_v2_emit_x(Geometry g, V2Plan pl,
     const uint32_t B = pl.B32;
     const uint32_t nwin_max = pl.L32 / B + 2;
     // slot table at LDS offset 0 (exchange addresses are 4 * slot, no base add), then the
-    // Feistel keys of the tile's windows
+    // Feistel keys of the tile's windows (MAPPED: then the segment map)
     uint32_t *buf = smem;
     uint32_t *rk = smem + ((P1 + 3u) & ~3u);
-    (void)nwin_max;
     const int lane = threadIdx.x;
     // 32-bit tile arithmetic from the plan's host-computed constants (T < 2^32)
     const uint32_t ngu = (uint32_t)ng;
@@ -566,6 +567,23 @@ __global__ __launch_bounds__(64) void k_v2_emit_x(Geometry g, V2Plan pl,
     const uint32_t e_lo = (uint32_t)(pos_lo > tlo ? (pos_lo - tlo < nvalid ? pos_lo - tlo : nvalid) : 0);
     const uint32_t e_hi = (uint32_t)(pos_hi < thi ? (pos_hi > tlo ? pos_hi - tlo : 0) : nvalid);
     int64_t *o = out + (int64_t)rl * count + ((int64_t)tlo - pos_lo);
+    const int64_t ebase = (int64_t)rl * count + ((int64_t)tlo - pos_lo);   // element index of tl = 0
+    SegMap sm;
+    if constexpr (MAPPED) {
+        // ids of the tile's windows and the kSegBackWin before them
+        const uint32_t vl = w_lo > kSegBackWin ? (w_lo - kSegBackWin) * B : 0u;
+        const int64_t vh64 = (int64_t)(w_lo + (uint32_t)nwin) * B;
+        const uint32_t vh = (uint32_t)(vh64 < g.ns ? vh64 : g.ns);
+        int64_t lo, hi;
+        seg_interval(vl, vh, w_lo * B, twoB, rd, g, lo, hi);
+        sm.build(ma, lo, hi, rk + kRoundKeyWords * nwin_max, lane);
+    }
+    auto put_m = [&](int64_t e, int64_t id) {
+        int32_t f, of;
+        sm.map(id, f, of);
+        ma.fpos[e] = f;
+        ma.off[e] = of;
+    };
     const uint32_t hB = pl.hB;
     const bool walk_full = pl.walk_full;                     // full windows need cycle walking
     const uint32_t w_last = pl.w_last;                       // last pool2 window (may be short)
@@ -663,9 +681,14 @@ __global__ __launch_bounds__(64) void k_v2_emit_x(Geometry g, V2Plan pl,
                         for (int j = 0; j < 4; j++) ins[j] = contig ? id_first + y[j] : to_slot(wB + y[j]);
 #pragma unroll
                         for (int j = 0; j < 4; j++) v[j] = atomicExch(&buf[k[j]], ins[j]);
-                        int64_t *ob = o + tl0;
+                        if constexpr (MAPPED) {
 #pragma unroll
-                        for (int j = 0; j < 4; j++) ob[64u * j + lane] = (int64_t)v[j];
+                            for (int j = 0; j < 4; j++) put_m(ebase + tl0 + 64u * j + lane, (int64_t)v[j]);
+                        } else {
+                            int64_t *ob = o + tl0;
+#pragma unroll
+                            for (int j = 0; j < 4; j++) ob[64u * j + lane] = (int64_t)v[j];
+                        }
                         tl0 += 256;
                         p0 += 256;
                     }
@@ -693,9 +716,14 @@ __global__ __launch_bounds__(64) void k_v2_emit_x(Geometry g, V2Plan pl,
 #pragma unroll
                     for (int j = 0; j < 4; j++) v[j] = atomicExch(&buf[k[j]], to_slot(wB + ins[j]));
                     // wave-uniform base: the stores take (lane * 8 + 512 j) as offset
-                    int64_t *ob = o + tl0;
+                    if constexpr (MAPPED) {
 #pragma unroll
-                    for (int j = 0; j < 4; j++) ob[64u * j + lane] = from_slot(v[j]);
+                        for (int j = 0; j < 4; j++) put_m(ebase + tl0 + 64u * j + lane, from_slot(v[j]));
+                    } else {
+                        int64_t *ob = o + tl0;
+#pragma unroll
+                        for (int j = 0; j < 4; j++) ob[64u * j + lane] = from_slot(v[j]);
+                    }
                     tl0 += 256;
                     p0 += 256;
                 }
@@ -717,7 +745,10 @@ __global__ __launch_bounds__(64) void k_v2_emit_x(Geometry g, V2Plan pl,
                 const uint32_t in = w * B + feistel(p, lastw ? len_last : B, lastw ? h_last : hB,
                                                     rk + kRoundKeyWords * (w - wl));
                 const uint32_t vv = atomicExch(&buf[kk], to_slot(in));
-                if (tl >= e_lo && tl < e_hi) o[tl] = from_slot(vv);
+                if (tl >= e_lo && tl < e_hi) {
+                    if constexpr (MAPPED) put_m(ebase + tl, from_slot(vv));
+                    else o[tl] = from_slot(vv);
+                }
             }
         }
         p0 += 256;
@@ -743,6 +774,7 @@ __global__ __launch_bounds__(64) void k_v2_emit_x(Geometry g, V2Plan pl,
         tail_keys_t(g, rank, kt, rl, tk);
         const uint32_t hT = feistel_half_bits(P1);
         int64_t *ot = out + (int64_t)rl * count - pos_lo + pl.T;
+        const int64_t etail = (int64_t)rl * count - pos_lo + pl.T;
         const bool whole = pl.T >= pos_lo && pl.T + pl.P1 <= pos_hi;
         if (whole && (P1 & 255u) == 0 && hT <= 8 && P1 == (1u << (2 * hT))) {
             // P1 = 4^hT: no cycle walking; four independent chains per lane, packed in pairs
@@ -757,14 +789,17 @@ __global__ __launch_bounds__(64) void k_v2_emit_x(Geometry g, V2Plan pl,
 #pragma unroll
                 for (int u = 0; u < 4; u++) v[u] = buf[y[u]];
 #pragma unroll
-                for (int u = 0; u < 4; u++)
-                    ot[j0 + 64u * u + lane] = from_slot(v[u]);
+                for (int u = 0; u < 4; u++) {
+                    if constexpr (MAPPED) put_m(etail + j0 + 64u * u + lane, from_slot(v[u]));
+                    else ot[j0 + 64u * u + lane] = from_slot(v[u]);
+                }
             }
         } else {
             for (uint32_t j = lane; j < P1; j += 64) {
                 const int64_t pos = pl.T + j;
                 if (pos < pos_lo || pos >= pos_hi) continue;
-                ot[j] = from_slot(buf[feistel(j, P1, hT, tk)]);
+                if constexpr (MAPPED) put_m(etail + j, from_slot(buf[feistel(j, P1, hT, tk)]));
+                else ot[j] = from_slot(buf[feistel(j, P1, hT, tk)]);
             }
         }
     }
@@ -837,7 +872,7 @@ __global__ __launch_bounds__(256) void k_v2_tail_f(Geometry g, V2Plan pl,
                                                   const RankDesc *__restrict__ ranks,
                                                   int32_t rank_lo, const uint32_t *__restrict__ VAL,
                                                   int64_t pos_lo, int64_t count,
-                                                  int64_t *__restrict__ out, KeyTab kt) {
+                                                  int64_t *__restrict__ out, KeyTab kt, MapArgs ma) {
     const int32_t rl = (int32_t)blockIdx.y;
     const uint32_t rank = (uint32_t)(rank_lo + rl);
     const RankDesc rd = ranks[rank];
@@ -852,7 +887,17 @@ __global__ __launch_bounds__(256) void k_v2_tail_f(Geometry g, V2Plan pl,
         const int64_t pos = pl.T + j;
         if (pos < pos_lo || pos >= pos_hi) continue;
         const uint32_t s = feistel(j, P1, hT, tk);
-        o[pos] = v2_id(slot_value_after(VALr, pl.P1, pl.G - 1, s), rd, g);
+        const int64_t id = v2_id(slot_value_after(VALr, pl.P1, pl.G - 1, s), rd, g);
+        if (ma.fpos) {      // mapped output: the global bucketed map (P1 ids per rank)
+            int32_t f;
+            int64_t of;
+            map_one_bucketed(ma.prefix, ma.F, ma.BT, ma.kb, ma.nb, id, f, of);
+            const int64_t e = (int64_t)rl * count - pos_lo + pos;
+            ma.fpos[e] = f;
+            ma.off[e] = (int32_t)of;
+        } else {
+            o[pos] = id;
+        }
     }
 }
 
@@ -951,16 +996,27 @@ size_t v2_buf_bytes(const Geometry &, int32_t) {
     return 0;   // no HBM slot tables: small pools replay in LDS, big ones in LDS groups
 }
 
+// pss_generate_mapped fuses the map into the V2 replay for pools that fit LDS, on the exchange
+// path: a tile's ids then span ~(L / B + kSegBackWin) windows, a few hundred files at most.  A
+// grouped replay wave covers its rank's whole stream (too many files to stage): generate + map.
+bool v2_mapped_fused(const Geometry &g, int emit_path) {
+    if (v2_grouped(g)) return false;
+    if (emit_path == EMIT_AUTO) emit_path = lds_xchg_ordered() ? EMIT_XCHG : EMIT_PROBE;
+    return emit_path == EMIT_XCHG;
+}
+
 size_t v2_sort_bytes(const Geometry &, int32_t) {
     return 0;   // the tail order is a Feistel bijection: no sort workspace
 }
 
 hipError_t launch_v2_tail_vals(const Geometry &g, const V2Plan &pl, const RankDesc *ranks,
                                int32_t rank_lo, int32_t nr, const uint32_t *VAL, int64_t pos_lo,
-                               int64_t count, int64_t *out, hipStream_t s, KeyTab kt) {
+                               int64_t count, int64_t *out, hipStream_t s, KeyTab kt,
+                               const MapArgs *mapped) {
     const dim3 grid((uint32_t)cdiv(pl.P1 < 65536 ? pl.P1 : 65536, 256), (uint32_t)nr);
+    const MapArgs ma = mapped ? *mapped : MapArgs{};
     hipLaunchKernelGGL(k_v2_tail_f, grid, dim3(256), 0, s, g, pl, ranks, rank_lo, VAL, pos_lo,
-                       count, out, kt);
+                       count, out, kt, ma);
     return hipGetLastError();
 }
 
@@ -982,8 +1038,9 @@ bool v2_stage_split(const Geometry &g, int32_t nr, int emit_path) {
 hipError_t launch_v2(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, int32_t nr,
                      int64_t pos_lo, int64_t count, int64_t *out, uint32_t *VAL, uint32_t *gbuf,
                      uint32_t *sort_ws, int32_t *err, hipStream_t s, const Marker &mk,
-                     int emit_path, int stage) {
+                     int emit_path, int stage, const MapArgs *mapped) {
     if (emit_path == EMIT_AUTO) emit_path = lds_xchg_ordered() ? EMIT_XCHG : EMIT_PROBE;
+    if (mapped && !v2_mapped_fused(g, emit_path)) return hipErrorNotSupported;
     // stage: V2_STAGE_ALL, or the split the runtime pipelines over two streams --
     // V2_STAGE_PRE (key table + last-occurrence pass, writes VAL) then V2_STAGE_EMIT (replay +
     // tail, reads VAL).  Only the LDS exchange path splits; everything else runs whole in the
@@ -1051,13 +1108,17 @@ hipError_t launch_v2(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, 
             const dim3 grid((uint32_t)(nr * ng));
             if (emit_path == EMIT_XCHG) {
                 mk(K_V2_EMIT, s);
-                const size_t need = lds_keys + (size_t)((pl.P1 + 3) & ~3) * 4;
+                const size_t need = lds_keys + (size_t)((pl.P1 + 3) & ~3) * 4 +
+                                    (mapped ? (size_t)kSegLdsWords * 4 : 0);
                 const size_t lds = need > (size_t)pl.emit_lds ? need : (size_t)pl.emit_lds;
                 tail_fused = need_tail && last_emit == pl.G - 1;
                 const int dt = tail_fused ? 1 : 0;
                 const bool pow2 = pl.P1 >= 2 && slot_paired((uint32_t)pl.P1);   // paired draws
-#define PSS_EX(N, P2) hipLaunchKernelGGL((k_v2_emit_x<N, P2>), grid, dim3(64), lds, s, g, pl, ranks, rank_lo, \
-                                         g_lo, ng, (const uint32_t *)VAL, pos_lo, count, dt, out, kt)
+                const MapArgs ma = mapped ? *mapped : MapArgs{};
+#define PSS_EX(N, P2) do { if (mapped) hipLaunchKernelGGL((k_v2_emit_x<N, P2, true>), grid, dim3(64), lds, s, g, pl, ranks, rank_lo, \
+                                         g_lo, ng, (const uint32_t *)VAL, pos_lo, count, dt, out, kt, ma); \
+                           else hipLaunchKernelGGL((k_v2_emit_x<N, P2, false>), grid, dim3(64), lds, s, g, pl, ranks, rank_lo, \
+                                         g_lo, ng, (const uint32_t *)VAL, pos_lo, count, dt, out, kt, ma); } while (0)
                 if (narrow && pow2) PSS_EX(true, true);
                 else if (narrow) PSS_EX(true, false);
                 else if (pow2) PSS_EX(false, true);
@@ -1080,7 +1141,7 @@ hipError_t launch_v2(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, 
     if (!do_emit) return hipGetLastError();
     if (need_tail && !tail_fused) {
         mk(K_V2_TAIL, s);
-        hipError_t e = launch_v2_tail_vals(g, pl, ranks, rank_lo, nr, VAL, pos_lo, count, out, s, kt);
+        hipError_t e = launch_v2_tail_vals(g, pl, ranks, rank_lo, nr, VAL, pos_lo, count, out, s, kt, mapped);
         if (e != hipSuccess) return e;
     }
     mk(-1, s);
@@ -1150,10 +1211,14 @@ hipError_t init_kernel_attributes_v2() {
     PSS_ATTR((k_v2_lastocc<512, false, false>));
     PSS_ATTR((k_v2_lastocc<1024, false, true>));
     PSS_ATTR((k_v2_lastocc<1024, false, false>));
-    PSS_ATTR((k_v2_emit_x<true, true>));
-    PSS_ATTR((k_v2_emit_x<true, false>));
-    PSS_ATTR((k_v2_emit_x<false, true>));
-    PSS_ATTR((k_v2_emit_x<false, false>));
+    PSS_ATTR((k_v2_emit_x<true, true, false>));
+    PSS_ATTR((k_v2_emit_x<true, false, false>));
+    PSS_ATTR((k_v2_emit_x<false, true, false>));
+    PSS_ATTR((k_v2_emit_x<false, false, false>));
+    PSS_ATTR((k_v2_emit_x<true, true, true>));
+    PSS_ATTR((k_v2_emit_x<true, false, true>));
+    PSS_ATTR((k_v2_emit_x<false, true, true>));
+    PSS_ATTR((k_v2_emit_x<false, false, true>));
     PSS_ATTR((k_v2_emit<true, false>));
     PSS_ATTR((k_v2_emit<false, false>));
     PSS_ATTR((k_v2_emit<true, true>));

@@ -285,6 +285,42 @@ def test_v2_emit_paths_match_oracle(path, B, R, F, lo, hi):
         assert np.array_equal(part[:, :c], full[:, pos_lo:pos_lo + c]), (pos_lo, count)
 
 
+@pytest.mark.parametrize("F,lo,hi,R,B,extra", [
+    (40, 5000, 9000, 3, 4096, 0),      # many tiles, a few files per staged interval
+    (3000, 1, 6, 2, 256, 0),           # hundreds of tiny files per interval: global fallback
+    (60, 500, 3000, 4, 1000, 777),     # N past the files' total: reflected ids (fallback)
+    (50, 100, 400, 5, 64, 0),          # tiny windows
+    (13, 1, 50, 5, 100, 0),            # ns < B: tail only
+    (8, 20000, 60000, 2, 16384, 0)])   # the largest LDS pool
+def test_v2_fused_mapping_matches_generate_then_map(F, lo, hi, R, B, extra):
+    """pss_generate_mapped on V2 pools that fit LDS maps inside the replay (LDS segment map per
+    tile, global bucketed map outside it): equal to generate + pss_map for full epochs, ragged
+    and tail-only position ranges, and consecutive epochs served by the lookahead."""
+    rng = np.random.default_rng(F + B + extra)
+    lengths = rng.integers(lo, hi, F)
+    N = int(lengths.sum()) + extra
+    eng = _engine(lengths, N, R, B, 2, seed=5)
+    ns = eng.num_samples
+    for epoch in (0, 1, 2, 3):
+        eng.init_iter(epoch)
+        ids = eng.generate(0, R)
+        fpos, off = eng.map(ids.reshape(-1))
+        fpos, off = fpos.reshape(R, -1), off.reshape(R, -1)
+        for r0, r1, pos_lo, count in ((0, R, 0, ns), (1, R, 7, 3 * B + 5), (0, R - 1, ns // 2, 999),
+                                      (0, R, max(0, ns - 5), 5), (0, R, max(0, ns - B - 3), B + 9)):
+            f2, o2 = eng.generate_mapped(r0, r1, pos_lo, count)
+            eng.check()
+            c = min(count, ns - pos_lo)
+            assert torch.equal(f2[:, :c].cpu(), fpos[r0:r1, pos_lo:pos_lo + c].cpu()), (epoch, r0, pos_lo, count)
+            assert torch.equal(o2[:, :c].long().cpu(), off[r0:r1, pos_lo:pos_lo + c].cpu()), (epoch, r0, pos_lo, count)
+        # the full epoch again as the first call of the epoch (the lookahead's replay stage)
+        eng.init_iter(epoch + 10)
+        f3, o3 = eng.generate_mapped(0, R)
+        ids3 = eng.generate(0, R)
+        fp3, of3 = eng.map(ids3.reshape(-1))
+        assert torch.equal(f3.cpu(), fp3.reshape(R, -1).cpu()) and torch.equal(o3.long().cpu(), of3.reshape(R, -1).cpu())
+
+
 @pytest.mark.parametrize("path", ["xchg", "probe"])
 @pytest.mark.parametrize("B,R,F,lo,hi", [(20000, 3, 30, 5000, 20000), (65536, 2, 40, 10000, 30000),
                                          (16385, 4, 20, 3000, 9000), (131072, 2, 12, 40000, 80000),
