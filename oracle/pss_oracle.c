@@ -334,15 +334,15 @@ int64_t orc_v1_philox_stream(uint64_t key64, uint32_t rank, int64_t start, int64
     return n_out;
 }
 
-/* V2 slot draw of step t (pss_common.h slot_hash): keyed 2-round multiply-xorshift mixer,
- * key = the first two words of Philox block (0, 0, rank, DOM_V2_SLOT). */
+/* V2 slot draw of step t (pss_common.h slot_hash): keyed 2-round multiply-xorshift mixer on
+ * 24-bit operands, key = the first two words of Philox block (0, 0, rank, DOM_V2_SLOT). */
 static inline uint32_t orc_slot_hash(uint32_t t, uint32_t s0, uint32_t s1) {
     uint32_t x = t ^ s0;
     x ^= x >> 16;
-    x *= 0x21F0AAADu;
+    x = (x & 0xFFFFFFu) * 0xA2F0ADu;
     x ^= x >> 15;
     x ^= s1;
-    x *= 0x735A2D97u;
+    x = (x & 0xFFFFFFu) * 0x5A2D97u;
     x ^= x >> 15;
     return x;
 }

@@ -125,18 +125,20 @@ PSS_HD uint32_t feistel_half_bits(uint32_t n) {
 }
 
 // V2 slot draw of step t (t < 2^32: ns >= 2^32 is rejected).  A keyed 32-bit mixer: two
-// multiply-xorshift rounds with the constants of the lowest-bias published 2-round integer
-// hash (16 / 0x21F0AAAD / 15 / 0x735A2D97 / 15), keyed by (s0, s1) = the first two words of the
-// Philox block (0, 0, rank, DOM_V2_SLOT) under the epoch key.  2 multiplies per step instead
-// of a quarter Philox4x32-10 block (5 64-bit multiplies); tests/test_schedule_quality.py
-// checks that the V2 displacement law still matches the reference's.
+// multiply-xorshift rounds (16 / x 0xA2F0AD / 15 / x 0x5A2D97 / 15), keyed by (s0, s1) = the
+// first two words of the Philox block (0, 0, rank, DOM_V2_SLOT) under the epoch key.  Each
+// multiply takes the low 24 bits of its operand (after the xorshift above it has folded the top
+// bits down) by a 24-bit odd constant: one full-rate v_mul_u32_u24 on gfx950, where a 32-bit
+// multiply is quarter rate -- the replay and the last-occurrence pass evaluate this for every
+// step.  tests/test_schedule_quality.py checks the slot law and that the V2 displacement law
+// still matches the reference's.
 PSS_HD uint32_t slot_hash(uint32_t t, uint32_t s0, uint32_t s1) {
     uint32_t x = t ^ s0;
     x ^= x >> 16;
-    x *= 0x21F0AAADu;
+    x = (x & 0xFFFFFFu) * 0xA2F0ADu;
     x ^= x >> 15;
     x ^= s1;
-    x *= 0x735A2D97u;
+    x = (x & 0xFFFFFFu) * 0x5A2D97u;
     x ^= x >> 15;
     return x;
 }

@@ -632,10 +632,10 @@ __global__ __launch_bounds__(64) void k_v2_emit_x(Geometry g, V2Plan pl,
             };
             auto hash2 = [&](uint32_t x) -> uint32_t {   // slot_hash after the s0 xor
                 x ^= x >> 16;
-                x *= 0x21F0AAADu;
+                x = (x & 0xFFFFFFu) * 0xA2F0ADu;
                 x ^= x >> 15;
                 x ^= sk.s1;
-                x *= 0x735A2D97u;
+                x = (x & 0xFFFFFFu) * 0x5A2D97u;
                 x ^= x >> 15;
                 return x;
             };
