@@ -4,6 +4,7 @@
 // history (init_iter, V1:100-132 / V2:124-159) evaluated on the host with a CPython-exact
 // MT19937, the device buffers of the current epoch, and the kernel launches.
 #include <hip/hip_runtime.h>
+#include <sched.h>
 
 #include <chrono>
 #include <cmath>
@@ -45,11 +46,17 @@ int fail(int code, const std::string &msg) {
 
 // The file-order permutation of an epoch (V1:114-117 seed(e + 1), V2:143-144 seed(e)):
 // MT19937 Fisher-Yates of range(F).  A pure function of (version, epoch, F), so it can be
-// computed ahead of time: the sampler prefetches the next two epochs' permutations on worker
+// computed ahead of time: the sampler prefetches the coming epochs' permutations on worker
 // threads while the current epoch runs (init_iter then only composes it with the current
-// order), and the O(F) host shuffle leaves the epoch's critical path.
-std::shared_ptr<std::vector<int32_t>> file_permutation(int32_t version, int64_t epoch, int64_t F) {
-    auto v = std::make_shared<std::vector<int32_t>>(F);
+// order), and the O(F) host shuffle leaves the epoch's critical path.  One permutation costs
+// ~16-25 ns per file, so at F = 80K (8 GPUs of C2 files) it is 1.3-2 ms against a ~0.2 ms
+// epoch on the GPU: the prefetch depth, and the worker count, grow with F (one epoch ahead per
+// 4096 files, 2..16, at most half the CPUs of the process's affinity mask).  Consumed
+// permutation buffers are recycled to the workers (no per-epoch 320 KB mmap / munmap).
+std::shared_ptr<std::vector<int32_t>> file_permutation(int32_t version, int64_t epoch, int64_t F,
+                                                       std::shared_ptr<std::vector<int32_t>> v = nullptr) {
+    if (!v) v = std::make_shared<std::vector<int32_t>>();
+    v->resize(F);
     for (int64_t i = 0; i < F; i++) (*v)[i] = (int32_t)i;
     CPythonMT mt;
     mt.seed(version == 1 ? epoch + 1 : epoch);
@@ -59,7 +66,17 @@ std::shared_ptr<std::vector<int32_t>> file_permutation(int32_t version, int64_t 
 
 class PermPrefetcher {
   public:
-    PermPrefetcher(int32_t version, int64_t F) : version_(version), F_(F) {}
+    PermPrefetcher(int32_t version, int64_t F) : version_(version), F_(F) {
+        int64_t a = F / 4096;
+        // the CPUs this process may run on (one process per GPU shares the node)
+        int64_t hw = (int64_t)std::thread::hardware_concurrency();
+        cpu_set_t set;
+        CPU_ZERO(&set);
+        if (sched_getaffinity(0, sizeof(set), &set) == 0 && CPU_COUNT(&set) > 0) hw = CPU_COUNT(&set);
+        const int64_t cap = hw >= 4 ? hw / 2 : 2;
+        a = a < 2 ? 2 : (a > 16 ? 16 : a);
+        ahead_ = a < cap ? a : (cap < 2 ? 2 : cap);
+    }
     ~PermPrefetcher() {
         {
             std::lock_guard<std::mutex> lk(mu_);
@@ -79,16 +96,22 @@ class PermPrefetcher {
             if (it != done_.end()) { r = it->second; done_.erase(it); }
             // drop stale entries (epochs behind the caller, or far ahead)
             for (auto j = done_.begin(); j != done_.end();)
-                j = (j->first < epoch || j->first > epoch + kAhead) ? done_.erase(j) : std::next(j);
+                j = (j->first < epoch || j->first > epoch + ahead_) ? done_.erase(j) : std::next(j);
         }
-        if (!r) r = file_permutation(version_, epoch, F_);
-        request(epoch + 1);
-        request(epoch + 2);
+        if (!r) r = file_permutation(version_, epoch, F_, spare());
+        for (int64_t d = 1; d <= ahead_; d++) request(epoch + d);
         return r;
+    }
+    // a consumed permutation's buffer back to the workers: no per-epoch allocation (a 320 KB
+    // vector is an mmap, and its free an munmap with a TLB shootdown across the workers)
+    void recycle(std::shared_ptr<std::vector<int32_t>> v) {
+        if (!v || v.use_count() != 1) return;
+        std::lock_guard<std::mutex> lk(mu_);
+        if (free_.size() < (size_t)ahead_ + 2) free_.push_back(std::move(v));
     }
 
   private:
-    static constexpr int64_t kAhead = 2;
+    int64_t ahead_ = 2;
     int32_t version_;
     int64_t F_;
     std::mutex mu_;
@@ -97,7 +120,16 @@ class PermPrefetcher {
     std::map<int64_t, bool> busy_;
     std::vector<int64_t> queue_;
     std::vector<std::thread> workers_;
+    std::vector<std::shared_ptr<std::vector<int32_t>>> free_;
     bool stop_ = false;
+
+    std::shared_ptr<std::vector<int32_t>> spare() {
+        std::lock_guard<std::mutex> lk(mu_);
+        if (free_.empty()) return nullptr;
+        auto v = std::move(free_.back());
+        free_.pop_back();
+        return v;
+    }
 
     void request(int64_t e) {
         {
@@ -105,7 +137,7 @@ class PermPrefetcher {
             if (done_.count(e) || busy_.count(e)) return;
             for (int64_t q : queue_) if (q == e) return;
             queue_.push_back(e);
-            if (workers_.size() < (size_t)kAhead) workers_.emplace_back([this] { run(); });
+            if (workers_.size() < (size_t)ahead_) workers_.emplace_back([this] { run(); });
         }
         cv_.notify_all();
     }
@@ -117,8 +149,10 @@ class PermPrefetcher {
             const int64_t e = queue_.front();
             queue_.erase(queue_.begin());
             busy_[e] = true;
+            std::shared_ptr<std::vector<int32_t>> buf;
+            if (!free_.empty()) { buf = std::move(free_.back()); free_.pop_back(); }
             lk.unlock();
-            auto v = file_permutation(version_, e, F_);
+            auto v = file_permutation(version_, e, F_, std::move(buf));
             lk.lock();
             busy_.erase(e);
             done_[e] = v;
@@ -173,6 +207,7 @@ struct pss_sampler {
     uint64_t seed = 0;
     // history state
     std::vector<int32_t> order;   // self.files as dataset positions
+    std::vector<int32_t> order_next;   // init_iter's composition buffer (kept: no per-epoch allocation)
     std::vector<int32_t> blocks;  // self.blocks
     std::vector<pss::RankDesc> ranks;
     int64_t epoch = 0;
@@ -451,10 +486,12 @@ int pss_init_iter(pss_sampler *h, int64_t epoch) {
         mt.shuffle(h->blocks.data(), h->R);
     }
     if (files) {                                       // cumulative: self.files is re-shuffled
-        std::vector<int32_t> o(h->F);
+        std::vector<int32_t> &o = h->order_next;
+        o.resize(h->F);
         const int32_t *f = fid->data();
         for (int64_t i = 0; i < h->F; i++) o[i] = h->order[f[i]];
         h->order.swap(o);
+        h->perms->recycle(std::move(fid));
     }
     for (int32_t r = 0; r < h->R; r++) h->ranks[r].new_start = h->ns * (int64_t)h->blocks[r];
     h->epoch = epoch;
