@@ -2,7 +2,7 @@
 // synthetic C2 shape (8 ranks x 12.5M ids, B = 4096); prints per-phase clock statistics of
 // the last-occurrence pass.  Build (from the repo root):
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -DPSS_STAMPS -Ipartiallyshuffledistributedsampler_amd/csrc \
-//     -o build/stamp_v2 tools/stamp_v2.hip partiallyshuffledistributedsampler_amd/csrc/pss_bigsort.hip
+//     -o build/stamp_v2 tools/stamp_v2.hip partiallyshuffledistributedsampler_amd/csrc/pss_v2grp.hip
 #include "../partiallyshuffledistributedsampler_amd/csrc/pss_v2.hip"
 #include <cstdio>
 #include <vector>
