@@ -243,6 +243,12 @@ __device__ __forceinline__ uint32_t slot_value_after(const uint32_t *VALr, int64
     return (uint32_t)s;  // initial pool1 = window 0 in slot order
 }
 
+// At most two waves per SIMD.  The replay kernels are sized for eight waves per CU (LDS padding
+// caps the CU), but with <= 128 VGPRs a SIMD could take three or four of them and another one
+// or none; the waves sharing a SIMD then run at a fraction of the issue rate and set the
+// kernel's time.  Claiming VGPRs through v180 (> 512 / 3) leaves room for two per SIMD only.
+#define PSS_TWO_WAVES_PER_SIMD() asm volatile("" ::: "v180")
+
 // Progress-based wave priority.  Co-resident waves with equal work are arbitrated by age, so
 // the older one runs ahead and the younger finishes alone at half the issue rate.  A wave
 // lowers its own priority as it passes 1/4, 1/2 and 3/4 of its work: whoever is behind wins

@@ -464,6 +464,7 @@ __global__ __launch_bounds__(64) void k_v2_emit_x(Geometry g, V2Plan pl,
                                                   int64_t pos_lo, int64_t count, int do_tail,
                                                   int64_t *__restrict__ out, KeyTab kt, MapArgs ma) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+    PSS_TWO_WAVES_PER_SIMD();
 #ifdef PSS_STAMPS
     if (threadIdx.x == 0 && blockIdx.x < (1u << 16)) pss_stamps[blockIdx.x][2] = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -946,7 +947,15 @@ V2Plan v2_plan(const Geometry &g, int32_t nr) {
     if (wpc >= 4) wpc &= ~3;
     if (wpc_env && wpc_env < wpc) wpc = wpc_env;
     p.emit_lds = lds;
-    if (wpc >= 1 && kCuLdsBytes / (wpc + 1) >= lds) p.emit_lds = kCuLdsBytes / (wpc + 1) + 16;
+    // No LDS padding: k_v2_emit_x claims VGPRs for two waves per SIMD (PSS_TWO_WAVES_PER_SIMD),
+    // which caps a CU at eight replay waves, and the LDS left over (25 KB at P1 = 4096) takes a
+    // last-occurrence workgroup of the next epoch's lookahead beside them (C2 487-496 ->
+    // 511-516 G idx/s, same box).  PSS_V2_LDS_PAD=1 pads as round 1 did (A/B knob).
+    static const bool pad = [] {
+        const char *e = getenv("PSS_V2_LDS_PAD");
+        return e && e[0] == '1';
+    }();
+    if (pad && wpc >= 1 && kCuLdsBytes / (wpc + 1) >= lds) p.emit_lds = kCuLdsBytes / (wpc + 1) + 16;
     static const int64_t lds_env = [] {   // experiment knob: explicit emit LDS bytes per wave
         const char *e = getenv("PSS_V2_EMIT_LDS");
         return (int64_t)(e ? atol(e) : 0);
