@@ -122,10 +122,13 @@ int pss_digest_range_host(int64_t lo, int64_t hi, uint64_t *acc);
 /* device ordinal of the handle, or PSS_DEVICE_CPU */
 int pss_device(const pss_sampler *h, int32_t *device);
 
-/* Kernel timing: while enabled, every launch of this handle is bracketed by HIP events on
- * its stream.  pss_profile_read synchronises on them and returns, per kernel kind
- * (0 scan, 1 v1_window, 2 v2_lastocc, 3 v2_emit, 4 v2_tail, 5 map, 6 partition, 7 digest),
- * the summed milliseconds and launch counts since the last read; it then clears them. */
+/* Kernel timing: enable = 1 brackets every launch of this handle with HIP events on its
+ * stream; enable = n >= 2 only the index-generation kernels (v1_window, v2_emit), every
+ * (n - 1)-th of their launches (two events per timed generate: live timing of the dominant
+ * kernel at a fraction of the events' cost).  pss_profile_read synchronises on
+ * them and returns, per kernel kind (0 scan, 1 v1_window, 2 v2_lastocc, 3 v2_emit, 4 v2_tail,
+ * 5 map, 6 partition, 7 digest), the summed milliseconds and launch counts since the last
+ * read; it then clears them. */
 int pss_profile(pss_sampler *h, int32_t enable);
 int pss_profile_read(pss_sampler *h, double *total_ms, int64_t *launches, int32_t nkinds);
 

@@ -63,6 +63,8 @@ V2Plan v2_plan(const Geometry &g, int32_t nr);
 constexpr int32_t kArgRanks = 128;
 constexpr int32_t kArgRanksMax = 1024;
 hipError_t launch_put_ranks(const RankDesc *host, int32_t R, RankDesc *dst, hipStream_t s);
+// up to kArgRanks rank descriptors by value (kernel arguments): [0, nr) = ranks rank_lo..
+struct RankArgs { RankDesc r[kArgRanks]; };
 
 // exclusive prefix over the shuffled file order: prefix[f] = sum_{j<f} len[order[j]]
 // scratch: scan_scratch_words(F) words
@@ -137,7 +139,11 @@ hipError_t launch_v2(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, 
                      int64_t pos_lo, int64_t count, int64_t *out, uint32_t *val_ws,
                      uint32_t *buf_ws, uint32_t *sort_ws, int32_t *err, hipStream_t s,
                      const Marker &mk = Marker(), int emit_path = EMIT_AUTO,
-                     int stage = V2_STAGE_ALL, const MapArgs *mapped = nullptr);
+                     int stage = V2_STAGE_ALL, const MapArgs *mapped = nullptr,
+                     const RankArgs *rank_args = nullptr);
+// launch_v2 can take this launch's rank descriptors by value (rank_args, nr <= kArgRanks): the
+// exchange replay then reads no device rank table, and the epoch path launches no upload
+bool v2_ranks_by_value(const Geometry &g, int32_t nr, int emit_path);
 // mapped != nullptr (v2_mapped_fused shapes only): (file, offset) instead of ids
 bool v2_mapped_fused(const Geometry &g, int emit_path);
 size_t v2_val_bytes(const Geometry &g, int32_t nr);
@@ -153,7 +159,8 @@ size_t v2_grp_val_bytes(const Geometry &g, int32_t nr);
 int64_t v2_grp_tiles(const Geometry &g, int32_t nr);   // tiles per (rank, group) stream
 hipError_t launch_v2_grp(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, int32_t nr,
                          int64_t pos_lo, int64_t count, int64_t *out, uint32_t *val_ws,
-                         hipStream_t s, const Marker &mk, bool ordered, int stage);
+                         hipStream_t s, const Marker &mk, bool ordered, int stage,
+                         const RankArgs *rank_args = nullptr);
 hipError_t init_kernel_attributes_v2grp();
 // launch_v2 splits into V2_STAGE_PRE / V2_STAGE_EMIT for this shape and emit path (EMIT_AUTO resolved)
 bool v2_stage_split(const Geometry &g, int32_t nr, int emit_path);

@@ -326,8 +326,6 @@ __global__ __launch_bounds__(64) void k_v1_feistel(Geometry g, V1Plan vp, const 
 // ------------------------------------------------------------------------------------------
 static inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
-struct RankArgs { RankDesc r[kArgRanks]; };
-
 __global__ __launch_bounds__(kArgRanks) void k_put_ranks(RankArgs a, int32_t n, RankDesc *dst) {
     if ((int32_t)threadIdx.x < n) dst[threadIdx.x] = a.r[threadIdx.x];
 }

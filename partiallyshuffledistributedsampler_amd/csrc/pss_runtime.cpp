@@ -231,6 +231,8 @@ struct pss_sampler {
     bool upload_pending = false;
     // optional per-kernel timing (pss_profile): events recorded around every launch
     bool profiling = false;
+    int32_t profile_mode = 0;     // 1 every launch, n >= 2 every (n-1)-th generation launch
+    int64_t prof_seen = 0;        // generation launches seen in mode >= 2
     std::vector<hipEvent_t> ev_pool;
     size_t ev_used = 0;
     struct Span { int kind; size_t a, b; };
@@ -277,6 +279,13 @@ namespace {
 // Marker callback: close the open span (if any) and open one for `kind` (kind < 0: close).
 void prof_mark(void *ctx, int kind, hipStream_t s) {
     pss_sampler *h = (pss_sampler *)ctx;
+    // mode n >= 2: generation kernels only, every (n - 1)-th launch; any other mark just closes
+    // (nothing open: no event)
+    if (h->profile_mode >= 2) {
+        if (kind != pss::K_V1 && kind != pss::K_V2_EMIT) kind = -1;
+        else if (h->prof_seen++ % (h->profile_mode - 1) != 0) kind = -1;
+    }
+    if (kind < 0 && h->open_kind < 0) return;
     if (h->ev_used == h->ev_pool.size()) {
         hipEvent_t e;
         if (hipEventCreate(&e) != hipSuccess) return;
@@ -545,7 +554,7 @@ bool lookahead_on() {
 // call had this shape at epoch - 1, the pass of epoch + 1 on the side stream.
 int generate_v2_lookahead(pss_sampler *h, const pss::Geometry &g, int32_t rank_lo, int32_t nr,
                           int64_t pos_lo, int64_t count, int64_t *out_dev, hipStream_t s,
-                          const pss::Marker &mk, const pss::MapArgs *ma) {
+                          const pss::Marker &mk, const pss::MapArgs *ma, const pss::RankArgs *ra) {
     constexpr int NB = pss_sampler::kLaBufs;
     const size_t words = (pss::v2_val_bytes(g, nr) + sizeof(uint32_t) - 1) / sizeof(uint32_t);
     const size_t bwords = (pss::v2_buf_bytes(g, nr) + sizeof(uint32_t) - 1) / sizeof(uint32_t);
@@ -597,7 +606,7 @@ int generate_v2_lookahead(pss_sampler *h, const pss::Geometry &g, int32_t rank_l
         PSS_HIP(hipStreamWaitEvent(s, h->ev_done[buf], 0));
         PSS_HIP(pss::launch_v2(g, h->d_ranks.p, rank_lo, nr, pos_lo, count, out_dev, V[buf]->p,
                                bwords ? W[buf]->p : nullptr, nullptr, h->d_err.p, s, mk, h->emit_path,
-                               pss::V2_STAGE_EMIT, ma));
+                               pss::V2_STAGE_EMIT, ma, ra));
     } else {
         // a buffer no queued lookahead holds, after its last reader and its last writer
         for (int b = 0; b < NB && buf < 0; b++) if (!held(b)) buf = b;
@@ -606,7 +615,7 @@ int generate_v2_lookahead(pss_sampler *h, const pss::Geometry &g, int32_t rank_l
         PSS_HIP(hipStreamWaitEvent(s, h->ev_done[buf], 0));
         PSS_HIP(pss::launch_v2(g, h->d_ranks.p, rank_lo, nr, pos_lo, count, out_dev, V[buf]->p,
                                bwords ? W[buf]->p : nullptr, nullptr, h->d_err.p, s, mk, h->emit_path,
-                               pss::V2_STAGE_ALL, ma));
+                               pss::V2_STAGE_ALL, ma, ra));
     }
     PSS_HIP(hipEventRecord(h->ev_read[buf], s));
     const bool sequential = h->last_valid && h->last_shape == shape && h->last_epoch == h->epoch - 1;
@@ -676,11 +685,24 @@ int generate_impl(pss_sampler *h, int32_t rank_lo, int32_t rank_hi, int64_t pos_
     }
     DeviceGuard dg(h->device);
     hipStream_t s = (hipStream_t)stream;
-    int rc = prepare(h, s);
+    if (!h->iterated) return fail(PSS_ESTATE, "pss_init_iter must be called before device work");
+    int rc = ensure_device(h);
     if (rc) return rc;
     const int32_t nr = rank_hi - rank_lo;
-    if (nr == 0 || count == 0 || pos_lo >= h->ns) return PSS_OK;
     const pss::Geometry g = h->geometry();
+    // the V2 exchange replay takes its ranks' descriptors as kernel arguments: no upload kernel
+    // ahead of it on the epoch path (the device table is refreshed on first other use)
+    const bool by_value = h->version == 2 && h->order_mode == PSS_ORDER_COUNTER && nr > 0 &&
+                          pss::v2_ranks_by_value(g, nr, h->emit_path);
+    pss::RankArgs ra;
+    if (by_value) {
+        for (int32_t i = 0; i < nr; i++) ra.r[i] = h->ranks[rank_lo + i];
+    } else {
+        rc = prepare(h, s);
+        if (rc) return rc;
+    }
+    const pss::RankArgs *rap = by_value ? &ra : nullptr;
+    if (nr == 0 || count == 0 || pos_lo >= h->ns) return PSS_OK;
     const pss::Marker mk = marker_of(h);
     auto words = [](size_t bytes) { return (bytes + sizeof(uint32_t) - 1) / sizeof(uint32_t); };
     if (h->version == 1 && h->order_mode == PSS_ORDER_EXACT && g.shuffle) {
@@ -698,7 +720,7 @@ int generate_impl(pss_sampler *h, int32_t rank_lo, int32_t rank_hi, int64_t pos_
         PSS_HIP(pss::launch_v2_exact(g, h->d_ranks.p, rank_lo, nr, pos_lo, count, h->epoch, out_dev,
                                      h->d_sort.p, s));
     } else if (lookahead_on() && pss::v2_stage_split(g, nr, h->emit_path)) {
-        return generate_v2_lookahead(h, g, rank_lo, nr, pos_lo, count, out_dev, s, mk, ma);
+        return generate_v2_lookahead(h, g, rank_lo, nr, pos_lo, count, out_dev, s, mk, ma, rap);
     } else {
         for (auto &p : h->pend) p.valid = false;
         h->last_valid = false;
@@ -712,7 +734,7 @@ int generate_impl(pss_sampler *h, int32_t rank_lo, int32_t rank_hi, int64_t pos_
         if (sb) PSS_HIP(h->d_sort.ensure(words(sb)));
         PSS_HIP(pss::launch_v2(g, h->d_ranks.p, rank_lo, nr, pos_lo, count, out_dev, h->d_val.p,
                                h->d_buf.p, h->d_sort.p, h->d_err.p, s, mk, h->emit_path,
-                               pss::V2_STAGE_ALL, ma));
+                               pss::V2_STAGE_ALL, ma, rap));
         if (h->ev_read[0]) PSS_HIP(hipEventRecord(h->ev_read[0], s));   // last user of d_val
     }
     return PSS_OK;
@@ -766,7 +788,10 @@ int pss_emit_path(pss_sampler *h, int32_t *path) {
 
 int pss_profile(pss_sampler *h, int32_t enable) {
     if (!h) return fail(PSS_EINVAL, "NULL handle");
+    if (enable < 0) return fail(PSS_EINVAL, "profile mode must be >= 0");
     h->profiling = enable != 0;
+    h->profile_mode = enable;
+    h->prof_seen = 0;
     h->spans.clear();
     h->ev_used = 0;
     h->open_kind = -1;

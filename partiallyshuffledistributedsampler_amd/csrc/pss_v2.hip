@@ -462,7 +462,8 @@ __global__ __launch_bounds__(64) void k_v2_emit_x(Geometry g, V2Plan pl,
                                                   int32_t rank_lo, int64_t g_lo, int64_t ng,
                                                   const uint32_t *__restrict__ VAL,
                                                   int64_t pos_lo, int64_t count, int do_tail,
-                                                  int64_t *__restrict__ out, KeyTab kt, MapArgs ma) {
+                                                  int64_t *__restrict__ out, KeyTab kt, MapArgs ma,
+                                                  RankArgs ra, int use_ra) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     PSS_TWO_WAVES_PER_SIMD();
 #ifdef PSS_STAMPS
@@ -481,7 +482,7 @@ __global__ __launch_bounds__(64) void k_v2_emit_x(Geometry g, V2Plan pl,
     const int32_t rl = (int32_t)(blockIdx.x / ngu);
     const uint32_t tile = (uint32_t)g_lo + (blockIdx.x - (uint32_t)rl * ngu);
     const uint32_t rank = (uint32_t)(rank_lo + rl);
-    const RankDesc rd = ranks[rank];
+    const RankDesc rd = use_ra ? ra.r[rl] : ranks[rank];   // (kernel argument: a scalar load)
     const uint32_t twoB = pl.twoB;
     const uint32_t old32 = (uint32_t)rd.old_start, new32 = (uint32_t)rd.new_start;
     const uint32_t N32 = (uint32_t)g.N;
@@ -1029,6 +1030,11 @@ hipError_t launch_v2_tail_vals(const Geometry &g, const V2Plan &pl, const RankDe
     return hipGetLastError();
 }
 
+bool v2_ranks_by_value(const Geometry &g, int32_t nr, int emit_path) {
+    if (emit_path == EMIT_AUTO) emit_path = lds_xchg_ordered() ? EMIT_XCHG : EMIT_PROBE;
+    return emit_path == EMIT_XCHG && nr >= 1 && nr <= kArgRanks;   // k_v2_emit_x, k_g_emit
+}
+
 bool v2_stage_split(const Geometry &g, int32_t nr, int emit_path) {
     if (emit_path == EMIT_AUTO) emit_path = lds_xchg_ordered() ? EMIT_XCHG : EMIT_PROBE;
     // grouped pools always split: their pre-pass (key table, last occurrences of tiled
@@ -1047,9 +1053,10 @@ bool v2_stage_split(const Geometry &g, int32_t nr, int emit_path) {
 hipError_t launch_v2(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, int32_t nr,
                      int64_t pos_lo, int64_t count, int64_t *out, uint32_t *VAL, uint32_t *gbuf,
                      uint32_t *sort_ws, int32_t *err, hipStream_t s, const Marker &mk,
-                     int emit_path, int stage, const MapArgs *mapped) {
+                     int emit_path, int stage, const MapArgs *mapped, const RankArgs *rank_args) {
     if (emit_path == EMIT_AUTO) emit_path = lds_xchg_ordered() ? EMIT_XCHG : EMIT_PROBE;
     if (mapped && !v2_mapped_fused(g, emit_path)) return hipErrorNotSupported;
+    if (rank_args && !v2_ranks_by_value(g, nr, emit_path)) return hipErrorInvalidValue;
     // stage: V2_STAGE_ALL, or the split the runtime pipelines over two streams --
     // V2_STAGE_PRE (key table + last-occurrence pass, writes VAL) then V2_STAGE_EMIT (replay +
     // tail, reads VAL).  Only the LDS exchange path splits; everything else runs whole in the
@@ -1061,7 +1068,7 @@ hipError_t launch_v2(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, 
     const bool do_pre = stage != V2_STAGE_EMIT, do_emit = stage != V2_STAGE_PRE;
     if (v2_grouped(g))   // pools beyond LDS: the grouped slot machine (pss_v2grp.hip)
         return launch_v2_grp(g, ranks, rank_lo, nr, pos_lo, count, out, VAL, s, mk,
-                             emit_path == EMIT_XCHG, stage);
+                             emit_path == EMIT_XCHG, stage, rank_args);
     (void)err; (void)sort_ws; (void)gbuf;
     const V2Plan pl = v2_plan(g, nr);
     const int64_t pos_hi = pos_lo + count < g.ns ? pos_lo + count : g.ns;
@@ -1124,10 +1131,13 @@ hipError_t launch_v2(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, 
                 const int dt = tail_fused ? 1 : 0;
                 const bool pow2 = pl.P1 >= 2 && slot_paired((uint32_t)pl.P1);   // paired draws
                 const MapArgs ma = mapped ? *mapped : MapArgs{};
+                RankArgs ra;
+                const int use_ra = rank_args ? 1 : 0;
+                if (rank_args) ra = *rank_args;
 #define PSS_EX(N, P2) do { if (mapped) hipLaunchKernelGGL((k_v2_emit_x<N, P2, true>), grid, dim3(64), lds, s, g, pl, ranks, rank_lo, \
-                                         g_lo, ng, (const uint32_t *)VAL, pos_lo, count, dt, out, kt, ma); \
+                                         g_lo, ng, (const uint32_t *)VAL, pos_lo, count, dt, out, kt, ma, ra, use_ra); \
                            else hipLaunchKernelGGL((k_v2_emit_x<N, P2, false>), grid, dim3(64), lds, s, g, pl, ranks, rank_lo, \
-                                         g_lo, ng, (const uint32_t *)VAL, pos_lo, count, dt, out, kt, ma); } while (0)
+                                         g_lo, ng, (const uint32_t *)VAL, pos_lo, count, dt, out, kt, ma, ra, use_ra); } while (0)
                 if (narrow && pow2) PSS_EX(true, true);
                 else if (narrow) PSS_EX(true, false);
                 else if (pow2) PSS_EX(false, true);
@@ -1149,6 +1159,12 @@ hipError_t launch_v2(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, 
     }
     if (!do_emit) return hipGetLastError();
     if (need_tail && !tail_fused) {
+        // the tail kernel reads the device rank table: this launch's ranks first, when they came
+        // by value (the runtime uploads the whole table later, on first other use)
+        if (rank_args) {
+            hipError_t e = launch_put_ranks(rank_args->r, nr, const_cast<RankDesc *>(ranks) + rank_lo, s);
+            if (e != hipSuccess) return e;
+        }
         mk(K_V2_TAIL, s);
         hipError_t e = launch_v2_tail_vals(g, pl, ranks, rank_lo, nr, VAL, pos_lo, count, out, s, kt, mapped);
         if (e != hipSuccess) return e;

@@ -282,7 +282,7 @@ __global__ __launch_bounds__(64) void k_g_emit(Geometry g, GPlan pl, const RankD
                                                int32_t rank_lo, const uint32_t *__restrict__ KT,
                                                const uint32_t *__restrict__ VAL, int do_tail,
                                                int64_t pos_lo, int64_t count,
-                                               int64_t *__restrict__ out) {
+                                               int64_t *__restrict__ out, RankArgs ra, int use_ra) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     uint32_t *buf = smem;                                            // Smax slot words
     g_lds_vu8 *mark = (g_lds_vu8 *)(smem + pl.Smax);                  // !ORDERED: Smax bytes
@@ -308,7 +308,7 @@ __global__ __launch_bounds__(64) void k_g_emit(Geometry g, GPlan pl, const RankD
         full_emit = tf >= pos_lo && tl < pos_hi;
     }
     if (!emits && !drain) return;
-    const RankDesc rd = ranks[rank];
+    const RankDesc rd = use_ra ? ra.r[rl] : ranks[rank];   // (kernel argument: a scalar load)
     GIds<NARROW> ids;
     ids.twoB = pl.twoB;
     ids.old32 = (uint32_t)rd.old_start; ids.new32 = (uint32_t)rd.new_start;
@@ -522,7 +522,8 @@ size_t v2_grp_val_bytes(const Geometry &g, int32_t nr) {
 
 hipError_t launch_v2_grp(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, int32_t nr,
                          int64_t pos_lo, int64_t count, int64_t *out, uint32_t *VALws,
-                         hipStream_t s, const Marker &mk, bool ordered, int stage) {
+                         hipStream_t s, const Marker &mk, bool ordered, int stage,
+                         const RankArgs *rank_args) {
     const int64_t pos_hi = pos_lo + count < g.ns ? pos_lo + count : g.ns;
     if (nr <= 0 || pos_hi <= pos_lo) return hipSuccess;
     const GPlan pl = gplan(g, nr, gcus());
@@ -548,10 +549,14 @@ hipError_t launch_v2_grp(const Geometry &g, const RankDesc *ranks, int32_t rank_
     size_t lds = (size_t)pl.Smax * 4 + (ordered ? 0 : (size_t)pl.Smax) + 16;
     if (lds * 9 <= 160 * 1024) lds = 160 * 1024 / 9 + 16;
     const int dt = need_tail ? 1 : 0;
+    RankArgs ra;
+    const int use_ra = rank_args ? 1 : 0;
+    if (rank_args) ra = *rank_args;
     const bool packed = pl.hB <= 8;
     const bool pow2 = pl.gr.r == 0 && (pl.gr.q & (pl.gr.q - 1u)) == 0u;   // every group 2^b slots
 #define PSS_GE(O, N, PK, P2) hipLaunchKernelGGL((k_g_emit<O, N, PK, P2>), grid, dim3(64), lds, s, g, pl, ranks, \
-                                                rank_lo, (const uint32_t *)KT, (const uint32_t *)VAL, dt, pos_lo, count, out)
+                                                rank_lo, (const uint32_t *)KT, (const uint32_t *)VAL, dt, pos_lo, count, out, \
+                                                ra, use_ra)
 #define PSS_GE2(O, N) do { if (packed && pow2) PSS_GE(O, N, true, true); else if (packed) PSS_GE(O, N, true, false); \
                            else if (pow2) PSS_GE(O, N, false, true); else PSS_GE(O, N, false, false); } while (0)
     if (ordered && narrow) PSS_GE2(true, true);

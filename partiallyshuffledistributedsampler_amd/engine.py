@@ -221,9 +221,11 @@ class IndexEngine:
     KERNEL_KINDS = ("scan", "v1_window", "v2_lastocc", "v2_emit", "v2_tail", "map",
                     "partition", "digest")
 
-    def profile(self, enable=True):
-        """Bracket every launch of this handle with HIP events on its stream."""
-        _lib.call("pss_profile", self._h, int(bool(enable)))
+    def profile(self, enable=True, generation_only=False, every=1):
+        """Bracket every launch of this handle with HIP events on its stream (generation_only:
+        only the index-generation kernels, two events per timed generate, every `every`-th)."""
+        mode = 0 if not enable else (1 + max(1, int(every)) if generation_only else 1)
+        _lib.call("pss_profile", self._h, mode)
 
     def profile_read(self):
         """{kind: (total_ms, launches)} since the last read (synchronises on the events)."""
