@@ -271,36 +271,9 @@ __global__ __launch_bounds__(64) void k_v1_feistel(Geometry g, V1Plan vp, const 
     };
     const uint32_t *ktr = kt + (int64_t)rl * vp.nw * kRoundKeyWords;
     const int64_t B = vp.B;
-    for (int64_t sb = sb0; sb < sb1; sb++) {
+    // one super-block through the general path (range edges, short or cycle-walking windows)
+    auto slow_sb = [&](int64_t sb) {
         const int64_t p0 = sb * 256;
-        const int64_t w = p0 / B;                    // wave-uniform
-        const int64_t wB = w * B;
-        const bool fast = vp.fast_ok && p0 >= pos_lo && p0 + 256 <= pos_hi && wB + B <= g.ns &&
-                          p0 + 256 <= wB + B;
-        if (fast) {
-            // whole super-block inside one full window of 4^hB elements: no cycle walking
-            const uint32_t *kw = ktr + (w - vp.w_lo) * kRoundKeyWords;
-            const uint32_t x0 = (uint32_t)(p0 - wB);
-            const int64_t base = start + wB;
-            uint32_t y[4];
-            if constexpr (PACKED) {
-                uint32_t kp[kFeistelRounds];
-#pragma unroll
-                for (int i = 0; i < kFeistelRounds; i++)
-                    kp[i] = (__builtin_amdgcn_readfirstlane(kw[i]) & 0xFFFFu) * 0x10001u;
-                const uint32_t x[4] = {x0 + lane, x0 + 64u + lane, x0 + 128u + lane, x0 + 192u + lane};
-                feistel4_pk16(x, vp.hB, kp, y);
-            } else {
-                uint32_t kk[kFeistelRounds];
-#pragma unroll
-                for (int i = 0; i < kFeistelRounds; i++) kk[i] = __builtin_amdgcn_readfirstlane(kw[i]);
-#pragma unroll
-                for (int j = 0; j < 4; j++) y[j] = feistel_once(x0 + 64u * j + lane, vp.hB, kk);
-            }
-#pragma unroll
-            for (int j = 0; j < 4; j++) put(p0 + 64 * j + lane, wrap_id(base + y[j], g.N));
-            continue;
-        }
 #pragma unroll
         for (int j = 0; j < 4; j++) {
             const int64_t p = p0 + 64 * j + lane;
@@ -317,6 +290,43 @@ __global__ __launch_bounds__(64) void k_v1_feistel(Geometry g, V1Plan vp, const 
                                      feistel_half_bits((uint32_t)len), kk);
             }
             put(p, wrap_id(start + y, g.N));
+        }
+    };
+    int64_t sb = sb0;
+    while (sb < sb1) {
+        if (!vp.fast_ok) { slow_sb(sb++); continue; }
+        // the wave's super-blocks inside window w (B % 256 == 0: super-blocks never straddle
+        // windows): one division and one key load per window, not per super-block
+        const int64_t w = (sb * 256) / B;
+        const int64_t wB = w * B;
+        const int64_t sb_w_end = (wB + B) / 256 < sb1 ? (wB + B) / 256 : sb1;
+        if (wB + B > g.ns) {   // the short last window: cycle walking
+            for (; sb < sb_w_end; sb++) slow_sb(sb);
+            continue;
+        }
+        const uint32_t *kw = ktr + (w - vp.w_lo) * kRoundKeyWords;
+        const int64_t base = start + wB;
+        uint32_t kp[kFeistelRounds];
+#pragma unroll
+        for (int i = 0; i < kFeistelRounds; i++) {
+            const uint32_t k = __builtin_amdgcn_readfirstlane(kw[i]);
+            kp[i] = PACKED ? (k & 0xFFFFu) * 0x10001u : k;
+        }
+        for (; sb < sb_w_end; sb++) {
+            const int64_t p0 = sb * 256;
+            if (p0 < pos_lo || p0 + 256 > pos_hi) { slow_sb(sb); continue; }
+            // whole super-block inside one full window of 4^hB elements: no cycle walking
+            const uint32_t x0 = (uint32_t)(p0 - wB);
+            uint32_t y[4];
+            if constexpr (PACKED) {
+                const uint32_t x[4] = {x0 + lane, x0 + 64u + lane, x0 + 128u + lane, x0 + 192u + lane};
+                feistel4_pk16(x, vp.hB, kp, y);
+            } else {
+#pragma unroll
+                for (int j = 0; j < 4; j++) y[j] = feistel_once(x0 + 64u * j + lane, vp.hB, kp);
+            }
+#pragma unroll
+            for (int j = 0; j < 4; j++) put(p0 + 64 * j + lane, wrap_id(base + y[j], g.N));
         }
     }
 }
@@ -463,7 +473,12 @@ hipError_t launch_v1(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, 
     vp.fast_ok = g.shuffle && !vp.walk_full && (g.B % 256) == 0;
     // ~16 super-blocks (4096 positions, 32 KB of output) per wave, at least 8 waves per CU
     const int64_t total = (int64_t)nr * vp.nsb;
-    int64_t per = 16;
+    static const int64_t per_env = [] {   // A/B knob: super-blocks per wave
+        const char *e = getenv("PSS_V1_PER_WAVE");
+        const long v = e ? atol(e) : 0;
+        return (int64_t)(v > 0 && v <= 1024 ? v : 16);
+    }();
+    int64_t per = per_env;
     while (per > 1 && total / per < 8 * 256) per >>= 1;
     vp.per_wave = per;
     const int64_t waves = (int64_t)nr * cdiv(vp.nsb, per);
