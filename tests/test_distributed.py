@@ -1,8 +1,9 @@
-"""Multi-process (gloo, world_size 2, CPU) coverage of the N>1 path: logical-rank sharding,
-the (count, digest) all-gather and the coverage check.  Each process drives the product's
+"""Multi-process (gloo, world_size 2) coverage of the N>1 path: logical-rank sharding, the
+(count, digest) all-gather and the coverage check.  On CPU each process drives the product's
 IndexEngine in the library's CPU mode (the same schedule the GPU runs, bit for bit -- see
 test_cpu_mode.py / test_gpu_parity.py) and digests its shard with the library's host digest;
-the coverage target comes from the oracle."""
+the -m gpu variant drives the HIP engine on cuda:0 from both processes.  The coverage target
+comes from the oracle."""
 import os
 import socket
 
@@ -22,7 +23,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, version, corrupt, q):
+def _worker(rank, world, port, version, corrupt, q, device="cpu"):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     os.environ.setdefault("PSS_CPU_THREADS", "2")
@@ -32,14 +33,16 @@ def _worker(rank, world, port, version, corrupt, q):
     rng = np.random.default_rng(2)
     lengths = rng.integers(100, 900, 50)
     N, R, B, seed, epoch = int(lengths.sum()), 7, 128, 11, 4
-    eng = IndexEngine(lengths, N, R, B, version, seed=seed, device="cpu")
+    eng = IndexEngine(lengths, N, R, B, version, seed=seed, device=device)
     ns = eng.num_samples
     eng.init_iter(epoch)
     lo, hi = shard(R, world, rank)
-    ids = eng.generate(lo, hi)                     # [hi - lo, ns] host tensor
+    ids = eng.generate(lo, hi)                     # [hi - lo, ns] host or device tensor
+    if device != "cpu":
+        eng.check()
     if corrupt and rank == 1:
         ids[-1, 0] = ids[-1, 1]                    # a duplicate + a drop: the digest must notice
-    pairs = gather_pairs(ids.numel(), as_u64(digest(ids.view(-1))))
+    pairs = gather_pairs(ids.numel(), as_u64(digest(ids.view(-1))))   # gloo, host tensors
     pad = ns * R - N
     expect = (O.digest_range(0, N) + O.digest_range(0, pad)) & ((1 << 64) - 1)
     q.put((rank, coverage_ok(pairs, ns, R, expect), len(pairs)))
@@ -56,6 +59,24 @@ def test_two_process_coverage(version, corrupt):
     for p in procs:
         p.start()
     res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert [r[2] for r in res] == [2, 2]
+    assert all(r[1] == (not corrupt) for r in res)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("version,corrupt", [(2, False), (1, False), (2, True)])
+def test_two_process_coverage_gpu(version, corrupt):
+    """The same flow with both processes driving the HIP engine on cuda:0 (the one-GPU stand-in
+    for two GPUs): GPU generation -> GPU digest -> gloo all-gather -> coverage check."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, version, corrupt, q, 0)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=180) for _ in procs)
     for p in procs:
         p.join(timeout=60)
     assert [r[2] for r in res] == [2, 2]
