@@ -6,6 +6,8 @@ beyond 16384 and B > ns all occur), shuffle on/off, a seed and a start epoch.
 
   * CPU (`-m "not gpu"`): the library's CPU mode == the oracle twin (oracle/pss_oracle.c) for
     every rank, plus full coverage of [0, N) and the wrap-around pad (V1:161-163);
+  * exact order (`order="exact"`, the reference's MT19937 draws) on the GPU == CPU mode, with
+    B capped at the GPU's LDS bounds (V1 8192, V2 4096; pss.h);
   * GPU (`-m gpu`): the HIP kernels (through the C-ABI) == CPU mode over three consecutive
     epochs (the V2 epoch lookahead), on both V2 emit paths, for random (rank, position)
     sub-ranges, the id -> (file, offset) map and the fused mapped generation, with the device
@@ -19,8 +21,9 @@ from oracle import oracle as O
 
 pss = pytest.importorskip("partiallyshuffledistributedsampler_amd.engine")
 
-N_CPU_CASES = 48
-N_GPU_CASES = 40
+N_CPU_CASES = 96
+N_GPU_CASES = 200
+N_EXACT_CASES = 48
 MAX_N = 2_000_000
 
 
@@ -122,3 +125,21 @@ def test_gpu_fuzz_equals_cpu_mode(i, device=0):
             ref_f = fc.numpy().reshape(R, ns)[r0:r1, p0:p0 + cnt]
             ref_o = oc.numpy().reshape(R, ns)[r0:r1, p0:p0 + cnt]
             assert np.array_equal(mf.cpu().numpy(), ref_f) and np.array_equal(mo.cpu().numpy(), ref_o)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("i", range(N_EXACT_CASES))
+def test_gpu_fuzz_exact_order_equals_cpu_mode(i, device=0):
+    g = _geometry(i)
+    B = min(g["B"], 8192 if g["version"] == 1 else 4096)
+    args = (g["lengths"], g["N"], g["R"], B, g["version"])
+    kw = dict(shuffle=g["shuffle"], seed=g["seed"], order="exact")
+    gpu = pss.IndexEngine(*args, device=device, **kw)
+    cpu = pss.IndexEngine(*args, device="cpu", **kw)
+    R = g["R"]
+    for epoch in (g["epoch"], g["epoch"] + 1):
+        gpu.init_iter(epoch)
+        cpu.init_iter(epoch)
+        a = gpu.generate(0, R)
+        gpu.check()
+        assert np.array_equal(a.cpu().numpy(), cpu.generate(0, R).numpy()), (i, epoch)
