@@ -763,7 +763,7 @@ int pss_set_order_mode(pss_sampler *h, int32_t mode) {
         if (h->version == 1 && !pss::v1_exact_supported(h->geometry()))
             return fail(PSS_ENOTSUP, "V1 exact order needs shuffle_buffer <= 8192");
         if (h->version == 2 && !pss::v2_exact_supported(h->geometry()))
-            return fail(PSS_ENOTSUP, "V2 exact order needs shuffle_buffer <= 4096 and num_samples < 2^31");
+            return fail(PSS_ENOTSUP, "V2 exact order needs num_samples < 2^31 and shuffle_buffer < 2^30");
     }
     h->order_mode = mode;
     return PSS_OK;

@@ -18,7 +18,13 @@
 //           left block is q + #{i : D_i - i <= q} for its sorted deletions D -- and merging
 //           the sorted deletion lists.  Bottom-up, this is a merge sort of (position, step)
 //           pairs: 12 levels in LDS per 4096-step tile, then global levels.  pool2 windows
-//           (no insertions) finish inside one tile.
+//           (no insertions) finish inside one tile when B <= 4096; larger windows are decoded
+//           first, as sequences of their own (B alive, no insertions) through the same tile
+//           and global levels.  A short last window is padded to B steps of k = 0: its
+//           W' real deletions never reach the B - W' padding elements at the end of the
+//           order, so its real answers are unchanged.  Above 4096 alive entries the global
+//           levels map right blocks by a binary search over the left block's deletions instead
+//           of survivor tables (pairs x P words would not fit).
 //   output  position p < P is old_start + p (initial pool1, V2:135-136); position P + u is
 //           the element step u moved over from pool2: window base + its decoded pool2 rank.
 //
@@ -38,6 +44,7 @@ static_assert(kTileNT * 4 == kTile, "the tile merge gives each thread four outpu
 struct V2xGeo {                   // one rank's stream, host-computed
     uint32_t P, T, S, B;          // pool1 size, main steps, pool2 windows, shuffle_buffer
     uint32_t ns, tiles1;          // steps, pool1 decode tiles
+    uint32_t T2;                  // pool2 draws / decoded ranks per rank, padded: S * B
 };
 
 __device__ __forceinline__ uint32_t alive_at(uint32_t B0, uint32_t insu, uint32_t x) {
@@ -69,7 +76,7 @@ __global__ __launch_bounds__(64) void k_v2x_draws(V2xGeo x, int64_t epoch, uint3
     __shared__ uint32_t mt[kMtN];
     const uint32_t rl = blockIdx.x / jobs, job = blockIdx.x % jobs;
     uint32_t *k1 = K1 + (size_t)rl * x.ns;
-    uint32_t *k2 = K2 + (size_t)rl * x.T;
+    uint32_t *k2 = K2 + (size_t)rl * x.T2;
     if (job < x.S) {          // pool2 window s: k1, k2 alternating from its own stream
         const uint32_t s = job;
         const uint32_t W = x.T - s * x.B < x.B ? x.T - s * x.B : x.B, t0 = s * x.B;
@@ -80,6 +87,7 @@ __global__ __launch_bounds__(64) void k_v2x_draws(V2xGeo x, int64_t epoch, uint3
                      if (d & 1u) k2[t0 + (d >> 1)] = r;
                      else k1[t0 + (d >> 1)] = r;
                  });
+        for (uint32_t u = W + threadIdx.x; u < x.B; u += 64) k2[t0 + u] = 0;   // padding steps
     } else {                  // tail step j: the first draw after its reseed
         const uint32_t j = job - x.S;
         const int64_t seed = x.S >= 1 ? epoch + (int64_t)(x.S - 1 + j) * 10000
@@ -112,7 +120,7 @@ __global__ __launch_bounds__(kTileNT) void k_v2x_tile(V2xGeo x, uint32_t per_ran
         t0 = 0;
         n = x.T - s * x.B < x.B ? x.T - s * x.B : x.B;
         B0 = n; insu = 0;
-        src = K2 + (size_t)rl * x.T + (size_t)s * x.B;
+        src = K2 + (size_t)rl * x.T2 + (size_t)s * x.B;
     }
     for (uint32_t u = threadIdx.x; u < n; u += kTileNT) { va[u] = src[u]; oa[u] = u; }
     __syncthreads();
@@ -166,7 +174,7 @@ __global__ __launch_bounds__(kTileNT) void k_v2x_tile(V2xGeo x, uint32_t per_ran
         uint32_t *v = V + (size_t)rl * x.ns + t0, *o = O + (size_t)rl * x.ns + t0;
         for (uint32_t u = threadIdx.x; u < n; u += kTileNT) { v[u] = va[u]; o[u] = t0 + oa[u]; }
     } else {
-        uint32_t *q = Q2 + (size_t)rl * x.T + (size_t)(job - x.tiles1) * x.B;
+        uint32_t *q = Q2 + (size_t)rl * x.T2 + (size_t)(job - x.tiles1) * x.B;
         for (uint32_t u = threadIdx.x; u < n; u += kTileNT) q[oa[u]] = va[u];
     }
 }
@@ -251,6 +259,29 @@ __global__ __launch_bounds__(256) void k_v2x_gmap(V2xGeo x, uint32_t nr, uint32_
     v[u] = q < Bm ? q + C[((size_t)rl * pairs + pair) * x.P + q] : q - Bm + Ba + insL;
 }
 
+// the same without tables: q + #{left deletions at or before its q-th survivor} by a binary
+// search over the left block's sorted deletions (only right-block entries are rewritten, so the
+// left block is stable while it is read)
+__global__ __launch_bounds__(256) void k_v2x_gmap_bs(V2xGeo x, uint32_t nr, uint32_t w, uint32_t *__restrict__ V) {
+    const uint64_t gi = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    const uint32_t rl = (uint32_t)(gi / x.ns), u = (uint32_t)(gi % x.ns);
+    if (rl >= nr) return;
+    const uint32_t blk = u / w;
+    if (!(blk & 1u)) return;
+    const uint32_t a = (blk - 1) * w, m = blk * w;
+    uint32_t *v = V + (size_t)rl * x.ns;
+    v[u] = map_right(v + a, w, v[u], alive_at(x.P, x.T, a), alive_at(x.P, x.T, m), ins_in(x.T, a, m));
+}
+
+// decoded pool2 windows (as sequences of B steps) -> Q2[window step] = its pool2 rank
+__global__ __launch_bounds__(256) void k_v2x_q2(uint64_t n, uint32_t B, const uint32_t *__restrict__ V,
+                                                const uint32_t *__restrict__ O, uint32_t *__restrict__ Q2) {
+    const uint64_t gi = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (gi >= n) return;
+    const uint64_t seq = gi / B;
+    Q2[seq * B + O[gi]] = V[gi];
+}
+
 // merge sibling blocks (sorted by position, carrying the step of each entry)
 __global__ __launch_bounds__(kGNT) void k_v2x_gmerge(V2xGeo x, uint32_t w, const uint32_t *__restrict__ V,
                                                     const uint32_t *__restrict__ O, uint32_t *__restrict__ Vd,
@@ -315,7 +346,7 @@ __global__ __launch_bounds__(256) void k_v2x_out(Geometry g, V2xGeo x, uint32_t 
     } else {
         const uint32_t uu = q - x.P, s = uu / x.B;
         const int64_t wbase = s == 0 ? rd.old_start + x.B : rd.new_start + (int64_t)(s + 1) * x.B;
-        id = wbase + Q2[(size_t)rl * x.T + uu];
+        id = wbase + Q2[(size_t)rl * x.T2 + uu];
     }
     out[(int64_t)rl * count + (t - pos_lo)] = wrap_id(id, g.N);
 }
@@ -331,21 +362,65 @@ static V2xGeo v2x_geo(const Geometry &g) {
     x.S = x.T ? (uint32_t)v2x_cdiv(x.T, g.B) : 0u;
     x.ns = (uint32_t)g.ns;
     x.tiles1 = (uint32_t)v2x_cdiv(g.ns, kTile);
+    x.T2 = x.S * x.B;
     return x;
 }
 
+// pool2 windows of B steps as sequences of their own: B alive, no insertions
+static V2xGeo v2x_window_geo(const V2xGeo &x) {
+    V2xGeo w{};
+    w.P = x.B; w.T = 0; w.S = 0; w.B = x.B; w.ns = x.B; w.T2 = 0;
+    w.tiles1 = (uint32_t)v2x_cdiv(x.B, kTile);
+    return w;
+}
+
+static bool v2x_tables(const V2xGeo &x) { return x.P <= (uint32_t)kTile; }
+
+static size_t v2x_split_words(const V2xGeo &x, int32_t nr) {
+    size_t t = (size_t)nr * (size_t)v2x_cdiv(x.ns, kGTile);
+    if (x.B > (uint32_t)kTile) {
+        const size_t tw = (size_t)nr * x.S * (size_t)v2x_cdiv(x.B, kGTile);
+        t = t > tw ? t : tw;
+    }
+    return 2 * t + 64;
+}
+
 bool v2_exact_supported(const Geometry &g) {
-    return g.B <= kTile && g.ns < ((int64_t)1 << 31);
+    return g.ns < ((int64_t)1 << 31) && g.B < ((int64_t)1 << 30);
 }
 
 size_t v2_exact_ws_bytes(const Geometry &g, int32_t nr) {
     if (!v2_exact_supported(g)) return 0;
     const V2xGeo x = v2x_geo(g);
-    // K1, V, O, Vd, Od (ns each) + K2, Q2 (T each), per local rank; tile splits; survivor
-    // tables of the first global level (the most pairs)
+    // K1, V, O, Vd, Od (ns each) + K2, Q2 (T2 each), per local rank; tile splits; survivor
+    // tables of the first global level (the most pairs) when the pool has <= kTile entries.
+    // Windows beyond kTile are decoded in V, O, Vd, Od (S * B <= ns per rank).
     const size_t pairs = (size_t)v2x_cdiv(x.ns, 2 * kTile);
-    return ((size_t)nr * ((size_t)5 * x.ns + (size_t)2 * x.T) +
-            (size_t)2 * nr * (size_t)v2x_cdiv(x.ns, kGTile) + 64 + (size_t)nr * pairs * x.P) * sizeof(uint32_t);
+    const size_t ctab = v2x_tables(x) ? (size_t)nr * pairs * x.P : 0;
+    return ((size_t)nr * ((size_t)5 * x.ns + (size_t)2 * x.T2) + v2x_split_words(x, nr) + ctab) *
+           sizeof(uint32_t);
+}
+
+// global merge levels w = kTile, 2 kTile, ... of nr sequences of x.ns steps (V, O sorted per
+// block of w on entry); returns the buffers holding the result
+static void v2x_global_levels(const V2xGeo &x, uint32_t nr, uint32_t *&V, uint32_t *&O, uint32_t *&Vd,
+                              uint32_t *&Od, uint32_t *SP, uint32_t *C, hipStream_t s) {
+    const uint64_t nsr = (uint64_t)nr * x.ns;
+    const dim3 grid1((uint32_t)v2x_cdiv((int64_t)nsr, 256));
+    const int64_t tiles = (int64_t)nr * v2x_cdiv(x.ns, kGTile);
+    const dim3 gridt((uint32_t)tiles), grids((uint32_t)v2x_cdiv(2 * tiles, 256));
+    for (uint32_t w = kTile; w < x.ns; w <<= 1) {
+        if (v2x_tables(x)) {
+            hipLaunchKernelGGL(k_v2x_ctab, grid1, dim3(256), 0, s, x, nr, w, V, C);
+            hipLaunchKernelGGL(k_v2x_gmap, grid1, dim3(256), 0, s, x, nr, w, V, C);
+        } else {
+            hipLaunchKernelGGL(k_v2x_gmap_bs, grid1, dim3(256), 0, s, x, nr, w, V);
+        }
+        hipLaunchKernelGGL(k_v2x_gsplit, grids, dim3(256), 0, s, x, nr, w, V, SP);
+        hipLaunchKernelGGL(k_v2x_gmerge, gridt, dim3(kGNT), 0, s, x, w, V, O, Vd, Od, SP);
+        uint32_t *t = V; V = Vd; Vd = t;
+        t = O; O = Od; Od = t;
+    }
 }
 
 hipError_t launch_v2_exact(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, int32_t nr,
@@ -355,7 +430,7 @@ hipError_t launch_v2_exact(const Geometry &g, const RankDesc *ranks, int32_t ran
     if (nr <= 0 || pos_hi <= pos_lo) return hipSuccess;
     if (!v2_exact_supported(g) || !ws) return hipErrorInvalidValue;
     const V2xGeo x = v2x_geo(g);
-    const size_t nsr = (size_t)nr * x.ns, tr = (size_t)nr * x.T;
+    const size_t nsr = (size_t)nr * x.ns, tr = (size_t)nr * x.T2;
     uint32_t *K1 = ws, *V = K1 + nsr, *O = V + nsr, *Vd = O + nsr, *Od = Vd + nsr;
     uint32_t *K2 = Od + nsr, *Q2 = K2 + tr;
     static const hipError_t attr = hipFuncSetAttribute((const void *)k_v2x_tile,
@@ -364,24 +439,27 @@ hipError_t launch_v2_exact(const Geometry &g, const RankDesc *ranks, int32_t ran
     if (attr != hipSuccess) return attr;
     const uint32_t jobs = x.S + x.P;
     hipLaunchKernelGGL(k_v2x_draws, dim3(jobs * (uint32_t)nr), dim3(64), 0, s, x, epoch, jobs, K1, K2);
-    const uint32_t per_rank = x.tiles1 + x.S;
-    hipLaunchKernelGGL(k_v2x_tile, dim3(per_rank * (uint32_t)nr), dim3(kTileNT),
-                       4 * kTile * sizeof(uint32_t), s, x, per_rank, K1, K2, V, O, Q2);
-    const dim3 grid1((uint32_t)v2x_cdiv((int64_t)nsr, 256));   // one thread per (rank, step)
-    // one workgroup per kGTile entries of a rank (the last tile of a rank may be short)
-    const int64_t tiles = (int64_t)nr * v2x_cdiv(x.ns, kGTile);
-    const dim3 gridt((uint32_t)tiles), grids((uint32_t)v2x_cdiv(2 * tiles, 256));
     const uint32_t nru = (uint32_t)nr;
-    uint32_t *SP = Q2 + tr;                    // 2 words per tile
-    uint32_t *C = SP + 2 * tiles + 64;         // survivor tables: pairs x P words per rank
-    for (uint32_t w = kTile; w < x.ns; w <<= 1) {
-        hipLaunchKernelGGL(k_v2x_ctab, grid1, dim3(256), 0, s, x, nru, w, V, C);
-        hipLaunchKernelGGL(k_v2x_gmap, grid1, dim3(256), 0, s, x, nru, w, V, C);
-        hipLaunchKernelGGL(k_v2x_gsplit, grids, dim3(256), 0, s, x, nru, w, V, SP);
-        hipLaunchKernelGGL(k_v2x_gmerge, gridt, dim3(kGNT), 0, s, x, w, V, O, Vd, Od, SP);
-        uint32_t *t = V; V = Vd; Vd = t;
-        t = O; O = Od; Od = t;
+    uint32_t *SP = Q2 + tr;                    // merge-path splits: 2 words per tile
+    uint32_t *C = SP + v2x_split_words(x, nr); // survivor tables: pairs x P words per rank
+    const bool big_windows = x.B > (uint32_t)kTile && x.S > 0;
+    if (big_windows) {          // pool2 windows first, as nr * S sequences of B steps
+        const V2xGeo xw = v2x_window_geo(x);
+        const uint32_t nseq = nru * x.S;
+        hipLaunchKernelGGL(k_v2x_tile, dim3(xw.tiles1 * nseq), dim3(kTileNT), 4 * kTile * sizeof(uint32_t),
+                           s, xw, xw.tiles1, K2, K2, V, O, Q2);
+        uint32_t *wv = V, *wo = O, *wvd = Vd, *wod = Od;
+        v2x_global_levels(xw, nseq, wv, wo, wvd, wod, SP, C, s);
+        const uint64_t nw = (uint64_t)nseq * x.B;
+        hipLaunchKernelGGL(k_v2x_q2, dim3((uint32_t)v2x_cdiv((int64_t)nw, 256)), dim3(256), 0, s, nw, x.B,
+                           wv, wo, Q2);
     }
+    // pool1 tiles (and, for B <= kTile, the windows in the same launch)
+    const uint32_t per_rank = x.tiles1 + (big_windows ? 0u : x.S);
+    hipLaunchKernelGGL(k_v2x_tile, dim3(per_rank * nru), dim3(kTileNT),
+                       4 * kTile * sizeof(uint32_t), s, x, per_rank, K1, K2, V, O, Q2);
+    v2x_global_levels(x, nru, V, O, Vd, Od, SP, C, s);
+    const dim3 grid1((uint32_t)v2x_cdiv((int64_t)nsr, 256));   // one thread per (rank, step)
     hipLaunchKernelGGL(k_v2x_out, grid1, dim3(256), 0, s, g, x, nru, ranks, rank_lo, V, O, Q2,
                        pos_lo, count, out);
     return hipGetLastError();

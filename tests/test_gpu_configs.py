@@ -156,3 +156,22 @@ def test_c5_big_pool_consecutive_epochs():
     eng.init_iter(9)
     assert _coverage(eng, N, R, R)
     eng.close()
+
+
+def test_c5_pool_exact_order_equals_cpu_mode():
+    """order="exact" (the reference's MT19937 draws, V2:96-116) at C5's pool, B = 2^20: three
+    pool2 windows of 2^20 steps (the last partial) decoded through the global merge levels, a
+    2^20-step tail whose reseeds take two-word MT keys.  GPU == CPU mode (pinned to the exact
+    oracle up to B = 2^18 by tools/exact_big.py and test_cpu_mode.py)."""
+    R, B = 2, 1 << 20
+    ns = int(3.5 * B)
+    N, F = ns * R, 70
+    lengths = np.full(F, N // F)
+    lengths[-1] += N - lengths.sum()
+    kw = dict(shuffle=True, seed=3, order="exact")
+    gpu = pss.IndexEngine(lengths, N, R, B, 2, device=0, **kw)
+    cpu = pss.IndexEngine(lengths, N, R, B, 2, device="cpu", **kw)
+    gpu.init_iter(5)
+    cpu.init_iter(5)
+    a = _gen(gpu, 0, R).cpu().numpy()
+    assert np.array_equal(a, cpu.generate(0, R).numpy())

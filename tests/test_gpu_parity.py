@@ -405,8 +405,6 @@ def test_exact_order_unsupported_configs():
     from partiallyshuffledistributedsampler_amd import _lib
     lengths = np.full(10, 1000)
     with pytest.raises(_lib.PSSError):
-        pss.IndexEngine(lengths, 10000, 2, 8192, 2, device=0, order="exact")     # V2, B > 4096
-    with pytest.raises(_lib.PSSError):
         pss.IndexEngine(lengths, 10000, 2, 16384, 1, device=0, order="exact")    # V1, B > 8192
 
 
@@ -439,6 +437,10 @@ def test_v2_exact_order_matches_reference_streams(name):
     (9, 20, 40, 2, 70, (3,)),                       # B < ns < 2B
     (100, 1, 3, 8, 7, (0,)),                        # tiny pools
     (64, 3000, 3001, 2, 1000, (4,)),                # many global decode levels (ns = 96000)
+    (40, 2000, 9000, 2, 4097, (1,)),                # windows beyond one decode tile
+    (30, 2000, 4000, 3, 5000, (0, 2)),              # ... partial last window (padded steps)
+    (60, 3000, 4000, 2, 20000, (3,)),               # pool1 > 4096: table-free global levels
+    (25, 3000, 9000, 1, 70001, (1,)),               # a big pool, one rank, few windows
 ])
 def test_v2_exact_order_matches_exact_oracle(F, lo, hi, R, B, epochs):
     rng = np.random.default_rng(F * 7 + B)
