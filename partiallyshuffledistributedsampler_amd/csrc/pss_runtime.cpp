@@ -761,7 +761,7 @@ int pss_set_order_mode(pss_sampler *h, int32_t mode) {
     if (mode != PSS_ORDER_COUNTER && mode != PSS_ORDER_EXACT) return fail(PSS_EINVAL, "bad order mode");
     if (mode == PSS_ORDER_EXACT && !h->cpu) {   // the CPU mode has no LDS bounds
         if (h->version == 1 && !pss::v1_exact_supported(h->geometry()))
-            return fail(PSS_ENOTSUP, "V1 exact order needs shuffle_buffer <= 8192");
+            return fail(PSS_ENOTSUP, "V1 exact order needs shuffle_buffer <= 16000");
         if (h->version == 2 && !pss::v2_exact_supported(h->geometry()))
             return fail(PSS_ENOTSUP, "V2 exact order needs num_samples < 2^31 and shuffle_buffer < 2^30");
     }

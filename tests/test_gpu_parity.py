@@ -377,7 +377,9 @@ def test_v1_exact_order_matches_reference_streams(name):
     (64, 10000, 10001, 2, 4096, (0, 1)),            # C1 (BASELINE configs[0])
     (37, 1, 900, 7, 40, (0, 5)),
     (50, 1000, 5000, 3, 3000, (2,)),                # partial last window
-    (40, 2000, 9000, 2, 8192, (1,)),                # largest exact window
+    (40, 2000, 9000, 2, 8192, (1,)),
+    (30, 5000, 9000, 2, 12345, (3,)),               # partial last window, odd size
+    (40, 5000, 9000, 2, 16000, (1,)),               # largest exact window (LDS)
     (13, 1, 50, 5, 100, (0, 9)),                    # ns < B
     (100, 1, 3, 8, 7, (0,)),                        # tiny windows
     (30, 100, 400, 3, 257, (2 ** 32 - 30000,)),     # window seeds cross 2^32 (two-word MT keys)
@@ -405,7 +407,7 @@ def test_exact_order_unsupported_configs():
     from partiallyshuffledistributedsampler_amd import _lib
     lengths = np.full(10, 1000)
     with pytest.raises(_lib.PSSError):
-        pss.IndexEngine(lengths, 10000, 2, 16384, 1, device=0, order="exact")    # V1, B > 8192
+        pss.IndexEngine(lengths, 10000, 2, 16384, 1, device=0, order="exact")    # V1, B > 16000
 
 
 @pytest.mark.parametrize("name", scenario_names("v2"))
