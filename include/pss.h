@@ -160,7 +160,7 @@ int pss_emit_path(pss_sampler *h, int32_t *path);
  *       §3): per-sampler, independent of the process-global `random` state;
  *   PSS_ORDER_EXACT   (1) -- the reference's own draws with CPython's MT19937, so the id
  *       stream is bit-identical to the reference's: V1 windows `seed(epoch + b*10000);
- *       shuffle(range(n))` (V1:102,114-115,165-171, shuffle_buffer <= 16000); V2 get_index's
+ *       shuffle(range(n))` (V1:102,114-115,165-171, shuffle_buffer < 2^31); V2 get_index's
  *       choice / remove / append with its per-window and per-tail-step reseeding (V2:96-116,
  *       num_samples < 2^31, shuffle_buffer < 2^30).  PSS_ENOTSUP outside those bounds.
  * Replaces nothing in the reference: its order IS the exact one. */

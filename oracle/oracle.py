@@ -56,6 +56,8 @@ def lib():
         L.orc_v2_exact_stream.restype = ctypes.c_int64
         L.orc_v2_exact_prefix.argtypes = [ctypes.c_int64] * 7 + [I64P]
         L.orc_v2_exact_prefix.restype = ctypes.c_int64
+        L.orc_v2_exact_stream_rs.argtypes = [ctypes.c_int64] * 7 + [I64P]
+        L.orc_v2_exact_stream_rs.restype = ctypes.c_int64
         L.orc_philox4x32.argtypes = [U32P, ctypes.c_uint64, U32P]
         L.orc_mix64.argtypes = [ctypes.c_uint64]
         L.orc_mix64.restype = ctypes.c_uint64
@@ -182,6 +184,14 @@ def v1_exact_stream(epoch, start, ns, B, N, shuffle=True, resume_pos=-1):
 def v2_exact_stream(epoch, old_start, new_start, ns, B, N, skip=0):
     out = np.empty(ns, dtype=np.int64)
     n = lib().orc_v2_exact_stream(epoch, old_start, new_start, ns, B, N, skip, _p64(out))
+    return out[:n]
+
+
+def v2_exact_stream_rs(epoch, old_start, new_start, ns, B, N, skip=0):
+    """The same stream as v2_exact_stream with rank-select bitmaps in place of list.remove:
+    O(log B) per draw, the checker for pools far beyond the list.remove restatement's reach."""
+    out = np.empty(ns, dtype=np.int64)
+    n = lib().orc_v2_exact_stream_rs(epoch, old_start, new_start, ns, B, N, skip, _p64(out))
     return out[:n]
 
 

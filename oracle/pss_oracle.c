@@ -249,6 +249,153 @@ int64_t orc_v2_exact_prefix(int64_t epoch, int64_t old_start, int64_t new_start,
 }
 
 /* ------------------------------------------------------------------------------------ */
+/* (1d) the same V2 stream for big pools: rank-select bitmaps instead of list.remove      */
+/* ------------------------------------------------------------------------------------ */
+/* A Python list that only ever loses elements by position and gains them at its end is a
+ * bitmap over its insertion slots: element k of the list is the k-th set bit.  The bitmap
+ * keeps a 64-ary tree of set-bit counts above its words (node i of level l covers words
+ * [i*64^(l+1), (i+1)*64^(l+1))), so select / clear / append cost O(64 log_64 n) instead of
+ * list.remove's O(n) shift.  This is the whole of the speed-up: orc_v2_exact_stream_rs
+ * performs exactly the draws, reseeds and refills of v2_exact above (V2:96-116), and
+ * tests/test_oracle_golden.py checks the two against each other and against the goldens. */
+typedef struct {
+    int64_t nwords;
+    uint64_t *w;
+    int nlev;
+    int64_t len[8];
+    uint32_t *cnt[8];
+} orc_rsb;
+
+static void rsb_init(orc_rsb *b, int64_t nbits) {
+    memset(b, 0, sizeof(*b));
+    b->nwords = (nbits + 63) / 64;
+    if (b->nwords < 1) b->nwords = 1;
+    b->w = (uint64_t *)calloc((size_t)b->nwords, sizeof(uint64_t));
+    int64_t n = b->nwords;
+    do {
+        n = (n + 63) / 64;
+        b->len[b->nlev] = n;
+        b->cnt[b->nlev] = (uint32_t *)calloc((size_t)n, sizeof(uint32_t));
+        b->nlev++;
+    } while (n > 1);
+}
+
+static void rsb_free(orc_rsb *b) {
+    free(b->w);
+    for (int l = 0; l < b->nlev; l++) free(b->cnt[l]);
+}
+
+/* bits [0, n) set, the rest clear (a fresh list(range(lo, lo + n))) */
+static void rsb_fill(orc_rsb *b, int64_t n) {
+    memset(b->w, 0, sizeof(uint64_t) * (size_t)b->nwords);
+    for (int l = 0; l < b->nlev; l++) memset(b->cnt[l], 0, sizeof(uint32_t) * (size_t)b->len[l]);
+    for (int64_t i = 0; i < n / 64; i++) b->w[i] = ~0ull;
+    if (n % 64) b->w[n / 64] = (1ull << (n % 64)) - 1ull;
+    for (int64_t i = 0; i < b->nwords; i++) b->cnt[0][i / 64] += (uint32_t)__builtin_popcountll(b->w[i]);
+    for (int l = 1; l < b->nlev; l++)
+        for (int64_t i = 0; i < b->len[l - 1]; i++) b->cnt[l][i / 64] += b->cnt[l - 1][i];
+}
+
+static void rsb_add(orc_rsb *b, int64_t pos, int delta) {
+    int64_t node = pos / 64;
+    for (int l = 0; l < b->nlev; l++) {
+        node /= 64;
+        b->cnt[l][node] = (uint32_t)((int64_t)b->cnt[l][node] + delta);
+    }
+}
+
+static void rsb_set(orc_rsb *b, int64_t pos) {
+    b->w[pos / 64] |= 1ull << (pos % 64);
+    rsb_add(b, pos, 1);
+}
+
+static void rsb_clear(orc_rsb *b, int64_t pos) {
+    b->w[pos / 64] &= ~(1ull << (pos % 64));
+    rsb_add(b, pos, -1);
+}
+
+/* position of the k-th set bit (k counted from 0; k < number of set bits) */
+static int64_t rsb_select(const orc_rsb *b, int64_t k) {
+    int64_t node = 0;                       /* the root: the single node of the top level */
+    for (int l = b->nlev - 2; l >= 0; l--) {
+        int64_t c = node * 64, e = c + 64 < b->len[l] ? c + 64 : b->len[l];
+        while (c < e - 1 && (int64_t)b->cnt[l][c] <= k) { k -= b->cnt[l][c]; c++; }
+        node = c;
+    }
+    int64_t wi = node * 64, we = wi + 64 < b->nwords ? wi + 64 : b->nwords;
+    for (;;) {
+        const int64_t pc = __builtin_popcountll(b->w[wi]);
+        if (k < pc || wi == we - 1) break;
+        k -= pc;
+        wi++;
+    }
+    uint64_t x = b->w[wi];
+    for (; k > 0; k--) x &= x - 1ull;
+    return wi * 64 + __builtin_ctzll(x);
+}
+
+static int64_t v2_exact_rs(int64_t epoch, int64_t old_start, int64_t new_start, int64_t ns,
+                           int64_t B, int64_t N, int64_t skip, int64_t limit, int64_t *out) {
+    orc_mt s;
+    /* pool1: insertion slots [0, P) hold old_start + slot (V2:135-136); every append takes the
+     * next slot, at most one per step */
+    const int64_t P = B < ns ? B : ns;
+    const int64_t cap1 = ns + 1;
+    int64_t *val1 = (int64_t *)malloc(sizeof(int64_t) * (size_t)cap1);
+    orc_rsb p1, p2;
+    rsb_init(&p1, cap1);
+    rsb_init(&p2, B > 0 ? B : 1);
+    for (int64_t v = 0; v < P; v++) val1[v] = old_start + v;
+    rsb_fill(&p1, P);
+    int64_t n1 = P, next1 = P;
+    /* pool2: the window list(range(lo2, hi2)) (V2:137-138, then V2:110-112) */
+    int64_t lo2 = old_start + B, hi2 = old_start + 2 * B;
+    if (hi2 > old_start + ns) hi2 = old_start + ns;
+    int64_t n2 = hi2 > lo2 ? hi2 - lo2 : 0;
+    rsb_fill(&p2, n2);
+    int64_t buffers = 0, n_out = 0, drawn = 0;
+    orc_mt_seed_i64(&s, epoch + 2);                              /* V2:147 */
+    while (n1 > 0 || n2 > 0) {
+        const int64_t k = (int64_t)orc_mt_randbelow(&s, (uint64_t)n1);   /* V2:101 */
+        if (n1 == 0) break;
+        const int64_t slot = rsb_select(&p1, k);
+        const int64_t index = val1[slot];
+        rsb_clear(&p1, slot);                                    /* V2:102 */
+        n1--;
+        if (n2 != 0) {                                           /* V2:103-106 */
+            const int64_t k2 = (int64_t)orc_mt_randbelow(&s, (uint64_t)n2);
+            const int64_t j = rsb_select(&p2, k2);
+            rsb_clear(&p2, j);
+            n2--;
+            val1[next1] = lo2 + j;
+            rsb_set(&p1, next1);
+            next1++;
+            n1++;
+        }
+        if (n2 == 0) {                                           /* V2:107-112 */
+            orc_mt_seed_i64(&s, epoch + buffers * 10000);
+            buffers++;
+            lo2 = new_start + (buffers + 1) * B;
+            hi2 = new_start + (buffers + 2) * B;
+            if (hi2 > new_start + ns) hi2 = new_start + ns;
+            n2 = hi2 > lo2 ? hi2 - lo2 : 0;
+            if (n2) rsb_fill(&p2, n2);
+        }
+        if (drawn++ >= skip) out[n_out++] = wrap_id(index, N);   /* V2:113-115 */
+        if (limit >= 0 && n_out >= limit) break;
+    }
+    free(val1);
+    rsb_free(&p1);
+    rsb_free(&p2);
+    return n_out;
+}
+
+int64_t orc_v2_exact_stream_rs(int64_t epoch, int64_t old_start, int64_t new_start, int64_t ns,
+                               int64_t B, int64_t N, int64_t skip, int64_t *out) {
+    return v2_exact_rs(epoch, old_start, new_start, ns, B, N, skip, -1, out);
+}
+
+/* ------------------------------------------------------------------------------------ */
 /* (2) Philox schedule -- C twin of the HIP kernels                        */
 /* ------------------------------------------------------------------------------------ */
 #define PHILOX_M0 0xD2511F53U

@@ -111,16 +111,16 @@ hipError_t launch_v1(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, 
 size_t v1_workspace_bytes(const Geometry &g, int32_t nr, int64_t pos_lo, int64_t count);
 
 // V1 in the reference's exact order (CPython MT19937 per window, pss_v1exact.hip): windows up
-// to kV1ExactMaxB elements (LDS-resident draw and bucket arrays: (624 + n + 1) words and 3n
-// u16 <= 160 KB)
+// to kV1ExactMaxB elements resolve in LDS ((624 + n + 1) words and 3n u16 <= 160 KB), larger
+// ones (shuffle_buffer < 2^31) through HBM-staged draw and bucket arrays
 constexpr int64_t kV1ExactMaxB = 16000;
 bool v1_exact_supported(const Geometry &g);
 size_t v1_exact_ws_bytes(const Geometry &g, int32_t nr, int64_t pos_lo, int64_t count);
 hipError_t launch_v1_exact(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, int32_t nr,
-                           int64_t pos_lo, int64_t count, int64_t epoch, int64_t *out, uint16_t *ws,
+                           int64_t pos_lo, int64_t count, int64_t epoch, int64_t *out, void *ws,
                            hipStream_t s);
 
-// V2 in the reference's exact order (pss_v2exact.hip): shuffle_buffer <= 4096, ns < 2^31
+// V2 in the reference's exact order (pss_v2exact.hip): shuffle_buffer < 2^30, ns < 2^31
 bool v2_exact_supported(const Geometry &g);
 size_t v2_exact_ws_bytes(const Geometry &g, int32_t nr);
 hipError_t launch_v2_exact(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, int32_t nr,

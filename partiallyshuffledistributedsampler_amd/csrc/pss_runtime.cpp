@@ -709,7 +709,7 @@ int generate_impl(pss_sampler *h, int32_t rank_lo, int32_t rank_hi, int64_t pos_
         PSS_HIP(h->d_sort.ensure(words(pss::v1_exact_ws_bytes(g, nr, pos_lo, count))));
         mk(pss::K_V1, s);
         PSS_HIP(pss::launch_v1_exact(g, h->d_ranks.p, rank_lo, nr, pos_lo, count, h->epoch, out_dev,
-                                     (uint16_t *)h->d_sort.p, s));
+                                     h->d_sort.p, s));
     } else if (h->version == 1) {
         const size_t sb = pss::v1_workspace_bytes(g, nr, pos_lo, count);
         if (sb) PSS_HIP(h->d_sort.ensure(words(sb)));
@@ -761,7 +761,7 @@ int pss_set_order_mode(pss_sampler *h, int32_t mode) {
     if (mode != PSS_ORDER_COUNTER && mode != PSS_ORDER_EXACT) return fail(PSS_EINVAL, "bad order mode");
     if (mode == PSS_ORDER_EXACT && !h->cpu) {   // the CPU mode has no LDS bounds
         if (h->version == 1 && !pss::v1_exact_supported(h->geometry()))
-            return fail(PSS_ENOTSUP, "V1 exact order needs shuffle_buffer <= 16000");
+            return fail(PSS_ENOTSUP, "V1 exact order needs shuffle_buffer < 2^31");
         if (h->version == 2 && !pss::v2_exact_supported(h->geometry()))
             return fail(PSS_ENOTSUP, "V2 exact order needs num_samples < 2^31 and shuffle_buffer < 2^30");
     }

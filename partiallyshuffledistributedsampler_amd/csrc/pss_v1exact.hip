@@ -3,7 +3,8 @@
 // b >= 1 is `seed(epoch + b*10000); shuffle(range(len))` (V1:165-171), both with CPython
 // 3.10's MT19937 (`random.py:128-168` seeding, `:239-249` _randbelow, `:380-396` shuffle).
 // Every window reseeds, so windows are independent: one 256-thread workgroup per
-// (rank, window), three phases.
+// (rank, window), three phases, for windows up to kV1ExactMaxB entries (LDS-resident); larger
+// windows run the same three phases through HBM (k_v1x_*, below).
 //
 //   1. seeding (wave 0, uniform/scalar code): init_by_array over the compile-time
 //      init_genrand(19650218) table -- two serial chains of 624 + 623 steps.
@@ -40,7 +41,7 @@ __global__ __launch_bounds__(64) void k_v1x_draws(Geometry g, int64_t w_lo, int6
     const int64_t wb = w * g.B;
     const int n = (int)(g.ns - wb < g.B ? g.ns - wb : g.B);
     if (n <= 1) return;
-    uint16_t *jw = J + (size_t)blockIdx.x * (size_t)g.B;
+    uint16_t *jw = J + (size_t)blockIdx.x * (size_t)(g.B < g.ns ? g.B : g.ns);
     mt_seed_int(mt, w == 0 ? epoch : epoch + w * 10000);
     mt_draws(mt, (uint32_t)(n - 1), [&](uint32_t d) { return (uint32_t)n - d; },
              [&](uint32_t d, uint32_t r) { jw[n - 1 - (int)d] = (uint16_t)r; });
@@ -67,7 +68,7 @@ __global__ __launch_bounds__(kExactNT) void k_v1_exact(Geometry g, const RankDes
     __shared__ uint32_t tot[kExactNT / 64];
 
     if (J) {                 // draws already made by k_v1x_draws
-        const uint16_t *jw = J + (size_t)blockIdx.x * (size_t)g.B;
+        const uint16_t *jw = J + (size_t)blockIdx.x * (size_t)(g.B < g.ns ? g.B : g.ns);
         for (int i = tid; i < n; i += kExactNT) jv[i] = jw[i];
     } else if (wid == 0 && n > 1) {
         // ---- 1. seed(a): key = 32-bit words of abs(a) (random_seed) ----
@@ -138,25 +139,203 @@ __global__ __launch_bounds__(kExactNT) void k_v1_exact(Geometry g, const RankDes
     }
 }
 
+// ---- windows beyond LDS (n > kV1ExactMaxB): the same resolution through HBM ----------------
+// One pass covers `nj` jobs (rank, window) of the launch, jobs j0 .. j0 + nj - 1 (job -> local
+// rank job / nw, window w_lo + job % nw), each with B-entry slices of four u32 arrays:
+//   J   the draws j_i (k_v1x_draws32, one wave per window: the MT stream is serial)
+//   CNT bucket counts of j -> exclusive offsets -> bucket ends (count, scan, scatter)
+//   LST the steps bucketed by j
+//   NXT parent(k) = the smallest k' > k with j_k' = k, else k
+// and the output walks each x[i]'s parent chain to its root (expected length O(1): parent(k)
+// is about k * U^-1 for a uniform U, so chains climb geometrically towards n).
+struct V1xBig {
+    int64_t w_lo, nw;       // windows of the launch
+    uint64_t j0;            // first job of the pass
+    uint32_t nj;            // jobs in the pass
+    uint32_t B;             // slice length: min(shuffle_buffer, num_samples)
+    uint32_t *J, *CNT, *LST, *NXT;
+};
+
+__device__ __forceinline__ int v1x_len(const Geometry &g, int64_t w) {
+    const int64_t wb = w * g.B;
+    return (int)(g.ns - wb < g.B ? g.ns - wb : g.B);
+}
+
+__global__ __launch_bounds__(64) void k_v1x_draws32(Geometry g, V1xBig b, int64_t epoch) {
+    __shared__ uint32_t mt[kMtN];
+    const uint64_t job = b.j0 + blockIdx.x;
+    const int64_t w = b.w_lo + (int64_t)(job % (uint64_t)b.nw);
+    const int n = v1x_len(g, w);
+    if (n <= 1) return;
+    uint32_t *jw = b.J + (size_t)blockIdx.x * b.B;
+    mt_seed_int(mt, w == 0 ? epoch : epoch + w * 10000);
+    mt_draws(mt, (uint32_t)(n - 1), [&](uint32_t d) { return (uint32_t)n - d; },
+             [&](uint32_t d, uint32_t r) { jw[n - 1 - (int)d] = r; });
+}
+
+// blockIdx.y = slot of the pass, x-threads over the window's entries
+#define V1X_SLOT_PROLOGUE                                                          \
+    const uint32_t slot = blockIdx.y;                                              \
+    const uint64_t job = b.j0 + slot;                                              \
+    const int64_t w = b.w_lo + (int64_t)(job % (uint64_t)b.nw);                    \
+    const int n = v1x_len(g, w);                                                   \
+    const uint32_t *J = b.J + (size_t)slot * b.B;                                  \
+    uint32_t *CNT = b.CNT + (size_t)slot * ((size_t)b.B + 1);                      \
+    (void)J; (void)CNT;
+
+__global__ __launch_bounds__(256) void k_v1x_count(Geometry g, V1xBig b) {
+    V1X_SLOT_PROLOGUE
+    const int k = (int)(blockIdx.x * 256 + threadIdx.x);
+    if (k >= 1 && k < n) atomicAdd(&CNT[J[k]], 1u);
+}
+
+// exclusive scan of CNT[0, n) in place, one workgroup per window
+constexpr int kV1xScanNT = 1024;
+__global__ __launch_bounds__(kV1xScanNT) void k_v1x_scan(Geometry g, V1xBig b) {
+    const uint32_t slot = blockIdx.x;
+    const uint64_t job = b.j0 + slot;
+    const int64_t w = b.w_lo + (int64_t)(job % (uint64_t)b.nw);
+    const int n = v1x_len(g, w);
+    uint32_t *CNT = b.CNT + (size_t)slot * ((size_t)b.B + 1);
+    __shared__ uint32_t tot[kV1xScanNT / 64];
+    const int per = (n + kV1xScanNT - 1) / kV1xScanNT;
+    const int lo = (int)threadIdx.x * per, hi = lo + per < n ? lo + per : n;
+    uint32_t sum = 0;
+    for (int p = lo; p < hi; p++) sum += CNT[p];
+    uint32_t total;
+    uint32_t run = block_excl_scan<kV1xScanNT>(sum, tot, total);
+    for (int p = lo; p < hi; p++) { const uint32_t c = CNT[p]; CNT[p] = run; run += c; }
+}
+
+__global__ __launch_bounds__(256) void k_v1x_scatter(Geometry g, V1xBig b) {
+    V1X_SLOT_PROLOGUE
+    const int k = (int)(blockIdx.x * 256 + threadIdx.x);
+    if (k >= 1 && k < n) b.LST[(size_t)slot * b.B + atomicAdd(&CNT[J[k]], 1u)] = (uint32_t)k;
+}
+
+// smallest k > above in bucket p (bucket p = LST[p ? CNT[p-1] : 0, CNT[p])), or -1
+__device__ __forceinline__ int v1x_succ(const uint32_t *CNT, const uint32_t *LST, int p, int above) {
+    const int b0 = p ? (int)CNT[p - 1] : 0, b1 = (int)CNT[p];
+    int best = -1;
+    for (int x = b0; x < b1; x++) {
+        const int k = (int)LST[x];
+        if (k > above && (best < 0 || k < best)) best = k;
+    }
+    return best;
+}
+
+__global__ __launch_bounds__(256) void k_v1x_parent(Geometry g, V1xBig b) {
+    V1X_SLOT_PROLOGUE
+    const int k = (int)(blockIdx.x * 256 + threadIdx.x);
+    if (k >= n) return;
+    const int pk = v1x_succ(CNT, b.LST + (size_t)slot * b.B, k, k);
+    b.NXT[(size_t)slot * b.B + k] = (uint32_t)(pk < 0 ? k : pk);
+}
+
+__global__ __launch_bounds__(256) void k_v1x_out(Geometry g, V1xBig b, const RankDesc *__restrict__ ranks,
+                                                 int32_t rank_lo, int64_t pos_lo, int64_t count,
+                                                 int64_t *__restrict__ out) {
+    V1X_SLOT_PROLOGUE
+    const int64_t wb = w * g.B;
+    const int64_t p = wb + (int64_t)(blockIdx.x * 256 + threadIdx.x);
+    const int i = (int)(p - wb);
+    if (i >= n || p < pos_lo || p >= pos_lo + count) return;
+    const uint32_t *LST = b.LST + (size_t)slot * b.B, *NXT = b.NXT + (size_t)slot * b.B;
+    auto root = [&](int k) {
+        for (;;) {
+            const int nk = (int)NXT[k];
+            if (nk == k) return k;
+            k = nk;
+        }
+    };
+    int x;
+    if (n <= 1) {
+        x = 0;
+    } else if (i == 0) {
+        const int k = v1x_succ(CNT, LST, 0, 0);
+        x = k < 0 ? 0 : root(k);
+    } else {
+        const int pj = (int)J[i];
+        if (pj == i) {
+            x = root(i);
+        } else {
+            const int k = v1x_succ(CNT, LST, pj, i);
+            x = k < 0 ? pj : root(k);
+        }
+    }
+    const int32_t rl = (int32_t)(job / (uint64_t)b.nw);
+    out[(int64_t)rl * count + (p - pos_lo)] = wrap_id(ranks[rank_lo + rl].new_start + wb + x, g.N);
+}
+
+namespace {
+// entries per pass of the HBM path (16 B each: a pass's workspace is <= 2 GB)
+constexpr int64_t kV1xPassEntries = (int64_t)1 << 27;
+int64_t v1x_jobs_per_pass(int64_t B) {
+    const int64_t j = kV1xPassEntries / B;
+    return j < 1 ? 1 : (j > 65535 ? 65535 : j);
+}
+}  // namespace
+
 size_t v1_exact_lds_bytes(int64_t n) {
     return (size_t)(kMtN + n + 1) * sizeof(uint32_t) + (size_t)3 * n * sizeof(uint16_t) + 16;
 }
 
-bool v1_exact_supported(const Geometry &g) { return g.B <= kV1ExactMaxB; }
+bool v1_exact_supported(const Geometry &g) { return g.B < ((int64_t)1 << 31); }
 
 size_t v1_exact_ws_bytes(const Geometry &g, int32_t nr, int64_t pos_lo, int64_t count) {
     const int64_t pos_hi = pos_lo + count < g.ns ? pos_lo + count : g.ns;
     if (nr <= 0 || pos_hi <= pos_lo || !v1_exact_supported(g)) return 0;
     const int64_t nw = (pos_hi - 1) / g.B - pos_lo / g.B + 1;
-    return (size_t)nr * (size_t)nw * (size_t)g.B * sizeof(uint16_t);
+    const int64_t jobs = (int64_t)nr * nw;
+    const int64_t W = g.B < g.ns ? g.B : g.ns;   // the longest window
+    if (W <= kV1ExactMaxB) return (size_t)jobs * (size_t)W * sizeof(uint16_t);
+    const int64_t pj = jobs < v1x_jobs_per_pass(W) ? jobs : v1x_jobs_per_pass(W);
+    return (size_t)pj * ((size_t)4 * W + 1) * sizeof(uint32_t);
+}
+
+static hipError_t launch_v1_exact_big(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, int32_t nr,
+                                      int64_t pos_lo, int64_t count, int64_t epoch, int64_t *out,
+                                      uint32_t *ws, hipStream_t s) {
+    const int64_t pos_hi = pos_lo + count < g.ns ? pos_lo + count : g.ns;
+    const int64_t w_lo = pos_lo / g.B, w_hi = (pos_hi - 1) / g.B;
+    const int64_t nw = w_hi - w_lo + 1;
+    const uint64_t jobs = (uint64_t)nr * (uint64_t)nw;
+    const int64_t W = g.B < g.ns ? g.B : g.ns;   // the longest window: the slice length
+    const uint64_t per = (uint64_t)v1x_jobs_per_pass(W);
+    const uint32_t B = (uint32_t)W;
+    for (uint64_t j0 = 0; j0 < jobs; j0 += per) {
+        V1xBig b{};
+        b.w_lo = w_lo; b.nw = nw; b.j0 = j0; b.B = B;
+        b.nj = (uint32_t)(jobs - j0 < per ? jobs - j0 : per);
+        b.J = ws;
+        b.CNT = b.J + (size_t)b.nj * B;
+        b.LST = b.CNT + (size_t)b.nj * ((size_t)B + 1);
+        b.NXT = b.LST + (size_t)b.nj * B;
+        hipError_t e = hipMemsetAsync(b.CNT, 0, sizeof(uint32_t) * (size_t)b.nj * ((size_t)B + 1), s);
+        if (e != hipSuccess) return e;
+        const dim3 flat((B + 255) / 256, b.nj);
+        hipLaunchKernelGGL(k_v1x_draws32, dim3(b.nj), dim3(64), 0, s, g, b, epoch);
+        hipLaunchKernelGGL(k_v1x_count, flat, dim3(256), 0, s, g, b);
+        hipLaunchKernelGGL(k_v1x_scan, dim3(b.nj), dim3(kV1xScanNT), 0, s, g, b);
+        hipLaunchKernelGGL(k_v1x_scatter, flat, dim3(256), 0, s, g, b);
+        hipLaunchKernelGGL(k_v1x_parent, flat, dim3(256), 0, s, g, b);
+        hipLaunchKernelGGL(k_v1x_out, flat, dim3(256), 0, s, g, b, ranks, rank_lo, pos_lo, count, out);
+        e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
 
 hipError_t launch_v1_exact(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, int32_t nr,
-                           int64_t pos_lo, int64_t count, int64_t epoch, int64_t *out, uint16_t *ws,
+                           int64_t pos_lo, int64_t count, int64_t epoch, int64_t *out, void *ws,
                            hipStream_t s) {
     const int64_t pos_hi = pos_lo + count < g.ns ? pos_lo + count : g.ns;
     if (nr <= 0 || pos_hi <= pos_lo) return hipSuccess;
     if (!v1_exact_supported(g)) return hipErrorInvalidValue;
+    if ((g.B < g.ns ? g.B : g.ns) > kV1ExactMaxB) {
+        if (!ws) return hipErrorInvalidValue;
+        return launch_v1_exact_big(g, ranks, rank_lo, nr, pos_lo, count, epoch, out, (uint32_t *)ws, s);
+    }
     const int64_t w_lo = pos_lo / g.B, w_hi = (pos_hi - 1) / g.B;
     const int64_t nw = w_hi - w_lo + 1;
     const size_t lds = v1_exact_lds_bytes(g.B < g.ns ? g.B : g.ns);
@@ -167,7 +346,7 @@ hipError_t launch_v1_exact(const Geometry &g, const RankDesc *ranks, int32_t ran
     const dim3 grid((uint32_t)(nr * nw));
     // with a workspace, the serial MT phases run one wave per window (many windows in flight)
     // ahead of the resolution; without one, each workgroup's first wave does them in place
-    if (ws) hipLaunchKernelGGL(k_v1x_draws, grid, dim3(64), 0, s, g, w_lo, nw, epoch, ws);
+    if (ws) hipLaunchKernelGGL(k_v1x_draws, grid, dim3(64), 0, s, g, w_lo, nw, epoch, (uint16_t *)ws);
     hipLaunchKernelGGL(k_v1_exact, grid, dim3(kExactNT), lds, s, g, ranks, rank_lo, w_lo, nw, pos_lo,
                        count, epoch, (const uint16_t *)ws, out);
     return hipGetLastError();

@@ -811,8 +811,11 @@ __global__ __launch_bounds__(64) void k_v2_emit_x(Geometry g, V2Plan pl,
 }
 
 // Start-up check of the exchange order k_v2_emit_x relies on: random slot patterns (heavy
-// collisions at 64 slots, sparse at 4096) against the sequential lane-order model.
-__global__ __launch_bounds__(64) void k_xchg_order_check(int iters, uint32_t P, uint32_t *bad) {
+// collisions at 64 slots in blocks 0..63, sparse at 4096 in blocks 64..127) against the
+// sequential lane-order model.  Once per device per process, on the first V2 replay.
+__global__ __launch_bounds__(64) void k_xchg_order_check(int iters, uint32_t *bad) {
+    const uint32_t P = blockIdx.x < 64 ? 64u : 4096u;
+    bad += blockIdx.x < 64 ? 0 : 1;
     // two exchanges and two plain stores per iteration, back to back (no wait in between), as
     // the replay kernels issue them; the model replays them in (instruction, lane) order
     __shared__ uint32_t buf[4096];
@@ -1189,8 +1192,7 @@ hipError_t check_lds_xchg_order() {
     if (e != hipSuccess) return e;
     e = hipMemset(bad, 0, sizeof(hbad));
     if (e == hipSuccess) {
-        hipLaunchKernelGGL(k_xchg_order_check, dim3(64), dim3(64), 0, 0, 24, 64u, bad);
-        hipLaunchKernelGGL(k_xchg_order_check, dim3(64), dim3(64), 0, 0, 24, 4096u, bad + 1);
+        hipLaunchKernelGGL(k_xchg_order_check, dim3(128), dim3(64), 0, 0, 24, bad);
         e = hipGetLastError();
     }
     if (e == hipSuccess) e = hipMemcpy(hbad, bad, sizeof(hbad), hipMemcpyDeviceToHost);
@@ -1225,8 +1227,9 @@ bool lds_xchg_ordered() {
 
 hipError_t init_kernel_attributes_v2() {
     const int big = 160 * 1024;
-    hipError_t e = check_lds_xchg_order();
-    if (e == hipSuccess) e = init_kernel_attributes_v2grp();
+    // the exchange-order check runs lazily, on the first query (lds_*_ordered): V1-only
+    // handles never pay for it, V2 ones once per device per process
+    hipError_t e = init_kernel_attributes_v2grp();
 #define PSS_ATTR(fn) { hipError_t x = hipFuncSetAttribute((const void *)(fn), hipFuncAttributeMaxDynamicSharedMemorySize, big); if (x != hipSuccess) e = x; }
     PSS_ATTR((k_v2_lastocc<64, true, true>));
     PSS_ATTR((k_v2_lastocc<64, true, false>));

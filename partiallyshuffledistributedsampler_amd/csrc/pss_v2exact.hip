@@ -37,7 +37,7 @@
 namespace pss {
 
 namespace {
-constexpr int kTile = 4096;       // steps per LDS decode tile; also the largest pool2 window
+constexpr int kTile = 4096;       // steps per LDS decode tile; pool2 windows up to this size decode in one
 constexpr int kTileNT = 1024;   // 4 steps per thread: the searches are latency-bound, occupancy hides them
 static_assert(kTileNT * 4 == kTile, "the tile merge gives each thread four outputs");
 
@@ -71,10 +71,11 @@ __device__ __forceinline__ uint32_t map_right(const uint32_t *DL, uint32_t nL, u
 }  // namespace
 
 // ---- draws: one wave per MT stream (pool2 windows, then tail steps) -------------------------
-__global__ __launch_bounds__(64) void k_v2x_draws(V2xGeo x, int64_t epoch, uint32_t jobs,
+__global__ __launch_bounds__(64) void k_v2x_draws(V2xGeo x, int64_t epoch, uint32_t jobs, uint64_t blk0,
                                                   uint32_t *__restrict__ K1, uint32_t *__restrict__ K2) {
     __shared__ uint32_t mt[kMtN];
-    const uint32_t rl = blockIdx.x / jobs, job = blockIdx.x % jobs;
+    const uint64_t b = blk0 + blockIdx.x;
+    const uint32_t rl = (uint32_t)(b / jobs), job = (uint32_t)(b % jobs);
     uint32_t *k1 = K1 + (size_t)rl * x.ns;
     uint32_t *k2 = K2 + (size_t)rl * x.T2;
     if (job < x.S) {          // pool2 window s: k1, k2 alternating from its own stream
@@ -99,14 +100,15 @@ __global__ __launch_bounds__(64) void k_v2x_draws(V2xGeo x, int64_t epoch, uint3
 }
 
 // ---- decode tiles in LDS: pool1 tiles of kTile steps and whole pool2 windows ---------------
-__global__ __launch_bounds__(kTileNT) void k_v2x_tile(V2xGeo x, uint32_t per_rank,
+__global__ __launch_bounds__(kTileNT) void k_v2x_tile(V2xGeo x, uint32_t per_rank, uint64_t blk0,
                                                       const uint32_t *__restrict__ K1,
                                                       const uint32_t *__restrict__ K2,
                                                       uint32_t *__restrict__ V, uint32_t *__restrict__ O,
                                                       uint32_t *__restrict__ Q2) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     uint32_t *va = smem, *oa = smem + kTile, *vb = smem + 2 * kTile, *ob = smem + 3 * kTile;
-    const uint32_t rl = blockIdx.x / per_rank, job = blockIdx.x % per_rank;
+    const uint64_t bi = blk0 + blockIdx.x;
+    const uint32_t rl = (uint32_t)(bi / per_rank), job = (uint32_t)(bi % per_rank);
     const bool pool1 = job < x.tiles1;
     uint32_t t0, n, B0, insu;
     const uint32_t *src;
@@ -389,8 +391,25 @@ bool v2_exact_supported(const Geometry &g) {
     return g.ns < ((int64_t)1 << 31) && g.B < ((int64_t)1 << 30);
 }
 
-size_t v2_exact_ws_bytes(const Geometry &g, int32_t nr) {
-    if (!v2_exact_supported(g)) return 0;
+// Ranks decoded per pass: every flat kernel of the decode launches one thread per (rank, step)
+// and the draw / tile launches one block per (rank, job), so a pass keeps ranks x steps below
+// 2^30 (thread counts below 2^32) and the workspace is sized for one pass, reused by the next.
+static int32_t v2x_ranks_per_pass(const Geometry &g, int32_t nr) {
+    const int64_t cap = ((int64_t)1 << 30) / (g.ns > 0 ? g.ns : 1);
+    return (int32_t)(nr < cap ? nr : (cap > 1 ? cap : 1));
+}
+
+// launches of one block per job, cut into pieces of at most 2^20 blocks (2^30 threads)
+template <class F>
+static void v2x_launch_blocks(uint64_t blocks, F &&launch) {
+    constexpr uint64_t kMaxBlocks = (uint64_t)1 << 20;
+    for (uint64_t b0 = 0; b0 < blocks; b0 += kMaxBlocks)
+        launch(b0, (uint32_t)(blocks - b0 < kMaxBlocks ? blocks - b0 : kMaxBlocks));
+}
+
+size_t v2_exact_ws_bytes(const Geometry &g, int32_t nr_all) {
+    if (!v2_exact_supported(g) || nr_all <= 0) return 0;
+    const int32_t nr = v2x_ranks_per_pass(g, nr_all);
     const V2xGeo x = v2x_geo(g);
     // K1, V, O, Vd, Od (ns each) + K2, Q2 (T2 each), per local rank; tile splits; survivor
     // tables of the first global level (the most pairs) when the pool has <= kTile entries.
@@ -423,31 +442,29 @@ static void v2x_global_levels(const V2xGeo &x, uint32_t nr, uint32_t *&V, uint32
     }
 }
 
-hipError_t launch_v2_exact(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, int32_t nr,
-                           int64_t pos_lo, int64_t count, int64_t epoch, int64_t *out, uint32_t *ws,
-                           hipStream_t s) {
-    const int64_t pos_hi = pos_lo + count < g.ns ? pos_lo + count : g.ns;
-    if (nr <= 0 || pos_hi <= pos_lo) return hipSuccess;
-    if (!v2_exact_supported(g) || !ws) return hipErrorInvalidValue;
-    const V2xGeo x = v2x_geo(g);
+// one pass over nr ranks (nr * ns < 2^30)
+static hipError_t v2x_pass(const Geometry &g, const V2xGeo &x, const RankDesc *ranks, int32_t rank_lo,
+                           int32_t nr, int64_t pos_lo, int64_t count, int64_t epoch, int64_t *out,
+                           uint32_t *ws, hipStream_t s) {
     const size_t nsr = (size_t)nr * x.ns, tr = (size_t)nr * x.T2;
     uint32_t *K1 = ws, *V = K1 + nsr, *O = V + nsr, *Vd = O + nsr, *Od = Vd + nsr;
     uint32_t *K2 = Od + nsr, *Q2 = K2 + tr;
-    static const hipError_t attr = hipFuncSetAttribute((const void *)k_v2x_tile,
-                                                       hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                       4 * kTile * (int)sizeof(uint32_t));
-    if (attr != hipSuccess) return attr;
     const uint32_t jobs = x.S + x.P;
-    hipLaunchKernelGGL(k_v2x_draws, dim3(jobs * (uint32_t)nr), dim3(64), 0, s, x, epoch, jobs, K1, K2);
+    v2x_launch_blocks((uint64_t)jobs * (uint64_t)nr, [&](uint64_t b0, uint32_t nb) {
+        hipLaunchKernelGGL(k_v2x_draws, dim3(nb), dim3(64), 0, s, x, epoch, jobs, b0, K1, K2);
+    });
     const uint32_t nru = (uint32_t)nr;
     uint32_t *SP = Q2 + tr;                    // merge-path splits: 2 words per tile
     uint32_t *C = SP + v2x_split_words(x, nr); // survivor tables: pairs x P words per rank
     const bool big_windows = x.B > (uint32_t)kTile && x.S > 0;
+    constexpr size_t kTileLds = 4 * kTile * sizeof(uint32_t);
     if (big_windows) {          // pool2 windows first, as nr * S sequences of B steps
         const V2xGeo xw = v2x_window_geo(x);
         const uint32_t nseq = nru * x.S;
-        hipLaunchKernelGGL(k_v2x_tile, dim3(xw.tiles1 * nseq), dim3(kTileNT), 4 * kTile * sizeof(uint32_t),
-                           s, xw, xw.tiles1, K2, K2, V, O, Q2);
+        v2x_launch_blocks((uint64_t)xw.tiles1 * nseq, [&](uint64_t b0, uint32_t nb) {
+            hipLaunchKernelGGL(k_v2x_tile, dim3(nb), dim3(kTileNT), kTileLds, s, xw, xw.tiles1, b0, K2, K2,
+                               V, O, Q2);
+        });
         uint32_t *wv = V, *wo = O, *wvd = Vd, *wod = Od;
         v2x_global_levels(xw, nseq, wv, wo, wvd, wod, SP, C, s);
         const uint64_t nw = (uint64_t)nseq * x.B;
@@ -456,13 +473,35 @@ hipError_t launch_v2_exact(const Geometry &g, const RankDesc *ranks, int32_t ran
     }
     // pool1 tiles (and, for B <= kTile, the windows in the same launch)
     const uint32_t per_rank = x.tiles1 + (big_windows ? 0u : x.S);
-    hipLaunchKernelGGL(k_v2x_tile, dim3(per_rank * nru), dim3(kTileNT),
-                       4 * kTile * sizeof(uint32_t), s, x, per_rank, K1, K2, V, O, Q2);
+    v2x_launch_blocks((uint64_t)per_rank * nru, [&](uint64_t b0, uint32_t nb) {
+        hipLaunchKernelGGL(k_v2x_tile, dim3(nb), dim3(kTileNT), kTileLds, s, x, per_rank, b0, K1, K2, V, O, Q2);
+    });
     v2x_global_levels(x, nru, V, O, Vd, Od, SP, C, s);
     const dim3 grid1((uint32_t)v2x_cdiv((int64_t)nsr, 256));   // one thread per (rank, step)
     hipLaunchKernelGGL(k_v2x_out, grid1, dim3(256), 0, s, g, x, nru, ranks, rank_lo, V, O, Q2,
                        pos_lo, count, out);
     return hipGetLastError();
+}
+
+hipError_t launch_v2_exact(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, int32_t nr,
+                           int64_t pos_lo, int64_t count, int64_t epoch, int64_t *out, uint32_t *ws,
+                           hipStream_t s) {
+    const int64_t pos_hi = pos_lo + count < g.ns ? pos_lo + count : g.ns;
+    if (nr <= 0 || pos_hi <= pos_lo) return hipSuccess;
+    if (!v2_exact_supported(g) || !ws) return hipErrorInvalidValue;
+    const V2xGeo x = v2x_geo(g);
+    static const hipError_t attr = hipFuncSetAttribute((const void *)k_v2x_tile,
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                       4 * kTile * (int)sizeof(uint32_t));
+    if (attr != hipSuccess) return attr;
+    const int32_t per = v2x_ranks_per_pass(g, nr);
+    for (int32_t r0 = 0; r0 < nr; r0 += per) {
+        const int32_t n = nr - r0 < per ? nr - r0 : per;
+        const hipError_t e = v2x_pass(g, x, ranks, rank_lo + r0, n, pos_lo, count, epoch,
+                                      out + (int64_t)r0 * count, ws, s);
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
 
 }  // namespace pss

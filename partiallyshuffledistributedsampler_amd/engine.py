@@ -209,8 +209,9 @@ class IndexEngine:
 
     def set_order_mode(self, mode):
         """Order of ids inside a pool: "counter" (the counter-based schedule, default) or
-        "exact" (V1 only: each window shuffled with CPython's MT19937 exactly as the reference
-        does, V1:102,114-115,165-171 -- the id stream is bit-identical to the reference's)."""
+        "exact" (the reference's own CPython-MT19937 draws: V1 windows shuffled as
+        V1:102,114-115,165-171 do, V2's choice / remove / append of V2:96-116 -- the id stream is
+        bit-identical to the reference's)."""
         _lib.call("pss_set_order_mode", self._h, self.ORDER_MODES[mode])
 
     def order_mode(self):

@@ -79,6 +79,25 @@ def test_cpu_mode_exact_order_matches_exact_oracle(version, F, lo, hi, R, B):
             assert np.array_equal(out[r], ref), (F, B, epoch, r)
 
 
+@pytest.mark.parametrize("B", [1 << 16, 1 << 18])
+def test_cpu_mode_exact_order_big_pools_match_rank_select_oracle(B):
+    """CPU mode's exact V2 (Fenwick trees) against the oracle's rank-select restatement
+    (orc_v2_exact_stream_rs) on pools beyond the list.remove restatement's reach: two ranks of
+    ns = 3.5 B, the last block wrapping at N."""
+    R = 2
+    ns = int(3.5 * B)
+    N = ns * R - 1
+    lengths = np.full(10, N // 10)
+    lengths[-1] += N - lengths.sum()
+    eng = IndexEngine(lengths, N, R, B, 2, seed=7, device="cpu", order="exact")
+    eng.init_iter(4)
+    old, new = eng.rank_starts()
+    out = eng.generate(0, R).numpy()
+    for r in range(R):
+        assert np.array_equal(out[r], O.v2_exact_stream_rs(4, int(old[r]), int(new[r]), ns, B, N)), (B, r)
+    eng.close()
+
+
 def test_c1_runs_end_to_end_on_cpu():
     """BASELINE configs[0]: V1, 64 files x 10K, R=2, B=4096 -- every rank's epoch, exact
     coverage, through the drop-in class with device="cpu"."""

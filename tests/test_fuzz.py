@@ -6,8 +6,8 @@ beyond 16384 and B > ns all occur), shuffle on/off, a seed and a start epoch.
 
   * CPU (`-m "not gpu"`): the library's CPU mode == the oracle twin (oracle/pss_oracle.c) for
     every rank, plus full coverage of [0, N) and the wrap-around pad (V1:161-163);
-  * exact order (`order="exact"`, the reference's MT19937 draws) on the GPU == CPU mode, with
-    V1's B capped at the GPU's LDS bound (16000; pss.h), V2 at any pool size;
+  * exact order (`order="exact"`, the reference's MT19937 draws) on the GPU == CPU mode at every
+    pool size (V1 windows beyond 16000 take the HBM-staged resolution);
   * GPU (`-m gpu`): the HIP kernels (through the C-ABI) == CPU mode over three consecutive
     epochs (the V2 epoch lookahead), on both V2 emit paths, for random (rank, position)
     sub-ranges, the id -> (file, offset) map and the fused mapped generation, with the device
@@ -131,8 +131,7 @@ def test_gpu_fuzz_equals_cpu_mode(i, device=0):
 @pytest.mark.parametrize("i", range(N_EXACT_CASES))
 def test_gpu_fuzz_exact_order_equals_cpu_mode(i, device=0):
     g = _geometry(i)
-    B = min(g["B"], 16000) if g["version"] == 1 else g["B"]
-    args = (g["lengths"], g["N"], g["R"], B, g["version"])
+    args = (g["lengths"], g["N"], g["R"], g["B"], g["version"])
     kw = dict(shuffle=g["shuffle"], seed=g["seed"], order="exact")
     gpu = pss.IndexEngine(*args, device=device, **kw)
     cpu = pss.IndexEngine(*args, device="cpu", **kw)

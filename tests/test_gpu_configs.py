@@ -158,11 +158,35 @@ def test_c5_big_pool_consecutive_epochs():
     eng.close()
 
 
+@pytest.mark.parametrize("B", [1 << 16, 1 << 18, 1 << 20])
+def test_big_pool_exact_order_matches_rank_select_oracle(B):
+    """order="exact" (the reference's MT19937 draws, V2:96-116) on pools far beyond the
+    list.remove restatement's reach, up to C5's B = 2^20: two ranks of ns = 3.5 B steps -- three
+    pool2 windows of B steps (the last partial) decoded through the global merge levels, and a
+    B-step tail whose reseeds take two-word MT keys.  Every rank's stream == the exact oracle's
+    rank-select restatement (oracle/pss_oracle.c orc_v2_exact_stream_rs, itself checked against
+    the list.remove restatement and the reference's goldens in tests/test_oracle_golden.py)."""
+    R = 2
+    ns = int(3.5 * B)
+    N, F = ns * R - 1, 70          # one pad id: the last rank's block wraps at N
+    lengths = np.full(F, N // F)
+    lengths[-1] += N - lengths.sum()
+    gpu = pss.IndexEngine(lengths, N, R, B, 2, device=0, shuffle=True, seed=3, order="exact")
+    assert gpu.num_samples == ns
+    for epoch in (5, 2 ** 32 - 2):
+        gpu.init_iter(epoch)
+        old, new = gpu.rank_starts()
+        a = _gen(gpu, 0, R).cpu().numpy()
+        for r in range(R):
+            ref = O.v2_exact_stream_rs(epoch, int(old[r]), int(new[r]), ns, B, N)
+            assert np.array_equal(a[r], ref), (B, epoch, r, int(np.argmax(a[r] != ref)))
+    gpu.close()
+
+
 def test_c5_pool_exact_order_equals_cpu_mode():
-    """order="exact" (the reference's MT19937 draws, V2:96-116) at C5's pool, B = 2^20: three
-    pool2 windows of 2^20 steps (the last partial) decoded through the global merge levels, a
-    2^20-step tail whose reseeds take two-word MT keys.  GPU == CPU mode (pinned to the exact
-    oracle up to B = 2^18 by tools/exact_big.py and test_cpu_mode.py)."""
+    """The same C5 pool (B = 2^20) through the product's CPU mode (Fenwick trees,
+    pss_cpu.cpp): GPU == CPU mode bit for bit (both are checked against the rank-select oracle
+    above and in tests/test_cpu_mode.py)."""
     R, B = 2, 1 << 20
     ns = int(3.5 * B)
     N, F = ns * R, 70
@@ -175,3 +199,21 @@ def test_c5_pool_exact_order_equals_cpu_mode():
     cpu.init_iter(5)
     a = _gen(gpu, 0, R).cpu().numpy()
     assert np.array_equal(a, cpu.generate(0, R).numpy())
+
+
+def test_exact_order_launch_sizes_beyond_2_32_threads():
+    """Exact V2 with tiny pools over long streams: B = 2 makes every rank ~1.1M pool2 windows,
+    i.e. 1.1M decode-tile blocks of 1024 threads per rank -- more than 2^32 threads for the
+    four ranks together, which the launches must split.  GPU == CPU mode."""
+    R, B, ns = 4, 2, 2_200_001
+    N = ns * R
+    lengths = np.full(9, N // 9)
+    lengths[-1] += N - lengths.sum()
+    kw = dict(shuffle=True, seed=1, order="exact")
+    gpu = pss.IndexEngine(lengths, N, R, B, 2, device=0, **kw)
+    cpu = pss.IndexEngine(lengths, N, R, B, 2, device="cpu", **kw)
+    gpu.init_iter(0)
+    cpu.init_iter(0)
+    a = _gen(gpu, 0, R).cpu().numpy()
+    assert np.array_equal(a, cpu.generate(0, R).numpy())
+    gpu.close()

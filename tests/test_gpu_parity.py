@@ -379,7 +379,11 @@ def test_v1_exact_order_matches_reference_streams(name):
     (50, 1000, 5000, 3, 3000, (2,)),                # partial last window
     (40, 2000, 9000, 2, 8192, (1,)),
     (30, 5000, 9000, 2, 12345, (3,)),               # partial last window, odd size
-    (40, 5000, 9000, 2, 16000, (1,)),               # largest exact window (LDS)
+    (40, 5000, 9000, 2, 16000, (1,)),               # largest exact window in LDS
+    (40, 5000, 9000, 2, 16001, (1,)),               # smallest window of the HBM path
+    (40, 5000, 9000, 2, 16384, (0, 1)),             # HBM path, partial last window
+    (30, 20000, 60000, 3, 65536, (2,)),
+    (70, 100000, 100001, 2, 1 << 20, (0, 2 ** 32 - 3)),   # C5's pool: B = 2^20, 3.3 windows per rank
     (13, 1, 50, 5, 100, (0, 9)),                    # ns < B
     (100, 1, 3, 8, 7, (0,)),                        # tiny windows
     (30, 100, 400, 3, 257, (2 ** 32 - 30000,)),     # window seeds cross 2^32 (two-word MT keys)
@@ -404,10 +408,18 @@ def test_v1_exact_order_matches_exact_oracle(F, lo, hi, R, B, epochs):
 
 
 def test_exact_order_unsupported_configs():
+    """The GPU exact orders' bounds (pss.h): V1 shuffle_buffer < 2^31, V2 num_samples < 2^31
+    and shuffle_buffer < 2^30; the handle refuses others at pss_set_order_mode (no launch)."""
     from partiallyshuffledistributedsampler_amd import _lib
     lengths = np.full(10, 1000)
     with pytest.raises(_lib.PSSError):
-        pss.IndexEngine(lengths, 10000, 2, 16384, 1, device=0, order="exact")    # V1, B > 16000
+        pss.IndexEngine(lengths, 10000, 2, 2 ** 31, 1, device=0, order="exact")     # V1, B >= 2^31
+    with pytest.raises(_lib.PSSError):
+        pss.IndexEngine(lengths, 10000, 2, 2 ** 30, 2, device=0, order="exact")     # V2, B >= 2^30
+    big = np.full(4, 2 ** 30)
+    with pytest.raises(_lib.PSSError):
+        pss.IndexEngine(big, 2 ** 32, 2, 4096, 2, device=0, order="exact")          # V2, ns = 2^31
+    pss.IndexEngine(lengths, 10000, 2, 2 ** 20, 1, device=0, order="exact").close()  # V1 big windows: accepted
 
 
 @pytest.mark.parametrize("name", scenario_names("v2"))
@@ -434,7 +446,7 @@ def test_v2_exact_order_matches_reference_streams(name):
 @pytest.mark.parametrize("F,lo,hi,R,B,epochs", [
     (37, 1, 900, 7, 40, (0, 5)),
     (50, 1000, 5000, 3, 3000, (2,)),                # partial last pool2 window
-    (40, 2000, 9000, 2, 4096, (1,)),                # largest exact pool
+    (40, 2000, 9000, 2, 4096, (1,)),                # pool2 windows of one decode tile
     (13, 1, 50, 5, 100, (0, 9)),                    # ns < B: tail only
     (9, 20, 40, 2, 70, (3,)),                       # B < ns < 2B
     (100, 1, 3, 8, 7, (0,)),                        # tiny pools

@@ -72,6 +72,9 @@ def test_history_and_exact_streams(ver, name):
             else:
                 skip = resume * bs if resume is not None else 0
                 got = O.v2_exact_stream(ep, h.old_start, h.start, h.ns, B, N, skip)
+                # the rank-select restatement (the checker of big pools) reproduces it too
+                got_rs = O.v2_exact_stream_rs(ep, h.old_start, h.start, h.ns, B, N, skip)
+                assert np.array_equal(got_rs, got), (name, rank, ep)
             # the recorded stream stops early only via the tmp_count == 1 quirk
             assert got[:len(stream)].tolist() == stream, (name, rank, ep)
             if er["num_batches"] * bs < len(got):
@@ -149,3 +152,33 @@ def test_pyref_loops_reproduce_reference_streams():
             got = [d.get_index() for _ in range(len(want))]
             got = [x - N if x >= N else x for x in got]
             assert got == want, (name, rrec["rank"])
+
+
+def _rs_cases():
+    rng = np.random.default_rng(2024)
+    cases = [(300, 2000, 3), (4096, 4096 * 5 + 17, 2), (1, 50, 1), (7, 7, 2), (70, 130, 4),
+             (20000, 20000 * 3 + 5, 1), (5000, 4999, 2), (64, 64 * 40, 3), (3, 200, 2)]
+    for _ in range(24):
+        B = int(np.exp(rng.uniform(0, np.log(20000))))
+        ns = int(rng.integers(1, 4 * B + 3))
+        cases.append((max(B, 1), ns, int(rng.integers(1, 5))))
+    return cases
+
+
+@pytest.mark.parametrize("B,ns,R", _rs_cases())
+def test_v2_rank_select_oracle_equals_list_remove_restatement(B, ns, R):
+    """orc_v2_exact_stream_rs (rank-select bitmaps, O(log B) per draw) against the list.remove
+    restatement (V2:101-106 verbatim) on random geometries up to B = 20000, including ns < B,
+    ns between B and 2B, the per-step reseeding tail, epochs whose seeds need two MT key words,
+    resume skips, and ranks whose blocks wrap at N."""
+    N = ns * R - (R - 1) if R > 1 else ns
+    rng = np.random.default_rng(B * 7919 + ns)
+    for _ in range(2):
+        old = ns * int(rng.integers(0, R))
+        new = ns * int(rng.integers(0, R))
+        epoch = int(rng.choice([0, 3, 2 ** 32 - 5, 10 ** 10]))
+        skip = int(rng.integers(0, ns)) if rng.random() < 0.3 else 0
+        a = O.v2_exact_stream(epoch, old, new, ns, B, N, skip)
+        b = O.v2_exact_stream_rs(epoch, old, new, ns, B, N, skip)
+        assert len(a) == ns - skip
+        assert np.array_equal(a, b), (B, ns, R, old, new, epoch, skip)
