@@ -429,9 +429,19 @@ uint64_t orc_epoch_key(uint64_t seed, int64_t epoch) {
     return orc_mix64(orc_mix64(seed) ^ (uint64_t)epoch);
 }
 
-/* keyed bijection of [0,n): 6-round balanced Feistel on 2h bits + cycle walking.  Round
- * function: halves of h <= 8 bits -> top h bits of the low 16 bits of (R ^ k) * 0x9E37;
- * wider halves -> bits [24 - h, 24) of ((R ^ k) mod 2^24) * 0x9E3779. */
+/* keyed bijection of [0,n): balanced Feistel on 2h bits + cycle walking.  Halves of h <= 5
+ * bits (n <= 1024): 8 rounds of f = top h bits of murmur3 fmix32(R ^ k_i), k_i = rk[i % 6] +
+ * i * 0x9E3779B9.  Wider halves, 6 rounds: h <= 8 -> top h bits of the low 16 bits of
+ * (R ^ k) * 0x9E37; h > 8 -> bits [24 - h, 24) of ((R ^ k) mod 2^24) * 0x9E3779. */
+static uint32_t orc_fmix32(uint32_t x) {
+    x ^= x >> 16;
+    x *= 0x85EBCA6BU;
+    x ^= x >> 13;
+    x *= 0xC2B2AE35U;
+    x ^= x >> 16;
+    return x;
+}
+
 uint32_t orc_feistel(uint32_t x, uint32_t n, const uint32_t rk[6]) {
     if (n <= 1) return 0;
     int bits = 0; while ((1ull << bits) < (uint64_t)n) bits++;
@@ -439,11 +449,19 @@ uint32_t orc_feistel(uint32_t x, uint32_t n, const uint32_t rk[6]) {
     uint32_t mask = (1u << h) - 1u;
     do {
         uint32_t L = x >> h, R = x & mask;
-        for (int i = 0; i < 6; i++) {
-            uint32_t f = h <= 8 ? ((((R ^ rk[i]) * 0x9E37u) & 0xFFFFu) >> (16 - h))
-                                : (((((R ^ rk[i]) & 0xFFFFFFu) * 0x9E3779u) >> (24 - h)) & mask);
-            uint32_t t = L ^ f;
-            L = R; R = t;
+        if (h <= 5) {
+            for (int i = 0; i < 8; i++) {
+                uint32_t f = orc_fmix32(R ^ (rk[i % 6] + (uint32_t)i * 0x9E3779B9U)) >> (32 - h);
+                uint32_t t = L ^ f;
+                L = R; R = t;
+            }
+        } else {
+            for (int i = 0; i < 6; i++) {
+                uint32_t f = h <= 8 ? ((((R ^ rk[i]) * 0x9E37u) & 0xFFFFu) >> (16 - h))
+                                    : (((((R ^ rk[i]) & 0xFFFFFFu) * 0x9E3779u) >> (24 - h)) & mask);
+                uint32_t t = L ^ f;
+                L = R; R = t;
+            }
         }
         x = (L << h) | R;
     } while (x >= n);

@@ -61,7 +61,8 @@ PSS_HD int ceil_log2_u64(uint64_t n) {  // smallest b with 2^b >= n (n >= 1)
 }
 
 // Keyed bijection of [0, n): 6-round balanced Feistel over 2h bits + cycle walking.
-// Round function: multiplicative hashing of the keyed right half (one multiply per round).
+// Round function: multiplicative hashing of the keyed right half (one multiply per round);
+// halves of <= 5 bits take 8 rounds of a stronger mixer (feistel_fsmall, below).
 constexpr int kFeistelRounds = 6;
 
 // Round function for halves of h <= 8 bits (windows up to 65536): the top h bits of the low
@@ -79,10 +80,36 @@ PSS_HD uint32_t feistel_f24(uint32_t r, uint32_t k, uint32_t h) {
     return ((((r ^ k) & 0xFFFFFFu) * kFeistelM24) >> (24u - h)) & ((1u << h) - 1u);
 }
 
+// Halves of <= kFeistelSmallH bits (domains up to 1024 elements: V1 windows and V2 pools of
+// B <= 1024, off the bandwidth-bound paths): the one-multiply round functions above are nearly
+// linear in a 2..5-bit R and leave neighbouring images dependent (tests/test_schedule_quality.py
+// measured z = 20-120 on the law of (pi(0), pi(1)) at n = 16..256).  These domains take 8 rounds
+// of a full 32-bit mixer instead -- the top h bits of murmur3's fmix32(R ^ k_i), round key
+// k_i = k[i mod 6] + i * 0x9E3779B9 (the same six key words) -- which leaves no measurable
+// dependence (|z| < 3 down to n = 2).
+constexpr uint32_t kFeistelSmallH = 5;
+constexpr int kFeistelSmallRounds = 8;
+
+PSS_HD uint32_t feistel_fsmall(uint32_t r, uint32_t k, uint32_t h) {
+    uint32_t x = r ^ k;
+    x ^= x >> 16;
+    x *= 0x85EBCA6Bu;
+    x ^= x >> 13;
+    x *= 0xC2B2AE35u;
+    x ^= x >> 16;
+    return x >> (32u - h);
+}
+
 PSS_HD uint32_t feistel_pass(uint32_t x, uint32_t h, const uint32_t *k) {
     const uint32_t mask = (1u << h) - 1u;
     uint32_t L = x >> h, R = x & mask;
-    if (h <= 8) {
+    if (h <= kFeistelSmallH) {
+        for (int i = 0; i < kFeistelSmallRounds; i++) {
+            const uint32_t t = L ^ feistel_fsmall(R, k[i % kFeistelRounds] + (uint32_t)i * 0x9E3779B9u, h);
+            L = R;
+            R = t;
+        }
+    } else if (h <= 8) {
         const uint32_t sh = 16u - h;
 #pragma unroll
         for (int i = 0; i < kFeistelRounds; i++) {
@@ -100,6 +127,9 @@ PSS_HD uint32_t feistel_pass(uint32_t x, uint32_t h, const uint32_t *k) {
     }
     return (L << h) | R;
 }
+
+// the 16-bit packed forms (feistel2_pk16 / feistel4_pk16) serve halves in (kFeistelSmallH, 8]
+PSS_HD bool feistel_packed_ok(uint32_t h) { return h > kFeistelSmallH && h <= 8; }
 
 PSS_HD uint32_t feistel(uint32_t x, uint32_t n, uint32_t h, const uint32_t *k) {
     if (n <= 1) return 0;

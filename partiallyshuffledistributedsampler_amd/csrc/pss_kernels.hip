@@ -485,8 +485,8 @@ hipError_t launch_v1(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, 
     const MapArgs ma = mapped ? *mapped : MapArgs{};
 #define PSS_V1(PK, MP) hipLaunchKernelGGL((k_v1_feistel<PK, MP>), dim3((uint32_t)waves), dim3(64), 0, s, g, vp, \
                                           ranks, rank_lo, (const uint32_t *)key_ws, pos_lo, count, out, ma)
-    if (vp.hB <= 8 && mapped) PSS_V1(true, true);
-    else if (vp.hB <= 8) PSS_V1(true, false);
+    if (feistel_packed_ok(vp.hB) && mapped) PSS_V1(true, true);
+    else if (feistel_packed_ok(vp.hB)) PSS_V1(true, false);
     else if (mapped) PSS_V1(false, true);
     else PSS_V1(false, false);
 #undef PSS_V1

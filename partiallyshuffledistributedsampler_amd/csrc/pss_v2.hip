@@ -605,7 +605,7 @@ __global__ __launch_bounds__(64) void k_v2_emit_x(Geometry g, V2Plan pl,
     const bool fast_tile = e_lo == 0 && e_hi == nvalid && B >= 256 && !walk_full;
     Pacer pace(nvalid);
     uint32_t tl0 = 0;
-    if (fast_tile && (B & 255u) == 0 && w_last > w_lo + 1) {
+    if (fast_tile && (B & 255u) == 0 && w_last > w_lo + 1 && feistel_packed_ok(hB)) {
         // Fast phase: whole super-batches of windows w_lo .. w_last - 2 (full, no cycle walk),
         // as one counted loop per window with the window's round keys in SGPRs.  B % 256 == 0
         // and tlo % 256 == 0 put every super-batch inside one window.
@@ -778,7 +778,7 @@ __global__ __launch_bounds__(64) void k_v2_emit_x(Geometry g, V2Plan pl,
         int64_t *ot = out + (int64_t)rl * count - pos_lo + pl.T;
         const int64_t etail = (int64_t)rl * count - pos_lo + pl.T;
         const bool whole = pl.T >= pos_lo && pl.T + pl.P1 <= pos_hi;
-        if (whole && (P1 & 255u) == 0 && hT <= 8 && P1 == (1u << (2 * hT))) {
+        if (whole && (P1 & 255u) == 0 && feistel_packed_ok(hT) && P1 == (1u << (2 * hT))) {
             // P1 = 4^hT: no cycle walking; four independent chains per lane, packed in pairs
             uint32_t kp[kFeistelRounds];
 #pragma unroll

@@ -264,8 +264,9 @@ __device__ __forceinline__ void feistel_table(uint32_t off, uint32_t cnt, uint32
             uint32_t x[4], y[4];
 #pragma unroll
             for (int j = 0; j < 4; j++) x[j] = off + s0 + 64u * j + (uint32_t)lane;
-            if (h <= 8) feistel4_uniform<true>(x, h, K, y);
-            else feistel4_uniform<false>(x, h, K, y);
+            if (feistel_packed_ok(h)) feistel4_uniform<true>(x, h, K, y);
+            else if (h > 8) feistel4_uniform<false>(x, h, K, y);
+            else for (int j = 0; j < 4; j++) y[j] = feistel_once(x[j], h, K);
 #pragma unroll
             for (int j = 0; j < 4; j++) {
                 const uint32_t s = s0 + 64u * j + (uint32_t)lane;
@@ -552,7 +553,7 @@ hipError_t launch_v2_grp(const Geometry &g, const RankDesc *ranks, int32_t rank_
     RankArgs ra;
     const int use_ra = rank_args ? 1 : 0;
     if (rank_args) ra = *rank_args;
-    const bool packed = pl.hB <= 8;
+    const bool packed = pl.hB <= 8;   // grouped pools: B > 16384, so hB >= 8 (never the small-half rounds)
     const bool pow2 = pl.gr.r == 0 && (pl.gr.q & (pl.gr.q - 1u)) == 0u;   // every group 2^b slots
 #define PSS_GE(O, N, PK, P2) hipLaunchKernelGGL((k_g_emit<O, N, PK, P2>), grid, dim3(64), lds, s, g, pl, ranks, \
                                                 rank_lo, (const uint32_t *)KT, (const uint32_t *)VAL, dt, pos_lo, count, out, \

@@ -65,21 +65,46 @@ def test_v1_window_permutation_is_uniform(B, ns):
     assert abs(d.mean()) < 0.02 * B
 
 
-@pytest.mark.parametrize("B,ns", [(20000, 160000)])
-def test_v2_grouped_pool_law_matches_reference(B, ns):
-    # pools beyond LDS (P1 > 16384) draw in bursts of 16 inside G = ceil(P1 / 4096) slot groups
-    # (DESIGN.md §3.2.1); the displacement law must still be the reference's single-pool law
+def _burst_stats(streams, B, T):
+    """Per aligned run of 16 consecutive outputs among the replacement steps (a grouped pool's
+    burst: one 4096-slot group draws all 16): the spread (max - min) / B, and |diff| / B of
+    consecutive outputs inside the run."""
+    spread, step = [], []
+    for s in streams:
+        x = np.asarray(s[:T // 16 * 16], dtype=np.float64).reshape(-1, 16)
+        spread.append((x.max(1) - x.min(1)) / B)
+        step.append(np.abs(np.diff(x, axis=1)).ravel() / B)
+    return np.concatenate(spread), np.concatenate(step)
+
+
+@pytest.mark.parametrize("B,ns,nex,atol", [(20000, 160000, 3, 0.02), (65536, 4 * 65536, 4, 0.01),
+                                           (1 << 20, 3 << 20, 2, 0.015)])
+def test_v2_grouped_pool_law_matches_reference(B, ns, nex, atol):
+    """Pools beyond LDS (P1 > 16384) draw in bursts of 16 inside G = ceil(P1 / 4096) slot
+    groups.  Against the reference's own single-pool draws (V2:101-106, the
+    exact restatement -- rank-select form for the big pools), on the grouped geometries: B =
+    20000 (G = 5, groups of 4000: multiply-shift draws), 65536 (G = 16) and C5's 2^20 (G = 256,
+    groups of 4096 with paired draws): displacement quantiles, spread, consecutive-output
+    statistics, and within-burst statistics (the spread of each run of 16 outputs and the gaps
+    inside it) against the same positions of the reference's stream."""
     N = 10**12
-    ex = [O.v2_exact_stream(e, 0, 0, ns, B, N) for e in range(3)]
+    T = ns - B
+    ex = [O.v2_exact_stream_rs(e, 0, 0, ns, B, N) for e in range(nex)]
     ph = [O.v2_philox_stream(O.epoch_key(s, e), r, 0, 0, ns, B, N)
-          for s in (0, 3) for e in range(2) for r in range(2)]
+          for s in (0, 3) for e in range(2) for r in range(2)][:max(4, 2 * nex)]
     dx, upx, lagx = _stats(ex, B)
     dp, upp, lagp = _stats(ph, B)
     assert dp.min() >= -2.0 and dx.min() >= -2.0
-    np.testing.assert_allclose(np.quantile(dp, QS), np.quantile(dx, QS), atol=0.02)
+    np.testing.assert_allclose(np.quantile(dp, QS), np.quantile(dx, QS), atol=atol)
     assert abs(dp.std() / dx.std() - 1) < 0.01
     assert abs(upp - upx) < 0.005
     assert abs(lagp - lagx) < 0.005
+    sx, gx = _burst_stats(ex, B, T)
+    sp, gp = _burst_stats(ph, B, T)
+    BQ = [0.05, 0.25, 0.5, 0.75, 0.95]
+    np.testing.assert_allclose(np.quantile(sp, BQ), np.quantile(sx, BQ), atol=2 * atol)
+    np.testing.assert_allclose(np.quantile(gp, BQ), np.quantile(gx, BQ), atol=2 * atol)
+    assert abs(sp.mean() / sx.mean() - 1) < 0.01 and abs(gp.mean() / gx.mean() - 1) < 0.01
 
 
 # ---- randomness of the counter schedule's primitives ------------------------------------------
@@ -132,26 +157,49 @@ def test_paired_draws_are_independent(P1):
         assert ok, stat
 
 
-@pytest.mark.parametrize("n", [1024, 4096, 65536, 1 << 20, 5000, 3 << 20])
+def _pair_counts_expected(n, bins, K):
+    """Expected (pi(a), pi(b)) bin counts for K uniform random permutations of [0, n): an
+    ordered pair of DISTINCT elements (a permutation never maps two positions to one value)."""
+    c = np.bincount(np.arange(n) * bins // n, minlength=bins).astype(np.float64)
+    return K * (np.outer(c, c) - np.diag(c)) / (n * (n - 1))
+
+
+def _chi2_expected_ok(counts, exp, z=5.0):
+    counts, exp = np.asarray(counts, np.float64).ravel(), np.asarray(exp, np.float64).ravel()
+    m = exp > 0
+    x, k = ((counts[m] - exp[m]) ** 2 / exp[m]).sum(), int(m.sum()) - 1
+    return abs(x - k) < z * np.sqrt(2 * k), (x, k)
+
+
+@pytest.mark.parametrize("n", [4, 16, 64, 100, 256, 700, 1024, 4096, 65536, 1 << 20, 5000, 3 << 20])
 def test_feistel_insertion_order_is_uniform(n):
-    """The keyed Feistel bijections (16-bit round function for halves <= 8 bits, 24-bit one
-    above; cycle walking when n is not a power of 4): over many keys, the images of the first
-    positions are uniform over [0, n) (chi-square on 32 bins) and the images of two neighbours
-    are independent (chi-square on 8 x 8 bins).  (Below 1024 elements, halves of <= 5 bits,
-    the 16-bit rounds leave a small neighbour dependence: z ~ 3-6 at n = 256)"""
+    """The keyed Feistel bijections (8 fmix32 rounds for halves <= 5 bits, the 16-bit round
+    function up to 8 bits, the 24-bit one above; cycle walking when n is not a power of 4): over
+    many keys the images of single positions are uniform over [0, n) (chi-square on up to 32
+    bins) and the images of two neighbours follow the law of a uniform random permutation
+    (chi-square on up to 8 x 8 bins against the distinct-pair law) -- the law of the
+    reference's Fisher-Yates windows (V1:169-170).  Before the small-half rounds, n = 16 / 64 /
+    256 failed this at z = 74 / 122 / 22."""
     rng = np.random.default_rng(n)
-    keys = rng.integers(0, 2 ** 32, (4000, 6), dtype=np.uint64).astype(np.uint32)
+    K = 6000
+    keys = rng.integers(0, 2 ** 32, (K, 6), dtype=np.uint64).astype(np.uint32)
     y0 = np.array([O.feistel(0, n, k) for k in keys], dtype=np.int64)
     y1 = np.array([O.feistel(1, n, k) for k in keys], dtype=np.int64)
-    y7 = np.array([O.feistel(7, n, k) for k in keys], dtype=np.int64)
+    y7 = np.array([O.feistel(min(7, n - 1), n, k) for k in keys], dtype=np.int64)
+    b1 = min(32, n)
     for y in (y0, y1, y7):
-        ok, stat = _chi2_ok(np.bincount(y * 32 // n, minlength=32))
+        exp = K * np.bincount(np.arange(n) * b1 // n, minlength=b1) / n
+        ok, stat = _chi2_expected_ok(np.bincount(y * b1 // n, minlength=b1), exp)
         assert ok, stat
-    ok, stat = _chi2_ok(np.bincount((y0 * 8 // n) * 8 + y1 * 8 // n, minlength=64))
-    assert ok, stat
+    b2 = min(8, n)
+    for a, b in ((y0, y1), (y1, y7)):
+        got = np.bincount((a * b2 // n) * b2 + b * b2 // n, minlength=b2 * b2)
+        ok, stat = _chi2_expected_ok(got, _pair_counts_expected(n, b2, K))
+        assert ok, stat
     # one key: a permutation of [0, n) whose neighbouring images are uncorrelated
-    if n <= 65536:
+    if 64 <= n <= 65536:
         perm = np.array([O.feistel(i, n, keys[0]) for i in range(n)], dtype=np.int64)
         assert np.array_equal(np.sort(perm), np.arange(n))
-        assert abs(np.corrcoef(perm[:-1], perm[1:])[0, 1]) < 0.05
-        assert abs(np.corrcoef(np.arange(n), perm)[0, 1]) < 0.05
+        lim = 0.05 if n >= 1024 else 4.0 / np.sqrt(n)
+        assert abs(np.corrcoef(perm[:-1], perm[1:])[0, 1]) < lim
+        assert abs(np.corrcoef(np.arange(n), perm)[0, 1]) < lim
