@@ -97,7 +97,7 @@ PSS_HD uint32_t feistel_fsmall(uint32_t r, uint32_t k, uint32_t h) {
     x ^= x >> 13;
     x *= 0xC2B2AE35u;
     x ^= x >> 16;
-    return x >> (32u - h);
+    return h ? x >> (32u - h) : 0u;   // h = 0: a one-element domain (feistel_once with n = 1)
 }
 
 PSS_HD uint32_t feistel_pass(uint32_t x, uint32_t h, const uint32_t *k) {

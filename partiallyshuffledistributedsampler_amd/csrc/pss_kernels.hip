@@ -237,6 +237,7 @@ struct V1Plan {
     int64_t per_wave;          // super-blocks per wave
     int64_t w_lo, nw;          // windows of the key table
     uint32_t B, hB, walk_full, fast_ok;
+    uint32_t pairs;            // fast super-blocks in the 16-B pair layout (PSS_V1_PAIRS=0: off)
 };
 
 // One wave per (rank, run of per_wave super-blocks).  Lane l computes positions p0 + 64 j + l,
@@ -315,18 +316,47 @@ __global__ __launch_bounds__(64) void k_v1_feistel(Geometry g, V1Plan vp, const 
         for (; sb < sb_w_end; sb++) {
             const int64_t p0 = sb * 256;
             if (p0 < pos_lo || p0 + 256 > pos_hi) { slow_sb(sb); continue; }
-            // whole super-block inside one full window of 4^hB elements: no cycle walking
+            // whole super-block inside one full window of 4^hB elements: no cycle walking.
+            // Pair layout (16-B aligned output): lane l owns positions p0 + 2l, 2l + 1 and
+            // p0 + 128 + 2l, 2l + 1, written by two 16-byte stores (8-byte pairs when mapped)
+            // instead of four 8-byte ones.
             const uint32_t x0 = (uint32_t)(p0 - wB);
+            const bool pair = vp.pairs && !MAPPED ? ((uintptr_t)(o + p0) & 15u) == 0
+                                                  : vp.pairs && (((uintptr_t)(ofp + p0) | (uintptr_t)(ooff + p0)) & 7u) == 0;
+            const uint32_t l2 = 2u * (uint32_t)lane;
+            uint32_t x[4];
+            if (pair) { x[0] = x0 + l2; x[1] = x0 + l2 + 1u; x[2] = x0 + 128u + l2; x[3] = x0 + 129u + l2; }
+            else { x[0] = x0 + lane; x[1] = x0 + 64u + lane; x[2] = x0 + 128u + lane; x[3] = x0 + 192u + lane; }
             uint32_t y[4];
             if constexpr (PACKED) {
-                const uint32_t x[4] = {x0 + lane, x0 + 64u + lane, x0 + 128u + lane, x0 + 192u + lane};
                 feistel4_pk16(x, vp.hB, kp, y);
             } else {
 #pragma unroll
-                for (int j = 0; j < 4; j++) y[j] = feistel_once(x0 + 64u * j + lane, vp.hB, kp);
+                for (int j = 0; j < 4; j++) y[j] = feistel_once(x[j], vp.hB, kp);
             }
+            if (pair) {
 #pragma unroll
-            for (int j = 0; j < 4; j++) put(p0 + 64 * j + lane, wrap_id(base + y[j], g.N));
+                for (int h = 0; h < 2; h++) {
+                    const int64_t p = p0 + 128 * h + l2;
+                    const int64_t a = wrap_id(base + y[2 * h], g.N), b = wrap_id(base + y[2 * h + 1], g.N);
+                    if constexpr (MAPPED) {
+                        int32_t fa, fb;
+                        int64_t oa, ob;
+                        map_one_bucketed(ma.prefix, ma.F, ma.BT, ma.kb, ma.nb, a, fa, oa);
+                        map_one_bucketed(ma.prefix, ma.F, ma.BT, ma.kb, ma.nb, b, fb, ob);
+                        *(int2 *)(ofp + p) = make_int2(fa, fb);
+                        *(int2 *)(ooff + p) = make_int2((int32_t)oa, (int32_t)ob);
+                    } else {
+                        longlong2 v;
+                        v.x = a;
+                        v.y = b;
+                        *(longlong2 *)(o + p) = v;
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < 4; j++) put(p0 + 64 * j + lane, wrap_id(base + y[j], g.N));
+            }
         }
     }
 }
@@ -471,6 +501,11 @@ hipError_t launch_v1(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, 
     vp.walk_full = vp.B != (1u << (2 * vp.hB));
     // fast super-blocks: inside one full window that needs no cycle walking
     vp.fast_ok = g.shuffle && !vp.walk_full && (g.B % 256) == 0;
+    static const uint32_t pairs_env = [] {   // A/B knob: 16-byte pair stores on fast super-blocks
+        const char *e = getenv("PSS_V1_PAIRS");
+        return (uint32_t)!(e && e[0] == '0');
+    }();
+    vp.pairs = pairs_env;
     // ~16 super-blocks (4096 positions, 32 KB of output) per wave, at least 8 waves per CU
     const int64_t total = (int64_t)nr * vp.nsb;
     static const int64_t per_env = [] {   // A/B knob: super-blocks per wave

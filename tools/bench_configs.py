@@ -12,6 +12,8 @@ survey names, each as the share one of 8 GPUs would generate:
   c3     V2, 100K files x 10K = 1B, R=1024 -> ranks [0, 128)         B=4096
   c4     V2, Zipf(1.5)*150 files (N=2.59e9 > 2^31), R=4096 -> [0, 512)  B=4096
   c5     V2, C2 files, B=2^20 (HBM slot-table path), 100 epochs       (reports per-epoch mean)
+  c5x    c5 with order="exact"
+  c5v1x  V1 on c5's shape (B=2^20 windows, HBM-staged resolution) with order="exact"
 Prints one JSON line per config: ids per step, ms per step, G idx/s, per-kernel ms.
 """
 import json
@@ -75,6 +77,10 @@ def main():
             run(w, z, 4096, 512, 4096, 2, 10)
         elif w == "c5":
             run(w, c2, 8, 8, 1 << 20, 2, 100)
+        elif w == "c5x":
+            run(w, c2, 8, 8, 1 << 20, 2, 2, warmup=1, order="exact")
+        elif w == "c5v1x":
+            run(w, c2, 8, 8, 1 << 20, 1, 3, warmup=1, order="exact")
 
 
 if __name__ == "__main__":
