@@ -173,6 +173,62 @@ __device__ void mt_draws(uint32_t *mt, uint32_t nd, Bound bound, Emit emit) {
         }
     }
 }
+
+// The first _randbelow(n) draw of a freshly seeded stream, ONE SEED PER LANE (V2's tail steps
+// reseed before every draw, V2:107-112, and use only its first word or few).  Seeding is
+// init_by_array over the 1-2 key words (klen), two serial chains of 624 + 623 steps; draw word
+// w < 227 of the first twist needs only s[w], s[w + 1] and s[w + 397] of the seeded state, so
+// each lane runs the chains itself (loop 1 twice: once for its wrap value, once beside loop 2)
+// and keeps s[0 .. kFirstWords] and s[397 .. 397 + kFirstWords).  Returns false when all
+// kFirstWords words were rejected (probability < 2^-16 per lane): the caller then runs the
+// wave path (mt_seed + mt_draws) for that lane's seed.  The init_genrand(19650218) chain is
+// the same for every lane (scalar code).
+constexpr int kFirstWords = 16;
+
+__device__ __forceinline__ bool mt_first_draw_lane(uint32_t key0, uint32_t key1, int klen, uint32_t n,
+                                                   uint32_t &out) {
+    const uint32_t add_even = key0, add_odd = klen == 2 ? key1 + 1u : key0;
+    auto f1 = [](uint32_t p) { return (p ^ (p >> 30)) * 1664525u; };
+    auto f2 = [](uint32_t p) { return (p ^ (p >> 30)) * 1566083941u; };
+    // pass 1: loop 1's chain a[1 .. 623] (a[i] = (g[i] ^ f1(a[i-1])) + key term, a[0] = g[0]),
+    // then its wrap iteration (k = 623, i = 1): a'[1]
+    uint32_t g = 19650218u, a = g, a1 = 0u;
+    for (int i = 1; i < kMtN; i++) {
+        g = 1812433253u * (g ^ (g >> 30)) + (uint32_t)i;
+        a = (g ^ f1(a)) + (((i - 1) & 1) ? add_odd : add_even);
+        if (i == 1) a1 = a;
+    }
+    const uint32_t a1w = (a1 ^ f1(a)) + add_odd;
+    // pass 2: loop 2 (b[i] = (a[i] ^ f2(b[i-1])) - i, i = 2 .. 623, b[1] = a'[1]) with loop 1's
+    // a[i] regenerated beside it
+    g = 1812433253u * (19650218u ^ (19650218u >> 30)) + 1u;   // g[1]
+    a = a1;
+    uint32_t b = a1w;
+    uint32_t lo[kFirstWords + 1], hi[kFirstWords];   // s[0 .. K], s[397 .. 397 + K)
+    auto step = [&](int i) {
+        g = 1812433253u * (g ^ (g >> 30)) + (uint32_t)i;
+        a = (g ^ f1(a)) + (((i - 1) & 1) ? add_odd : add_even);
+        b = (a ^ f2(b)) - (uint32_t)i;
+    };
+#pragma unroll
+    for (int i = 2; i <= kFirstWords; i++) { step(i); lo[i] = b; }
+    for (int i = kFirstWords + 1; i < kMtM; i++) step(i);
+#pragma unroll
+    for (int i = kMtM; i < kMtM + kFirstWords; i++) { step(i); hi[i - kMtM] = b; }
+    for (int i = kMtM + kFirstWords; i < kMtN; i++) step(i);
+    lo[1] = (a1w ^ f2(b)) - 1u;     // loop 2's wrap (i = 1, mt[0] = b[623])
+    lo[0] = 0x80000000u;
+    const uint32_t kbits = 32u - (uint32_t)__builtin_clz(n);   // n.bit_length()
+    bool found = false;
+    uint32_t r = 0;
+#pragma unroll
+    for (int w = 0; w < kFirstWords; w++) {
+        const uint32_t y = mt_temper(mt_twist_word(lo[w], lo[w + 1], hi[w])) >> (32u - kbits);
+        if (!found && y < n) { r = y; found = true; }
+    }
+    out = r;
+    return found;
+}
 }  // namespace
 
 }  // namespace pss

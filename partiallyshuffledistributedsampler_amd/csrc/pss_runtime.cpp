@@ -710,6 +710,7 @@ int generate_impl(pss_sampler *h, int32_t rank_lo, int32_t rank_hi, int64_t pos_
         mk(pss::K_V1, s);
         PSS_HIP(pss::launch_v1_exact(g, h->d_ranks.p, rank_lo, nr, pos_lo, count, h->epoch, out_dev,
                                      h->d_sort.p, s));
+        mk(-1, s);
     } else if (h->version == 1) {
         const size_t sb = pss::v1_workspace_bytes(g, nr, pos_lo, count);
         if (sb) PSS_HIP(h->d_sort.ensure(words(sb)));
@@ -719,6 +720,7 @@ int generate_impl(pss_sampler *h, int32_t rank_lo, int32_t rank_hi, int64_t pos_
         mk(pss::K_V2_EMIT, s);
         PSS_HIP(pss::launch_v2_exact(g, h->d_ranks.p, rank_lo, nr, pos_lo, count, h->epoch, out_dev,
                                      h->d_sort.p, s));
+        mk(-1, s);
     } else if (lookahead_on() && pss::v2_stage_split(g, nr, h->emit_path)) {
         return generate_v2_lookahead(h, g, rank_lo, nr, pos_lo, count, out_dev, s, mk, ma, rap);
     } else {

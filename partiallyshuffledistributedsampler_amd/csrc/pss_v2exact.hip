@@ -8,8 +8,9 @@
 //
 //   draws   every pool2 window is drawn from its own freshly seeded stream (segment 0 from
 //           seed(e+2) of init_iter, V2:147; segment s >= 1 from seed(e + (s-1)*10000)), k1 and
-//           k2 alternating; once pool2 stays empty every step reseeds, so each tail step's k1
-//           is the first draw of its own stream.  One wave per stream (pss_mt.h).
+//           k2 alternating: one wave per stream (pss_mt.h).  Once pool2 stays empty every step
+//           reseeds, so each tail step's k1 is the first draw of its own stream: one LANE per
+//           tail step (mt_first_draw_lane), 64 seeds per wave.
 //   decode  "remove the k-th, append at the end" is a rank-deletion problem: with the
 //           elements numbered in insertion order, step t removes the k_t-th alive one.  A block
 //           of steps [a, b) is solved in the frame of its start (alive elements 0..B_a-1, its
@@ -70,7 +71,7 @@ __device__ __forceinline__ uint32_t map_right(const uint32_t *DL, uint32_t nL, u
 }
 }  // namespace
 
-// ---- draws: one wave per MT stream (pool2 windows, then tail steps) -------------------------
+// ---- draws: one wave per pool2 window's MT stream -----------------------------------------------
 __global__ __launch_bounds__(64) void k_v2x_draws(V2xGeo x, int64_t epoch, uint32_t jobs, uint64_t blk0,
                                                   uint32_t *__restrict__ K1, uint32_t *__restrict__ K2) {
     __shared__ uint32_t mt[kMtN];
@@ -89,13 +90,43 @@ __global__ __launch_bounds__(64) void k_v2x_draws(V2xGeo x, int64_t epoch, uint3
                      else k1[t0 + (d >> 1)] = r;
                  });
         for (uint32_t u = W + threadIdx.x; u < x.B; u += 64) k2[t0 + u] = 0;   // padding steps
-    } else {                  // tail step j: the first draw after its reseed
-        const uint32_t j = job - x.S;
-        const int64_t seed = x.S >= 1 ? epoch + (int64_t)(x.S - 1 + j) * 10000
-                                      : (j == 0 ? epoch + 2 : epoch + (int64_t)(j - 1) * 10000);
-        mt_seed_int(mt, seed);
-        const uint32_t n = x.P - j, t = x.T + j;
-        mt_draws(mt, 1u, [&](uint32_t) { return n; }, [&](uint32_t, uint32_t r) { k1[t] = r; });
+    }
+}
+
+// seed of tail step j (pool2 stays empty: every step reseeds first, V2:107-109)
+__device__ __forceinline__ int64_t v2x_tail_seed(const V2xGeo &x, int64_t epoch, uint32_t j) {
+    return x.S >= 1 ? epoch + (int64_t)(x.S - 1 + j) * 10000
+                    : (j == 0 ? epoch + 2 : epoch + (int64_t)(j - 1) * 10000);
+}
+
+// ---- tail draws: one lane per tail step (its own reseeded stream's first draw) ---------------
+// 64 tail steps per wave, each lane seeding its own MT (mt_first_draw_lane); the rare lane whose
+// first kFirstWords words are all rejected is redone by the whole wave (mt_seed + mt_draws).
+__global__ __launch_bounds__(64) void k_v2x_tail_draws(V2xGeo x, int64_t epoch, uint32_t per_rank,
+                                                       uint64_t blk0, uint32_t *__restrict__ K1) {
+    __shared__ uint32_t mt[kMtN];
+    const uint64_t b = blk0 + blockIdx.x;
+    const uint32_t rl = (uint32_t)(b / per_rank), j0 = (uint32_t)(b % per_rank) * 64u;
+    uint32_t *k1 = K1 + (size_t)rl * x.ns;
+    const int lane = threadIdx.x;
+    const uint32_t j = j0 + (uint32_t)lane;
+    const bool valid = j < x.P;
+    const int64_t seed = v2x_tail_seed(x, epoch, valid ? j : 0u);
+    const uint64_t m = seed < 0 ? (uint64_t)(-(seed + 1)) + 1u : (uint64_t)seed;
+    const uint32_t key0 = (uint32_t)m, key1 = (uint32_t)(m >> 32);
+    const uint32_t n = valid ? x.P - j : 1u;
+    uint32_t r = 0;
+    const bool ok = mt_first_draw_lane(key0, key1, key1 ? 2 : 1, n, r);
+    if (valid && ok) k1[x.T + j] = r;
+    uint64_t redo = __ballot(valid && !ok);
+    while (redo) {
+        const int l = __ffsll((long long)redo) - 1;
+        redo &= redo - 1ull;
+        const uint32_t jl = j0 + (uint32_t)l;
+        mt_seed_int(mt, v2x_tail_seed(x, epoch, jl));
+        const uint32_t nl = x.P - jl, t = x.T + jl;
+        mt_draws(mt, 1u, [&](uint32_t) { return nl; }, [&](uint32_t, uint32_t rr) { k1[t] = rr; });
+        wave_lds_order();
     }
 }
 
@@ -104,7 +135,7 @@ __global__ __launch_bounds__(kTileNT) void k_v2x_tile(V2xGeo x, uint32_t per_ran
                                                       const uint32_t *__restrict__ K1,
                                                       const uint32_t *__restrict__ K2,
                                                       uint32_t *__restrict__ V, uint32_t *__restrict__ O,
-                                                      uint32_t *__restrict__ Q2) {
+                                                      uint32_t *__restrict__ Q2, uint32_t *__restrict__ SV) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     uint32_t *va = smem, *oa = smem + kTile, *vb = smem + 2 * kTile, *ob = smem + 3 * kTile;
     const uint64_t bi = blk0 + blockIdx.x;
@@ -172,7 +203,16 @@ __global__ __launch_bounds__(kTileNT) void k_v2x_tile(V2xGeo x, uint32_t per_ran
         uint32_t *t = va; va = vb; vb = t;
         t = oa; oa = ob; ob = t;
     }
-    if (pool1) {
+    if (pool1 && SV) {
+        // chain mode (pools of <= kTile entries): each step's answer in step order, and the
+        // tile's survivors -- the frame positions still alive at its end, in order: survivor r
+        // is r + #{i : D_i - i <= r} over the sorted deletions D (k_v2x_compose / _emit)
+        uint32_t *ans = V + (size_t)rl * x.ns + t0;
+        for (uint32_t u = threadIdx.x; u < n; u += kTileNT) ans[oa[u]] = va[u];
+        const uint32_t Bm = alive_at(B0, insu, t0 + n);
+        uint32_t *sv = SV + ((size_t)rl * x.tiles1 + job) * x.P;
+        for (uint32_t r = threadIdx.x; r < Bm; r += kTileNT) sv[r] = r + count_e_le(va, n, r);
+    } else if (pool1) {
         uint32_t *v = V + (size_t)rl * x.ns + t0, *o = O + (size_t)rl * x.ns + t0;
         for (uint32_t u = threadIdx.x; u < n; u += kTileNT) { v[u] = va[u]; o[u] = t0 + oa[u]; }
     } else {
@@ -329,6 +369,122 @@ __global__ __launch_bounds__(kGNT) void k_v2x_gmerge(V2xGeo x, uint32_t w, const
     for (uint32_t u = threadIdx.x; u < on; u += kGNT) { vd[o0 + u] = tv[u]; od[o0 + u] = to[u]; }
 }
 
+// ---- chain mode (pools of <= kTile entries): tiles linked by their survivor lists ----------
+// A_j = the absolute insertion numbers of the elements alive at tile j's start (sorted; initial
+// element p is number p, the element step t moves over from pool2 is P + t).  Frame position q of
+// tile j is A_j[q] below B_j = alive_at(t0_j), else the tile's own insertion P + t0_j + q - B_j,
+// and A_{j+1}[r] is frame position S_j[r] of tile j.  Three kernels replace the global merge
+// levels: per chunk of tiles the composite survivor map relative to the chunk's start
+// (compose), the chunks' A in rank order (link, one workgroup per rank), then every tile again
+// from its chunk's A, emitting the ids of its steps (emit).
+constexpr uint32_t kAbs = 0x80000000u;   // composite entry: an absolute insertion number
+constexpr int kChainNT = 1024;
+
+struct V2xChain {
+    uint32_t nch, tpc;     // chunks per rank, tiles per chunk
+    uint32_t *SV, *CC, *AA;
+};
+
+__global__ __launch_bounds__(kChainNT) void k_v2x_compose(V2xGeo x, V2xChain ch) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+    uint32_t *G = smem, *Gn = smem + x.P;
+    const uint32_t rl = blockIdx.x / ch.nch, c = blockIdx.x % ch.nch;
+    const uint32_t j0 = c * ch.tpc, j1 = j0 + ch.tpc < x.tiles1 ? j0 + ch.tpc : x.tiles1;
+    const uint32_t Ba0 = alive_at(x.P, x.T, j0 * (uint32_t)kTile);
+    for (uint32_t r = threadIdx.x; r < Ba0; r += kChainNT) G[r] = r;
+    __syncthreads();
+    uint32_t Bend = Ba0;
+    for (uint32_t j = j0; j < j1; j++) {
+        const uint32_t t0 = j * (uint32_t)kTile, n = x.ns - t0 < (uint32_t)kTile ? x.ns - t0 : (uint32_t)kTile;
+        const uint32_t Ba = alive_at(x.P, x.T, t0), Bm = alive_at(x.P, x.T, t0 + n);
+        const uint32_t *sv = ch.SV + ((size_t)rl * x.tiles1 + j) * x.P;
+        for (uint32_t r = threadIdx.x; r < Bm; r += kChainNT) {
+            const uint32_t q = sv[r];
+            Gn[r] = q < Ba ? G[q] : (kAbs | (x.P + t0 + (q - Ba)));
+        }
+        __syncthreads();
+        uint32_t *t = G; G = Gn; Gn = t;
+        Bend = Bm;
+    }
+    uint32_t *cc = ch.CC + ((size_t)rl * ch.nch + c) * x.P;
+    for (uint32_t r = threadIdx.x; r < Bend; r += kChainNT) cc[r] = G[r];
+}
+
+__global__ __launch_bounds__(kChainNT) void k_v2x_link(V2xGeo x, V2xChain ch) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+    uint32_t *A = smem, *An = smem + x.P;
+    const uint32_t rl = blockIdx.x;
+    for (uint32_t r = threadIdx.x; r < x.P; r += kChainNT) A[r] = r;   // alive_at(0) = P
+    __syncthreads();
+    for (uint32_t c = 0; c < ch.nch; c++) {
+        const uint32_t j0 = c * ch.tpc, j1 = j0 + ch.tpc < x.tiles1 ? j0 + ch.tpc : x.tiles1;
+        const uint32_t Ba = alive_at(x.P, x.T, j0 * (uint32_t)kTile);
+        const uint32_t te = j1 * (uint32_t)kTile < x.ns ? j1 * (uint32_t)kTile : x.ns;
+        const uint32_t Bm = alive_at(x.P, x.T, te);
+        uint32_t *aa = ch.AA + ((size_t)rl * ch.nch + c) * x.P;
+        const uint32_t *cc = ch.CC + ((size_t)rl * ch.nch + c) * x.P;
+        for (uint32_t r = threadIdx.x; r < Ba; r += kChainNT) aa[r] = A[r];
+        for (uint32_t r = threadIdx.x; r < Bm; r += kChainNT) {
+            const uint32_t v = cc[r];
+            An[r] = (v & kAbs) ? (v & ~kAbs) : A[v];
+        }
+        __syncthreads();
+        uint32_t *t = A; A = An; An = t;
+    }
+}
+
+__global__ __launch_bounds__(kChainNT) void k_v2x_emit(Geometry g, V2xGeo x, V2xChain ch,
+                                                       const RankDesc *__restrict__ ranks, int32_t rank_lo,
+                                                       const uint32_t *__restrict__ ANS,
+                                                       const uint32_t *__restrict__ Q2, int64_t pos_lo,
+                                                       int64_t count, int64_t *__restrict__ out) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+    uint32_t *A = smem, *An = smem + x.P;
+    const uint32_t rl = blockIdx.x / ch.nch, c = blockIdx.x % ch.nch;
+    const uint32_t j0 = c * ch.tpc, j1 = j0 + ch.tpc < x.tiles1 ? j0 + ch.tpc : x.tiles1;
+    const int64_t pos_hi = pos_lo + count;
+    if ((int64_t)j0 * kTile >= pos_hi) return;   // every step of the chunk past the range
+    const uint32_t Ba0 = alive_at(x.P, x.T, j0 * (uint32_t)kTile);
+    const uint32_t *aa = ch.AA + ((size_t)rl * ch.nch + c) * x.P;
+    for (uint32_t r = threadIdx.x; r < Ba0; r += kChainNT) A[r] = aa[r];
+    const RankDesc rd = ranks[rank_lo + (int32_t)rl];
+    const uint32_t *ans = ANS + (size_t)rl * x.ns;
+    const uint32_t *q2 = Q2 + (size_t)rl * x.T2;
+    int64_t *o = out + (int64_t)rl * count - pos_lo;
+    __syncthreads();
+    for (uint32_t j = j0; j < j1; j++) {
+        const uint32_t t0 = j * (uint32_t)kTile, n = x.ns - t0 < (uint32_t)kTile ? x.ns - t0 : (uint32_t)kTile;
+        if ((int64_t)t0 >= pos_hi) break;
+        const uint32_t Ba = alive_at(x.P, x.T, t0), Bm = alive_at(x.P, x.T, t0 + n);
+        if ((int64_t)(t0 + n) > pos_lo) {
+            for (uint32_t u = threadIdx.x; u < n; u += kChainNT) {
+                const int64_t t = (int64_t)t0 + u;
+                if (t < pos_lo || t >= pos_hi) continue;
+                const uint32_t q = ans[t];
+                const uint32_t a = q < Ba ? A[q] : x.P + t0 + (q - Ba);
+                int64_t id;
+                if (a < x.P) {
+                    id = rd.old_start + a;              // initial pool1 (V2:135-136)
+                } else {                                // moved over from pool2 at step a - P
+                    const uint32_t uu = a - x.P, s = uu / x.B;
+                    const int64_t wbase = s == 0 ? rd.old_start + x.B : rd.new_start + (int64_t)(s + 1) * x.B;
+                    id = wbase + q2[uu];
+                }
+                o[t] = wrap_id(id, g.N);
+            }
+        }
+        if (j + 1 < j1) {
+            const uint32_t *sv = ch.SV + ((size_t)rl * x.tiles1 + j) * x.P;
+            for (uint32_t r = threadIdx.x; r < Bm; r += kChainNT) {
+                const uint32_t q = sv[r];
+                An[r] = q < Ba ? A[q] : x.P + t0 + (q - Ba);
+            }
+            __syncthreads();
+            uint32_t *t = A; A = An; An = t;
+        }
+    }
+}
+
 // ---- ids of the decoded positions ------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_v2x_out(Geometry g, V2xGeo x, uint32_t nr, const RankDesc *__restrict__ ranks,
                                                  int32_t rank_lo, const uint32_t *__restrict__ V,
@@ -407,10 +563,36 @@ static void v2x_launch_blocks(uint64_t blocks, F &&launch) {
         launch(b0, (uint32_t)(blocks - b0 < kMaxBlocks ? blocks - b0 : kMaxBlocks));
 }
 
+// chain mode: pools of at most kTile entries (one decode tile's frame holds the whole pool);
+// PSS_V2X_CHAIN=0 keeps the global merge levels there too (A/B)
+static bool v2x_chain(const V2xGeo &x) {
+    static const bool on = [] {
+        const char *e = getenv("PSS_V2X_CHAIN");
+        return !(e && e[0] == '0');
+    }();
+    return on && x.P <= (uint32_t)kTile;
+}
+
+// chunks of tiles per rank: about two 1024-thread workgroups per CU over the pass's ranks
+static V2xChain v2x_chain_plan(const V2xGeo &x, int32_t nr) {
+    V2xChain ch{};
+    uint32_t want = (uint32_t)((512 + nr - 1) / (nr > 0 ? nr : 1));
+    if (want < 1) want = 1;
+    if (want > x.tiles1) want = x.tiles1;
+    ch.tpc = (x.tiles1 + want - 1) / want;
+    ch.nch = (x.tiles1 + ch.tpc - 1) / ch.tpc;
+    return ch;
+}
+
 size_t v2_exact_ws_bytes(const Geometry &g, int32_t nr_all) {
     if (!v2_exact_supported(g) || nr_all <= 0) return 0;
     const int32_t nr = v2x_ranks_per_pass(g, nr_all);
     const V2xGeo x = v2x_geo(g);
+    if (v2x_chain(x)) {   // K1, ANS (ns each), K2, Q2 (T2 each), survivors, chunk maps, chunk starts
+        const V2xChain ch = v2x_chain_plan(x, nr);
+        return (size_t)nr * ((size_t)2 * x.ns + (size_t)2 * x.T2 + (size_t)x.tiles1 * x.P +
+                             (size_t)2 * ch.nch * x.P) * sizeof(uint32_t);
+    }
     // K1, V, O, Vd, Od (ns each) + K2, Q2 (T2 each), per local rank; tile splits; survivor
     // tables of the first global level (the most pairs) when the pool has <= kTile entries.
     // Windows beyond kTile are decoded in V, O, Vd, Od (S * B <= ns per rank).
@@ -444,16 +626,44 @@ static void v2x_global_levels(const V2xGeo &x, uint32_t nr, uint32_t *&V, uint32
 
 // one pass over nr ranks (nr * ns < 2^30)
 static hipError_t v2x_pass(const Geometry &g, const V2xGeo &x, const RankDesc *ranks, int32_t rank_lo,
-                           int32_t nr, int64_t pos_lo, int64_t count, int64_t epoch, int64_t *out,
-                           uint32_t *ws, hipStream_t s) {
+                           int32_t nr, int32_t nr_plan, int64_t pos_lo, int64_t count, int64_t epoch,
+                           int64_t *out, uint32_t *ws, hipStream_t s) {
     const size_t nsr = (size_t)nr * x.ns, tr = (size_t)nr * x.T2;
-    uint32_t *K1 = ws, *V = K1 + nsr, *O = V + nsr, *Vd = O + nsr, *Od = Vd + nsr;
-    uint32_t *K2 = Od + nsr, *Q2 = K2 + tr;
-    const uint32_t jobs = x.S + x.P;
-    v2x_launch_blocks((uint64_t)jobs * (uint64_t)nr, [&](uint64_t b0, uint32_t nb) {
-        hipLaunchKernelGGL(k_v2x_draws, dim3(nb), dim3(64), 0, s, x, epoch, jobs, b0, K1, K2);
+    // merge-levels layout: K1 | V | O | Vd | Od | K2 | Q2 | splits | tables
+    // chain layout:        K1 | V (answers) | K2 | Q2 | survivors | chunk maps | chunk starts
+    const bool chain = v2x_chain(x);
+    uint32_t *K1 = ws, *V = K1 + nsr;
+    uint32_t *O = chain ? nullptr : V + nsr, *Vd = chain ? nullptr : O + nsr, *Od = chain ? nullptr : Vd + nsr;
+    uint32_t *K2 = chain ? V + nsr : Od + nsr, *Q2 = K2 + tr;
+    if (x.S) {
+        v2x_launch_blocks((uint64_t)x.S * (uint64_t)nr, [&](uint64_t b0, uint32_t nb) {
+            hipLaunchKernelGGL(k_v2x_draws, dim3(nb), dim3(64), 0, s, x, epoch, x.S, b0, K1, K2);
+        });
+    }
+    const uint32_t tail_blocks = (x.P + 63u) / 64u;
+    v2x_launch_blocks((uint64_t)tail_blocks * (uint64_t)nr, [&](uint64_t b0, uint32_t nb) {
+        hipLaunchKernelGGL(k_v2x_tail_draws, dim3(nb), dim3(64), 0, s, x, epoch, tail_blocks, b0, K1);
     });
     const uint32_t nru = (uint32_t)nr;
+    constexpr size_t kTileLds0 = 4 * kTile * sizeof(uint32_t);
+    if (chain) {
+        uint32_t *ANS = V;
+        V2xChain ch = v2x_chain_plan(x, nr_plan);   // the workspace's plan (a last pass may be short)
+        ch.SV = Q2 + tr;
+        ch.CC = ch.SV + (size_t)nr * x.tiles1 * x.P;
+        ch.AA = ch.CC + (size_t)nr * ch.nch * x.P;
+        const uint32_t per_rank = x.tiles1 + x.S;
+        v2x_launch_blocks((uint64_t)per_rank * nru, [&](uint64_t b0, uint32_t nb) {
+            hipLaunchKernelGGL(k_v2x_tile, dim3(nb), dim3(kTileNT), kTileLds0, s, x, per_rank, b0, K1, K2, ANS,
+                               (uint32_t *)nullptr, Q2, ch.SV);
+        });
+        const size_t lds = 2 * (size_t)x.P * sizeof(uint32_t);
+        hipLaunchKernelGGL(k_v2x_compose, dim3(nru * ch.nch), dim3(kChainNT), lds, s, x, ch);
+        hipLaunchKernelGGL(k_v2x_link, dim3(nru), dim3(kChainNT), lds, s, x, ch);
+        hipLaunchKernelGGL(k_v2x_emit, dim3(nru * ch.nch), dim3(kChainNT), lds, s, g, x, ch, ranks, rank_lo, ANS,
+                           (const uint32_t *)Q2, pos_lo, count, out);
+        return hipGetLastError();
+    }
     uint32_t *SP = Q2 + tr;                    // merge-path splits: 2 words per tile
     uint32_t *C = SP + v2x_split_words(x, nr); // survivor tables: pairs x P words per rank
     const bool big_windows = x.B > (uint32_t)kTile && x.S > 0;
@@ -463,7 +673,7 @@ static hipError_t v2x_pass(const Geometry &g, const V2xGeo &x, const RankDesc *r
         const uint32_t nseq = nru * x.S;
         v2x_launch_blocks((uint64_t)xw.tiles1 * nseq, [&](uint64_t b0, uint32_t nb) {
             hipLaunchKernelGGL(k_v2x_tile, dim3(nb), dim3(kTileNT), kTileLds, s, xw, xw.tiles1, b0, K2, K2,
-                               V, O, Q2);
+                               V, O, Q2, (uint32_t *)nullptr);
         });
         uint32_t *wv = V, *wo = O, *wvd = Vd, *wod = Od;
         v2x_global_levels(xw, nseq, wv, wo, wvd, wod, SP, C, s);
@@ -474,7 +684,8 @@ static hipError_t v2x_pass(const Geometry &g, const V2xGeo &x, const RankDesc *r
     // pool1 tiles (and, for B <= kTile, the windows in the same launch)
     const uint32_t per_rank = x.tiles1 + (big_windows ? 0u : x.S);
     v2x_launch_blocks((uint64_t)per_rank * nru, [&](uint64_t b0, uint32_t nb) {
-        hipLaunchKernelGGL(k_v2x_tile, dim3(nb), dim3(kTileNT), kTileLds, s, x, per_rank, b0, K1, K2, V, O, Q2);
+        hipLaunchKernelGGL(k_v2x_tile, dim3(nb), dim3(kTileNT), kTileLds, s, x, per_rank, b0, K1, K2, V, O, Q2,
+                           (uint32_t *)nullptr);
     });
     v2x_global_levels(x, nru, V, O, Vd, Od, SP, C, s);
     const dim3 grid1((uint32_t)v2x_cdiv((int64_t)nsr, 256));   // one thread per (rank, step)
@@ -497,7 +708,7 @@ hipError_t launch_v2_exact(const Geometry &g, const RankDesc *ranks, int32_t ran
     const int32_t per = v2x_ranks_per_pass(g, nr);
     for (int32_t r0 = 0; r0 < nr; r0 += per) {
         const int32_t n = nr - r0 < per ? nr - r0 : per;
-        const hipError_t e = v2x_pass(g, x, ranks, rank_lo + r0, n, pos_lo, count, epoch,
+        const hipError_t e = v2x_pass(g, x, ranks, rank_lo + r0, n, per, pos_lo, count, epoch,
                                       out + (int64_t)r0 * count, ws, s);
         if (e != hipSuccess) return e;
     }
