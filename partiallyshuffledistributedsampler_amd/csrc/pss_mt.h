@@ -174,6 +174,81 @@ __device__ void mt_draws(uint32_t *mt, uint32_t nd, Bound bound, Emit emit) {
     }
 }
 
+// Draws of one V2 pool2 window's stream (V2:101-106): k1 = _randbelow(P) and k2 =
+// _randbelow(W - j) alternating, k1 first, until W k2 draws are made; emit(false, i, r) for the
+// i-th k1, emit(true, j, r) for the j-th k2.  mt_draws's fixed point re-derives every lane's
+// draw index after each pass, and with two alternating bounds one rejection flips the role of
+// every later lane, so a block settles only after about as many passes as it has rejections.
+// Here the roles come from a 2-state automaton instead: lane l maps the role it is offered
+// (0 = k1, 1 = k2) to the role the next lane is offered (f(0) = accepted as k1 ? 1 : 0, f(1) =
+// accepted as k2 ? 0 : 1), and an inclusive DPP scan of the composed maps gives every lane its
+// role in one pass.  Only the k2 bound depends on the lane's k2 index j, and only through values
+// within a few counts of a threshold: the block guesses j, derives the roles and the true j, and
+// repeats until no guess changes (almost always after two passes).
+__device__ __forceinline__ uint32_t role_compose(uint32_t g, uint32_t f) {   // g after f
+    return ((g >> (f & 1u)) & 1u) | (((g >> ((f >> 1) & 1u)) & 1u) << 1);
+}
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ uint32_t dpp_role(uint32_t x) {
+    // lanes without a source (or in masked rows) read the identity map (0b10)
+    return (uint32_t)__builtin_amdgcn_update_dpp(2, (int)x, CTRL, ROWMASK, 0xF, false);
+}
+__device__ __forceinline__ uint32_t wave_role_scan(uint32_t x) {
+    x = role_compose(x, dpp_role<0x111, 0xF>(x));
+    x = role_compose(x, dpp_role<0x112, 0xF>(x));
+    x = role_compose(x, dpp_role<0x114, 0xF>(x));
+    x = role_compose(x, dpp_role<0x118, 0xF>(x));
+    x = role_compose(x, dpp_role<0x142, 0xA>(x));
+    x = role_compose(x, dpp_role<0x143, 0xC>(x));
+    return x;
+}
+
+template <class Emit>
+__device__ void mt_draws_pair(uint32_t *mt, uint32_t W, uint32_t P, Emit emit) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t kb1 = 32u - (uint32_t)__builtin_clz(P);
+    const uint64_t below = lanemask_lt();
+    uint32_t i1 = 0, i2 = 0, st = 0;   // k1 / k2 draws made, role offered to the next word
+    while (i2 < W) {
+        mt_twist(mt);
+        for (int q0 = 0; q0 < kMtN && i2 < W; q0 += 64) {
+            const int nval = kMtN - q0 < 64 ? kMtN - q0 : 64;
+            const bool valid = lane < nval;
+            const uint32_t word = valid ? mt_temper(mt[q0 + lane]) : 0u;
+            const uint32_t r1 = word >> (32u - kb1);
+            const bool a1 = valid && r1 < P;
+            uint32_t jg = i2 + (uint32_t)lane / 3u, j = 0, r2 = 0, role = 0, Fx = 0;
+            bool a2 = false;
+            for (;;) {
+                const uint32_t n2 = jg < W ? W - jg : 1u;
+                r2 = word >> (32u - (32u - (uint32_t)__builtin_clz(n2)));
+                a2 = valid && r2 < n2;
+                const uint32_t f = (a1 ? 1u : 0u) | ((a2 ? 0u : 1u) << 1);
+                Fx = wave_role_scan(f);
+                const uint32_t Fp = (uint32_t)__shfl((int)Fx, lane > 0 ? lane - 1 : 0);
+                role = lane ? (Fp >> st) & 1u : st;
+                const uint64_t m2 = __ballot(valid && role == 1u && a2);
+                j = i2 + (uint32_t)__popcll(m2 & below);
+                if (__ballot(valid && j != jg) == 0) break;
+                jg = j;
+            }
+            const bool acc = valid && (role ? a2 : a1);
+            const uint64_t m1 = __ballot(acc && role == 0u), m2 = __ballot(acc && role == 1u);
+            if (acc) {
+                if (role == 0u) {
+                    const uint32_t i = i1 + (uint32_t)__popcll(m1 & below);
+                    if (i < W) emit(false, i, r1);
+                } else if (j < W) {
+                    emit(true, j, r2);
+                }
+            }
+            i1 += (uint32_t)__popcll(m1);
+            i2 += (uint32_t)__popcll(m2);
+            st = ((uint32_t)__shfl((int)Fx, 63) >> st) & 1u;
+        }
+    }
+}
+
 // The first _randbelow(n) draw of a freshly seeded stream, ONE SEED PER LANE (V2's tail steps
 // reseed before every draw, V2:107-112, and use only its first word or few).  Seeding is
 // init_by_array over the 1-2 key words (klen), two serial chains of 624 + 623 steps; draw word

@@ -14,18 +14,23 @@
 //   decode  "remove the k-th, append at the end" is a rank-deletion problem: with the
 //           elements numbered in insertion order, step t removes the k_t-th alive one.  A block
 //           of steps [a, b) is solved in the frame of its start (alive elements 0..B_a-1, its
-//           own insertions after them); two sibling blocks combine by mapping the right
-//           block's answers through the left block's deletions -- the q-th survivor of the
-//           left block is q + #{i : D_i - i <= q} for its sorted deletions D -- and merging
-//           the sorted deletion lists.  Bottom-up, this is a merge sort of (position, step)
-//           pairs: 12 levels in LDS per 4096-step tile, then global levels.  pool2 windows
-//           (no insertions) finish inside one tile when B <= 4096; larger windows are decoded
-//           first, as sequences of their own (B alive, no insertions) through the same tile
-//           and global levels.  A short last window is padded to B steps of k = 0: its
-//           W' real deletions never reach the B - W' padding elements at the end of the
-//           order, so its real answers are unchanged.  Above 4096 alive entries the global
-//           levels map right blocks by a binary search over the left block's deletions instead
-//           of survivor tables (pairs x P words would not fit).
+//           own insertions after them).  Two sibling blocks combine in ONE merge: the right
+//           block's answer q (its own frame) is the q-th survivor of the left block, q +
+//           #{i : D_i - i <= q} for the left block's sorted deletions D, and it sorts right after
+//           exactly those left entries -- so merging E_i = D_i - i with the right answers (left
+//           first on ties) orders the pair and maps the right block at once (a right answer
+//           taken after i left entries becomes q + i).  Bottom-up this is a merge sort of
+//           (position, step) pairs: 12 levels in LDS per 4096-step tile.  Pools of <= 4096
+//           entries then chain the tiles (below); bigger pools merge on through global levels.
+//           pool2 windows (no insertions) finish inside one tile when B <= 4096; larger windows
+//           are decoded first, as sequences of their own (B alive, no insertions) through the
+//           same tile and global levels.  A short last window is padded to B steps of k = 0: its
+//           W' real deletions never reach the B - W' padding elements at the end of the order,
+//           so its real answers are unchanged.
+//   chain   (pools <= 4096) each tile also leaves its survivor list -- the frame positions still
+//           alive at its end, in order; the elements alive at a tile's start follow from the
+//           previous tile's by that list, so per chunk of tiles the composite map is built in
+//           parallel, chunks are linked per rank, and every tile's answers become ids.
 //   output  position p < P is old_start + p (initial pool1, V2:135-136); position P + u is
 //           the element step u moved over from pool2: window base + its decoded pool2 rank.
 //
@@ -51,10 +56,6 @@ struct V2xGeo {                   // one rank's stream, host-computed
 __device__ __forceinline__ uint32_t alive_at(uint32_t B0, uint32_t insu, uint32_t x) {
     return B0 - (x > insu ? x - insu : 0u);
 }
-__device__ __forceinline__ uint32_t ins_in(uint32_t insu, uint32_t a, uint32_t b) {
-    const uint32_t e = b < insu ? b : insu;
-    return e > a ? e - a : 0u;
-}
 // #{i < n : D[i] - i <= q} for sorted distinct D (D[i] - i is non-decreasing)
 __device__ __forceinline__ uint32_t count_e_le(const uint32_t *D, uint32_t n, uint32_t q) {
     uint32_t lo = 0, hi = n;
@@ -63,11 +64,6 @@ __device__ __forceinline__ uint32_t count_e_le(const uint32_t *D, uint32_t n, ui
         if (D[mid] - mid <= q) lo = mid + 1; else hi = mid;
     }
     return lo;
-}
-// position q of the frame at m (sibling-right block) in the frame at a (left block start)
-__device__ __forceinline__ uint32_t map_right(const uint32_t *DL, uint32_t nL, uint32_t q, uint32_t Ba,
-                                              uint32_t Bm, uint32_t insL) {
-    return q < Bm ? q + count_e_le(DL, nL, q) : q - Bm + Ba + insL;
 }
 }  // namespace
 
@@ -83,12 +79,10 @@ __global__ __launch_bounds__(64) void k_v2x_draws(V2xGeo x, int64_t epoch, uint3
         const uint32_t s = job;
         const uint32_t W = x.T - s * x.B < x.B ? x.T - s * x.B : x.B, t0 = s * x.B;
         mt_seed_int(mt, s == 0 ? epoch + 2 : epoch + (int64_t)(s - 1) * 10000);
-        const uint32_t P = x.P;
-        mt_draws(mt, 2u * W, [&](uint32_t d) { return (d & 1u) ? W - (d >> 1) : P; },
-                 [&](uint32_t d, uint32_t r) {
-                     if (d & 1u) k2[t0 + (d >> 1)] = r;
-                     else k1[t0 + (d >> 1)] = r;
-                 });
+        mt_draws_pair(mt, W, x.P, [&](bool second, uint32_t i, uint32_t r) {
+            if (second) k2[t0 + i] = r;
+            else k1[t0 + i] = r;
+        });
         for (uint32_t u = W + threadIdx.x; u < x.B; u += 64) k2[t0 + u] = 0;   // padding steps
     }
 }
@@ -157,45 +151,40 @@ __global__ __launch_bounds__(kTileNT) void k_v2x_tile(V2xGeo x, uint32_t per_ran
     }
     for (uint32_t u = threadIdx.x; u < n; u += kTileNT) { va[u] = src[u]; oa[u] = u; }
     __syncthreads();
+    // merge levels: sibling blocks [a, m), [m, e) -> [a, e), each sorted by its frame position.
+    // Left entries (deletions D, frame a) keep their values; a right entry q (frame m) is the
+    // q-th survivor of the left block, i.e. q + #{i : D_i - i <= q} in frame a, and it falls
+    // after exactly those left entries -- so one merge of E_i = D_i - i (non-decreasing) with the
+    // right values (left first on ties) both orders the pair and maps the right block: a right
+    // entry taken after i left ones becomes q + i.  (q beyond the left block's survivors are the
+    // right block's own insertions: every E_i <= q there, and q + nL is their frame-a position.)
     for (uint32_t w = 1; w < n; w <<= 1) {
-        for (uint32_t u = threadIdx.x; u < n; u += kTileNT) {     // right blocks -> left frame
-            const uint32_t blk = u / w;
-            if (blk & 1u) {
-                const uint32_t a = (blk - 1) * w, m = blk * w;
-                va[u] = map_right(va + a, m - a, va[u], alive_at(B0, insu, t0 + a),
-                                  alive_at(B0, insu, t0 + m), ins_in(insu, t0 + a, t0 + m));
+        const uint32_t p0 = threadIdx.x * 4u;   // four consecutive outputs per thread
+        if (w == 1) {                           // two pairs per thread
+            for (uint32_t a = p0; a < p0 + 4u && a < n; a += 2u) {
+                if (a + 1u >= n) { vb[a] = va[a]; ob[a] = oa[a]; continue; }
+                const uint32_t L0 = va[a], R0 = va[a + 1], oL = oa[a], oR = oa[a + 1];
+                if (L0 <= R0) { vb[a] = L0; ob[a] = oL; vb[a + 1] = R0 + 1u; ob[a + 1] = oR; }
+                else { vb[a] = R0; ob[a] = oR; vb[a + 1] = L0; ob[a + 1] = oL; }
             }
-        }
-        __syncthreads();
-        if (w == 1) {                                            // merge sibling lists
-            for (uint32_t u = threadIdx.x; u < n; u += kTileNT) {
-                const uint32_t a = u & ~1u, m = a + 1;
-                if (m >= n) { vb[u] = va[u]; ob[u] = oa[u]; continue; }
-                const uint32_t pos = u < m ? (va[u] > va[m] ? 1u : 0u) : (va[u] > va[a] ? 1u : 0u);
-                vb[a + pos] = va[u];
-                ob[a + pos] = oa[u];
-            }
-        } else {   // kTileNT * 4 == kTile: four consecutive outputs per thread, one merge-path search
-            const uint32_t p0 = threadIdx.x * 4u;
-            if (p0 < n) {
-                const uint32_t a = (p0 / (2 * w)) * (2 * w), m = a + w;
-                const uint32_t pe = p0 + 4u < n ? p0 + 4u : n;
-                if (m >= n) {
-                    for (uint32_t p = p0; p < pe; p++) { vb[p] = va[p]; ob[p] = oa[p]; }
-                } else {
-                    const uint32_t e = m + w < n ? m + w : n, nL = w, nR = e - m, d = p0 - a;
-                    const uint32_t *L = va + a, *R = va + m;
-                    uint32_t lo = d > nR ? d - nR : 0u, hi = d < nL ? d : nL;
-                    while (lo < hi) {
-                        const uint32_t mid = (lo + hi) >> 1;
-                        if (L[mid] < R[d - mid - 1]) lo = mid + 1; else hi = mid;
-                    }
-                    uint32_t i = lo, j = d - lo;
-                    for (uint32_t p = p0; p < pe; p++) {
-                        const bool takeL = j >= nR || (i < nL && L[i] < R[j]);
-                        if (takeL) { vb[p] = L[i]; ob[p] = oa[a + i]; i++; }
-                        else { vb[p] = R[j]; ob[p] = oa[m + j]; j++; }
-                    }
+        } else if (p0 < n) {
+            const uint32_t a = (p0 / (2 * w)) * (2 * w), m = a + w;
+            const uint32_t pe = p0 + 4u < n ? p0 + 4u : n;
+            if (m >= n) {
+                for (uint32_t p = p0; p < pe; p++) { vb[p] = va[p]; ob[p] = oa[p]; }
+            } else {
+                const uint32_t e = m + w < n ? m + w : n, nL = w, nR = e - m, d = p0 - a;
+                const uint32_t *L = va + a, *R = va + m;
+                uint32_t lo = d > nR ? d - nR : 0u, hi = d < nL ? d : nL;
+                while (lo < hi) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if (L[mid] - mid <= R[d - mid - 1]) lo = mid + 1; else hi = mid;
+                }
+                uint32_t i = lo, j = d - lo;
+                for (uint32_t p = p0; p < pe; p++) {
+                    const bool takeL = j >= nR || (i < nL && L[i] - i <= R[j]);
+                    if (takeL) { vb[p] = L[i]; ob[p] = oa[a + i]; i++; }
+                    else { vb[p] = R[j] + i; ob[p] = oa[m + j]; j++; }
                 }
             }
         }
@@ -247,72 +236,14 @@ __global__ __launch_bounds__(256) void k_v2x_gsplit(V2xGeo x, uint32_t nr, uint3
             const uint32_t *L = v + a, *R = v + m;
             const uint32_t d = u0 - a + (endp ? un : 0u);
             uint32_t lo = d > nR ? d - nR : 0u, hi = d < nL ? d : nL;
-            while (lo < hi) {
+            while (lo < hi) {   // the fused map-and-merge order of k_v2x_tile
                 const uint32_t mid = (lo + hi) >> 1;
-                if (L[mid] < R[d - mid - 1]) lo = mid + 1; else hi = mid;
+                if (L[mid] - mid <= R[d - mid - 1]) lo = mid + 1; else hi = mid;
             }
             r = lo;
         }
     }
     SP[gi] = r;
-}
-
-// right blocks -> the left block's frame (in place)
-// Survivor tables: for the left block [a, m) of every pair, C[q] = #{i : D_i - i <= q} for
-// q < B_m (the alive count at m, <= P) -- the number of the left block's deletions at or
-// before its q-th survivor.  D_i - i is non-decreasing, so entry i owns C[q] for
-// q in [D_i - i, D_{i+1} - (i+1)): one thread per left-block entry, B_m writes per pair.
-__global__ __launch_bounds__(256) void k_v2x_ctab(V2xGeo x, uint32_t nr, uint32_t w,
-                                                  const uint32_t *__restrict__ V, uint32_t *__restrict__ C) {
-    const uint64_t gi = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    const uint32_t rl = (uint32_t)(gi / x.ns), u = (uint32_t)(gi % x.ns);
-    if (rl >= nr) return;
-    const uint32_t pair = u / (2 * w), a = pair * 2 * w, m = a + w;
-    if (u >= m || m >= x.ns) return;          // left-block entries of pairs with a right block
-    const uint32_t i = u - a, nL = w;
-    const uint32_t Bm = alive_at(x.P, x.T, m);
-    const uint32_t *DL = V + (size_t)rl * x.ns + a;
-    const uint32_t pairs = (x.ns + 2 * w - 1) / (2 * w);
-    uint32_t *c = C + ((size_t)rl * pairs + pair) * x.P;
-    const uint32_t e = DL[i] - i;
-    const uint32_t en = i + 1 < nL ? DL[i + 1] - (i + 1) : Bm;
-    const uint32_t hi = en < Bm ? en : Bm;
-    for (uint32_t q = e; q < hi; q++) c[q] = i + 1;
-    if (i == 0) {
-        const uint32_t z = e < Bm ? e : Bm;
-        for (uint32_t q = 0; q < z; q++) c[q] = 0;
-    }
-}
-
-// right blocks -> the left block's frame (in place): q < B_m is the q-th survivor of the
-// left block, q + C[q]; larger q are the right block's own insertions
-__global__ __launch_bounds__(256) void k_v2x_gmap(V2xGeo x, uint32_t nr, uint32_t w, uint32_t *__restrict__ V,
-                                                  const uint32_t *__restrict__ C) {
-    const uint64_t gi = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    const uint32_t rl = (uint32_t)(gi / x.ns), u = (uint32_t)(gi % x.ns);
-    if (rl >= nr) return;
-    const uint32_t blk = u / w;
-    if (!(blk & 1u)) return;
-    const uint32_t a = (blk - 1) * w, m = blk * w, pair = blk >> 1;
-    const uint32_t Ba = alive_at(x.P, x.T, a), Bm = alive_at(x.P, x.T, m), insL = ins_in(x.T, a, m);
-    const uint32_t pairs = (x.ns + 2 * w - 1) / (2 * w);
-    uint32_t *v = V + (size_t)rl * x.ns;
-    const uint32_t q = v[u];
-    v[u] = q < Bm ? q + C[((size_t)rl * pairs + pair) * x.P + q] : q - Bm + Ba + insL;
-}
-
-// the same without tables: q + #{left deletions at or before its q-th survivor} by a binary
-// search over the left block's sorted deletions (only right-block entries are rewritten, so the
-// left block is stable while it is read)
-__global__ __launch_bounds__(256) void k_v2x_gmap_bs(V2xGeo x, uint32_t nr, uint32_t w, uint32_t *__restrict__ V) {
-    const uint64_t gi = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    const uint32_t rl = (uint32_t)(gi / x.ns), u = (uint32_t)(gi % x.ns);
-    if (rl >= nr) return;
-    const uint32_t blk = u / w;
-    if (!(blk & 1u)) return;
-    const uint32_t a = (blk - 1) * w, m = blk * w;
-    uint32_t *v = V + (size_t)rl * x.ns;
-    v[u] = map_right(v + a, w, v[u], alive_at(x.P, x.T, a), alive_at(x.P, x.T, m), ins_in(x.T, a, m));
 }
 
 // decoded pool2 windows (as sequences of B steps) -> Q2[window step] = its pool2 rank
@@ -351,18 +282,20 @@ __global__ __launch_bounds__(kGNT) void k_v2x_gmerge(V2xGeo x, uint32_t w, const
     __syncthreads();
     const uint32_t p0 = threadIdx.x * kPer;
     if (p0 < on) {
+        // the fused map-and-merge of k_v2x_tile: E_i = D_i - i against the right values (frame
+        // m), a right entry after i0 + i left ones becomes q + i0 + i (frame a)
         const uint32_t *lv = sv, *rv = sv + sL;
         uint32_t lo = p0 > sR ? p0 - sR : 0u, hi = p0 < sL ? p0 : sL;
         while (lo < hi) {
             const uint32_t mid = (lo + hi) >> 1;
-            if (lv[mid] < rv[p0 - mid - 1]) lo = mid + 1; else hi = mid;
+            if (lv[mid] - (i0 + mid) <= rv[p0 - mid - 1]) lo = mid + 1; else hi = mid;
         }
         uint32_t i = lo, j = p0 - lo;
         const uint32_t pe = p0 + kPer < on ? p0 + kPer : on;
         for (uint32_t p = p0; p < pe; p++) {
-            const bool takeL = j >= sR || (i < sL && lv[i] < rv[j]);
+            const bool takeL = j >= sR || (i < sL && lv[i] - (i0 + i) <= rv[j]);
             if (takeL) { tv[p] = lv[i]; to[p] = so[i]; i++; }
-            else { tv[p] = rv[j]; to[p] = so[sL + j]; j++; }
+            else { tv[p] = rv[j] + i0 + i; to[p] = so[sL + j]; j++; }
         }
     }
     __syncthreads();
@@ -532,7 +465,6 @@ static V2xGeo v2x_window_geo(const V2xGeo &x) {
     return w;
 }
 
-static bool v2x_tables(const V2xGeo &x) { return x.P <= (uint32_t)kTile; }
 
 static size_t v2x_split_words(const V2xGeo &x, int32_t nr) {
     size_t t = (size_t)nr * (size_t)v2x_cdiv(x.ns, kGTile);
@@ -593,30 +525,18 @@ size_t v2_exact_ws_bytes(const Geometry &g, int32_t nr_all) {
         return (size_t)nr * ((size_t)2 * x.ns + (size_t)2 * x.T2 + (size_t)x.tiles1 * x.P +
                              (size_t)2 * ch.nch * x.P) * sizeof(uint32_t);
     }
-    // K1, V, O, Vd, Od (ns each) + K2, Q2 (T2 each), per local rank; tile splits; survivor
-    // tables of the first global level (the most pairs) when the pool has <= kTile entries.
-    // Windows beyond kTile are decoded in V, O, Vd, Od (S * B <= ns per rank).
-    const size_t pairs = (size_t)v2x_cdiv(x.ns, 2 * kTile);
-    const size_t ctab = v2x_tables(x) ? (size_t)nr * pairs * x.P : 0;
-    return ((size_t)nr * ((size_t)5 * x.ns + (size_t)2 * x.T2) + v2x_split_words(x, nr) + ctab) *
-           sizeof(uint32_t);
+    // K1, V, O, Vd, Od (ns each) + K2, Q2 (T2 each), per local rank; tile splits.  Windows
+    // beyond kTile are decoded in V, O, Vd, Od (S * B <= ns per rank).
+    return ((size_t)nr * ((size_t)5 * x.ns + (size_t)2 * x.T2) + v2x_split_words(x, nr)) * sizeof(uint32_t);
 }
 
 // global merge levels w = kTile, 2 kTile, ... of nr sequences of x.ns steps (V, O sorted per
 // block of w on entry); returns the buffers holding the result
 static void v2x_global_levels(const V2xGeo &x, uint32_t nr, uint32_t *&V, uint32_t *&O, uint32_t *&Vd,
-                              uint32_t *&Od, uint32_t *SP, uint32_t *C, hipStream_t s) {
-    const uint64_t nsr = (uint64_t)nr * x.ns;
-    const dim3 grid1((uint32_t)v2x_cdiv((int64_t)nsr, 256));
+                              uint32_t *&Od, uint32_t *SP, hipStream_t s) {
     const int64_t tiles = (int64_t)nr * v2x_cdiv(x.ns, kGTile);
     const dim3 gridt((uint32_t)tiles), grids((uint32_t)v2x_cdiv(2 * tiles, 256));
-    for (uint32_t w = kTile; w < x.ns; w <<= 1) {
-        if (v2x_tables(x)) {
-            hipLaunchKernelGGL(k_v2x_ctab, grid1, dim3(256), 0, s, x, nr, w, V, C);
-            hipLaunchKernelGGL(k_v2x_gmap, grid1, dim3(256), 0, s, x, nr, w, V, C);
-        } else {
-            hipLaunchKernelGGL(k_v2x_gmap_bs, grid1, dim3(256), 0, s, x, nr, w, V);
-        }
+    for (uint32_t w = kTile; w < x.ns; w <<= 1) {   // each level: fused map-and-merge
         hipLaunchKernelGGL(k_v2x_gsplit, grids, dim3(256), 0, s, x, nr, w, V, SP);
         hipLaunchKernelGGL(k_v2x_gmerge, gridt, dim3(kGNT), 0, s, x, w, V, O, Vd, Od, SP);
         uint32_t *t = V; V = Vd; Vd = t;
@@ -665,7 +585,6 @@ static hipError_t v2x_pass(const Geometry &g, const V2xGeo &x, const RankDesc *r
         return hipGetLastError();
     }
     uint32_t *SP = Q2 + tr;                    // merge-path splits: 2 words per tile
-    uint32_t *C = SP + v2x_split_words(x, nr); // survivor tables: pairs x P words per rank
     const bool big_windows = x.B > (uint32_t)kTile && x.S > 0;
     constexpr size_t kTileLds = 4 * kTile * sizeof(uint32_t);
     if (big_windows) {          // pool2 windows first, as nr * S sequences of B steps
@@ -676,7 +595,7 @@ static hipError_t v2x_pass(const Geometry &g, const V2xGeo &x, const RankDesc *r
                                V, O, Q2, (uint32_t *)nullptr);
         });
         uint32_t *wv = V, *wo = O, *wvd = Vd, *wod = Od;
-        v2x_global_levels(xw, nseq, wv, wo, wvd, wod, SP, C, s);
+        v2x_global_levels(xw, nseq, wv, wo, wvd, wod, SP, s);
         const uint64_t nw = (uint64_t)nseq * x.B;
         hipLaunchKernelGGL(k_v2x_q2, dim3((uint32_t)v2x_cdiv((int64_t)nw, 256)), dim3(256), 0, s, nw, x.B,
                            wv, wo, Q2);
@@ -687,7 +606,7 @@ static hipError_t v2x_pass(const Geometry &g, const V2xGeo &x, const RankDesc *r
         hipLaunchKernelGGL(k_v2x_tile, dim3(nb), dim3(kTileNT), kTileLds, s, x, per_rank, b0, K1, K2, V, O, Q2,
                            (uint32_t *)nullptr);
     });
-    v2x_global_levels(x, nru, V, O, Vd, Od, SP, C, s);
+    v2x_global_levels(x, nru, V, O, Vd, Od, SP, s);
     const dim3 grid1((uint32_t)v2x_cdiv((int64_t)nsr, 256));   // one thread per (rank, step)
     hipLaunchKernelGGL(k_v2x_out, grid1, dim3(256), 0, s, g, x, nru, ranks, rank_lo, V, O, Q2,
                        pos_lo, count, out);
