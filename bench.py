@@ -290,12 +290,13 @@ def sampler_data_path(device, reps=3):
 
 
 def handoff_figures(device, reps=5):
-    """The fused hand-off at C2 (all 8 logical ranks, 100M positions): pss_generate_mapped ->
-    (int32 file, int32 offset) per position in HBM -- V1 fused into the generation kernel, V2
-    generation + bucket-indexed map; and the standalone map of 100M int64 ids."""
+    """The fused hand-off (all 8 logical ranks, 100M positions): pss_generate_mapped -> (int32
+    file, int32 offset) per position in HBM, mapped inside the generation kernels -- V1 and V2 at
+    C2, V2 at C5 (the grouped replay); and the standalone map of 100M int64 ids."""
     lengths, N, R, B, _ = W.shape("c2")
     out = {}
-    for ver in (1, 2):
+    for ver, cfg in ((1, "c2"), (2, "c2"), (2, "c5")):
+        lengths, N, R, B, _ = W.shape(cfg)
         eng = IndexEngine(lengths, N, R, B, ver, seed=0, device=device)
         eng.init_iter(0)
         eng.generate_mapped(0, R)
@@ -306,8 +307,9 @@ def handoff_figures(device, reps=5):
             eng.generate_mapped(0, R)
         torch.cuda.synchronize(device)
         ms = (time.perf_counter() - t0) / reps * 1e3
-        out["v%d_mapped" % ver] = {"ms_per_epoch": ms, "G_pos_per_s": R * eng.num_samples / ms / 1e6}
-        if ver == 2:
+        key = "v%d_mapped" % ver if cfg == "c2" else "c5_v2_mapped"
+        out[key] = {"ms_per_epoch": ms, "G_pos_per_s": R * eng.num_samples / ms / 1e6}
+        if ver == 2 and cfg == "c2":
             ids = eng.generate(0, R)
             fp, off = eng.map(ids.view(-1))
             torch.cuda.synchronize(device)
@@ -319,8 +321,45 @@ def handoff_figures(device, reps=5):
             out["map_100M_ids_ms"] = ms
             del ids, fp, off
         eng.close()
-    out["config"] = "C2, 8 logical ranks x 12.5M positions -> (int32 file_pos, int32 offset)"
+    out["config"] = ("C2 (V1, V2) and C5 (V2, B = 2^20: the grouped replay), 8 logical ranks x 12.5M "
+                     "positions -> (int32 file_pos, int32 offset)")
     return out
+
+
+def exact_order_figures(device):
+    """order="exact" (the reference's own CPython-MT19937 draws, bit-identical id streams) at
+    the bench shapes: C2 (V2 and V1, B = 4096) and C5's pool (B = 2^20), all 8 logical ranks,
+    one warm-up epoch then timed epochs; ms per epoch (init_iter + generate, synchronised), G
+    idx/s, and the exact pipeline's span on the stream (HIP events around the launch)."""
+    res = {}
+    for name, cfg, ver, reps in (("c2_v2", "c2", 2, 3), ("c2_v1", "c2", 1, 3), ("c5_v2", "c5", 2, 2),
+                                 ("c5_v1", "c5", 1, 2)):
+        lengths, N, R, B, _ = W.shape(cfg)
+        eng = IndexEngine(lengths, N, R, B, ver, seed=0, device=device, order="exact")
+        ns = eng.num_samples
+        out = torch.empty((R, ns), dtype=torch.int64, device=device)
+        eng.init_iter(0)
+        eng.generate(0, R, out=out)
+        torch.cuda.synchronize(device)
+        eng.profile(True)
+        t0 = time.perf_counter()
+        for e in range(reps):
+            eng.init_iter(1 + e)
+            eng.generate(0, R, out=out)
+        torch.cuda.synchronize(device)
+        ms = (time.perf_counter() - t0) / reps * 1e3
+        prof = eng.profile_read()
+        eng.check()
+        eng.close()
+        kname = "v2_emit" if ver == 2 else "v1_window"
+        k_ms, k_n = prof.get(kname, (0.0, 0))
+        res[name] = {"ms_per_epoch": ms, "G_idx_per_s": R * ns / ms / 1e6,
+                     "pipeline_ms_per_epoch": k_ms / max(1, k_n), "ids_per_epoch": R * ns,
+                     "shuffle_buffer": B}
+        del out
+    res["config"] = ("order='exact' (CPython MT19937 draws: the reference's id streams bit for bit); "
+                     "c2: 10K files x 10K, R=8, B=4096; c5: the same files, B=2^20; all 8 ranks per epoch")
+    return res
 
 
 # ---- main ------------------------------------------------------------------------------------
@@ -332,6 +371,7 @@ def main():
     ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-latency", action="store_true")
+    ap.add_argument("--no-exact", action="store_true", help="skip the exact-order figures")
     ap.add_argument("--no-kernel-timing", action="store_true",
                     help="time the steps without the per-launch HIP events (roofline omitted)")
     ap.add_argument("--timing-every", type=int, default=4,
@@ -437,6 +477,7 @@ def main():
         "vs_baseline": None,
         "dtype": "int64",
         "data": "synthetic",
+        "value_scope": "aggregate over all n_gpus GPUs (the metric's per-GPU figure is per_gpu)",
         "per_gpu": value / world,
         "aggregate": value,
         "config": {"workload": ("%s; %s" % (desc, "per GPU" if scaling == "weak"
@@ -462,6 +503,8 @@ def main():
         line["latency"] = latency_dropin(local)
         line["sampler_data_path"] = sampler_data_path(local)
         line["handoff"] = handoff_figures(local)
+    if rank == 0 and world == 1 and not args.no_exact:
+        line["exact_order"] = exact_order_figures(local)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -88,11 +88,12 @@ int pss_map(pss_sampler *h, const int64_t *ids_dev, int64_t n, int32_t *file_pos
 /* Fused hand-off: the positions of pss_generate delivered directly as
  * (int32 file position in the shuffled order, int32 offset) -- 8 bytes per id, the form the
  * reader and an on-GPU gather consume (V1:181-221).  Same layout as pss_generate
- * ([r - rank_lo][pos - pos_lo]) and the same reflection flag as pss_map.  Counter order, V1
- * and V2 pools up to 16384 (exchange kernel): one kernel, each id mapped where it is emitted
- * (V2 through a per-tile LDS map of the files its ids can come from); V2 grouped pools and the
- * exact orders: generation into handle scratch, then the bucket-indexed map.  PSS_ENOTSUP if a
- * file holds 2^31 samples or more. */
+ * ([r - rank_lo][pos - pos_lo]) and the same reflection flag as pss_map.  Counter order (V1,
+ * and V2 on the exchange replays): one kernel, each id mapped where it is emitted (V2 pools up
+ * to 16384 through a per-tile LDS map of the files its ids can come from, grouped pools
+ * through the bucket-indexed map); the exact orders and the V2 collision-probe path:
+ * generation into handle scratch, then the bucket-indexed map.  PSS_ENOTSUP if a file holds
+ * 2^31 samples or more. */
 int pss_generate_mapped(pss_sampler *h, int32_t rank_lo, int32_t rank_hi, int64_t pos_lo,
                         int64_t count, int32_t *file_pos_dev, int32_t *offset_dev, void *stream);
 

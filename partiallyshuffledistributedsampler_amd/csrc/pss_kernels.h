@@ -161,7 +161,7 @@ int64_t v2_grp_tiles(const Geometry &g, int32_t nr);   // tiles per (rank, group
 hipError_t launch_v2_grp(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, int32_t nr,
                          int64_t pos_lo, int64_t count, int64_t *out, uint32_t *val_ws,
                          hipStream_t s, const Marker &mk, bool ordered, int stage,
-                         const RankArgs *rank_args = nullptr);
+                         const RankArgs *rank_args = nullptr, const MapArgs *mapped = nullptr);
 hipError_t init_kernel_attributes_v2grp();
 // launch_v2 splits into V2_STAGE_PRE / V2_STAGE_EMIT for this shape and emit path (EMIT_AUTO resolved)
 bool v2_stage_split(const Geometry &g, int32_t nr, int emit_path);

@@ -1013,7 +1013,9 @@ size_t v2_buf_bytes(const Geometry &, int32_t) {
 // path: a tile's ids then span ~(L / B + kSegBackWin) windows, a few hundred files at most.  A
 // grouped replay wave covers its rank's whole stream (too many files to stage): generate + map.
 bool v2_mapped_fused(const Geometry &g, int emit_path) {
-    if (v2_grouped(g)) return false;
+    // the exchange replays map in-kernel: the small-pool one through its per-tile LDS segment
+    // map, the grouped one through the global bucketed map
+    (void)g;
     if (emit_path == EMIT_AUTO) emit_path = lds_xchg_ordered() ? EMIT_XCHG : EMIT_PROBE;
     return emit_path == EMIT_XCHG;
 }
@@ -1071,7 +1073,7 @@ hipError_t launch_v2(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, 
     const bool do_pre = stage != V2_STAGE_EMIT, do_emit = stage != V2_STAGE_PRE;
     if (v2_grouped(g))   // pools beyond LDS: the grouped slot machine (pss_v2grp.hip)
         return launch_v2_grp(g, ranks, rank_lo, nr, pos_lo, count, out, VAL, s, mk,
-                             emit_path == EMIT_XCHG, stage, rank_args);
+                             emit_path == EMIT_XCHG, stage, rank_args, mapped);
     (void)err; (void)sort_ws; (void)gbuf;
     const V2Plan pl = v2_plan(g, nr);
     const int64_t pos_hi = pos_lo + count < g.ns ? pos_lo + count : g.ns;

@@ -44,8 +44,8 @@ namespace pss {
 
 namespace {
 constexpr int kTile = 4096;       // steps per LDS decode tile; pool2 windows up to this size decode in one
-constexpr int kTileNT = 1024;   // 4 steps per thread: the searches are latency-bound, occupancy hides them
-static_assert(kTileNT * 4 == kTile, "the tile merge gives each thread four outputs");
+constexpr int kTileOut = 8;     // consecutive merge outputs per thread (one search each per level)
+constexpr int kTileNT = kTile / kTileOut;
 
 struct V2xGeo {                   // one rank's stream, host-computed
     uint32_t P, T, S, B;          // pool1 size, main steps, pool2 windows, shuffle_buffer
@@ -55,15 +55,6 @@ struct V2xGeo {                   // one rank's stream, host-computed
 
 __device__ __forceinline__ uint32_t alive_at(uint32_t B0, uint32_t insu, uint32_t x) {
     return B0 - (x > insu ? x - insu : 0u);
-}
-// #{i < n : D[i] - i <= q} for sorted distinct D (D[i] - i is non-decreasing)
-__device__ __forceinline__ uint32_t count_e_le(const uint32_t *D, uint32_t n, uint32_t q) {
-    uint32_t lo = 0, hi = n;
-    while (lo < hi) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (D[mid] - mid <= q) lo = mid + 1; else hi = mid;
-    }
-    return lo;
 }
 }  // namespace
 
@@ -125,13 +116,34 @@ __global__ __launch_bounds__(64) void k_v2x_tail_draws(V2xGeo x, int64_t epoch, 
 }
 
 // ---- decode tiles in LDS: pool1 tiles of kTile steps and whole pool2 windows ---------------
+// An entry is one word: (frame position << kStepBits) | step within the tile -- 32-bit when
+// every frame position of the launch stays below 2^20 (pools <= 2^20 - kTile: every C2-shaped
+// launch), 64-bit otherwise -- so a merge step moves one LDS word, not a value and its step.
+// kTileNT threads, kTileOut consecutive outputs each: one merge-path search per thread per
+// level, then a walk that reads each entry once.
+constexpr int kStepBits = 12;
+static_assert((1 << kStepBits) == kTile, "a tile's steps fit the entry's step field");
+template <typename EW> struct TileEntry {
+    static constexpr int SH = sizeof(EW) == 4 ? kStepBits : 32;
+    static __device__ __forceinline__ uint32_t val(EW e) { return (uint32_t)(e >> SH); }
+    static __device__ __forceinline__ uint32_t step(EW e) { return (uint32_t)(e & (EW)(kTile - 1)); }
+    static __device__ __forceinline__ EW make(uint32_t v, uint32_t st) { return ((EW)v << SH) | (EW)st; }
+    static __device__ __forceinline__ EW add(EW e, uint32_t d) { return e + ((EW)d << SH); }
+};
+// largest frame position a launch can produce: pool1 tiles P + kTile, windows B
+static bool v2x_narrow(uint32_t P, uint32_t B) {
+    return (uint64_t)P + kTile <= ((uint64_t)1 << (32 - kStepBits)) && (uint64_t)B <= ((uint64_t)1 << (32 - kStepBits));
+}
+
+template <typename EW>
 __global__ __launch_bounds__(kTileNT) void k_v2x_tile(V2xGeo x, uint32_t per_rank, uint64_t blk0,
                                                       const uint32_t *__restrict__ K1,
                                                       const uint32_t *__restrict__ K2,
                                                       uint32_t *__restrict__ V, uint32_t *__restrict__ O,
                                                       uint32_t *__restrict__ Q2, uint32_t *__restrict__ SV) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-    uint32_t *va = smem, *oa = smem + kTile, *vb = smem + 2 * kTile, *ob = smem + 3 * kTile;
+    using TE = TileEntry<EW>;
+    extern __shared__ __attribute__((aligned(16))) uint32_t smem_u32[];
+    EW *va = (EW *)smem_u32, *vb = va + kTile;
     const uint64_t bi = blk0 + blockIdx.x;
     const uint32_t rl = (uint32_t)(bi / per_rank), job = (uint32_t)(bi % per_rank);
     const bool pool1 = job < x.tiles1;
@@ -149,7 +161,7 @@ __global__ __launch_bounds__(kTileNT) void k_v2x_tile(V2xGeo x, uint32_t per_ran
         B0 = n; insu = 0;
         src = K2 + (size_t)rl * x.T2 + (size_t)s * x.B;
     }
-    for (uint32_t u = threadIdx.x; u < n; u += kTileNT) { va[u] = src[u]; oa[u] = u; }
+    for (uint32_t u = threadIdx.x; u < n; u += kTileNT) va[u] = TE::make(src[u], u);
     __syncthreads();
     // merge levels: sibling blocks [a, m), [m, e) -> [a, e), each sorted by its frame position.
     // Left entries (deletions D, frame a) keep their values; a right entry q (frame m) is the
@@ -158,55 +170,65 @@ __global__ __launch_bounds__(kTileNT) void k_v2x_tile(V2xGeo x, uint32_t per_ran
     // right values (left first on ties) both orders the pair and maps the right block: a right
     // entry taken after i left ones becomes q + i.  (q beyond the left block's survivors are the
     // right block's own insertions: every E_i <= q there, and q + nL is their frame-a position.)
+    const uint32_t p0 = threadIdx.x * (uint32_t)kTileOut;
     for (uint32_t w = 1; w < n; w <<= 1) {
-        const uint32_t p0 = threadIdx.x * 4u;   // four consecutive outputs per thread
-        if (w == 1) {                           // two pairs per thread
-            for (uint32_t a = p0; a < p0 + 4u && a < n; a += 2u) {
-                if (a + 1u >= n) { vb[a] = va[a]; ob[a] = oa[a]; continue; }
-                const uint32_t L0 = va[a], R0 = va[a + 1], oL = oa[a], oR = oa[a + 1];
-                if (L0 <= R0) { vb[a] = L0; ob[a] = oL; vb[a + 1] = R0 + 1u; ob[a + 1] = oR; }
-                else { vb[a] = R0; ob[a] = oR; vb[a + 1] = L0; ob[a + 1] = oL; }
-            }
-        } else if (p0 < n) {
-            const uint32_t a = (p0 / (2 * w)) * (2 * w), m = a + w;
-            const uint32_t pe = p0 + 4u < n ? p0 + 4u : n;
+        // a thread's outputs may span several pairs while 2w < kTileOut: one walk per pair
+        for (uint32_t q = p0; q < p0 + (uint32_t)kTileOut && q < n;) {
+            const uint32_t a = (q / (2 * w)) * (2 * w), m = a + w;
+            const uint32_t pe0 = a + 2 * w < p0 + (uint32_t)kTileOut ? a + 2 * w : p0 + (uint32_t)kTileOut;
+            const uint32_t pe = pe0 < n ? pe0 : n;
             if (m >= n) {
-                for (uint32_t p = p0; p < pe; p++) { vb[p] = va[p]; ob[p] = oa[p]; }
+                for (uint32_t p = q; p < pe; p++) vb[p] = va[p];
             } else {
-                const uint32_t e = m + w < n ? m + w : n, nL = w, nR = e - m, d = p0 - a;
-                const uint32_t *L = va + a, *R = va + m;
+                const uint32_t e = m + w < n ? m + w : n, nL = w, nR = e - m, d = q - a;
+                const EW *L = va + a, *R = va + m;
                 uint32_t lo = d > nR ? d - nR : 0u, hi = d < nL ? d : nL;
                 while (lo < hi) {
                     const uint32_t mid = (lo + hi) >> 1;
-                    if (L[mid] - mid <= R[d - mid - 1]) lo = mid + 1; else hi = mid;
+                    if (TE::val(L[mid]) - mid <= TE::val(R[d - mid - 1])) lo = mid + 1; else hi = mid;
                 }
                 uint32_t i = lo, j = d - lo;
-                for (uint32_t p = p0; p < pe; p++) {
-                    const bool takeL = j >= nR || (i < nL && L[i] - i <= R[j]);
-                    if (takeL) { vb[p] = L[i]; ob[p] = oa[a + i]; i++; }
-                    else { vb[p] = R[j] + i; ob[p] = oa[m + j]; j++; }
+                EW xl = i < nL ? L[i] : (EW)0, xr = j < nR ? R[j] : (EW)0;
+                for (uint32_t p = q; p < pe; p++) {
+                    const bool takeL = j >= nR || (i < nL && TE::val(xl) - i <= TE::val(xr));
+                    if (takeL) {
+                        vb[p] = xl;
+                        i++;
+                        if (i < nL) xl = L[i];
+                    } else {
+                        vb[p] = TE::add(xr, i);
+                        j++;
+                        if (j < nR) xr = R[j];
+                    }
                 }
             }
+            q = pe;
         }
         __syncthreads();
-        uint32_t *t = va; va = vb; vb = t;
-        t = oa; oa = ob; ob = t;
+        EW *t = va; va = vb; vb = t;
     }
     if (pool1 && SV) {
         // chain mode (pools of <= kTile entries): each step's answer in step order, and the
         // tile's survivors -- the frame positions still alive at its end, in order: survivor r
         // is r + #{i : D_i - i <= r} over the sorted deletions D (k_v2x_compose / _emit)
         uint32_t *ans = V + (size_t)rl * x.ns + t0;
-        for (uint32_t u = threadIdx.x; u < n; u += kTileNT) ans[oa[u]] = va[u];
+        for (uint32_t u = threadIdx.x; u < n; u += kTileNT) ans[TE::step(va[u])] = TE::val(va[u]);
         const uint32_t Bm = alive_at(B0, insu, t0 + n);
         uint32_t *sv = SV + ((size_t)rl * x.tiles1 + job) * x.P;
-        for (uint32_t r = threadIdx.x; r < Bm; r += kTileNT) sv[r] = r + count_e_le(va, n, r);
+        for (uint32_t r = threadIdx.x; r < Bm; r += kTileNT) {
+            uint32_t lo = 0, hi = n;   // #{i : D_i - i <= r}
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (TE::val(va[mid]) - mid <= r) lo = mid + 1; else hi = mid;
+            }
+            sv[r] = r + lo;
+        }
     } else if (pool1) {
         uint32_t *v = V + (size_t)rl * x.ns + t0, *o = O + (size_t)rl * x.ns + t0;
-        for (uint32_t u = threadIdx.x; u < n; u += kTileNT) { v[u] = va[u]; o[u] = t0 + oa[u]; }
+        for (uint32_t u = threadIdx.x; u < n; u += kTileNT) { v[u] = TE::val(va[u]); o[u] = t0 + TE::step(va[u]); }
     } else {
         uint32_t *q = Q2 + (size_t)rl * x.T2 + (size_t)(job - x.tiles1) * x.B;
-        for (uint32_t u = threadIdx.x; u < n; u += kTileNT) q[oa[u]] = va[u];
+        for (uint32_t u = threadIdx.x; u < n; u += kTileNT) q[TE::step(va[u])] = TE::val(va[u]);
     }
 }
 
@@ -565,7 +587,8 @@ static hipError_t v2x_pass(const Geometry &g, const V2xGeo &x, const RankDesc *r
         hipLaunchKernelGGL(k_v2x_tail_draws, dim3(nb), dim3(64), 0, s, x, epoch, tail_blocks, b0, K1);
     });
     const uint32_t nru = (uint32_t)nr;
-    constexpr size_t kTileLds0 = 4 * kTile * sizeof(uint32_t);
+    const bool narrow = v2x_narrow(x.P, x.B);
+    const size_t kTileLds0 = 2 * kTile * (narrow ? sizeof(uint32_t) : sizeof(uint64_t));
     if (chain) {
         uint32_t *ANS = V;
         V2xChain ch = v2x_chain_plan(x, nr_plan);   // the workspace's plan (a last pass may be short)
@@ -574,8 +597,12 @@ static hipError_t v2x_pass(const Geometry &g, const V2xGeo &x, const RankDesc *r
         ch.AA = ch.CC + (size_t)nr * ch.nch * x.P;
         const uint32_t per_rank = x.tiles1 + x.S;
         v2x_launch_blocks((uint64_t)per_rank * nru, [&](uint64_t b0, uint32_t nb) {
-            hipLaunchKernelGGL(k_v2x_tile, dim3(nb), dim3(kTileNT), kTileLds0, s, x, per_rank, b0, K1, K2, ANS,
-                               (uint32_t *)nullptr, Q2, ch.SV);
+            if (narrow)
+                hipLaunchKernelGGL(k_v2x_tile<uint32_t>, dim3(nb), dim3(kTileNT), kTileLds0, s, x, per_rank, b0, K1, K2,
+                                   ANS, (uint32_t *)nullptr, Q2, ch.SV);
+            else
+                hipLaunchKernelGGL(k_v2x_tile<uint64_t>, dim3(nb), dim3(kTileNT), kTileLds0, s, x, per_rank, b0, K1, K2,
+                                   ANS, (uint32_t *)nullptr, Q2, ch.SV);
         });
         const size_t lds = 2 * (size_t)x.P * sizeof(uint32_t);
         hipLaunchKernelGGL(k_v2x_compose, dim3(nru * ch.nch), dim3(kChainNT), lds, s, x, ch);
@@ -586,13 +613,17 @@ static hipError_t v2x_pass(const Geometry &g, const V2xGeo &x, const RankDesc *r
     }
     uint32_t *SP = Q2 + tr;                    // merge-path splits: 2 words per tile
     const bool big_windows = x.B > (uint32_t)kTile && x.S > 0;
-    constexpr size_t kTileLds = 4 * kTile * sizeof(uint32_t);
+    const size_t kTileLds = kTileLds0;
     if (big_windows) {          // pool2 windows first, as nr * S sequences of B steps
         const V2xGeo xw = v2x_window_geo(x);
         const uint32_t nseq = nru * x.S;
         v2x_launch_blocks((uint64_t)xw.tiles1 * nseq, [&](uint64_t b0, uint32_t nb) {
-            hipLaunchKernelGGL(k_v2x_tile, dim3(nb), dim3(kTileNT), kTileLds, s, xw, xw.tiles1, b0, K2, K2,
-                               V, O, Q2, (uint32_t *)nullptr);
+            if (narrow)
+                hipLaunchKernelGGL(k_v2x_tile<uint32_t>, dim3(nb), dim3(kTileNT), kTileLds, s, xw, xw.tiles1, b0, K2,
+                                   K2, V, O, Q2, (uint32_t *)nullptr);
+            else
+                hipLaunchKernelGGL(k_v2x_tile<uint64_t>, dim3(nb), dim3(kTileNT), kTileLds, s, xw, xw.tiles1, b0, K2,
+                                   K2, V, O, Q2, (uint32_t *)nullptr);
         });
         uint32_t *wv = V, *wo = O, *wvd = Vd, *wod = Od;
         v2x_global_levels(xw, nseq, wv, wo, wvd, wod, SP, s);
@@ -603,8 +634,12 @@ static hipError_t v2x_pass(const Geometry &g, const V2xGeo &x, const RankDesc *r
     // pool1 tiles (and, for B <= kTile, the windows in the same launch)
     const uint32_t per_rank = x.tiles1 + (big_windows ? 0u : x.S);
     v2x_launch_blocks((uint64_t)per_rank * nru, [&](uint64_t b0, uint32_t nb) {
-        hipLaunchKernelGGL(k_v2x_tile, dim3(nb), dim3(kTileNT), kTileLds, s, x, per_rank, b0, K1, K2, V, O, Q2,
-                           (uint32_t *)nullptr);
+        if (narrow)
+            hipLaunchKernelGGL(k_v2x_tile<uint32_t>, dim3(nb), dim3(kTileNT), kTileLds, s, x, per_rank, b0, K1, K2, V,
+                               O, Q2, (uint32_t *)nullptr);
+        else
+            hipLaunchKernelGGL(k_v2x_tile<uint64_t>, dim3(nb), dim3(kTileNT), kTileLds, s, x, per_rank, b0, K1, K2, V,
+                               O, Q2, (uint32_t *)nullptr);
     });
     v2x_global_levels(x, nru, V, O, Vd, Od, SP, s);
     const dim3 grid1((uint32_t)v2x_cdiv((int64_t)nsr, 256));   // one thread per (rank, step)
@@ -620,9 +655,9 @@ hipError_t launch_v2_exact(const Geometry &g, const RankDesc *ranks, int32_t ran
     if (nr <= 0 || pos_hi <= pos_lo) return hipSuccess;
     if (!v2_exact_supported(g) || !ws) return hipErrorInvalidValue;
     const V2xGeo x = v2x_geo(g);
-    static const hipError_t attr = hipFuncSetAttribute((const void *)k_v2x_tile,
+    static const hipError_t attr = hipFuncSetAttribute((const void *)k_v2x_tile<uint64_t>,
                                                        hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                       4 * kTile * (int)sizeof(uint32_t));
+                                                       2 * kTile * (int)sizeof(uint64_t));
     if (attr != hipSuccess) return attr;
     const int32_t per = v2x_ranks_per_pass(g, nr);
     for (int32_t r0 = 0; r0 < nr; r0 += per) {

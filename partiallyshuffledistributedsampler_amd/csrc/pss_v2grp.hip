@@ -278,12 +278,17 @@ __device__ __forceinline__ void feistel_table(uint32_t off, uint32_t cnt, uint32
     }
 }
 
-template <bool ORDERED, bool NARROW, bool PACKED, bool POW2>
+// MAPPED (pss_generate_mapped; ORDERED only): each id is written as (int32 file position, int32
+// offset) through the epoch's bucketed map (map_one_bucketed, the map of pss_map) into ma.fpos /
+// ma.off, where the plain replay writes the int64 id -- the same 8 bytes per step, no id pass.
+template <bool ORDERED, bool NARROW, bool PACKED, bool POW2, bool MAPPED = false>
 __global__ __launch_bounds__(64) void k_g_emit(Geometry g, GPlan pl, const RankDesc *__restrict__ ranks,
                                                int32_t rank_lo, const uint32_t *__restrict__ KT,
                                                const uint32_t *__restrict__ VAL, int do_tail,
                                                int64_t pos_lo, int64_t count,
-                                               int64_t *__restrict__ out, RankArgs ra, int use_ra) {
+                                               int64_t *__restrict__ out, RankArgs ra, int use_ra,
+                                               MapArgs ma) {
+    static_assert(ORDERED || !MAPPED, "the mapped replay runs on the lane-ordered exchange path");
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     uint32_t *buf = smem;                                            // Smax slot words
     g_lds_vu8 *mark = (g_lds_vu8 *)(smem + pl.Smax);                  // !ORDERED: Smax bytes
@@ -335,6 +340,18 @@ __global__ __launch_bounds__(64) void k_g_emit(Geometry g, GPlan pl, const RankD
     __syncthreads();
     const uint32_t s0 = ktr[kGKeySlot], s1 = ktr[kGKeySlot + 1];
     int64_t *o = out + (int64_t)rl * count - pos_lo;
+    int32_t *ofp = ma.fpos + (int64_t)rl * count - pos_lo, *ooff = ma.off + (int64_t)rl * count - pos_lo;
+    auto put = [&](int64_t pos, int64_t id) {   // one id, outside the runs' buffer stores
+        if constexpr (MAPPED) {
+            int32_t f;
+            int64_t of;
+            map_one_bucketed(ma.prefix, ma.F, ma.BT, ma.kb, ma.nb, id, f, of);
+            ofp[pos] = f;
+            ooff[pos] = (int32_t)of;
+        } else {
+            o[pos] = id;
+        }
+    };
     const uint32_t G = pl.gr.G, B = pl.B32;
     const uint32_t G64 = 64u * G, G256 = 256u * G;
     const uint32_t shS = 32u - (uint32_t)ceil_log2_u64(S);
@@ -395,12 +412,19 @@ __global__ __launch_bounds__(64) void k_g_emit(Geometry g, GPlan pl, const RankD
             // the run's stores through a buffer descriptor on its wave-uniform base: 32-bit
             // per-lane offsets, no 64-bit address registers rewritten under in-flight stores
             // (with those, hipcc drained vmcnt(0) every iteration)
-            const uint64_t obase = (uint64_t)(uintptr_t)(o + t_first);
-            const uint32_t ob_lo = __builtin_amdgcn_readfirstlane((uint32_t)obase);
-            const uint32_t ob_hi = __builtin_amdgcn_readfirstlane((uint32_t)(obase >> 32));
-            const __amdgpu_buffer_rsrc_t orsrc = __builtin_amdgcn_make_buffer_rsrc(
-                (void *)(((uint64_t)ob_hi << 32) | ob_lo), 0, (int)(n * G256 * 8u), 0x00020000);
-            uint32_t voff = c_lane * 8u;                              // per-lane byte offsets
+            auto rsrc_at = [&](const void *p, uint32_t bytes) {
+                const uint64_t b64 = (uint64_t)(uintptr_t)p;
+                const uint32_t lo32 = __builtin_amdgcn_readfirstlane((uint32_t)b64);
+                const uint32_t hi32 = __builtin_amdgcn_readfirstlane((uint32_t)(b64 >> 32));
+                return __builtin_amdgcn_make_buffer_rsrc((void *)(((uint64_t)hi32 << 32) | lo32), 0,
+                                                         (int)bytes, 0x00020000);
+            };
+            const __amdgpu_buffer_rsrc_t orsrc = rsrc_at(MAPPED ? (const void *)(ofp + t_first) : (const void *)(o + t_first),
+                                                         n * G256 * (MAPPED ? 4u : 8u));
+            const __amdgpu_buffer_rsrc_t frsrc = rsrc_at(MAPPED ? (const void *)(ooff + t_first) : (const void *)(o + t_first),
+                                                         n * G256 * (MAPPED ? 4u : 8u));
+            (void)frsrc;
+            uint32_t voff = c_lane * (MAPPED ? 4u : 8u);              // per-lane byte offsets
             const uint32_t hmask = (1u << pl.hB) - 1u;
             auto body = [&](auto ctg, auto rinv) {
                 constexpr bool RINV = decltype(rinv)::value;
@@ -437,13 +461,21 @@ __global__ __launch_bounds__(64) void k_g_emit(Geometry g, GPlan pl, const RankD
                     }
 #pragma unroll
                     for (int j = 0; j < 4; j++) {
-                        const uint64_t id = (uint64_t)ids.from_slot(v[j]);
-                        const g_u32x2 d = {(uint32_t)id, (uint32_t)(id >> 32)};
-                        __builtin_amdgcn_raw_buffer_store_b64(d, orsrc, (int)voff, (int)(8u * (uint32_t)j * G64), 0);
+                        if constexpr (MAPPED) {
+                            int32_t f;
+                            int64_t of;
+                            map_one_bucketed(ma.prefix, ma.F, ma.BT, ma.kb, ma.nb, ids.from_slot(v[j]), f, of);
+                            __builtin_amdgcn_raw_buffer_store_b32((uint32_t)f, orsrc, (int)voff, (int)(4u * (uint32_t)j * G64), 0);
+                            __builtin_amdgcn_raw_buffer_store_b32((uint32_t)of, frsrc, (int)voff, (int)(4u * (uint32_t)j * G64), 0);
+                        } else {
+                            const uint64_t id = (uint64_t)ids.from_slot(v[j]);
+                            const g_u32x2 d = {(uint32_t)id, (uint32_t)(id >> 32)};
+                            __builtin_amdgcn_raw_buffer_store_b64(d, orsrc, (int)voff, (int)(8u * (uint32_t)j * G64), 0);
+                        }
                     }
                     tb += G256;
                     xb += G256;
-                    voff += 8u * G256;
+                    voff += (MAPPED ? 4u : 8u) * G256;
                 }
             };
             if constexpr (!PACKED) {
@@ -486,7 +518,7 @@ __global__ __launch_bounds__(64) void k_g_emit(Geometry g, GPlan pl, const RankD
             uint32_t vv;
             if constexpr (ORDERED) vv = valid ? atomicExch(&buf[kk], in) : 0u;
             else vv = xchg_unordered(buf, mark, kk, in, valid, lane);
-            if (valid && (int64_t)t >= pos_lo && (int64_t)t < pos_hi) o[t] = ids.from_slot(vv);
+            if (valid && (int64_t)t >= pos_lo && (int64_t)t < pos_hi) put(t, ids.from_slot(vv));
         }
         t_first += G256;
         pa += G256;
@@ -501,7 +533,7 @@ __global__ __launch_bounds__(64) void k_g_emit(Geometry g, GPlan pl, const RankD
         const uint32_t hS = feistel_half_bits(S);
         feistel_table(0u, S, S, hS, tk, lane, [&](uint32_t e, uint32_t s) {
             const int64_t pos = pl.T + group_tail_pos(pl.gr, grp, e);
-            if (pos >= pos_lo && pos < pos_hi) o[pos] = ids.from_slot(buf[s]);
+            if (pos >= pos_lo && pos < pos_hi) put(pos, ids.from_slot(buf[s]));
         });
     }
 }
@@ -524,7 +556,8 @@ size_t v2_grp_val_bytes(const Geometry &g, int32_t nr) {
 hipError_t launch_v2_grp(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, int32_t nr,
                          int64_t pos_lo, int64_t count, int64_t *out, uint32_t *VALws,
                          hipStream_t s, const Marker &mk, bool ordered, int stage,
-                         const RankArgs *rank_args) {
+                         const RankArgs *rank_args, const MapArgs *mapped) {
+    if (mapped && !ordered) return hipErrorNotSupported;
     const int64_t pos_hi = pos_lo + count < g.ns ? pos_lo + count : g.ns;
     if (nr <= 0 || pos_hi <= pos_lo) return hipSuccess;
     const GPlan pl = gplan(g, nr, gcus());
@@ -555,9 +588,13 @@ hipError_t launch_v2_grp(const Geometry &g, const RankDesc *ranks, int32_t rank_
     if (rank_args) ra = *rank_args;
     const bool packed = pl.hB <= 8;   // grouped pools: B > 16384, so hB >= 8 (never the small-half rounds)
     const bool pow2 = pl.gr.r == 0 && (pl.gr.q & (pl.gr.q - 1u)) == 0u;   // every group 2^b slots
-#define PSS_GE(O, N, PK, P2) hipLaunchKernelGGL((k_g_emit<O, N, PK, P2>), grid, dim3(64), lds, s, g, pl, ranks, \
-                                                rank_lo, (const uint32_t *)KT, (const uint32_t *)VAL, dt, pos_lo, count, out, \
-                                                ra, use_ra)
+    const MapArgs ma = mapped ? *mapped : MapArgs{};
+#define PSS_GE(O, N, PK, P2) do { if (mapped) hipLaunchKernelGGL((k_g_emit<true, N, PK, P2, true>), grid, dim3(64), lds, s, g, pl, \
+                                                                     ranks, rank_lo, (const uint32_t *)KT, (const uint32_t *)VAL, dt, \
+                                                                     pos_lo, count, out, ra, use_ra, ma); \
+                                  else hipLaunchKernelGGL((k_g_emit<O, N, PK, P2>), grid, dim3(64), lds, s, g, pl, ranks, \
+                                                          rank_lo, (const uint32_t *)KT, (const uint32_t *)VAL, dt, pos_lo, count, \
+                                                          out, ra, use_ra, ma); } while (0)
 #define PSS_GE2(O, N) do { if (packed && pow2) PSS_GE(O, N, true, true); else if (packed) PSS_GE(O, N, true, false); \
                            else if (pow2) PSS_GE(O, N, false, true); else PSS_GE(O, N, false, false); } while (0)
     if (ordered && narrow) PSS_GE2(true, true);
@@ -590,6 +627,14 @@ hipError_t init_kernel_attributes_v2grp() {
     PSS_ATTR((k_g_emit<false, false, true, false>));
     PSS_ATTR((k_g_emit<false, false, false, true>));
     PSS_ATTR((k_g_emit<false, false, false, false>));
+    PSS_ATTR((k_g_emit<true, true, true, true, true>));
+    PSS_ATTR((k_g_emit<true, true, true, false, true>));
+    PSS_ATTR((k_g_emit<true, true, false, true, true>));
+    PSS_ATTR((k_g_emit<true, true, false, false, true>));
+    PSS_ATTR((k_g_emit<true, false, true, true, true>));
+    PSS_ATTR((k_g_emit<true, false, true, false, true>));
+    PSS_ATTR((k_g_emit<true, false, false, true, true>));
+    PSS_ATTR((k_g_emit<true, false, false, false, true>));
     PSS_ATTR(k_g_lastocc);
 #undef PSS_ATTR
     return e;

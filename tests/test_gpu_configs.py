@@ -158,6 +158,28 @@ def test_c5_big_pool_consecutive_epochs():
     eng.close()
 
 
+def test_c5_fused_mapping_equals_generate_then_map():
+    """pss_generate_mapped at C5 (B = 2^20, the grouped replay maps each id in-kernel): equal to
+    generate + pss_map over all 8 ranks, for two consecutive epochs (the second replay takes the
+    lookahead's key table) and a ragged position range."""
+    lengths, N, R, B, ver = W.shape("c5")
+    eng = _engine(lengths, N, R, B, ver, seed=0)
+    ns = eng.num_samples
+    for epoch in (0, 1):
+        eng.init_iter(epoch)
+        f, o = eng.generate_mapped(0, R)
+        eng.check()
+        ids = _gen(eng, 0, R)
+        fr, orr = eng.map(ids.view(-1))
+        assert torch.equal(f.view(-1), fr) and torch.equal(o.view(-1).long(), orr), epoch
+        del ids, fr, orr
+    f2, o2 = eng.generate_mapped(2, 5, 123_457, 3 * B + 11)
+    eng.check()
+    assert torch.equal(f2, f[2:5, 123_457:123_457 + 3 * B + 11])
+    assert torch.equal(o2, o[2:5, 123_457:123_457 + 3 * B + 11])
+    eng.close()
+
+
 @pytest.mark.parametrize("B", [1 << 16, 1 << 18, 1 << 20])
 def test_big_pool_exact_order_matches_rank_select_oracle(B):
     """order="exact" (the reference's MT19937 draws, V2:96-116) on pools far beyond the

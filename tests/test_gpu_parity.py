@@ -291,11 +291,15 @@ def test_v2_emit_paths_match_oracle(path, B, R, F, lo, hi):
     (60, 500, 3000, 4, 1000, 777),     # N past the files' total: reflected ids (fallback)
     (50, 100, 400, 5, 64, 0),          # tiny windows
     (13, 1, 50, 5, 100, 0),            # ns < B: tail only
-    (8, 20000, 60000, 2, 16384, 0)])   # the largest LDS pool
+    (8, 20000, 60000, 2, 16384, 0),    # the largest LDS pool
+    (20, 5000, 20000, 2, 20000, 0),    # grouped pools (P1 > 16384): mapped in the grouped replay
+    (12, 50000, 100000, 3, 70001, 555),  # ... odd pool, partial last window, reflected ids
+    (40, 20000, 20001, 2, 65536, 0)])  # ... groups of 4096 slots (paired draws, run loop)
 def test_v2_fused_mapping_matches_generate_then_map(F, lo, hi, R, B, extra):
-    """pss_generate_mapped on V2 pools that fit LDS maps inside the replay (LDS segment map per
-    tile, global bucketed map outside it): equal to generate + pss_map for full epochs, ragged
-    and tail-only position ranges, and consecutive epochs served by the lookahead."""
+    """pss_generate_mapped maps inside the V2 replay (pools that fit LDS: the per-tile LDS
+    segment map, global bucketed map outside it; grouped pools: the global bucketed map in the
+    grouped replay): equal to generate + pss_map for full epochs, ragged and tail-only position
+    ranges, and consecutive epochs served by the lookahead."""
     rng = np.random.default_rng(F + B + extra)
     lengths = rng.integers(lo, hi, F)
     N = int(lengths.sum()) + extra
