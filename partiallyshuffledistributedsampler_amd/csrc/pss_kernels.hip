@@ -249,6 +249,8 @@ __global__ __launch_bounds__(64) void k_v1_feistel(Geometry g, V1Plan vp, const 
                                                    int32_t rank_lo, const uint32_t *__restrict__ kt,
                                                    int64_t pos_lo, int64_t count,
                                                    int64_t *__restrict__ out, MapArgs ma) {
+    extern __shared__ uint32_t v1_pad[];   // occupancy limiter only (PSS_V1_WAVES_PER_CU)
+    if (vp.nsb < 0) v1_pad[threadIdx.x] = 0;
     const int lane = threadIdx.x;
     const int64_t waves_per_rank = (vp.nsb + vp.per_wave - 1) / vp.per_wave;
     const int32_t rl = (int32_t)(blockIdx.x / waves_per_rank);
@@ -514,11 +516,16 @@ hipError_t launch_v1(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, 
         return (int64_t)(v > 0 && v <= 1024 ? v : 16);
     }();
     int64_t per = per_env;
-    while (per > 1 && total / per < 8 * 256) per >>= 1;
+    while (per > 1 && total / per < 4 * 256) per >>= 1;   // at least one wave per SIMD
     vp.per_wave = per;
     const int64_t waves = (int64_t)nr * cdiv(vp.nsb, per);
     const MapArgs ma = mapped ? *mapped : MapArgs{};
-#define PSS_V1(PK, MP) hipLaunchKernelGGL((k_v1_feistel<PK, MP>), dim3((uint32_t)waves), dim3(64), 0, s, g, vp, \
+    static const size_t v1_lds = [] {   // A/B knob: cap the resident waves per CU by an LDS claim
+        const char *e = getenv("PSS_V1_WAVES_PER_CU");
+        const long v = e ? atol(e) : 0;
+        return (size_t)(v > 0 && v <= 32 ? 160 * 1024 / v - 64 : 0);
+    }();
+#define PSS_V1(PK, MP) hipLaunchKernelGGL((k_v1_feistel<PK, MP>), dim3((uint32_t)waves), dim3(64), v1_lds, s, g, vp, \
                                           ranks, rank_lo, (const uint32_t *)key_ws, pos_lo, count, out, ma)
     if (feistel_packed_ok(vp.hB) && mapped) PSS_V1(true, true);
     else if (feistel_packed_ok(vp.hB)) PSS_V1(true, false);
@@ -529,6 +536,15 @@ hipError_t launch_v1(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, 
     return hipGetLastError();
 }
 
-hipError_t init_kernel_attributes() { return init_kernel_attributes_v2(); }
+hipError_t init_kernel_attributes() {
+    hipError_t e = init_kernel_attributes_v2();
+#define PSS_ATTR1(fn) { hipError_t x = hipFuncSetAttribute((const void *)(fn), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024); if (x != hipSuccess) e = x; }
+    PSS_ATTR1((k_v1_feistel<true, true>));
+    PSS_ATTR1((k_v1_feistel<true, false>));
+    PSS_ATTR1((k_v1_feistel<false, true>));
+    PSS_ATTR1((k_v1_feistel<false, false>));
+#undef PSS_ATTR1
+    return e;
+}
 
 }  // namespace pss

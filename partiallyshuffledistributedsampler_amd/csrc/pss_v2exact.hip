@@ -388,6 +388,12 @@ __global__ __launch_bounds__(kChainNT) void k_v2x_link(V2xGeo x, V2xChain ch) {
     }
 }
 
+// Software-pipelined over the chunk's tiles: a thread's answers and survivor entries of tile
+// j + 1 are loaded (kChainPer of each) while tile j's ids are computed and stored, so each tile
+// costs one LDS round trip and the pool2 gathers, not three dependent global round trips.
+constexpr int kChainPer = kTile / kChainNT;
+static_assert(kChainPer * kChainNT == kTile, "a tile's steps and survivors: kChainPer per thread");
+
 __global__ __launch_bounds__(kChainNT) void k_v2x_emit(Geometry g, V2xGeo x, V2xChain ch,
                                                        const RankDesc *__restrict__ ranks, int32_t rank_lo,
                                                        const uint32_t *__restrict__ ANS,
@@ -406,36 +412,52 @@ __global__ __launch_bounds__(kChainNT) void k_v2x_emit(Geometry g, V2xGeo x, V2x
     const uint32_t *ans = ANS + (size_t)rl * x.ns;
     const uint32_t *q2 = Q2 + (size_t)rl * x.T2;
     int64_t *o = out + (int64_t)rl * count - pos_lo;
+    // tile j's answers (q) and survivors (sr) of this thread: u = threadIdx.x + k * kChainNT
+    auto load = [&](uint32_t j, uint32_t (&q)[kChainPer], uint32_t (&sr)[kChainPer]) {
+        const uint32_t t0 = j * (uint32_t)kTile, n = x.ns - t0 < (uint32_t)kTile ? x.ns - t0 : (uint32_t)kTile;
+        const uint32_t Bm = alive_at(x.P, x.T, t0 + n);
+        const uint32_t *sv = ch.SV + ((size_t)rl * x.tiles1 + j) * x.P;
+#pragma unroll
+        for (int k = 0; k < kChainPer; k++) {
+            const uint32_t u = threadIdx.x + (uint32_t)k * kChainNT;
+            q[k] = u < n ? ans[t0 + u] : 0u;
+            sr[k] = u < Bm ? sv[u] : 0u;
+        }
+    };
+    uint32_t q[kChainPer], sr[kChainPer], qn[kChainPer], srn[kChainPer];
+    load(j0, q, sr);
     __syncthreads();
     for (uint32_t j = j0; j < j1; j++) {
         const uint32_t t0 = j * (uint32_t)kTile, n = x.ns - t0 < (uint32_t)kTile ? x.ns - t0 : (uint32_t)kTile;
         if ((int64_t)t0 >= pos_hi) break;
+        if (j + 1 < j1) load(j + 1, qn, srn);
         const uint32_t Ba = alive_at(x.P, x.T, t0), Bm = alive_at(x.P, x.T, t0 + n);
-        if ((int64_t)(t0 + n) > pos_lo) {
-            for (uint32_t u = threadIdx.x; u < n; u += kChainNT) {
-                const int64_t t = (int64_t)t0 + u;
-                if (t < pos_lo || t >= pos_hi) continue;
-                const uint32_t q = ans[t];
-                const uint32_t a = q < Ba ? A[q] : x.P + t0 + (q - Ba);
-                int64_t id;
-                if (a < x.P) {
-                    id = rd.old_start + a;              // initial pool1 (V2:135-136)
-                } else {                                // moved over from pool2 at step a - P
-                    const uint32_t uu = a - x.P, s = uu / x.B;
-                    const int64_t wbase = s == 0 ? rd.old_start + x.B : rd.new_start + (int64_t)(s + 1) * x.B;
-                    id = wbase + q2[uu];
-                }
-                o[t] = wrap_id(id, g.N);
+#pragma unroll
+        for (int k = 0; k < kChainPer; k++) {
+            const uint32_t u = threadIdx.x + (uint32_t)k * kChainNT;
+            const int64_t t = (int64_t)t0 + u;
+            if (u >= n || t < pos_lo || t >= pos_hi) continue;
+            const uint32_t a = q[k] < Ba ? A[q[k]] : x.P + t0 + (q[k] - Ba);
+            int64_t id;
+            if (a < x.P) {
+                id = rd.old_start + a;              // initial pool1 (V2:135-136)
+            } else {                                // moved over from pool2 at step a - P
+                const uint32_t uu = a - x.P, s = uu / x.B;
+                const int64_t wbase = s == 0 ? rd.old_start + x.B : rd.new_start + (int64_t)(s + 1) * x.B;
+                id = wbase + q2[uu];
             }
+            o[t] = wrap_id(id, g.N);
         }
         if (j + 1 < j1) {
-            const uint32_t *sv = ch.SV + ((size_t)rl * x.tiles1 + j) * x.P;
-            for (uint32_t r = threadIdx.x; r < Bm; r += kChainNT) {
-                const uint32_t q = sv[r];
-                An[r] = q < Ba ? A[q] : x.P + t0 + (q - Ba);
+#pragma unroll
+            for (int k = 0; k < kChainPer; k++) {
+                const uint32_t r = threadIdx.x + (uint32_t)k * kChainNT;
+                if (r < Bm) An[r] = sr[k] < Ba ? A[sr[k]] : x.P + t0 + (sr[k] - Ba);
             }
             __syncthreads();
-            uint32_t *t = A; A = An; An = t;
+            uint32_t *tp = A; A = An; An = tp;
+#pragma unroll
+            for (int k = 0; k < kChainPer; k++) { q[k] = qn[k]; sr[k] = srn[k]; }
         }
     }
 }

@@ -495,6 +495,50 @@ __global__ __launch_bounds__(64) void k_g_emit(Geometry g, GPlan pl, const RankD
             u0 += 256u * n;
             continue;
         }
+        // one whole iteration straddling the boundary of two full windows wa, wa + 1 (both
+        // non-walking): the run machinery with each lane's round keys picked from the two
+        // windows' SGPR keys (one v_cndmask per key word) and the paired slot hashes
+        if (runs_ok && wa + 1u < pl.w_last && pa < B && pa + span >= B && uhi - u0 >= 256u) {
+            if (wa != wk) {
+                if (wa == wk + 1u) {
+#pragma unroll
+                    for (int i = 0; i < kFeistelRounds; i++) Kc[i] = Kn[i];
+                } else {
+                    win_keys(wa, Kc);
+                }
+                wk = wa;
+                win_keys(wk + 1u, Kn);
+            }
+            const uint32_t tb = t_first + c_lane;
+            uint32_t k[4];
+            if (POW2 || gpow2) {
+                const uint32_t h0 = slot_hash(tb, s0, s1), h2 = slot_hash(tb + 2u * G64, s0, s1);
+                k[0] = h0 >> shS; k[1] = (h0 << 16) >> shS;
+                k[2] = h2 >> shS; k[3] = (h2 << 16) >> shS;
+            } else {
+#pragma unroll
+                for (int j = 0; j < 4; j++) k[j] = scale32(slot_hash(tb + j * G64, s0, s1), S);
+            }
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                uint32_t p = pa + c_lane + j * G64;
+                const bool nxt = p >= B;
+                if (nxt) p -= B;
+                uint32_t Kl[kFeistelRounds];
+#pragma unroll
+                for (int i = 0; i < kFeistelRounds; i++) Kl[i] = nxt ? Kn[i] : Kc[i];
+                const uint32_t in = ids.to_slot((wa + (nxt ? 1u : 0u)) * B + feistel_once(p, pl.hB, Kl));
+                uint32_t vv;
+                if constexpr (ORDERED) vv = atomicExch(&buf[k[j]], in);
+                else vv = xchg_unordered(buf, mark, k[j], in, true, lane);
+                put((int64_t)tb + j * G64, ids.from_slot(vv));
+            }
+            t_first += G256;
+            pa += G256;
+            while (pa >= B) { pa -= B; wa++; }
+            u0 += 256u;
+            continue;
+        }
         // one iteration across a window boundary, partly valid or partly emitted
 #pragma unroll
         for (int j = 0; j < 4; j++) {

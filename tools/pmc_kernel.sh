@@ -7,7 +7,7 @@ set -e
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export TMPDIR=/tmp
 W=${1:-c2}; T=${2:-$W}
 mkdir -p gpurun_out/$T
-B="python3 bench.py --workload $W --steps 3 --warmup 1 --no-cpu-baseline --no-latency"
+B="python3 bench.py --workload $W --steps 3 --warmup 1 --no-cpu-baseline --no-latency --no-exact"
 i=0
 for C in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_WR SQ_INSTS_BRANCH" \
          "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INST_CYCLES_SALU" \
@@ -15,5 +15,5 @@ for C in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS SQ_I
   i=$((i+1))
   timeout -s KILL 90 rocprofv3 --pmc $C --output-format csv -d gpurun_out/$T/pmc_$i -o run -- $B > gpurun_out/$T/pmc_$i.log 2>&1
 done
-timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/$T/stats -o run -- python3 bench.py --workload $W --steps 20 --no-cpu-baseline --no-latency > gpurun_out/$T/bench.json 2> gpurun_out/$T/bench.err
+timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/$T/stats -o run -- python3 bench.py --workload $W --steps 20 --no-cpu-baseline --no-latency --no-exact > gpurun_out/$T/bench.json 2> gpurun_out/$T/bench.err
 echo done
