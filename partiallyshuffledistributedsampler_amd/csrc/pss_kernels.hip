@@ -467,6 +467,16 @@ hipError_t launch_debug_wave_scan(const uint64_t *in, uint64_t *out, int64_t n, 
     return hipGetLastError();
 }
 
+static int64_t gcus_v1() {
+    static const int64_t n = [] {
+        int dev = 0, c = 0;
+        if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+        if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c <= 0) c = 256;
+        return (int64_t)c;
+    }();
+    return n;
+}
+
 static bool v1_window_range(const Geometry &g, int64_t pos_lo, int64_t count, int64_t &w_lo,
                             int64_t &nw) {
     const int64_t pos_hi = pos_lo + count < g.ns ? pos_lo + count : g.ns;
@@ -508,23 +518,28 @@ hipError_t launch_v1(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, 
         return (uint32_t)!(e && e[0] == '0');
     }();
     vp.pairs = pairs_env;
-    // ~16 super-blocks (4096 positions, 32 KB of output) per wave, at least 8 waves per CU
-    const int64_t total = (int64_t)nr * vp.nsb;
-    static const int64_t per_env = [] {   // A/B knob: super-blocks per wave
+    // One round of waves: the stream is cut into exactly as many waves as the chip holds at
+    // PSS_V1_WAVES_PER_CU resident waves per CU (default 8: two per SIMD, an LDS claim caps it),
+    // each a run of consecutive super-blocks.  A round-1/2 shape of 16 super-blocks per wave at
+    // full occupancy (3 rounds of 8 waves per SIMD) stored at 4.3-4.6 TB/s (C2 V1: 184 us), one
+    // round of 2 per SIMD at 4.6 (175 us): fewer stores in flight, no tail round.
+    static const int64_t wpc = [] {
+        const char *e = getenv("PSS_V1_WAVES_PER_CU");
+        const long v = e ? atol(e) : 8;
+        return (int64_t)(v > 0 && v <= 32 ? v : 8);
+    }();
+    static const int64_t per_env = [] {   // A/B knob: super-blocks per wave (0: one round)
         const char *e = getenv("PSS_V1_PER_WAVE");
         const long v = e ? atol(e) : 0;
-        return (int64_t)(v > 0 && v <= 1024 ? v : 16);
+        return (int64_t)(v > 0 && v <= 4096 ? v : 0);
     }();
-    int64_t per = per_env;
-    while (per > 1 && total / per < 4 * 256) per >>= 1;   // at least one wave per SIMD
+    const int64_t slots_per_rank = wpc * gcus_v1() / nr;
+    int64_t per = per_env ? per_env : cdiv(vp.nsb, slots_per_rank > 1 ? slots_per_rank : 1);
+    if (per < 1) per = 1;
     vp.per_wave = per;
     const int64_t waves = (int64_t)nr * cdiv(vp.nsb, per);
     const MapArgs ma = mapped ? *mapped : MapArgs{};
-    static const size_t v1_lds = [] {   // A/B knob: cap the resident waves per CU by an LDS claim
-        const char *e = getenv("PSS_V1_WAVES_PER_CU");
-        const long v = e ? atol(e) : 0;
-        return (size_t)(v > 0 && v <= 32 ? 160 * 1024 / v - 64 : 0);
-    }();
+    const size_t v1_lds = (size_t)(160 * 1024 / wpc - 64);   // caps the resident waves per CU
 #define PSS_V1(PK, MP) hipLaunchKernelGGL((k_v1_feistel<PK, MP>), dim3((uint32_t)waves), dim3(64), v1_lds, s, g, vp, \
                                           ranks, rank_lo, (const uint32_t *)key_ws, pos_lo, count, out, ma)
     if (feistel_packed_ok(vp.hB) && mapped) PSS_V1(true, true);

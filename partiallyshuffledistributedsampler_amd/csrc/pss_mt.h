@@ -217,20 +217,37 @@ __device__ void mt_draws_pair(uint32_t *mt, uint32_t W, uint32_t P, Emit emit) {
             const uint32_t word = valid ? mt_temper(mt[q0 + lane]) : 0u;
             const uint32_t r1 = word >> (32u - kb1);
             const bool a1 = valid && r1 < P;
-            uint32_t jg = i2 + (uint32_t)lane / 3u, j = 0, r2 = 0, role = 0, Fx = 0;
+            uint32_t j = 0, r2 = 0, role = 0, Fx = 0;
             bool a2 = false;
-            for (;;) {
-                const uint32_t n2 = jg < W ? W - jg : 1u;
-                r2 = word >> (32u - (32u - (uint32_t)__builtin_clz(n2)));
-                a2 = valid && r2 < n2;
+            // one scan of the role maps for the k2 verdicts a2 (at k2 indices jg); returns the
+            // lanes' true k2 indices in j
+            auto pass = [&](uint32_t n2, uint32_t rr) {
+                r2 = rr;
+                a2 = valid && rr < n2;
                 const uint32_t f = (a1 ? 1u : 0u) | ((a2 ? 0u : 1u) << 1);
                 Fx = wave_role_scan(f);
                 const uint32_t Fp = (uint32_t)__shfl((int)Fx, lane > 0 ? lane - 1 : 0);
                 role = lane ? (Fp >> st) & 1u : st;
                 const uint64_t m2 = __ballot(valid && role == 1u && a2);
                 j = i2 + (uint32_t)__popcll(m2 & below);
-                if (__ballot(valid && j != jg) == 0) break;
-                jg = j;
+            };
+            // a block holds at most 32 k2 draws, so each lane's k2 index lies in [i2, i2 + 32]:
+            // where every lane's k2 verdict is the same over that whole range (all but ~1 % of
+            // lanes), one scan settles the block; otherwise iterate guess -> true index
+            const uint32_t nhi = i2 < W ? W - i2 : 1u, nlo = i2 + 32u < W ? W - (i2 + 32u) : 1u;
+            const uint32_t kbh = 32u - (uint32_t)__builtin_clz(nhi);
+            const uint32_t rh = word >> (32u - kbh);
+            const bool sure = kbh == 32u - (uint32_t)__builtin_clz(nlo) && (rh < nlo || rh >= nhi);
+            if (__ballot(valid && !sure) == 0) {
+                pass(nlo, rh);
+            } else {
+                uint32_t jg = i2 + (uint32_t)lane / 3u;
+                for (;;) {
+                    const uint32_t n2 = jg < W ? W - jg : 1u;
+                    pass(n2, word >> (32u - (32u - (uint32_t)__builtin_clz(n2))));
+                    if (__ballot(valid && j != jg) == 0) break;
+                    jg = j;
+                }
             }
             const bool acc = valid && (role ? a2 : a1);
             const uint64_t m1 = __ballot(acc && role == 0u), m2 = __ballot(acc && role == 1u);

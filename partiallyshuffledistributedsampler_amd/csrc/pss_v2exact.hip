@@ -129,6 +129,12 @@ template <typename EW> struct TileEntry {
     static __device__ __forceinline__ uint32_t step(EW e) { return (uint32_t)(e & (EW)(kTile - 1)); }
     static __device__ __forceinline__ EW make(uint32_t v, uint32_t st) { return ((EW)v << SH) | (EW)st; }
     static __device__ __forceinline__ EW add(EW e, uint32_t d) { return e + ((EW)d << SH); }
+    // LDS index of entry p, skewed by one slot per 128 bytes: a thread's outputs are kTileOut
+    // consecutive entries, so the lanes of a wave touch entries kTileOut apart -- unskewed that
+    // is 16 (32-bit) / 8 (64-bit) lanes per bank
+    static constexpr int SKEW = sizeof(EW) == 4 ? 5 : 4;
+    static __device__ __forceinline__ uint32_t ix(uint32_t p) { return p + (p >> SKEW); }
+    static constexpr uint32_t kSlots = kTile + (kTile >> SKEW);
 };
 // largest frame position a launch can produce: pool1 tiles P + kTile, windows B
 static bool v2x_narrow(uint32_t P, uint32_t B) {
@@ -143,7 +149,7 @@ __global__ __launch_bounds__(kTileNT) void k_v2x_tile(V2xGeo x, uint32_t per_ran
                                                       uint32_t *__restrict__ Q2, uint32_t *__restrict__ SV) {
     using TE = TileEntry<EW>;
     extern __shared__ __attribute__((aligned(16))) uint32_t smem_u32[];
-    EW *va = (EW *)smem_u32, *vb = va + kTile;
+    EW *va = (EW *)smem_u32, *vb = va + TE::kSlots;
     const uint64_t bi = blk0 + blockIdx.x;
     const uint32_t rl = (uint32_t)(bi / per_rank), job = (uint32_t)(bi % per_rank);
     const bool pool1 = job < x.tiles1;
@@ -161,7 +167,7 @@ __global__ __launch_bounds__(kTileNT) void k_v2x_tile(V2xGeo x, uint32_t per_ran
         B0 = n; insu = 0;
         src = K2 + (size_t)rl * x.T2 + (size_t)s * x.B;
     }
-    for (uint32_t u = threadIdx.x; u < n; u += kTileNT) va[u] = TE::make(src[u], u);
+    for (uint32_t u = threadIdx.x; u < n; u += kTileNT) va[TE::ix(u)] = TE::make(src[u], u);
     __syncthreads();
     // merge levels: sibling blocks [a, m), [m, e) -> [a, e), each sorted by its frame position.
     // Left entries (deletions D, frame a) keep their values; a right entry q (frame m) is the
@@ -178,27 +184,28 @@ __global__ __launch_bounds__(kTileNT) void k_v2x_tile(V2xGeo x, uint32_t per_ran
             const uint32_t pe0 = a + 2 * w < p0 + (uint32_t)kTileOut ? a + 2 * w : p0 + (uint32_t)kTileOut;
             const uint32_t pe = pe0 < n ? pe0 : n;
             if (m >= n) {
-                for (uint32_t p = q; p < pe; p++) vb[p] = va[p];
+                for (uint32_t p = q; p < pe; p++) vb[TE::ix(p)] = va[TE::ix(p)];
             } else {
                 const uint32_t e = m + w < n ? m + w : n, nL = w, nR = e - m, d = q - a;
-                const EW *L = va + a, *R = va + m;
+                auto L = [&](uint32_t i) { return va[TE::ix(a + i)]; };
+                auto R = [&](uint32_t j) { return va[TE::ix(m + j)]; };
                 uint32_t lo = d > nR ? d - nR : 0u, hi = d < nL ? d : nL;
                 while (lo < hi) {
                     const uint32_t mid = (lo + hi) >> 1;
-                    if (TE::val(L[mid]) - mid <= TE::val(R[d - mid - 1])) lo = mid + 1; else hi = mid;
+                    if (TE::val(L(mid)) - mid <= TE::val(R(d - mid - 1))) lo = mid + 1; else hi = mid;
                 }
                 uint32_t i = lo, j = d - lo;
-                EW xl = i < nL ? L[i] : (EW)0, xr = j < nR ? R[j] : (EW)0;
+                EW xl = i < nL ? L(i) : (EW)0, xr = j < nR ? R(j) : (EW)0;
                 for (uint32_t p = q; p < pe; p++) {
                     const bool takeL = j >= nR || (i < nL && TE::val(xl) - i <= TE::val(xr));
                     if (takeL) {
-                        vb[p] = xl;
+                        vb[TE::ix(p)] = xl;
                         i++;
-                        if (i < nL) xl = L[i];
+                        if (i < nL) xl = L(i);
                     } else {
-                        vb[p] = TE::add(xr, i);
+                        vb[TE::ix(p)] = TE::add(xr, i);
                         j++;
-                        if (j < nR) xr = R[j];
+                        if (j < nR) xr = R(j);
                     }
                 }
             }
@@ -212,23 +219,23 @@ __global__ __launch_bounds__(kTileNT) void k_v2x_tile(V2xGeo x, uint32_t per_ran
         // tile's survivors -- the frame positions still alive at its end, in order: survivor r
         // is r + #{i : D_i - i <= r} over the sorted deletions D (k_v2x_compose / _emit)
         uint32_t *ans = V + (size_t)rl * x.ns + t0;
-        for (uint32_t u = threadIdx.x; u < n; u += kTileNT) ans[TE::step(va[u])] = TE::val(va[u]);
+        for (uint32_t u = threadIdx.x; u < n; u += kTileNT) { const EW e = va[TE::ix(u)]; ans[TE::step(e)] = TE::val(e); }
         const uint32_t Bm = alive_at(B0, insu, t0 + n);
         uint32_t *sv = SV + ((size_t)rl * x.tiles1 + job) * x.P;
         for (uint32_t r = threadIdx.x; r < Bm; r += kTileNT) {
             uint32_t lo = 0, hi = n;   // #{i : D_i - i <= r}
             while (lo < hi) {
                 const uint32_t mid = (lo + hi) >> 1;
-                if (TE::val(va[mid]) - mid <= r) lo = mid + 1; else hi = mid;
+                if (TE::val(va[TE::ix(mid)]) - mid <= r) lo = mid + 1; else hi = mid;
             }
             sv[r] = r + lo;
         }
     } else if (pool1) {
         uint32_t *v = V + (size_t)rl * x.ns + t0, *o = O + (size_t)rl * x.ns + t0;
-        for (uint32_t u = threadIdx.x; u < n; u += kTileNT) { v[u] = TE::val(va[u]); o[u] = t0 + TE::step(va[u]); }
+        for (uint32_t u = threadIdx.x; u < n; u += kTileNT) { const EW e = va[TE::ix(u)]; v[u] = TE::val(e); o[u] = t0 + TE::step(e); }
     } else {
         uint32_t *q = Q2 + (size_t)rl * x.T2 + (size_t)(job - x.tiles1) * x.B;
-        for (uint32_t u = threadIdx.x; u < n; u += kTileNT) q[TE::step(va[u])] = TE::val(va[u]);
+        for (uint32_t u = threadIdx.x; u < n; u += kTileNT) { const EW e = va[TE::ix(u)]; q[TE::step(e)] = TE::val(e); }
     }
 }
 
@@ -610,7 +617,8 @@ static hipError_t v2x_pass(const Geometry &g, const V2xGeo &x, const RankDesc *r
     });
     const uint32_t nru = (uint32_t)nr;
     const bool narrow = v2x_narrow(x.P, x.B);
-    const size_t kTileLds0 = 2 * kTile * (narrow ? sizeof(uint32_t) : sizeof(uint64_t));
+    const size_t kTileLds0 = narrow ? 2 * TileEntry<uint32_t>::kSlots * sizeof(uint32_t)
+                                    : 2 * TileEntry<uint64_t>::kSlots * sizeof(uint64_t);
     if (chain) {
         uint32_t *ANS = V;
         V2xChain ch = v2x_chain_plan(x, nr_plan);   // the workspace's plan (a last pass may be short)
@@ -679,7 +687,7 @@ hipError_t launch_v2_exact(const Geometry &g, const RankDesc *ranks, int32_t ran
     const V2xGeo x = v2x_geo(g);
     static const hipError_t attr = hipFuncSetAttribute((const void *)k_v2x_tile<uint64_t>,
                                                        hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                       2 * kTile * (int)sizeof(uint64_t));
+                                                       2 * (int)TileEntry<uint64_t>::kSlots * (int)sizeof(uint64_t));
     if (attr != hipSuccess) return attr;
     const int32_t per = v2x_ranks_per_pass(g, nr);
     for (int32_t r0 = 0; r0 < nr; r0 += per) {

@@ -35,6 +35,7 @@ struct GPlan {
     Groups gr;
     uint32_t Smax;           // largest group
     uint32_t B32, hB, walk_full, w_last, len_last, h_last, hP, twoB;
+    uint32_t straddle;       // window-straddling iterations on the run machinery (PSS_G_STRADDLE)
 };
 
 
@@ -64,6 +65,11 @@ static GPlan gplan(const Geometry &g, int32_t nr, int cus) {
     p.h_last = feistel_half_bits(p.len_last > 0 ? p.len_last : 1);
     p.hP = feistel_half_bits((uint32_t)p.P1);
     p.twoB = (uint32_t)(2 * g.B < g.ns ? 2 * g.B : g.ns);
+    static const uint32_t straddle = [] {
+        const char *e = getenv("PSS_G_STRADDLE");
+        return (uint32_t)!(e && e[0] == '0');
+    }();
+    p.straddle = straddle;
     return p;
 }
 
@@ -498,7 +504,7 @@ __global__ __launch_bounds__(64) void k_g_emit(Geometry g, GPlan pl, const RankD
         // one whole iteration straddling the boundary of two full windows wa, wa + 1 (both
         // non-walking): the run machinery with each lane's round keys picked from the two
         // windows' SGPR keys (one v_cndmask per key word) and the paired slot hashes
-        if (runs_ok && wa + 1u < pl.w_last && pa < B && pa + span >= B && uhi - u0 >= 256u) {
+        if (pl.straddle && runs_ok && wa + 1u < pl.w_last && pa < B && pa + span >= B && uhi - u0 >= 256u) {
             if (wa != wk) {
                 if (wa == wk + 1u) {
 #pragma unroll
