@@ -45,7 +45,6 @@ namespace pss {
 namespace {
 constexpr int kTile = 4096;       // steps per LDS decode tile; pool2 windows up to this size decode in one
 constexpr int kTileOut = 8;     // consecutive merge outputs per thread (one search each per level)
-constexpr int kTileNT = kTile / kTileOut;
 
 struct V2xGeo {                   // one rank's stream, host-computed
     uint32_t P, T, S, B;          // pool1 size, main steps, pool2 windows, shuffle_buffer
@@ -141,13 +140,14 @@ static bool v2x_narrow(uint32_t P, uint32_t B) {
     return (uint64_t)P + kTile <= ((uint64_t)1 << (32 - kStepBits)) && (uint64_t)B <= ((uint64_t)1 << (32 - kStepBits));
 }
 
-template <typename EW>
-__global__ __launch_bounds__(kTileNT) void k_v2x_tile(V2xGeo x, uint32_t per_rank, uint64_t blk0,
+template <typename EW, int OUT>
+__global__ __launch_bounds__(kTile / OUT) void k_v2x_tile(V2xGeo x, uint32_t per_rank, uint64_t blk0,
                                                       const uint32_t *__restrict__ K1,
                                                       const uint32_t *__restrict__ K2,
                                                       uint32_t *__restrict__ V, uint32_t *__restrict__ O,
                                                       uint32_t *__restrict__ Q2, uint32_t *__restrict__ SV) {
     using TE = TileEntry<EW>;
+    constexpr uint32_t NT = kTile / OUT;
     extern __shared__ __attribute__((aligned(16))) uint32_t smem_u32[];
     EW *va = (EW *)smem_u32, *vb = va + TE::kSlots;
     const uint64_t bi = blk0 + blockIdx.x;
@@ -167,7 +167,7 @@ __global__ __launch_bounds__(kTileNT) void k_v2x_tile(V2xGeo x, uint32_t per_ran
         B0 = n; insu = 0;
         src = K2 + (size_t)rl * x.T2 + (size_t)s * x.B;
     }
-    for (uint32_t u = threadIdx.x; u < n; u += kTileNT) va[TE::ix(u)] = TE::make(src[u], u);
+    for (uint32_t u = threadIdx.x; u < n; u += NT) va[TE::ix(u)] = TE::make(src[u], u);
     __syncthreads();
     // merge levels: sibling blocks [a, m), [m, e) -> [a, e), each sorted by its frame position.
     // Left entries (deletions D, frame a) keep their values; a right entry q (frame m) is the
@@ -176,12 +176,12 @@ __global__ __launch_bounds__(kTileNT) void k_v2x_tile(V2xGeo x, uint32_t per_ran
     // right values (left first on ties) both orders the pair and maps the right block: a right
     // entry taken after i left ones becomes q + i.  (q beyond the left block's survivors are the
     // right block's own insertions: every E_i <= q there, and q + nL is their frame-a position.)
-    const uint32_t p0 = threadIdx.x * (uint32_t)kTileOut;
+    const uint32_t p0 = threadIdx.x * (uint32_t)OUT;
     for (uint32_t w = 1; w < n; w <<= 1) {
-        // a thread's outputs may span several pairs while 2w < kTileOut: one walk per pair
-        for (uint32_t q = p0; q < p0 + (uint32_t)kTileOut && q < n;) {
+        // a thread's outputs may span several pairs while 2w < OUT: one walk per pair
+        for (uint32_t q = p0; q < p0 + (uint32_t)OUT && q < n;) {
             const uint32_t a = (q / (2 * w)) * (2 * w), m = a + w;
-            const uint32_t pe0 = a + 2 * w < p0 + (uint32_t)kTileOut ? a + 2 * w : p0 + (uint32_t)kTileOut;
+            const uint32_t pe0 = a + 2 * w < p0 + (uint32_t)OUT ? a + 2 * w : p0 + (uint32_t)OUT;
             const uint32_t pe = pe0 < n ? pe0 : n;
             if (m >= n) {
                 for (uint32_t p = q; p < pe; p++) vb[TE::ix(p)] = va[TE::ix(p)];
@@ -219,10 +219,10 @@ __global__ __launch_bounds__(kTileNT) void k_v2x_tile(V2xGeo x, uint32_t per_ran
         // tile's survivors -- the frame positions still alive at its end, in order: survivor r
         // is r + #{i : D_i - i <= r} over the sorted deletions D (k_v2x_compose / _emit)
         uint32_t *ans = V + (size_t)rl * x.ns + t0;
-        for (uint32_t u = threadIdx.x; u < n; u += kTileNT) { const EW e = va[TE::ix(u)]; ans[TE::step(e)] = TE::val(e); }
+        for (uint32_t u = threadIdx.x; u < n; u += NT) { const EW e = va[TE::ix(u)]; ans[TE::step(e)] = TE::val(e); }
         const uint32_t Bm = alive_at(B0, insu, t0 + n);
         uint32_t *sv = SV + ((size_t)rl * x.tiles1 + job) * x.P;
-        for (uint32_t r = threadIdx.x; r < Bm; r += kTileNT) {
+        for (uint32_t r = threadIdx.x; r < Bm; r += NT) {
             uint32_t lo = 0, hi = n;   // #{i : D_i - i <= r}
             while (lo < hi) {
                 const uint32_t mid = (lo + hi) >> 1;
@@ -232,10 +232,10 @@ __global__ __launch_bounds__(kTileNT) void k_v2x_tile(V2xGeo x, uint32_t per_ran
         }
     } else if (pool1) {
         uint32_t *v = V + (size_t)rl * x.ns + t0, *o = O + (size_t)rl * x.ns + t0;
-        for (uint32_t u = threadIdx.x; u < n; u += kTileNT) { const EW e = va[TE::ix(u)]; v[u] = TE::val(e); o[u] = t0 + TE::step(e); }
+        for (uint32_t u = threadIdx.x; u < n; u += NT) { const EW e = va[TE::ix(u)]; v[u] = TE::val(e); o[u] = t0 + TE::step(e); }
     } else {
         uint32_t *q = Q2 + (size_t)rl * x.T2 + (size_t)(job - x.tiles1) * x.B;
-        for (uint32_t u = threadIdx.x; u < n; u += kTileNT) { const EW e = va[TE::ix(u)]; q[TE::step(e)] = TE::val(e); }
+        for (uint32_t u = threadIdx.x; u < n; u += NT) { const EW e = va[TE::ix(u)]; q[TE::step(e)] = TE::val(e); }
     }
 }
 
@@ -617,6 +617,22 @@ static hipError_t v2x_pass(const Geometry &g, const V2xGeo &x, const RankDesc *r
     });
     const uint32_t nru = (uint32_t)nr;
     const bool narrow = v2x_narrow(x.P, x.B);
+    static const int out16 = [] {   // A/B knob: 16 merge outputs per thread (256 threads) instead of 8
+        const char *e = getenv("PSS_V2X_OUT");
+        return e && atoi(e) == 16;
+    }();
+    // one decode-tile launch of nb blocks from block b0 (the entry width and outputs per thread)
+    auto tile = [&](uint64_t b0, uint32_t nb, const V2xGeo &xg, uint32_t per, const uint32_t *k1,
+                    const uint32_t *k2, uint32_t *v, uint32_t *o, uint32_t *q2, uint32_t *sv, size_t lds) {
+        if (narrow && out16)
+            hipLaunchKernelGGL((k_v2x_tile<uint32_t, 16>), dim3(nb), dim3(kTile / 16), lds, s, xg, per, b0, k1, k2, v, o, q2, sv);
+        else if (narrow)
+            hipLaunchKernelGGL((k_v2x_tile<uint32_t, kTileOut>), dim3(nb), dim3(kTile / kTileOut), lds, s, xg, per, b0, k1, k2, v, o, q2, sv);
+        else if (out16)
+            hipLaunchKernelGGL((k_v2x_tile<uint64_t, 16>), dim3(nb), dim3(kTile / 16), lds, s, xg, per, b0, k1, k2, v, o, q2, sv);
+        else
+            hipLaunchKernelGGL((k_v2x_tile<uint64_t, kTileOut>), dim3(nb), dim3(kTile / kTileOut), lds, s, xg, per, b0, k1, k2, v, o, q2, sv);
+    };
     const size_t kTileLds0 = narrow ? 2 * TileEntry<uint32_t>::kSlots * sizeof(uint32_t)
                                     : 2 * TileEntry<uint64_t>::kSlots * sizeof(uint64_t);
     if (chain) {
@@ -627,12 +643,7 @@ static hipError_t v2x_pass(const Geometry &g, const V2xGeo &x, const RankDesc *r
         ch.AA = ch.CC + (size_t)nr * ch.nch * x.P;
         const uint32_t per_rank = x.tiles1 + x.S;
         v2x_launch_blocks((uint64_t)per_rank * nru, [&](uint64_t b0, uint32_t nb) {
-            if (narrow)
-                hipLaunchKernelGGL(k_v2x_tile<uint32_t>, dim3(nb), dim3(kTileNT), kTileLds0, s, x, per_rank, b0, K1, K2,
-                                   ANS, (uint32_t *)nullptr, Q2, ch.SV);
-            else
-                hipLaunchKernelGGL(k_v2x_tile<uint64_t>, dim3(nb), dim3(kTileNT), kTileLds0, s, x, per_rank, b0, K1, K2,
-                                   ANS, (uint32_t *)nullptr, Q2, ch.SV);
+            tile(b0, nb, x, per_rank, K1, K2, ANS, (uint32_t *)nullptr, Q2, ch.SV, kTileLds0);
         });
         const size_t lds = 2 * (size_t)x.P * sizeof(uint32_t);
         hipLaunchKernelGGL(k_v2x_compose, dim3(nru * ch.nch), dim3(kChainNT), lds, s, x, ch);
@@ -648,12 +659,7 @@ static hipError_t v2x_pass(const Geometry &g, const V2xGeo &x, const RankDesc *r
         const V2xGeo xw = v2x_window_geo(x);
         const uint32_t nseq = nru * x.S;
         v2x_launch_blocks((uint64_t)xw.tiles1 * nseq, [&](uint64_t b0, uint32_t nb) {
-            if (narrow)
-                hipLaunchKernelGGL(k_v2x_tile<uint32_t>, dim3(nb), dim3(kTileNT), kTileLds, s, xw, xw.tiles1, b0, K2,
-                                   K2, V, O, Q2, (uint32_t *)nullptr);
-            else
-                hipLaunchKernelGGL(k_v2x_tile<uint64_t>, dim3(nb), dim3(kTileNT), kTileLds, s, xw, xw.tiles1, b0, K2,
-                                   K2, V, O, Q2, (uint32_t *)nullptr);
+            tile(b0, nb, xw, xw.tiles1, K2, K2, V, O, Q2, (uint32_t *)nullptr, kTileLds);
         });
         uint32_t *wv = V, *wo = O, *wvd = Vd, *wod = Od;
         v2x_global_levels(xw, nseq, wv, wo, wvd, wod, SP, s);
@@ -664,12 +670,7 @@ static hipError_t v2x_pass(const Geometry &g, const V2xGeo &x, const RankDesc *r
     // pool1 tiles (and, for B <= kTile, the windows in the same launch)
     const uint32_t per_rank = x.tiles1 + (big_windows ? 0u : x.S);
     v2x_launch_blocks((uint64_t)per_rank * nru, [&](uint64_t b0, uint32_t nb) {
-        if (narrow)
-            hipLaunchKernelGGL(k_v2x_tile<uint32_t>, dim3(nb), dim3(kTileNT), kTileLds, s, x, per_rank, b0, K1, K2, V,
-                               O, Q2, (uint32_t *)nullptr);
-        else
-            hipLaunchKernelGGL(k_v2x_tile<uint64_t>, dim3(nb), dim3(kTileNT), kTileLds, s, x, per_rank, b0, K1, K2, V,
-                               O, Q2, (uint32_t *)nullptr);
+        tile(b0, nb, x, per_rank, K1, K2, V, O, Q2, (uint32_t *)nullptr, kTileLds);
     });
     v2x_global_levels(x, nru, V, O, Vd, Od, SP, s);
     const dim3 grid1((uint32_t)v2x_cdiv((int64_t)nsr, 256));   // one thread per (rank, step)
@@ -685,9 +686,14 @@ hipError_t launch_v2_exact(const Geometry &g, const RankDesc *ranks, int32_t ran
     if (nr <= 0 || pos_hi <= pos_lo) return hipSuccess;
     if (!v2_exact_supported(g) || !ws) return hipErrorInvalidValue;
     const V2xGeo x = v2x_geo(g);
-    static const hipError_t attr = hipFuncSetAttribute((const void *)k_v2x_tile<uint64_t>,
-                                                       hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                       2 * (int)TileEntry<uint64_t>::kSlots * (int)sizeof(uint64_t));
+    static const hipError_t attr = [] {
+        const int lds = 2 * (int)TileEntry<uint64_t>::kSlots * (int)sizeof(uint64_t);
+        hipError_t e = hipFuncSetAttribute((const void *)k_v2x_tile<uint64_t, kTileOut>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+        if (e == hipSuccess)
+            e = hipFuncSetAttribute((const void *)k_v2x_tile<uint64_t, 16>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+        return e;
+    }();
     if (attr != hipSuccess) return attr;
     const int32_t per = v2x_ranks_per_pass(g, nr);
     for (int32_t r0 = 0; r0 < nr; r0 += per) {
