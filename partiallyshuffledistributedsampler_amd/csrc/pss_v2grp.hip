@@ -387,11 +387,17 @@ __global__ __launch_bounds__(64) void k_g_emit(Geometry g, GPlan pl, const RankD
     uint32_t wk = wa, Kc[kFeistelRounds], Kn[kFeistelRounds];
     win_keys(wk, Kc);
     win_keys(wk + 1u, Kn);
+    // the last pool2 window (len_last < B values) runs on the same machinery when its Feistel
+    // half width is B's: a first pass as in a full window, then the lanes whose image lies at or
+    // beyond len_last walk on (cycle walking, wave-uniform keys)
+    const bool last_runs = pl.h_last == pl.hB;
     while (u0 < uhi) {
-        // a run of whole iterations inside the full window wa: keys in SGPRs, no bookkeeping
+        // a run of whole iterations inside the window wa: keys in SGPRs, no bookkeeping
         uint32_t n = 0;
-        if (runs_ok && wa < pl.w_last && pa + span < B && uhi - u0 >= 256u) {
-            const uint32_t by_win = (B - 1u - span - pa) / G256 + 1u;
+        const bool wlast = wa == pl.w_last;
+        const uint32_t wlen = wlast ? pl.len_last : B;
+        if (runs_ok && (wa < pl.w_last || (wlast && last_runs)) && pa + span < wlen && uhi - u0 >= 256u) {
+            const uint32_t by_win = (wlen - 1u - span - pa) / G256 + 1u;
             const uint32_t by_end = (uhi - u0) / 256u;
             n = by_win < by_end ? by_win : by_end;
         }
@@ -411,9 +417,10 @@ __global__ __launch_bounds__(64) void k_g_emit(Geometry g, GPlan pl, const RankD
             for (int i = 0; i < kFeistelRounds; i++) K[i] = Kc[i];
             // ids of the window's values wa B + y: one add when the window maps contiguously
             const uint32_t wB = wa * B;
-            const uint32_t id_first = ids.to_slot(wB), id_last = ids.to_slot(wB + B - 1u);
-            const bool contig = NARROW && id_last - id_first == B - 1u &&
-                                ((wB < pl.twoB) == (wB + B - 1u < pl.twoB));
+            const uint32_t id_first = ids.to_slot(wB), id_last = ids.to_slot(wB + wlen - 1u);
+            const bool contig = NARROW && id_last - id_first == wlen - 1u &&
+                                ((wB < pl.twoB) == (wB + wlen - 1u < pl.twoB));
+            const bool walk = wlen != (1u << (2u * pl.hB));
             uint32_t tb = t_first + c_lane, xb = pa + c_lane;
             // the run's stores through a buffer descriptor on its wave-uniform base: 32-bit
             // per-lane offsets, no 64-bit address registers rewritten under in-flight stores
@@ -432,7 +439,7 @@ __global__ __launch_bounds__(64) void k_g_emit(Geometry g, GPlan pl, const RankD
             (void)frsrc;
             uint32_t voff = c_lane * (MAPPED ? 4u : 8u);              // per-lane byte offsets
             const uint32_t hmask = (1u << pl.hB) - 1u;
-            auto body = [&](auto ctg, auto rinv) {
+            auto body = [&](auto ctg, auto rinv, auto wlk) {
                 constexpr bool RINV = decltype(rinv)::value;
                 uint32_t A0 = 0u, C1 = 0u, lb = 0u;
                 const uint32_t g64h = G64 >> pl.hB, g256h = G256 >> pl.hB;
@@ -459,6 +466,11 @@ __global__ __launch_bounds__(64) void k_g_emit(Geometry g, GPlan pl, const RankD
                         const uint32_t x[4] = {xb, xb + G64, xb + 2u * G64, xb + 3u * G64};
                         feistel4_uniform<PACKED>(x, pl.hB, K, y);
                     }
+                    if constexpr (decltype(wlk)::value) {   // cycle walking in the last window
+#pragma unroll
+                        for (int j = 0; j < 4; j++)
+                            while (y[j] >= wlen) y[j] = feistel_once(y[j], pl.hB, K);
+                    }
 #pragma unroll
                     for (int j = 0; j < 4; j++) {
                         const uint32_t in = decltype(ctg)::value ? id_first + y[j] : ids.to_slot(wB + y[j]);
@@ -484,18 +496,22 @@ __global__ __launch_bounds__(64) void k_g_emit(Geometry g, GPlan pl, const RankD
                     voff += (MAPPED ? 4u : 8u) * G256;
                 }
             };
-            if constexpr (!PACKED) {
-                if ((G64 & hmask) == 0u) {   // run-invariant right halves (feistel4_rinv)
-                    if (contig) body(std::true_type{}, std::true_type{});
-                    else body(std::false_type{}, std::true_type{});
+            auto go = [&](auto wlk) {
+                if constexpr (!PACKED) {
+                    if ((G64 & hmask) == 0u) {   // run-invariant right halves (feistel4_rinv)
+                        if (contig) body(std::true_type{}, std::true_type{}, wlk);
+                        else body(std::false_type{}, std::true_type{}, wlk);
+                    } else {
+                        if (contig) body(std::true_type{}, std::false_type{}, wlk);
+                        else body(std::false_type{}, std::false_type{}, wlk);
+                    }
                 } else {
-                    if (contig) body(std::true_type{}, std::false_type{});
-                    else body(std::false_type{}, std::false_type{});
+                    if (contig) body(std::true_type{}, std::false_type{}, wlk);
+                    else body(std::false_type{}, std::false_type{}, wlk);
                 }
-            } else {
-                if (contig) body(std::true_type{}, std::false_type{});
-                else body(std::false_type{}, std::false_type{});
-            }
+            };
+            if (walk) go(std::true_type{});
+            else go(std::false_type{});
             t_first += n * G256;
             pa += n * G256;
             u0 += 256u * n;
