@@ -431,8 +431,8 @@ uint64_t orc_epoch_key(uint64_t seed, int64_t epoch) {
 
 /* keyed bijection of [0,n): balanced Feistel on 2h bits + cycle walking.  Halves of h <= 5
  * bits (n <= 1024): 8 rounds of f = top h bits of murmur3 fmix32(R ^ k_i), k_i = rk[i % 6] +
- * i * 0x9E3779B9.  Wider halves, 6 rounds: h <= 8 -> top h bits of the low 16 bits of
- * (R ^ k) * 0x9E37; h > 8 -> bits [24 - h, 24) of ((R ^ k) mod 2^24) * 0x9E3779. */
+ * i * 0x9E3779B9.  Wider halves, 6 rounds: h <= 10 -> top h bits of the low 16 bits of
+ * (R ^ k) * 0x9E37; h > 10 -> bits [24 - h, 24) of ((R ^ k) mod 2^24) * 0x9E3779. */
 static uint32_t orc_fmix32(uint32_t x) {
     x ^= x >> 16;
     x *= 0x85EBCA6BU;
@@ -457,7 +457,7 @@ uint32_t orc_feistel(uint32_t x, uint32_t n, const uint32_t rk[6]) {
             }
         } else {
             for (int i = 0; i < 6; i++) {
-                uint32_t f = h <= 8 ? ((((R ^ rk[i]) * 0x9E37u) & 0xFFFFu) >> (16 - h))
+                uint32_t f = h <= 10 ? ((((R ^ rk[i]) * 0x9E37u) & 0xFFFFu) >> (16 - h))
                                     : (((((R ^ rk[i]) & 0xFFFFFFu) * 0x9E3779u) >> (24 - h)) & mask);
                 uint32_t t = L ^ f;
                 L = R; R = t;

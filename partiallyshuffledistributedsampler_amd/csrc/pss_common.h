@@ -65,16 +65,18 @@ PSS_HD int ceil_log2_u64(uint64_t n) {  // smallest b with 2^b >= n (n >= 1)
 // halves of <= 5 bits take 8 rounds of a stronger mixer (feistel_fsmall, below).
 constexpr int kFeistelRounds = 6;
 
-// Round function for halves of h <= 8 bits (windows up to 65536): the top h bits of the low
-// 16 bits of (R ^ k) * 0x9E37 -- a 16-bit multiplicative hash, so two chains fit one 32-bit
-// register and run on packed 16-bit ops (feistel2_pk16).  Wider halves (h in 9..16): bits
+// Round function for halves of h <= 10 bits (domains up to 2^20, C5's pool): the top h bits of
+// the low 16 bits of (R ^ k) * 0x9E37 -- a 16-bit multiplicative hash, so two chains fit one
+// 32-bit register and run on packed 16-bit ops (feistel2_pk16; round 3 widened this from
+// h <= 8, halving the grouped replay's Feistel work at C5).  Wider halves (h in 11..16): bits
 // [24 - h, 24) of ((R ^ k) mod 2^24) * 0x9E3779 -- a 24 x 24-bit product (one full-rate
 // v_mul_u32_u24 on gfx950; a 32-bit v_mul_lo_u32 issues at quarter rate) and one v_bfe_u32.
-// The bits just below 2^24 are taken because there one input step moves the output by
-// 0x9E3779 / 2^(24-h), i.e. the golden-ratio fraction of the output range -- the top bits of
-// the 32-bit product would move by only ~2.5 at h = 10, and neighbouring positions then map
-// to neighbouring values (tests/test_schedule_quality.py measures both).
+// Both take the bits just below the product's width, where one input step moves the output by
+// the golden-ratio fraction of the output range -- the top bits of a 32-bit product would move
+// by only ~2.5 at h = 10, and neighbouring positions then map to neighbouring values
+// (tests/test_schedule_quality.py measures the neighbour law at every width).
 constexpr uint32_t kFeistelM16 = 0x9E37u, kFeistelM24 = 0x9E3779u;
+constexpr uint32_t kFeistelH16 = 10;   // widest half on the 16-bit round function
 
 PSS_HD uint32_t feistel_f24(uint32_t r, uint32_t k, uint32_t h) {
     return ((((r ^ k) & 0xFFFFFFu) * kFeistelM24) >> (24u - h)) & ((1u << h) - 1u);
@@ -109,7 +111,7 @@ PSS_HD uint32_t feistel_pass(uint32_t x, uint32_t h, const uint32_t *k) {
             L = R;
             R = t;
         }
-    } else if (h <= 8) {
+    } else if (h <= kFeistelH16) {
         const uint32_t sh = 16u - h;
 #pragma unroll
         for (int i = 0; i < kFeistelRounds; i++) {
@@ -128,8 +130,9 @@ PSS_HD uint32_t feistel_pass(uint32_t x, uint32_t h, const uint32_t *k) {
     return (L << h) | R;
 }
 
-// the 16-bit packed forms (feistel2_pk16 / feistel4_pk16) serve halves in (kFeistelSmallH, 8]
-PSS_HD bool feistel_packed_ok(uint32_t h) { return h > kFeistelSmallH && h <= 8; }
+// the 16-bit packed forms (feistel2_pk16 / feistel4_pk16: two chains per register, the halves
+// joined in 32 bits) serve every half on the 16-bit round function, (kFeistelSmallH, 10]
+PSS_HD bool feistel_packed_ok(uint32_t h) { return h > kFeistelSmallH && h <= kFeistelH16; }
 
 PSS_HD uint32_t feistel(uint32_t x, uint32_t n, uint32_t h, const uint32_t *k) {
     if (n <= 1) return 0;

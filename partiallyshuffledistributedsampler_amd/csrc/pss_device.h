@@ -113,7 +113,7 @@ __device__ __forceinline__ void slot4(uint32_t t, const SlotKey &sk, uint32_t P1
     }
 }
 
-// Two one-pass Feistel chains (feistel_pass with h <= 8) in one register, on packed 16-bit ops:
+// Two one-pass Feistel chains (feistel_pass with h <= kFeistelH16) in one register, on packed 16-bit ops:
 // chain 0 in the low half-word, chain 1 in the high one; kp[i] = (k[i] & 0xFFFF) * 0x10001
 // (both chains under the same round keys).  Same values as feistel_once on each chain.
 typedef unsigned short pss_u16x2 __attribute__((ext_vector_type(2)));

@@ -16,6 +16,8 @@
 // anywhere -- this is integer, memory/latency-bound work.
 #include <cstdlib>
 
+#include <type_traits>
+
 #include "pss_device.h"
 #include "pss_map.h"
 
@@ -261,7 +263,7 @@ __global__ __launch_bounds__(64) void k_v1_feistel(Geometry g, V1Plan vp, const 
     int64_t *o = out + (int64_t)rl * count - pos_lo;
     int32_t *ofp = ma.fpos + (int64_t)rl * count - pos_lo;
     int32_t *ooff = ma.off + (int64_t)rl * count - pos_lo;
-    auto put = [&](int64_t p, int64_t id) {
+    auto put = [&](int64_t p, int64_t id) __attribute__((always_inline)) {
         if constexpr (MAPPED) {
             int32_t f;
             int64_t of;
@@ -275,7 +277,7 @@ __global__ __launch_bounds__(64) void k_v1_feistel(Geometry g, V1Plan vp, const 
     const uint32_t *ktr = kt + (int64_t)rl * vp.nw * kRoundKeyWords;
     const int64_t B = vp.B;
     // one super-block through the general path (range edges, short or cycle-walking windows)
-    auto slow_sb = [&](int64_t sb) {
+    auto slow_sb = [&](int64_t sb) __attribute__((always_inline)) {
         const int64_t p0 = sb * 256;
 #pragma unroll
         for (int j = 0; j < 4; j++) {
@@ -295,6 +297,12 @@ __global__ __launch_bounds__(64) void k_v1_feistel(Geometry g, V1Plan vp, const 
             put(p, wrap_id(start + y, g.N));
         }
     };
+    // wave-uniform layout choices: the 16-B pair stores need the rank's output 16-B aligned
+    // (super-blocks start at multiples of 2 KB), the 32-bit ids N + ns < 2^32
+    const bool pair = __builtin_amdgcn_readfirstlane(
+        vp.pairs && (MAPPED ? (((uintptr_t)(ofp + sb0 * 256) | (uintptr_t)(ooff + sb0 * 256)) & 7u) == 0
+                            : ((uintptr_t)(o + sb0 * 256) & 15u) == 0));
+    const bool narrow = g.N + g.ns < (int64_t)UINT32_MAX;
     int64_t sb = sb0;
     while (sb < sb1) {
         if (!vp.fast_ok) { slow_sb(sb++); continue; }
@@ -315,51 +323,67 @@ __global__ __launch_bounds__(64) void k_v1_feistel(Geometry g, V1Plan vp, const 
             const uint32_t k = __builtin_amdgcn_readfirstlane(kw[i]);
             kp[i] = PACKED ? (k & 0xFFFFu) * 0x10001u : k;
         }
-        for (; sb < sb_w_end; sb++) {
-            const int64_t p0 = sb * 256;
-            if (p0 < pos_lo || p0 + 256 > pos_hi) { slow_sb(sb); continue; }
-            // whole super-block inside one full window of 4^hB elements: no cycle walking.
-            // Pair layout (16-B aligned output): lane l owns positions p0 + 2l, 2l + 1 and
-            // p0 + 128 + 2l, 2l + 1, written by two 16-byte stores (8-byte pairs when mapped)
-            // instead of four 8-byte ones.
-            const uint32_t x0 = (uint32_t)(p0 - wB);
-            const bool pair = vp.pairs && !MAPPED ? ((uintptr_t)(o + p0) & 15u) == 0
-                                                  : vp.pairs && (((uintptr_t)(ofp + p0) | (uintptr_t)(ooff + p0)) & 7u) == 0;
-            const uint32_t l2 = 2u * (uint32_t)lane;
-            uint32_t x[4];
-            if (pair) { x[0] = x0 + l2; x[1] = x0 + l2 + 1u; x[2] = x0 + 128u + l2; x[3] = x0 + 129u + l2; }
-            else { x[0] = x0 + lane; x[1] = x0 + 64u + lane; x[2] = x0 + 128u + lane; x[3] = x0 + 192u + lane; }
-            uint32_t y[4];
-            if constexpr (PACKED) {
-                feistel4_pk16(x, vp.hB, kp, y);
-            } else {
-#pragma unroll
-                for (int j = 0; j < 4; j++) y[j] = feistel_once(x[j], vp.hB, kp);
-            }
-            if (pair) {
-#pragma unroll
-                for (int h = 0; h < 2; h++) {
-                    const int64_t p = p0 + 128 * h + l2;
-                    const int64_t a = wrap_id(base + y[2 * h], g.N), b = wrap_id(base + y[2 * h + 1], g.N);
-                    if constexpr (MAPPED) {
-                        int32_t fa, fb;
-                        int64_t oa, ob;
-                        map_one_bucketed(ma.prefix, ma.F, ma.BT, ma.kb, ma.nb, a, fa, oa);
-                        map_one_bucketed(ma.prefix, ma.F, ma.BT, ma.kb, ma.nb, b, fb, ob);
-                        *(int2 *)(ofp + p) = make_int2(fa, fb);
-                        *(int2 *)(ooff + p) = make_int2((int32_t)oa, (int32_t)ob);
-                    } else {
-                        longlong2 v;
-                        v.x = a;
-                        v.y = b;
-                        *(longlong2 *)(o + p) = v;
-                    }
+        // the window's whole super-blocks; PAIR / NARROW are fixed per wave, so each combination
+        // is its own loop (no per-super-block branches, nothing hoisted across them)
+        auto run = [&](auto pair_c, auto narrow_c) __attribute__((always_inline)) {
+            constexpr bool PAIR = decltype(pair_c)::value, NARROW = decltype(narrow_c)::value;
+            // narrow: every id start + p < N + ns < 2^32 wraps with one 32-bit subtract and an
+            // unsigned min (id - N underflows exactly when id < N)
+            auto wrap = [&](uint32_t y) -> int64_t {
+                if constexpr (NARROW) {
+                    const uint32_t id = (uint32_t)base + y;
+                    return (int64_t)__builtin_elementwise_min(id, id - (uint32_t)g.N);
+                } else {
+                    return wrap_id(base + y, g.N);
                 }
-            } else {
+            };
+            const uint32_t l2 = 2u * (uint32_t)lane;
+            for (; sb < sb_w_end; sb++) {
+                const int64_t p0 = sb * 256;
+                if (p0 < pos_lo || p0 + 256 > pos_hi) { slow_sb(sb); continue; }
+                // whole super-block inside one full window of 4^hB elements: no cycle walking.
+                // Pair layout (16-B aligned output): lane l owns positions p0 + 2l, 2l + 1 and
+                // p0 + 128 + 2l, 2l + 1, written by two 16-byte stores (8-byte pairs when
+                // mapped) instead of four 8-byte ones.
+                const uint32_t x0 = (uint32_t)(p0 - wB);
+                uint32_t x[4], y[4];
+                if constexpr (PAIR) { x[0] = x0 + l2; x[1] = x0 + l2 + 1u; x[2] = x0 + 128u + l2; x[3] = x0 + 129u + l2; }
+                else { x[0] = x0 + lane; x[1] = x0 + 64u + lane; x[2] = x0 + 128u + lane; x[3] = x0 + 192u + lane; }
+                if constexpr (PACKED) {
+                    feistel4_pk16(x, vp.hB, kp, y);
+                } else {
 #pragma unroll
-                for (int j = 0; j < 4; j++) put(p0 + 64 * j + lane, wrap_id(base + y[j], g.N));
+                    for (int j = 0; j < 4; j++) y[j] = feistel_once(x[j], vp.hB, kp);
+                }
+                if constexpr (PAIR) {
+#pragma unroll
+                    for (int h = 0; h < 2; h++) {
+                        const int64_t p = p0 + 128 * h + l2;
+                        const int64_t ia = wrap(y[2 * h]), ib = wrap(y[2 * h + 1]);
+                        if constexpr (MAPPED) {
+                            int32_t fa, fb;
+                            int64_t oa, ob;
+                            map_one_bucketed(ma.prefix, ma.F, ma.BT, ma.kb, ma.nb, ia, fa, oa);
+                            map_one_bucketed(ma.prefix, ma.F, ma.BT, ma.kb, ma.nb, ib, fb, ob);
+                            *(int2 *)(ofp + p) = make_int2(fa, fb);
+                            *(int2 *)(ooff + p) = make_int2((int32_t)oa, (int32_t)ob);
+                        } else {
+                            longlong2 v;
+                            v.x = ia;
+                            v.y = ib;
+                            *(longlong2 *)(o + p) = v;
+                        }
+                    }
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 4; j++) put(p0 + 64 * j + lane, wrap(y[j]));
+                }
             }
-        }
+        };
+        if (pair && narrow) run(std::true_type{}, std::true_type{});
+        else if (pair) run(std::true_type{}, std::false_type{});
+        else if (narrow) run(std::false_type{}, std::true_type{});
+        else run(std::false_type{}, std::false_type{});
     }
 }
 

@@ -185,13 +185,27 @@ __device__ void mt_draws(uint32_t *mt, uint32_t nd, Bound bound, Emit emit) {
 // role in one pass.  Only the k2 bound depends on the lane's k2 index j, and only through values
 // within a few counts of a threshold: the block guesses j, derives the roles and the true j, and
 // repeats until no guess changes (almost always after two passes).
+// A map of the two roles is either a constant or "xor k": encoded as (const << 1) | k, where k =
+// its image of role 0 (so the identity is 0).  g after f: g if g is constant, else f with its k
+// flipped by g's -- two VALU ops and a select, where the table form took eight.
 __device__ __forceinline__ uint32_t role_compose(uint32_t g, uint32_t f) {   // g after f
-    return ((g >> (f & 1u)) & 1u) | (((g >> ((f >> 1) & 1u)) & 1u) << 1);
+    // g ^ (g constant ? 0 : f): the constant flag sign-extended into a mask (v_bfe_i32), then
+    // one v_bitop3 (table 0xB4 = S0 ^ (S1 & ~S2)); in plain C hipcc folds it back into a
+    // compare and a select
+    uint32_t cm, r;
+    asm("v_bfe_i32 %0, %1, 1, 1" : "=v"(cm) : "v"(g));
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xb4" : "=v"(r) : "v"(g), "v"(f), "v"(cm));
+    return r;
+}
+__device__ __forceinline__ uint32_t role_apply(uint32_t h, uint32_t s) {
+    return (h & 2u) ? (h & 1u) : (s ^ (h & 1u));
 }
 template <int CTRL, int ROWMASK>
 __device__ __forceinline__ uint32_t dpp_role(uint32_t x) {
-    // lanes without a source (or in masked rows) read the identity map (0b10)
-    return (uint32_t)__builtin_amdgcn_update_dpp(2, (int)x, CTRL, ROWMASK, 0xF, false);
+    // lanes without a source (or in masked rows) read the identity map (0): bound_ctrl zero-fill
+    // for the row shifts, the pre-set old value for the masked broadcast rows
+    if constexpr (ROWMASK == 0xF) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xF, 0xF, true);
+    else return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, ROWMASK, 0xF, false);
 }
 __device__ __forceinline__ uint32_t wave_role_scan(uint32_t x) {
     x = role_compose(x, dpp_role<0x111, 0xF>(x));
@@ -224,10 +238,11 @@ __device__ void mt_draws_pair(uint32_t *mt, uint32_t W, uint32_t P, Emit emit) {
             auto pass = [&](uint32_t n2, uint32_t rr) {
                 r2 = rr;
                 a2 = valid && rr < n2;
-                const uint32_t f = (a1 ? 1u : 0u) | ((a2 ? 0u : 1u) << 1);
+                // offered k1: accepted -> k2 next, else k1; offered k2: accepted -> k1, else k2
+                const uint32_t f = ((a1 != a2) ? 2u : 0u) | (a1 ? 1u : 0u);
                 Fx = wave_role_scan(f);
                 const uint32_t Fp = (uint32_t)__shfl((int)Fx, lane > 0 ? lane - 1 : 0);
-                role = lane ? (Fp >> st) & 1u : st;
+                role = lane ? role_apply(Fp, st) : st;
                 const uint64_t m2 = __ballot(valid && role == 1u && a2);
                 j = i2 + (uint32_t)__popcll(m2 & below);
             };
@@ -261,7 +276,7 @@ __device__ void mt_draws_pair(uint32_t *mt, uint32_t W, uint32_t P, Emit emit) {
             }
             i1 += (uint32_t)__popcll(m1);
             i2 += (uint32_t)__popcll(m2);
-            st = ((uint32_t)__shfl((int)Fx, 63) >> st) & 1u;
+            st = role_apply((uint32_t)__shfl((int)Fx, 63), st);
         }
     }
 }

@@ -605,7 +605,8 @@ __global__ __launch_bounds__(64) void k_v2_emit_x(Geometry g, V2Plan pl,
     const bool fast_tile = e_lo == 0 && e_hi == nvalid && B >= 256 && !walk_full;
     Pacer pace(nvalid);
     uint32_t tl0 = 0;
-    if (fast_tile && (B & 255u) == 0 && w_last > w_lo + 1 && feistel_packed_ok(hB)) {
+    if (fast_tile && (B & 255u) == 0 && w_last > w_lo + 1 && feistel_packed_ok(hB) && hB <= 8) {
+        // (hB <= 8: the keyed-carry form below joins the halves inside 16-bit lanes)
         // Fast phase: whole super-batches of windows w_lo .. w_last - 2 (full, no cycle walk),
         // as one counted loop per window with the window's round keys in SGPRs.  B % 256 == 0
         // and tlo % 256 == 0 put every super-batch inside one window.
@@ -643,7 +644,8 @@ __global__ __launch_bounds__(64) void k_v2_emit_x(Geometry g, V2Plan pl,
             };
             while (left) {
                 const uint32_t room = (B - p0) >> 8;
-                const uint32_t n = left < room ? left : room;
+                // wave-uniform trip count (readfirstlane: a scalar loop, not an exec-masked one)
+                const uint32_t n = __builtin_amdgcn_readfirstlane(left < room ? left : room);
                 uint32_t kw[kFeistelRounds];
 #pragma unroll
                 for (int i = 0; i < kFeistelRounds; i++)
@@ -656,41 +658,50 @@ __global__ __launch_bounds__(64) void k_v2_emit_x(Geometry g, V2Plan pl,
                 // ids of the window's values wB + y: one add when the window maps contiguously
                 const uint32_t wB = w0 * B;
                 const uint32_t id_first = to_slot(wB), id_last = to_slot(wB + B - 1);
-                const bool contiguous = id_last - id_first == B - 1 && ((wB < twoB) == (wB + B - 1 < twoB));
+                const bool contiguous = __builtin_amdgcn_readfirstlane(
+                    id_last - id_first == B - 1 && ((wB < twoB) == (wB + B - 1 < twoB)));
                 pace.step(tl0);
-                auto run = [&](auto contig) {
-                    for (uint32_t i = 0; i < n; i++) {
-                        const uint32_t pb = (t0 + tl0) >> 1;
-                        const uint32_t u0 = hash2(hx0 ^ pb), u2 = hash2(hx2 ^ pb);
-                        const uint32_t k[4] = {u0 >> sh, (u0 << 16) >> sh, u2 >> sh, (u2 << 16) >> sh};
-                        const uint32_t s = (p0 >> h) * 0x10001u;
-                        const uint32_t A10 = C0 ^ s, A11 = C1 ^ s;
-                        const uint32_t F10 = F(A10), F11 = F(A11);
-                        const uint32_t A20 = A00 ^ F10 ^ K02, A21 = A01 ^ F11 ^ K02;
-                        const uint32_t F20 = F(A20), F21 = F(A21);
-                        const uint32_t A30 = A10 ^ F20 ^ K13, A31 = A11 ^ F21 ^ K13;
-                        const uint32_t F30 = F(A30), F31 = F(A31);
-                        const uint32_t A40 = A20 ^ F30 ^ K24, A41 = A21 ^ F31 ^ K24;
-                        const uint32_t F40 = F(A40), F41 = F(A41);
-                        const uint32_t A50 = A30 ^ F40 ^ K35, A51 = A31 ^ F41 ^ K35;
-                        const uint32_t F50 = F(A50), F51 = F(A51);
-                        const uint32_t S0 = __builtin_bit_cast(uint32_t, __builtin_bit_cast(pss_u16x2, A50) << HS);
-                        const uint32_t S1 = __builtin_bit_cast(uint32_t, __builtin_bit_cast(pss_u16x2, A51) << HS);
-                        const uint32_t Y0 = S0 ^ (A40 ^ F50 ^ KY), Y1 = S1 ^ (A41 ^ F51 ^ KY);
-                        const uint32_t y[4] = {Y0 & 0xFFFFu, Y0 >> 16, Y1 & 0xFFFFu, Y1 >> 16};
-                        uint32_t ins[4], v[4];
+                // one 256-step super-batch at (tlx, px): its 4 slots and 4 inserted values
+                auto batch = [&](auto contig, uint32_t tlx, uint32_t px, uint32_t (&k)[4], uint32_t (&ins)[4]) {
+                    const uint32_t pb = (t0 + tlx) >> 1;
+                    const uint32_t u0 = hash2(hx0 ^ pb), u2 = hash2(hx2 ^ pb);
+                    k[0] = u0 >> sh; k[1] = (u0 << 16) >> sh; k[2] = u2 >> sh; k[3] = (u2 << 16) >> sh;
+                    const uint32_t s = (px >> h) * 0x10001u;
+                    const uint32_t A10 = C0 ^ s, A11 = C1 ^ s;
+                    const uint32_t F10 = F(A10), F11 = F(A11);
+                    const uint32_t A20 = A00 ^ F10 ^ K02, A21 = A01 ^ F11 ^ K02;
+                    const uint32_t F20 = F(A20), F21 = F(A21);
+                    const uint32_t A30 = A10 ^ F20 ^ K13, A31 = A11 ^ F21 ^ K13;
+                    const uint32_t F30 = F(A30), F31 = F(A31);
+                    const uint32_t A40 = A20 ^ F30 ^ K24, A41 = A21 ^ F31 ^ K24;
+                    const uint32_t F40 = F(A40), F41 = F(A41);
+                    const uint32_t A50 = A30 ^ F40 ^ K35, A51 = A31 ^ F41 ^ K35;
+                    const uint32_t F50 = F(A50), F51 = F(A51);
+                    const uint32_t S0 = __builtin_bit_cast(uint32_t, __builtin_bit_cast(pss_u16x2, A50) << HS);
+                    const uint32_t S1 = __builtin_bit_cast(uint32_t, __builtin_bit_cast(pss_u16x2, A51) << HS);
+                    const uint32_t Y0 = S0 ^ (A40 ^ F50 ^ KY), Y1 = S1 ^ (A41 ^ F51 ^ KY);
+                    const uint32_t y[4] = {Y0 & 0xFFFFu, Y0 >> 16, Y1 & 0xFFFFu, Y1 >> 16};
 #pragma unroll
-                        for (int j = 0; j < 4; j++) ins[j] = contig ? id_first + y[j] : to_slot(wB + y[j]);
+                    for (int j = 0; j < 4; j++) ins[j] = decltype(contig)::value ? id_first + y[j] : to_slot(wB + y[j]);
+                };
+                auto emit4 = [&](uint32_t tlx, const uint32_t (&v)[4]) {
+                    if constexpr (MAPPED) {
+#pragma unroll
+                        for (int j = 0; j < 4; j++) put_m(ebase + tlx + 64u * j + lane, (int64_t)v[j]);
+                    } else {
+                        int64_t *ob = o + tlx;
+#pragma unroll
+                        for (int j = 0; j < 4; j++) ob[64u * j + lane] = (int64_t)v[j];
+                    }
+                };
+                auto run = [&](auto contig) {
+                    uint32_t i = 0;
+                    for (; i < n; i++) {
+                        uint32_t k[4], ins[4], v[4];
+                        batch(contig, tl0, p0, k, ins);
 #pragma unroll
                         for (int j = 0; j < 4; j++) v[j] = atomicExch(&buf[k[j]], ins[j]);
-                        if constexpr (MAPPED) {
-#pragma unroll
-                            for (int j = 0; j < 4; j++) put_m(ebase + tl0 + 64u * j + lane, (int64_t)v[j]);
-                        } else {
-                            int64_t *ob = o + tl0;
-#pragma unroll
-                            for (int j = 0; j < 4; j++) ob[64u * j + lane] = (int64_t)v[j];
-                        }
+                        emit4(tl0, v);
                         tl0 += 256;
                         p0 += 256;
                     }

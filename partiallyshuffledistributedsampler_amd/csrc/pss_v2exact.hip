@@ -218,18 +218,42 @@ __global__ __launch_bounds__(kTile / OUT) void k_v2x_tile(V2xGeo x, uint32_t per
         // chain mode (pools of <= kTile entries): each step's answer in step order, and the
         // tile's survivors -- the frame positions still alive at its end, in order: survivor r
         // is r + #{i : D_i - i <= r} over the sorted deletions D (k_v2x_compose / _emit)
+        // both lists are staged in the free LDS buffer (32-bit words, skewed per 128 B) and
+        // stored coalesced
+        uint32_t *svl = (uint32_t *)vb;
         uint32_t *ans = V + (size_t)rl * x.ns + t0;
-        for (uint32_t u = threadIdx.x; u < n; u += NT) { const EW e = va[TE::ix(u)]; ans[TE::step(e)] = TE::val(e); }
+        for (uint32_t u = threadIdx.x; u < n; u += NT) {
+            const EW e = va[TE::ix(u)];
+            const uint32_t st = TE::step(e);
+            svl[st + (st >> 5)] = TE::val(e);
+        }
+        __syncthreads();
+        for (uint32_t u = threadIdx.x; u < n; u += NT) ans[u] = svl[u + (u >> 5)];
+        __syncthreads();
         const uint32_t Bm = alive_at(B0, insu, t0 + n);
         uint32_t *sv = SV + ((size_t)rl * x.tiles1 + job) * x.P;
-        for (uint32_t r = threadIdx.x; r < Bm; r += NT) {
-            uint32_t lo = 0, hi = n;   // #{i : D_i - i <= r}
+        // OUT consecutive survivors per thread: one search for the first, then a walk (E_i =
+        // D_i - i is non-decreasing)
+        static_assert(NT * OUT >= kTile, "a tile's survivors: OUT per thread");
+        const uint32_t r0 = threadIdx.x * (uint32_t)OUT;
+        if (r0 < Bm) {
+            uint32_t lo = 0, hi = n;   // #{i : D_i - i <= r0}
             while (lo < hi) {
                 const uint32_t mid = (lo + hi) >> 1;
-                if (TE::val(va[TE::ix(mid)]) - mid <= r) lo = mid + 1; else hi = mid;
+                if (TE::val(va[TE::ix(mid)]) - mid <= r0) lo = mid + 1; else hi = mid;
             }
-            sv[r] = r + lo;
+            uint32_t i = lo;
+            uint32_t e = i < n ? TE::val(va[TE::ix(i)]) - i : 0xFFFFFFFFu;
+            for (uint32_t r = r0; r < r0 + (uint32_t)OUT && r < Bm; r++) {
+                while (e <= r) {
+                    i++;
+                    e = i < n ? TE::val(va[TE::ix(i)]) - i : 0xFFFFFFFFu;
+                }
+                svl[r + (r >> 5)] = r + i;
+            }
         }
+        __syncthreads();
+        for (uint32_t r = threadIdx.x; r < Bm; r += NT) sv[r] = svl[r + (r >> 5)];
     } else if (pool1) {
         uint32_t *v = V + (size_t)rl * x.ns + t0, *o = O + (size_t)rl * x.ns + t0;
         for (uint32_t u = threadIdx.x; u < n; u += NT) { const EW e = va[TE::ix(u)]; v[u] = TE::val(e); o[u] = t0 + TE::step(e); }

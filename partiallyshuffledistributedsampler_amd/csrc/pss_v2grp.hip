@@ -194,7 +194,7 @@ __device__ __forceinline__ uint32_t xchg_unordered(uint32_t *buf, g_lds_vu8 *mar
 }
 
 // Four one-pass Feistel chains under wave-uniform round keys K (a full window of 4^h elements).
-// h <= 8: packed 16-bit pairs (feistel4_pk16).  h > 8: the keyed-carry form of feistel_pass --
+// h <= kFeistelH16: packed 16-bit pairs (feistel4_pk16).  Wider: the keyed-carry form of feistel_pass --
 // with A_i = R_i ^ K_i, A_{i+1} = A_{i-1} ^ F(A_i) ^ (K_{i-1} ^ K_{i+1}) (one 3-input xor per
 // round, F = one full-rate 24-bit multiply + bit-field extract); output L = A_5 ^ K_5, R = A_4 ^ F(A_5) ^ K_4.
 // Same values as feistel_once on each chain.
@@ -257,6 +257,32 @@ __device__ __forceinline__ void feistel4_rinv(uint32_t lb, uint32_t g64h, uint32
     }
 }
 
+// feistel4_rinv on the 16-bit round function (halves of up to kFeistelH16 bits), two chains per
+// register: chains 0, 1 in the half-words of the first, 2, 3 of the second.  Lp0 / Lp1 hold the
+// chains' left halves, A0p = A0 (both half-words), C1p = F16(A0) ^ K1 (both half-words); the
+// keys kp are the round keys' low half-words doubled.  Keyed carry as in feistel4_uniform, one
+// packed multiply, one packed shift and one 3-input xor per round and register.
+__device__ __forceinline__ void feistel4_rinv16(uint32_t Lp0, uint32_t Lp1, uint32_t A0p, uint32_t C1p,
+                                                uint32_t h, const uint32_t kp[6], uint32_t y[4]) {
+    const pss_u16x2 M = {(unsigned short)kFeistelM16, (unsigned short)kFeistelM16};
+    const pss_u16x2 SH = {(unsigned short)(16u - h), (unsigned short)(16u - h)};
+    auto F = [&](uint32_t a) -> uint32_t {
+        return __builtin_bit_cast(uint32_t, (__builtin_bit_cast(pss_u16x2, a) * M) >> SH);
+    };
+    const uint32_t K02 = kp[0] ^ kp[2], K13 = kp[1] ^ kp[3], K24 = kp[2] ^ kp[4], K35 = kp[3] ^ kp[5];
+    const uint32_t A10 = Lp0 ^ C1p, A11 = Lp1 ^ C1p;
+    const uint32_t A20 = xor3(A0p, F(A10), K02), A21 = xor3(A0p, F(A11), K02);
+    const uint32_t A30 = xor3(A10, F(A20), K13), A31 = xor3(A11, F(A21), K13);
+    const uint32_t A40 = xor3(A20, F(A30), K24), A41 = xor3(A21, F(A31), K24);
+    const uint32_t A50 = xor3(A30, F(A40), K35), A51 = xor3(A31, F(A41), K35);
+    const uint32_t L0 = A50 ^ kp[5], L1 = A51 ^ kp[5];
+    const uint32_t R0 = xor3(A40, F(A50), kp[4]), R1 = xor3(A41, F(A51), kp[4]);
+    y[0] = ((L0 & 0xFFFFu) << h) | (R0 & 0xFFFFu);
+    y[1] = ((L0 >> 16) << h) | (R0 >> 16);
+    y[2] = ((L1 & 0xFFFFu) << h) | (R1 & 0xFFFFu);
+    y[3] = ((L1 >> 16) << h) | (R1 >> 16);
+}
+
 // Table-wide Feistel pass of a wave: out[s] = f(feistel(off + s, n, h, K)) for s < cnt, four
 // chains per lane; the one-pass forms when n = 4^h (no cycle walking), else the walking one.
 template <class Put>
@@ -271,7 +297,7 @@ __device__ __forceinline__ void feistel_table(uint32_t off, uint32_t cnt, uint32
 #pragma unroll
             for (int j = 0; j < 4; j++) x[j] = off + s0 + 64u * j + (uint32_t)lane;
             if (feistel_packed_ok(h)) feistel4_uniform<true>(x, h, K, y);
-            else if (h > 8) feistel4_uniform<false>(x, h, K, y);
+            else if (h > kFeistelH16) feistel4_uniform<false>(x, h, K, y);
             else for (int j = 0; j < 4; j++) y[j] = feistel_once(x[j], h, K);
 #pragma unroll
             for (int j = 0; j < 4; j++) {
@@ -418,9 +444,11 @@ __global__ __launch_bounds__(64) void k_g_emit(Geometry g, GPlan pl, const RankD
             // ids of the window's values wa B + y: one add when the window maps contiguously
             const uint32_t wB = wa * B;
             const uint32_t id_first = ids.to_slot(wB), id_last = ids.to_slot(wB + wlen - 1u);
-            const bool contig = NARROW && id_last - id_first == wlen - 1u &&
-                                ((wB < pl.twoB) == (wB + wlen - 1u < pl.twoB));
-            const bool walk = wlen != (1u << (2u * pl.hB));
+            // wave-uniform branch conditions (readfirstlane: scalar branches, no exec-masked
+            // copies of the run loops)
+            const bool contig = __builtin_amdgcn_readfirstlane(
+                NARROW && id_last - id_first == wlen - 1u && ((wB < pl.twoB) == (wB + wlen - 1u < pl.twoB)));
+            const bool walk = __builtin_amdgcn_readfirstlane(wlen != (1u << (2u * pl.hB)));
             uint32_t tb = t_first + c_lane, xb = pa + c_lane;
             // the run's stores through a buffer descriptor on its wave-uniform base: 32-bit
             // per-lane offsets, no 64-bit address registers rewritten under in-flight stores
@@ -442,11 +470,22 @@ __global__ __launch_bounds__(64) void k_g_emit(Geometry g, GPlan pl, const RankD
             auto body = [&](auto ctg, auto rinv, auto wlk) {
                 constexpr bool RINV = decltype(rinv)::value;
                 uint32_t A0 = 0u, C1 = 0u, lb = 0u;
-                const uint32_t g64h = G64 >> pl.hB, g256h = G256 >> pl.hB;
+                uint32_t Lp0 = 0u, Lp1 = 0u, A0p = 0u, C1p = 0u, kp[kFeistelRounds];
+                const uint32_t g64h = G64 >> pl.hB, g256h = G256 >> pl.hB, g256p = g256h * 0x10001u;
                 if constexpr (RINV) {
                     A0 = (xb & hmask) ^ K[0];
-                    C1 = __builtin_amdgcn_ubfe((A0 & 0xFFFFFFu) * kFeistelM24, 24u - pl.hB, pl.hB) ^ K[1];
                     lb = xb >> pl.hB;
+                    if constexpr (PACKED) {   // the 16-bit round function, chains paired
+                        C1 = ((((A0 * kFeistelM16) & 0xFFFFu) >> (16u - pl.hB))) ^ K[1];
+                        A0p = (A0 & 0xFFFFu) * 0x10001u;
+                        C1p = (C1 & 0xFFFFu) * 0x10001u;
+                        Lp0 = lb | ((lb + g64h) << 16);
+                        Lp1 = (lb + 2u * g64h) | ((lb + 3u * g64h) << 16);
+#pragma unroll
+                        for (int i = 0; i < kFeistelRounds; i++) kp[i] = (K[i] & 0xFFFFu) * 0x10001u;
+                    } else {
+                        C1 = __builtin_amdgcn_ubfe((A0 & 0xFFFFFFu) * kFeistelM24, 24u - pl.hB, pl.hB) ^ K[1];
+                    }
                 }
                 for (uint32_t it = 0; it < n; it++) {
                     uint32_t k[4];
@@ -459,7 +498,11 @@ __global__ __launch_bounds__(64) void k_g_emit(Geometry g, GPlan pl, const RankD
                         for (int j = 0; j < 4; j++) k[j] = scale32(slot_hash(tb + j * G64, s0, s1), S);
                     }
                     uint32_t y[4], v[4];
-                    if constexpr (RINV) {
+                    if constexpr (RINV && PACKED) {
+                        feistel4_rinv16(Lp0, Lp1, A0p, C1p, pl.hB, kp, y);
+                        Lp0 += g256p;
+                        Lp1 += g256p;
+                    } else if constexpr (RINV) {
                         feistel4_rinv(lb, g64h, A0, C1, pl.hB, K, y);
                         lb += g256h;
                     } else {
@@ -497,14 +540,9 @@ __global__ __launch_bounds__(64) void k_g_emit(Geometry g, GPlan pl, const RankD
                 }
             };
             auto go = [&](auto wlk) {
-                if constexpr (!PACKED) {
-                    if ((G64 & hmask) == 0u) {   // run-invariant right halves (feistel4_rinv)
-                        if (contig) body(std::true_type{}, std::true_type{}, wlk);
-                        else body(std::false_type{}, std::true_type{}, wlk);
-                    } else {
-                        if (contig) body(std::true_type{}, std::false_type{}, wlk);
-                        else body(std::false_type{}, std::false_type{}, wlk);
-                    }
+                if ((G64 & hmask) == 0u) {   // run-invariant right halves (feistel4_rinv / _rinv16)
+                    if (contig) body(std::true_type{}, std::true_type{}, wlk);
+                    else body(std::false_type{}, std::true_type{}, wlk);
                 } else {
                     if (contig) body(std::true_type{}, std::false_type{}, wlk);
                     else body(std::false_type{}, std::false_type{}, wlk);
@@ -652,7 +690,7 @@ hipError_t launch_v2_grp(const Geometry &g, const RankDesc *ranks, int32_t rank_
     RankArgs ra;
     const int use_ra = rank_args ? 1 : 0;
     if (rank_args) ra = *rank_args;
-    const bool packed = pl.hB <= 8;   // grouped pools: B > 16384, so hB >= 8 (never the small-half rounds)
+    const bool packed = feistel_packed_ok(pl.hB);   // grouped pools: B > 16384, so hB >= 8
     const bool pow2 = pl.gr.r == 0 && (pl.gr.q & (pl.gr.q - 1u)) == 0u;   // every group 2^b slots
     const MapArgs ma = mapped ? *mapped : MapArgs{};
 #define PSS_GE(O, N, PK, P2) do { if (mapped) hipLaunchKernelGGL((k_g_emit<true, N, PK, P2, true>), grid, dim3(64), lds, s, g, pl, \

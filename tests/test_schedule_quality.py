@@ -171,10 +171,11 @@ def _chi2_expected_ok(counts, exp, z=5.0):
     return abs(x - k) < z * np.sqrt(2 * k), (x, k)
 
 
-@pytest.mark.parametrize("n", [4, 16, 64, 100, 256, 700, 1024, 4096, 65536, 1 << 20, 5000, 3 << 20])
+@pytest.mark.parametrize("n", [4, 16, 64, 100, 256, 700, 1024, 4096, 65536, 1 << 18, 300_000, 1 << 20, 5000,
+                               3 << 20])
 def test_feistel_insertion_order_is_uniform(n):
     """The keyed Feistel bijections (8 fmix32 rounds for halves <= 5 bits, the 16-bit round
-    function up to 8 bits, the 24-bit one above; cycle walking when n is not a power of 4): over
+    function up to 10 bits, the 24-bit one above; cycle walking when n is not a power of 4): over
     many keys the images of single positions are uniform over [0, n) (chi-square on up to 32
     bins) and the images of two neighbours follow the law of a uniform random permutation
     (chi-square on up to 8 x 8 bins against the distinct-pair law) -- the law of the

@@ -16,4 +16,6 @@ for i in 1 2; do
   PSS_LIB=$GRAFT_REPO_ROOT/build/head/libpss.so timeout -k 10 200 python tools/bench_configs.py c2x > $O/c2x_head_$i.json 2> $O/c2x_head_$i.err
   PSS_V2X_OUT=16 timeout -k 10 200 python tools/bench_configs.py c2x > $O/c2x_o16_$i.json 2> $O/c2x_o16_$i.err
 done
+timeout -k 10 200 python tools/bench_configs.py c5x > $O/c5x_new_1.json 2> $O/c5x_new_1.err
+PSS_LIB=$GRAFT_REPO_ROOT/build/head/libpss.so timeout -k 10 200 python tools/bench_configs.py c5x > $O/c5x_head_1.json 2> $O/c5x_head_1.err
 echo done
