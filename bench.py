@@ -439,7 +439,15 @@ def main():
     prof = eng.profile_read()
     eng.profile(False)
     eng.check()
-    # the box's achievable write-only rate for the same buffer: torch's fill_ of the output
+
+    # coverage of the last epoch across all GPUs: (count, digest) all-gather over RCCL
+    pairs = gather_pairs(out.numel(), as_u64(digest(out.view(-1))), device=cdev)
+    coverage = None
+    if rank == 0:
+        coverage = coverage_ok(pairs, ns, R, expected_digest_gpu(N, ns, R, dev))
+
+    # the box's achievable write-only rate for the same buffer (after the coverage digest: this
+    # overwrites the epoch's ids): torch's fill_ of the output
     # (a plain streaming-store kernel, no compute), HIP events on the same stream.  The HBM
     # roofline's `peak` stays the 8 TB/s spec; this says how much of it writes alone reach here.
     fill_ms = None
@@ -452,13 +460,6 @@ def main():
         ev1.record(stream)
         ev1.synchronize()
         fill_ms = ev0.elapsed_time(ev1) / 20
-
-    # coverage of the last epoch across all GPUs: (count, digest) all-gather over RCCL
-    pairs = gather_pairs(out.numel(), as_u64(digest(out.view(-1))), device=cdev)
-    coverage = None
-    if rank == 0:
-        coverage = coverage_ok(pairs, ns, R, expected_digest_gpu(N, ns, R, dev))
-
     ids_total = sum(c for c, _ in pairs) * args.steps
     value = ids_total / dt / 1e9
     kname = "v2_emit" if ver == 2 else "v1_window"

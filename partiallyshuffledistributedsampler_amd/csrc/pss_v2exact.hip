@@ -641,18 +641,21 @@ static hipError_t v2x_pass(const Geometry &g, const V2xGeo &x, const RankDesc *r
     });
     const uint32_t nru = (uint32_t)nr;
     const bool narrow = v2x_narrow(x.P, x.B);
-    static const int out16 = [] {   // A/B knob: 16 merge outputs per thread (256 threads) instead of 8
+    static const int outk = [] {   // A/B knob: merge outputs per thread (4, 8 = default, 16)
         const char *e = getenv("PSS_V2X_OUT");
-        return e && atoi(e) == 16;
+        const int v = e ? atoi(e) : kTileOut;
+        return v == 4 || v == 16 ? v : kTileOut;
     }();
     // one decode-tile launch of nb blocks from block b0 (the entry width and outputs per thread)
     auto tile = [&](uint64_t b0, uint32_t nb, const V2xGeo &xg, uint32_t per, const uint32_t *k1,
                     const uint32_t *k2, uint32_t *v, uint32_t *o, uint32_t *q2, uint32_t *sv, size_t lds) {
-        if (narrow && out16)
+        if (narrow && outk == 16)
             hipLaunchKernelGGL((k_v2x_tile<uint32_t, 16>), dim3(nb), dim3(kTile / 16), lds, s, xg, per, b0, k1, k2, v, o, q2, sv);
+        else if (narrow && outk == 4)
+            hipLaunchKernelGGL((k_v2x_tile<uint32_t, 4>), dim3(nb), dim3(kTile / 4), lds, s, xg, per, b0, k1, k2, v, o, q2, sv);
         else if (narrow)
             hipLaunchKernelGGL((k_v2x_tile<uint32_t, kTileOut>), dim3(nb), dim3(kTile / kTileOut), lds, s, xg, per, b0, k1, k2, v, o, q2, sv);
-        else if (out16)
+        else if (outk == 16)
             hipLaunchKernelGGL((k_v2x_tile<uint64_t, 16>), dim3(nb), dim3(kTile / 16), lds, s, xg, per, b0, k1, k2, v, o, q2, sv);
         else
             hipLaunchKernelGGL((k_v2x_tile<uint64_t, kTileOut>), dim3(nb), dim3(kTile / kTileOut), lds, s, xg, per, b0, k1, k2, v, o, q2, sv);
