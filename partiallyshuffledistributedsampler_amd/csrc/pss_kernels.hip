@@ -315,6 +315,9 @@ __global__ __launch_bounds__(64) void k_v1_feistel(Geometry g, V1Plan vp, const 
             for (; sb < sb_w_end; sb++) slow_sb(sb);
             continue;
         }
+        if (sb * 256 < pos_lo || sb * 256 + 256 > pos_hi) { slow_sb(sb++); continue; }   // range edges
+        // whole super-blocks of the range from here to the window's end
+        const int64_t sb_full_end = pos_hi / 256 < sb_w_end ? pos_hi / 256 : sb_w_end;
         const uint32_t *kw = ktr + (w - vp.w_lo) * kRoundKeyWords;
         const int64_t base = start + wB;
         uint32_t kp[kFeistelRounds];
@@ -338,9 +341,8 @@ __global__ __launch_bounds__(64) void k_v1_feistel(Geometry g, V1Plan vp, const 
                 }
             };
             const uint32_t l2 = 2u * (uint32_t)lane;
-            for (; sb < sb_w_end; sb++) {
+            for (; sb < sb_full_end; sb++) {
                 const int64_t p0 = sb * 256;
-                if (p0 < pos_lo || p0 + 256 > pos_hi) { slow_sb(sb); continue; }
                 // whole super-block inside one full window of 4^hB elements: no cycle walking.
                 // Pair layout (16-B aligned output): lane l owns positions p0 + 2l, 2l + 1 and
                 // p0 + 128 + 2l, 2l + 1, written by two 16-byte stores (8-byte pairs when
@@ -557,13 +559,19 @@ hipError_t launch_v1(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, 
         const long v = e ? atol(e) : 0;
         return (int64_t)(v > 0 && v <= 4096 ? v : 0);
     }();
-    const int64_t slots_per_rank = wpc * gcus_v1() / nr;
-    int64_t per = per_env ? per_env : cdiv(vp.nsb, slots_per_rank > 1 ? slots_per_rank : 1);
+    // the mapped form reads the bucket index and the prefix for every id (dependent global
+    // loads): it wants latency hiding, i.e. the full 32 waves per CU, where the plain form stores
+    // best at one round of 8 (C2 V1 mapped: 0.55-0.63 ms at 8 per CU, round 2's 0.32-0.36 at
+    // full occupancy)
+    const int64_t wpc_run = mapped ? 32 : wpc;
+    const int64_t slots_per_rank = wpc_run * gcus_v1() / nr;
+    // (mapped: round 2's shape, runs of 16 super-blocks at full occupancy, several rounds)
+    int64_t per = per_env ? per_env : mapped ? 16 : cdiv(vp.nsb, slots_per_rank > 1 ? slots_per_rank : 1);
     if (per < 1) per = 1;
     vp.per_wave = per;
     const int64_t waves = (int64_t)nr * cdiv(vp.nsb, per);
     const MapArgs ma = mapped ? *mapped : MapArgs{};
-    const size_t v1_lds = (size_t)(160 * 1024 / wpc - 64);   // caps the resident waves per CU
+    const size_t v1_lds = (size_t)(160 * 1024 / wpc_run - 64);   // caps the resident waves per CU
 #define PSS_V1(PK, MP) hipLaunchKernelGGL((k_v1_feistel<PK, MP>), dim3((uint32_t)waves), dim3(64), v1_lds, s, g, vp, \
                                           ranks, rank_lo, (const uint32_t *)key_ws, pos_lo, count, out, ma)
     if (feistel_packed_ok(vp.hB) && mapped) PSS_V1(true, true);

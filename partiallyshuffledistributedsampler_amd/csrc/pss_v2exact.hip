@@ -258,8 +258,16 @@ __global__ __launch_bounds__(kTile / OUT) void k_v2x_tile(V2xGeo x, uint32_t per
         uint32_t *v = V + (size_t)rl * x.ns + t0, *o = O + (size_t)rl * x.ns + t0;
         for (uint32_t u = threadIdx.x; u < n; u += NT) { const EW e = va[TE::ix(u)]; v[u] = TE::val(e); o[u] = t0 + TE::step(e); }
     } else {
+        // the window's pool2 ranks in step order, staged in the free LDS buffer, stored coalesced
         uint32_t *q = Q2 + (size_t)rl * x.T2 + (size_t)(job - x.tiles1) * x.B;
-        for (uint32_t u = threadIdx.x; u < n; u += NT) { const EW e = va[TE::ix(u)]; q[TE::step(e)] = TE::val(e); }
+        uint32_t *stg = (uint32_t *)vb;
+        for (uint32_t u = threadIdx.x; u < n; u += NT) {
+            const EW e = va[TE::ix(u)];
+            const uint32_t st = TE::step(e);
+            stg[st + (st >> 5)] = TE::val(e);
+        }
+        __syncthreads();
+        for (uint32_t u = threadIdx.x; u < n; u += NT) q[u] = stg[u + (u >> 5)];
     }
 }
 
