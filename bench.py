@@ -389,7 +389,11 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     cdev = torch.device("cpu") if rehearse else dev     # device of the collective tensors
-    if world > 1:
+    # PSS_BENCH_DIST=1: the process group and its collectives even at one process (an RCCL
+    # group of one GPU: the N-GPU code path -- barriers, the max-over-ranks time, the device
+    # all-gather of (count, digest) -- executed on a one-GPU box, tests/test_distributed.py)
+    distributed = world > 1 or os.environ.get("PSS_BENCH_DIST") == "1"
+    if distributed:
         if rehearse:
             dist.init_process_group("gloo")
         else:
@@ -419,7 +423,7 @@ def main():
         step(e)
     torch.cuda.synchronize(dev)
     eng.check()
-    if world > 1:
+    if distributed:
         dist.barrier()
     # live timing of the dominant kernel: two HIP events around the generation kernel on its
     # stream, on every 4th step of the timed region (events around every launch cost ~4 % of
@@ -431,7 +435,7 @@ def main():
         step(args.warmup + i)
     torch.cuda.synchronize(dev)
     dt = time.perf_counter() - t0
-    if world > 1:
+    if distributed:
         dist.barrier()
         t = torch.tensor([dt], dtype=torch.float64, device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -513,6 +517,7 @@ def main():
         "kernels_ms_per_launch": {k: v[0] / max(1, v[1]) for k, v in prof.items()},
         "timed_launches": k_n,
         "coverage_ok": coverage,
+        "collective": (dist.get_backend() if distributed else None),
     }
     eng.close()
     del out
@@ -527,7 +532,7 @@ def main():
         line["exact_order"] = exact_order_figures(local)
     if rank == 0:
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if distributed:
         dist.destroy_process_group()
 
 

@@ -428,8 +428,9 @@ __global__ __launch_bounds__(kChainNT) void k_v2x_link(V2xGeo x, V2xChain ch) {
 }
 
 // Software-pipelined over the chunk's tiles: a thread's answers and survivor entries of tile
-// j + 1 are loaded (kChainPer of each) while tile j's ids are computed and stored, so each tile
-// costs one LDS round trip and the pool2 gathers, not three dependent global round trips.
+// j + 1 are loaded (kChainPer of each) while tile j's ids are computed and stored, and tile
+// j + 1's pool2 gathers are issued as soon as its alive set is in LDS, one iteration ahead of
+// its stores (they land while the next alive set is built).
 constexpr int kChainPer = kTile / kChainNT;
 static_assert(kChainPer * kChainNT == kTile, "a tile's steps and survivors: kChainPer per thread");
 
@@ -464,39 +465,60 @@ __global__ __launch_bounds__(kChainNT) void k_v2x_emit(Geometry g, V2xGeo x, V2x
         }
     };
     uint32_t q[kChainPer], sr[kChainPer], qn[kChainPer], srn[kChainPer];
-    load(j0, q, sr);
-    __syncthreads();
-    for (uint32_t j = j0; j < j1; j++) {
+    // tile j's insertion numbers (av) and, for elements moved over from pool2, their pool2 ranks
+    // (g2), gathered one iteration ahead of the stores that need them
+    uint32_t av[kChainPer], g2[kChainPer];
+    auto prep = [&](uint32_t j, const uint32_t (&qq)[kChainPer]) {
         const uint32_t t0 = j * (uint32_t)kTile, n = x.ns - t0 < (uint32_t)kTile ? x.ns - t0 : (uint32_t)kTile;
-        if ((int64_t)t0 >= pos_hi) break;
-        if (j + 1 < j1) load(j + 1, qn, srn);
-        const uint32_t Ba = alive_at(x.P, x.T, t0), Bm = alive_at(x.P, x.T, t0 + n);
+        const uint32_t Ba = alive_at(x.P, x.T, t0);
 #pragma unroll
         for (int k = 0; k < kChainPer; k++) {
             const uint32_t u = threadIdx.x + (uint32_t)k * kChainNT;
-            const int64_t t = (int64_t)t0 + u;
-            if (u >= n || t < pos_lo || t >= pos_hi) continue;
-            const uint32_t a = q[k] < Ba ? A[q[k]] : x.P + t0 + (q[k] - Ba);
-            int64_t id;
-            if (a < x.P) {
-                id = rd.old_start + a;              // initial pool1 (V2:135-136)
-            } else {                                // moved over from pool2 at step a - P
-                const uint32_t uu = a - x.P, s = uu / x.B;
-                const int64_t wbase = s == 0 ? rd.old_start + x.B : rd.new_start + (int64_t)(s + 1) * x.B;
-                id = wbase + q2[uu];
-            }
-            o[t] = wrap_id(id, g.N);
+            const uint32_t a = u < n ? (qq[k] < Ba ? A[qq[k]] : x.P + t0 + (qq[k] - Ba)) : 0u;
+            av[k] = a;
+            g2[k] = (u < n && a >= x.P) ? q2[a - x.P] : 0u;
         }
-        if (j + 1 < j1) {
+    };
+    load(j0, q, sr);
+    __syncthreads();
+    prep(j0, q);
+    for (uint32_t j = j0; j < j1; j++) {
+        const uint32_t t0 = j * (uint32_t)kTile, n = x.ns - t0 < (uint32_t)kTile ? x.ns - t0 : (uint32_t)kTile;
+        if ((int64_t)t0 >= pos_hi) break;
+        const bool more = j + 1 < j1;
+        if (more) load(j + 1, qn, srn);
+        const uint32_t Ba = alive_at(x.P, x.T, t0), Bm = alive_at(x.P, x.T, t0 + n);
+        if (more) {   // the elements alive at tile j + 1's start (A is tile j's)
 #pragma unroll
             for (int k = 0; k < kChainPer; k++) {
                 const uint32_t r = threadIdx.x + (uint32_t)k * kChainNT;
                 if (r < Bm) An[r] = sr[k] < Ba ? A[sr[k]] : x.P + t0 + (sr[k] - Ba);
             }
+        }
+        // tile j's ids: insertion number a < P is initial pool1 (V2:135-136), else the element
+        // step a - P moved over from pool2
+#pragma unroll
+        for (int k = 0; k < kChainPer; k++) {
+            const uint32_t u = threadIdx.x + (uint32_t)k * kChainNT;
+            const int64_t t = (int64_t)t0 + u;
+            if (u >= n || t < pos_lo || t >= pos_hi) continue;
+            const uint32_t a = av[k];
+            int64_t id;
+            if (a < x.P) {
+                id = rd.old_start + a;
+            } else {
+                const uint32_t s = (a - x.P) / x.B;
+                const int64_t wbase = s == 0 ? rd.old_start + x.B : rd.new_start + (int64_t)(s + 1) * x.B;
+                id = wbase + g2[k];
+            }
+            o[t] = wrap_id(id, g.N);
+        }
+        if (more) {
             __syncthreads();
             uint32_t *tp = A; A = An; An = tp;
 #pragma unroll
             for (int k = 0; k < kChainPer; k++) { q[k] = qn[k]; sr[k] = srn[k]; }
+            prep(j + 1, q);
         }
     }
 }

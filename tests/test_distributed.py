@@ -90,3 +90,29 @@ def test_shard_is_a_partition():
             assert blocks[0][0] == 0 and blocks[-1][1] == R
             assert all(blocks[i][1] == blocks[i + 1][0] for i in range(world - 1))
             assert max(b - a for a, b in blocks) - min(b - a for a, b in blocks) <= 1
+
+
+@pytest.mark.gpu
+def test_rccl_group_of_one_gpu_runs_the_multi_gpu_bench_path():
+    """bench.py's N-GPU path under an RCCL ("nccl") process group, on the one GPU a test box has:
+    torch.distributed.run with one process and PSS_BENCH_DIST=1, so the barriers, the
+    max-over-ranks all-reduce and the device-tensor all-gather of (count, digest) run through
+    RCCL on hardware, and rank 0's coverage check passes on what the collective returned."""
+    import json
+    import socket
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    env = dict(os.environ, PSS_BENCH_DIST="1", MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "1",
+           "--steps", "3", "--warmup", "1", "--no-latency", "--no-exact", "--no-cpu-baseline"]
+    res = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=240)
+    assert res.returncode == 0, res.stderr[-2000:]
+    line = json.loads(res.stdout.strip().splitlines()[-1])
+    assert line["collective"] == "nccl"
+    assert line["coverage_ok"] is True
+    assert line["n_gpus"] == 1
