@@ -135,6 +135,59 @@ template <typename EW> struct TileEntry {
     static __device__ __forceinline__ uint32_t ix(uint32_t p) { return p + (p >> SKEW); }
     static constexpr uint32_t kSlots = kTile + (kTile >> SKEW);
 };
+// The first three merge levels (blocks of 1, 2, 4 -> 8) of a thread's 8 consecutive entries in
+// registers, 32-bit entries: the same fused map-and-merge as the LDS levels, as a sorting network.
+// A left entry i gets key (E_i << 4) | i with E_i = D_i - i, a right entry j key (q_j << 4) | 8 | j:
+// left-before-right exactly when E_i <= q_j (left first on ties), lefts keep their order on equal E
+// (the index below), rights are distinct.  Batcher's odd-even merge of the two sorted halves, then a
+// right entry landing at k gains k - j (the left entries now before it).
+__device__ __forceinline__ void tile_ce(uint32_t &ka, uint32_t &kb, uint32_t &ea, uint32_t &eb) {
+    const bool sw = ka > kb;
+    const uint32_t k0 = sw ? kb : ka, k1 = sw ? ka : kb, e0 = sw ? eb : ea, e1 = sw ? ea : eb;
+    ka = k0; kb = k1; ea = e0; eb = e1;
+}
+__device__ __forceinline__ void tile_merge8_regs(uint32_t (&e)[8]) {
+    using TE = TileEntry<uint32_t>;
+#pragma unroll
+    for (int p = 0; p < 4; p++) {   // blocks of 1
+        const uint32_t l = e[2 * p], r = e[2 * p + 1];
+        const bool take = TE::val(l) <= TE::val(r);
+        e[2 * p] = take ? l : r;
+        e[2 * p + 1] = take ? TE::add(r, 1u) : l;
+    }
+    auto keys = [&](int a, int w, uint32_t *k) {
+        for (int i = 0; i < w; i++) k[i] = ((TE::val(e[a + i]) - (uint32_t)i) << 4) | (uint32_t)i;
+        for (int j = 0; j < w; j++) k[w + j] = (TE::val(e[a + w + j]) << 4) | 8u | (uint32_t)j;
+    };
+    auto fix = [&](int a, int w, const uint32_t *k) {
+        for (int q = 0; q < 2 * w; q++) {
+            const uint32_t d = (k[q] & 8u) ? (uint32_t)q - (k[q] & 7u) : 0u;
+            e[a + q] = TE::add(e[a + q], d);
+        }
+    };
+#pragma unroll
+    for (int a = 0; a < 8; a += 4) {   // blocks of 2
+        uint32_t k[4];
+        keys(a, 2, k);
+        tile_ce(k[0], k[2], e[a], e[a + 2]);
+        tile_ce(k[1], k[3], e[a + 1], e[a + 3]);
+        tile_ce(k[1], k[2], e[a + 1], e[a + 2]);
+        fix(a, 2, k);
+    }
+    {   // blocks of 4
+        uint32_t k[8];
+        keys(0, 4, k);
+#pragma unroll
+        for (int i = 0; i < 4; i++) tile_ce(k[i], k[i + 4], e[i], e[i + 4]);
+        tile_ce(k[2], k[4], e[2], e[4]);
+        tile_ce(k[3], k[5], e[3], e[5]);
+        tile_ce(k[1], k[2], e[1], e[2]);
+        tile_ce(k[3], k[4], e[3], e[4]);
+        tile_ce(k[5], k[6], e[5], e[6]);
+        fix(0, 4, k);
+    }
+}
+
 // largest frame position a launch can produce: pool1 tiles P + kTile, windows B
 static bool v2x_narrow(uint32_t P, uint32_t B) {
     return (uint64_t)P + kTile <= ((uint64_t)1 << (32 - kStepBits)) && (uint64_t)B <= ((uint64_t)1 << (32 - kStepBits));
@@ -167,7 +220,21 @@ __global__ __launch_bounds__(kTile / OUT) void k_v2x_tile(V2xGeo x, uint32_t per
         B0 = n; insu = 0;
         src = K2 + (size_t)rl * x.T2 + (size_t)s * x.B;
     }
-    for (uint32_t u = threadIdx.x; u < n; u += NT) va[TE::ix(u)] = TE::make(src[u], u);
+    uint32_t w0 = 1;
+    if constexpr (sizeof(EW) == 4 && OUT == 8) {
+        if (n == (uint32_t)kTile) {   // full tile: a thread's 8 entries merged in registers first
+            const uint32_t b = threadIdx.x * 8u;
+            uint32_t e[8];
+#pragma unroll
+            for (int i = 0; i < 8; i++) e[i] = (uint32_t)TE::make(src[b + i], b + (uint32_t)i);
+            tile_merge8_regs(e);
+#pragma unroll
+            for (int i = 0; i < 8; i++) va[TE::ix(b + (uint32_t)i)] = e[i];
+            w0 = 8;
+        }
+    }
+    if (w0 == 1)
+        for (uint32_t u = threadIdx.x; u < n; u += NT) va[TE::ix(u)] = TE::make(src[u], u);
     __syncthreads();
     // merge levels: sibling blocks [a, m), [m, e) -> [a, e), each sorted by its frame position.
     // Left entries (deletions D, frame a) keep their values; a right entry q (frame m) is the
@@ -177,7 +244,7 @@ __global__ __launch_bounds__(kTile / OUT) void k_v2x_tile(V2xGeo x, uint32_t per
     // entry taken after i left ones becomes q + i.  (q beyond the left block's survivors are the
     // right block's own insertions: every E_i <= q there, and q + nL is their frame-a position.)
     const uint32_t p0 = threadIdx.x * (uint32_t)OUT;
-    for (uint32_t w = 1; w < n; w <<= 1) {
+    for (uint32_t w = w0; w < n; w <<= 1) {
         // a thread's outputs may span several pairs while 2w < OUT: one walk per pair
         for (uint32_t q = p0; q < p0 + (uint32_t)OUT && q < n;) {
             const uint32_t a = (q / (2 * w)) * (2 * w), m = a + w;
