@@ -217,11 +217,69 @@ __device__ __forceinline__ uint32_t wave_role_scan(uint32_t x) {
     return x;
 }
 
+// One 64-word block of a pool2 window's stream, exactly (the wave's lanes = the block's words):
+// the role scan settles it in one pass where every k2 verdict is fixed over the block's possible
+// k2 indices [i2, i2 + 32], else the lanes' k2 indices are guessed and re-derived to the fixed
+// point.  Emits the block's draws and advances (st, i1, i2).
+template <class Emit>
+__device__ __forceinline__ void pair_block(uint32_t word, bool valid, uint32_t W, uint32_t P, uint32_t kb1,
+                                           uint32_t &st, uint32_t &i1, uint32_t &i2, Emit &emit) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t below = lanemask_lt();
+    const uint32_t r1 = word >> (32u - kb1);
+    const bool a1 = valid && r1 < P;
+    uint32_t j = 0, r2 = 0, role = 0, Fx = 0;
+    bool a2 = false;
+    // one scan of the role maps for the k2 verdicts a2 (at k2 indices jg); returns the lanes'
+    // true k2 indices in j
+    auto pass = [&](uint32_t n2, uint32_t rr) {
+        r2 = rr;
+        a2 = valid && rr < n2;
+        // offered k1: accepted -> k2 next, else k1; offered k2: accepted -> k1, else k2
+        const uint32_t f = ((a1 != a2) ? 2u : 0u) | (a1 ? 1u : 0u);
+        Fx = wave_role_scan(f);
+        const uint32_t Fp = (uint32_t)__shfl((int)Fx, lane > 0 ? lane - 1 : 0);
+        role = lane ? role_apply(Fp, st) : st;
+        const uint64_t m2 = __ballot(valid && role == 1u && a2);
+        j = i2 + (uint32_t)__popcll(m2 & below);
+    };
+    // a block holds at most 32 k2 draws, so each lane's k2 index lies in [i2, i2 + 32]: where
+    // every lane's k2 verdict is the same over that whole range (all but ~1 % of lanes), one
+    // scan settles the block; otherwise iterate guess -> true index
+    const uint32_t nhi = i2 < W ? W - i2 : 1u, nlo = i2 + 32u < W ? W - (i2 + 32u) : 1u;
+    const uint32_t kbh = 32u - (uint32_t)__builtin_clz(nhi);
+    const uint32_t rh = word >> (32u - kbh);
+    const bool sure = kbh == 32u - (uint32_t)__builtin_clz(nlo) && (rh < nlo || rh >= nhi);
+    if (__ballot(valid && !sure) == 0) {
+        pass(nlo, rh);
+    } else {
+        uint32_t jg = i2 + (uint32_t)lane / 3u;
+        for (;;) {
+            const uint32_t n2 = jg < W ? W - jg : 1u;
+            pass(n2, word >> (32u - (32u - (uint32_t)__builtin_clz(n2))));
+            if (__ballot(valid && j != jg) == 0) break;
+            jg = j;
+        }
+    }
+    const bool acc = valid && (role ? a2 : a1);
+    const uint64_t m1 = __ballot(acc && role == 0u), m2 = __ballot(acc && role == 1u);
+    if (acc) {
+        if (role == 0u) {
+            const uint32_t i = i1 + (uint32_t)__popcll(m1 & below);
+            if (i < W) emit(false, i, r1);
+        } else if (j < W) {
+            emit(true, j, r2);
+        }
+    }
+    i1 += (uint32_t)__popcll(m1);
+    i2 += (uint32_t)__popcll(m2);
+    st = role_apply((uint32_t)__shfl((int)Fx, 63), st);
+}
+
 template <class Emit>
 __device__ void mt_draws_pair(uint32_t *mt, uint32_t W, uint32_t P, Emit emit) {
     const int lane = threadIdx.x & 63;
     const uint32_t kb1 = 32u - (uint32_t)__builtin_clz(P);
-    const uint64_t below = lanemask_lt();
     uint32_t i1 = 0, i2 = 0, st = 0;   // k1 / k2 draws made, role offered to the next word
     while (i2 < W) {
         mt_twist(mt);
@@ -229,55 +287,158 @@ __device__ void mt_draws_pair(uint32_t *mt, uint32_t W, uint32_t P, Emit emit) {
             const int nval = kMtN - q0 < 64 ? kMtN - q0 : 64;
             const bool valid = lane < nval;
             const uint32_t word = valid ? mt_temper(mt[q0 + lane]) : 0u;
-            const uint32_t r1 = word >> (32u - kb1);
-            const bool a1 = valid && r1 < P;
-            uint32_t j = 0, r2 = 0, role = 0, Fx = 0;
-            bool a2 = false;
-            // one scan of the role maps for the k2 verdicts a2 (at k2 indices jg); returns the
-            // lanes' true k2 indices in j
-            auto pass = [&](uint32_t n2, uint32_t rr) {
-                r2 = rr;
-                a2 = valid && rr < n2;
-                // offered k1: accepted -> k2 next, else k1; offered k2: accepted -> k1, else k2
-                const uint32_t f = ((a1 != a2) ? 2u : 0u) | (a1 ? 1u : 0u);
-                Fx = wave_role_scan(f);
-                const uint32_t Fp = (uint32_t)__shfl((int)Fx, lane > 0 ? lane - 1 : 0);
-                role = lane ? role_apply(Fp, st) : st;
-                const uint64_t m2 = __ballot(valid && role == 1u && a2);
-                j = i2 + (uint32_t)__popcll(m2 & below);
-            };
-            // a block holds at most 32 k2 draws, so each lane's k2 index lies in [i2, i2 + 32]:
-            // where every lane's k2 verdict is the same over that whole range (all but ~1 % of
-            // lanes), one scan settles the block; otherwise iterate guess -> true index
-            const uint32_t nhi = i2 < W ? W - i2 : 1u, nlo = i2 + 32u < W ? W - (i2 + 32u) : 1u;
+            pair_block(word, valid, W, P, kb1, st, i1, i2, emit);
+        }
+    }
+}
+
+// The same draws on a workgroup of kMtWgThreads (4 waves) per stream, for long windows (C5's
+// pool2 windows are 2^20 steps and there are only ~11 per rank: one wave per stream left most of
+// the chip idle).  Per twist:
+//   twist   the 624 new words in three barrier-separated phases of <= 227 words (new[k] needs
+//           new[k - 227] from k = 227 on), double-buffered, tempered into tw[]
+//   blocks  the ten 64-word blocks, wave w takes blocks w, w + 4, w + 8: where every k2 verdict
+//           of a block is fixed over all k2 indices the block can see in this twist ([i2, i2 +
+//           32 (b + 1)] for block b), its transfer -- the composed role map and the k1 / k2
+//           acceptances for either start role -- comes from one role scan without knowing
+//           where the block starts
+//   combine wave 0 chains the transfers from the twist's start state up to the first block
+//           that was not settled, then runs that block and all after it exactly (pair_block)
+//   emit    each wave emits its settled blocks from their now known start states
+constexpr int kMtWgThreads = 256;
+constexpr int kMtBlocks = (kMtN + 63) / 64;   // 10: nine of 64 words, one of 48
+
+struct MtWgShared {
+    uint32_t mt[2][kMtN];           // state, double-buffered across the twist
+    uint32_t tw[kMtN];              // tempered words of the current twist
+    uint32_t sum[kMtBlocks][6];     // settled?, role map, c1(st = 0), c1(st = 1), c2(0), c2(1)
+    uint32_t start[kMtBlocks][3];   // (st, i1, i2) at each block's start
+    uint32_t state[4];              // st, i1, i2, first unsettled block
+};
+
+template <class Emit>
+__device__ void mt_draws_pair_wg(MtWgShared &sh, int cur, uint32_t W, uint32_t P, Emit emit) {
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const uint32_t kb1 = 32u - (uint32_t)__builtin_clz(P);
+    const uint64_t below = lanemask_lt();
+    if (tid == 0) { sh.state[0] = 0u; sh.state[1] = 0u; sh.state[2] = 0u; }
+    __syncthreads();
+    for (;;) {
+        if (sh.state[2] >= W) break;   // (uniform: read after a barrier)
+        // ---- twist: old = mt[cur] -> new = mt[cur ^ 1], tempered into tw
+        const uint32_t *o = sh.mt[cur];
+        uint32_t *nw = sh.mt[cur ^ 1];
+        if (tid < kMtN - kMtM) {                                   // k in [0, 227)
+            const uint32_t v = mt_twist_word(o[tid], o[tid + 1], o[tid + kMtM]);
+            nw[tid] = v;
+            sh.tw[tid] = mt_temper(v);
+        }
+        __syncthreads();
+        if (tid < kMtN - kMtM) {                                   // k in [227, 454)
+            const int k = tid + (kMtN - kMtM);
+            const uint32_t v = mt_twist_word(o[k], o[k + 1], nw[k - (kMtN - kMtM)]);
+            nw[k] = v;
+            sh.tw[k] = mt_temper(v);
+        }
+        __syncthreads();
+        if (tid < kMtN - 2 * (kMtN - kMtM)) {                      // k in [454, 624)
+            const int k = tid + 2 * (kMtN - kMtM);
+            const uint32_t v = k < kMtN - 1 ? mt_twist_word(o[k], o[k + 1], nw[k - (kMtN - kMtM)])
+                                            : mt_twist_word(o[kMtN - 1], nw[0], nw[kMtM - 1]);
+            nw[k] = v;
+            sh.tw[k] = mt_temper(v);
+        }
+        cur ^= 1;
+        __syncthreads();
+        // ---- blocks: transfers of the settled ones
+        const uint32_t i2_0 = sh.state[2];
+        uint32_t Fkeep[3] = {0u, 0u, 0u};
+        bool a1k[3] = {false, false, false}, a2k[3] = {false, false, false};
+#pragma unroll
+        for (int s = 0; s < 3; s++) {
+            const int b = wv + 4 * s;
+            if (b >= kMtBlocks) break;
+            const int q0 = 64 * b, nval = kMtN - q0 < 64 ? kMtN - q0 : 64;
+            const bool valid = lane < nval;
+            const uint32_t word = valid ? sh.tw[q0 + lane] : 0u;
+            const bool a1 = valid && (word >> (32u - kb1)) < P;
+            const uint32_t jhi = i2_0 + 32u * (uint32_t)(b + 1);
+            const uint32_t nhi = i2_0 < W ? W - i2_0 : 1u, nlo = jhi < W ? W - jhi : 1u;
             const uint32_t kbh = 32u - (uint32_t)__builtin_clz(nhi);
             const uint32_t rh = word >> (32u - kbh);
             const bool sure = kbh == 32u - (uint32_t)__builtin_clz(nlo) && (rh < nlo || rh >= nhi);
-            if (__ballot(valid && !sure) == 0) {
-                pass(nlo, rh);
-            } else {
-                uint32_t jg = i2 + (uint32_t)lane / 3u;
-                for (;;) {
-                    const uint32_t n2 = jg < W ? W - jg : 1u;
-                    pass(n2, word >> (32u - (32u - (uint32_t)__builtin_clz(n2))));
-                    if (__ballot(valid && j != jg) == 0) break;
-                    jg = j;
+            const bool settled = __ballot(valid && !sure) == 0;
+            if (settled) {
+                const bool a2 = valid && rh < nlo;
+                const uint32_t Fx = wave_role_scan(((a1 != a2) ? 2u : 0u) | (a1 ? 1u : 0u));
+                const uint32_t Fp = (uint32_t)__shfl((int)Fx, lane > 0 ? lane - 1 : 0);
+                uint32_t c[4];
+#pragma unroll
+                for (uint32_t s0 = 0; s0 < 2; s0++) {
+                    const uint32_t role = lane ? role_apply(Fp, s0) : s0;
+                    const bool acc = valid && (role ? a2 : a1);
+                    c[s0] = (uint32_t)__popcll(__ballot(acc && role == 0u));
+                    c[2 + s0] = (uint32_t)__popcll(__ballot(acc && role == 1u));
                 }
+                const uint32_t F63 = (uint32_t)__shfl((int)Fx, 63);   // (all lanes: a shuffle reads active lanes)
+                if (lane == 0) {
+                    sh.sum[b][0] = 1u;
+                    sh.sum[b][1] = F63;
+                    sh.sum[b][2] = c[0]; sh.sum[b][3] = c[1]; sh.sum[b][4] = c[2]; sh.sum[b][5] = c[3];
+                }
+                Fkeep[s] = Fp;
+                a1k[s] = a1;
+                a2k[s] = a2;
+            } else if (lane == 0) {
+                sh.sum[b][0] = 0u;
             }
-            const bool acc = valid && (role ? a2 : a1);
+        }
+        __syncthreads();
+        // ---- combine (wave 0): chain the settled transfers, then the rest exactly
+        if (wv == 0) {
+            uint32_t st = sh.state[0], i1 = sh.state[1], i2 = sh.state[2];
+            int b = 0;
+            for (; b < kMtBlocks; b++) {
+                if (lane == 0) { sh.start[b][0] = st; sh.start[b][1] = i1; sh.start[b][2] = i2; }
+                if (!sh.sum[b][0]) break;
+                i1 += sh.sum[b][2 + st];
+                i2 += sh.sum[b][4 + st];
+                st = role_apply(sh.sum[b][1], st);
+            }
+            const int fu = b;
+            for (; b < kMtBlocks && i2 < W; b++) {
+                const int q0 = 64 * b, nval = kMtN - q0 < 64 ? kMtN - q0 : 64;
+                const bool valid = lane < nval;
+                pair_block(valid ? sh.tw[q0 + lane] : 0u, valid, W, P, kb1, st, i1, i2, emit);
+            }
+            if (lane == 0) { sh.state[0] = st; sh.state[1] = i1; sh.state[2] = i2; sh.state[3] = (uint32_t)fu; }
+        }
+        __syncthreads();
+        // ---- emit the settled blocks before the first unsettled one
+        const int fu = (int)sh.state[3];
+#pragma unroll
+        for (int s = 0; s < 3; s++) {
+            const int b = wv + 4 * s;
+            if (b >= fu) break;
+            const int q0 = 64 * b, nval = kMtN - q0 < 64 ? kMtN - q0 : 64;
+            const bool valid = lane < nval;
+            const uint32_t word = valid ? sh.tw[q0 + lane] : 0u;
+            const uint32_t st = sh.start[b][0], i1 = sh.start[b][1], i2 = sh.start[b][2];
+            const uint32_t role = lane ? role_apply(Fkeep[s], st) : st;
+            const bool acc = valid && (role ? a2k[s] : a1k[s]);
             const uint64_t m1 = __ballot(acc && role == 0u), m2 = __ballot(acc && role == 1u);
             if (acc) {
                 if (role == 0u) {
                     const uint32_t i = i1 + (uint32_t)__popcll(m1 & below);
-                    if (i < W) emit(false, i, r1);
-                } else if (j < W) {
-                    emit(true, j, r2);
+                    if (i < W) emit(false, i, word >> (32u - kb1));
+                } else {
+                    const uint32_t j = i2 + (uint32_t)__popcll(m2 & below);
+                    const uint32_t nhi = i2_0 < W ? W - i2_0 : 1u;
+                    if (j < W) emit(true, j, word >> (32u - (32u - (uint32_t)__builtin_clz(nhi))));
                 }
             }
-            i1 += (uint32_t)__popcll(m1);
-            i2 += (uint32_t)__popcll(m2);
-            st = role_apply((uint32_t)__shfl((int)Fx, 63), st);
         }
+        __syncthreads();
     }
 }
 

@@ -77,6 +77,27 @@ __global__ __launch_bounds__(64) void k_v2x_draws(V2xGeo x, int64_t epoch, uint3
     }
 }
 
+// The same draws with a workgroup per window (pss_mt.h mt_draws_pair_wg): long windows, few
+// streams (C5: 2^20 steps each, ~11 per rank).
+__global__ __launch_bounds__(kMtWgThreads) void k_v2x_draws_wg(V2xGeo x, int64_t epoch, uint32_t jobs, uint64_t blk0,
+                                                              uint32_t *__restrict__ K1, uint32_t *__restrict__ K2) {
+    __shared__ MtWgShared sh;
+    const uint64_t b = blk0 + blockIdx.x;
+    const uint32_t rl = (uint32_t)(b / jobs), job = (uint32_t)(b % jobs);
+    if (job >= x.S) return;
+    uint32_t *k1 = K1 + (size_t)rl * x.ns;
+    uint32_t *k2 = K2 + (size_t)rl * x.T2;
+    const uint32_t s = job;
+    const uint32_t W = x.T - s * x.B < x.B ? x.T - s * x.B : x.B, t0 = s * x.B;
+    if (threadIdx.x < 64) mt_seed_int(sh.mt[0], s == 0 ? epoch + 2 : epoch + (int64_t)(s - 1) * 10000);
+    __syncthreads();
+    mt_draws_pair_wg(sh, 0, W, x.P, [&](bool second, uint32_t i, uint32_t r) {
+        if (second) k2[t0 + i] = r;
+        else k1[t0 + i] = r;
+    });
+    for (uint32_t u = W + threadIdx.x; u < x.B; u += kMtWgThreads) k2[t0 + u] = 0;   // padding steps
+}
+
 // seed of tail step j (pool2 stays empty: every step reseeds first, V2:107-109)
 __device__ __forceinline__ int64_t v2x_tail_seed(const V2xGeo &x, int64_t epoch, uint32_t j) {
     return x.S >= 1 ? epoch + (int64_t)(x.S - 1 + j) * 10000
@@ -667,6 +688,17 @@ static void v2x_launch_blocks(uint64_t blocks, F &&launch) {
         launch(b0, (uint32_t)(blocks - b0 < kMaxBlocks ? blocks - b0 : kMaxBlocks));
 }
 
+// a workgroup per pool2 window's MT stream when the windows are long and few: fewer streams
+// than 4 per CU (PSS_V2X_DRAWS_WG=0 / 1 forces the wave / workgroup form)
+static bool v2x_draws_wg(uint64_t streams, uint32_t B) {
+    static const int env = [] {
+        const char *e = getenv("PSS_V2X_DRAWS_WG");
+        return e ? atoi(e) : -1;
+    }();
+    if (env == 0 || env == 1) return env == 1;
+    return B > (uint32_t)kTile && streams < 1024;
+}
+
 // chain mode: pools of at most kTile entries (one decode tile's frame holds the whole pool);
 // PSS_V2X_CHAIN=0 keeps the global merge levels there too (A/B)
 static bool v2x_chain(const V2xGeo &x) {
@@ -728,8 +760,11 @@ static hipError_t v2x_pass(const Geometry &g, const V2xGeo &x, const RankDesc *r
     uint32_t *O = chain ? nullptr : V + nsr, *Vd = chain ? nullptr : O + nsr, *Od = chain ? nullptr : Vd + nsr;
     uint32_t *K2 = chain ? V + nsr : Od + nsr, *Q2 = K2 + tr;
     if (x.S) {
+        // few long windows (the streams alone do not fill the chip): a workgroup per stream
+        const bool wg = v2x_draws_wg((uint64_t)x.S * (uint64_t)nr, x.B);
         v2x_launch_blocks((uint64_t)x.S * (uint64_t)nr, [&](uint64_t b0, uint32_t nb) {
-            hipLaunchKernelGGL(k_v2x_draws, dim3(nb), dim3(64), 0, s, x, epoch, x.S, b0, K1, K2);
+            if (wg) hipLaunchKernelGGL(k_v2x_draws_wg, dim3(nb), dim3(kMtWgThreads), 0, s, x, epoch, x.S, b0, K1, K2);
+            else hipLaunchKernelGGL(k_v2x_draws, dim3(nb), dim3(64), 0, s, x, epoch, x.S, b0, K1, K2);
         });
     }
     const uint32_t tail_blocks = (x.P + 63u) / 64u;
