@@ -292,12 +292,12 @@ __device__ void mt_draws_pair(uint32_t *mt, uint32_t W, uint32_t P, Emit emit) {
     }
 }
 
-// The same draws on a workgroup of kMtWgThreads (4 waves) per stream, for long windows (C5's
+// The same draws on a workgroup of kMtWgThreads (8 waves) per stream, for long windows (C5's
 // pool2 windows are 2^20 steps and there are only ~11 per rank: one wave per stream left most of
 // the chip idle).  Per twist:
 //   twist   the 624 new words in three barrier-separated phases of <= 227 words (new[k] needs
 //           new[k - 227] from k = 227 on), double-buffered, tempered into tw[]
-//   blocks  the ten 64-word blocks, wave w takes blocks w, w + 4, w + 8: where every k2 verdict
+//   blocks  the ten 64-word blocks, wave w takes blocks w and w + 8: where every k2 verdict
 //           of a block is fixed over all k2 indices the block can see in this twist ([i2, i2 +
 //           32 (b + 1)] for block b), its transfer -- the composed role map and the k1 / k2
 //           acceptances for either start role -- comes from one role scan without knowing
@@ -305,8 +305,10 @@ __device__ void mt_draws_pair(uint32_t *mt, uint32_t W, uint32_t P, Emit emit) {
 //   combine wave 0 chains the transfers from the twist's start state up to the first block
 //           that was not settled, then runs that block and all after it exactly (pair_block)
 //   emit    each wave emits its settled blocks from their now known start states
-constexpr int kMtWgThreads = 256;
+constexpr int kMtWgThreads = 512;
 constexpr int kMtBlocks = (kMtN + 63) / 64;   // 10: nine of 64 words, one of 48
+constexpr int kMtWgWaves = kMtWgThreads / 64;
+constexpr int kMtPerWave = (kMtBlocks + kMtWgWaves - 1) / kMtWgWaves;
 
 struct MtWgShared {
     uint32_t mt[2][kMtN];           // state, double-buffered across the twist
@@ -352,11 +354,12 @@ __device__ void mt_draws_pair_wg(MtWgShared &sh, int cur, uint32_t W, uint32_t P
         __syncthreads();
         // ---- blocks: transfers of the settled ones
         const uint32_t i2_0 = sh.state[2];
-        uint32_t Fkeep[3] = {0u, 0u, 0u};
-        bool a1k[3] = {false, false, false}, a2k[3] = {false, false, false};
+        uint32_t Fkeep[kMtPerWave];
+        bool a1k[kMtPerWave], a2k[kMtPerWave];
 #pragma unroll
-        for (int s = 0; s < 3; s++) {
-            const int b = wv + 4 * s;
+        for (int s = 0; s < kMtPerWave; s++) {
+            Fkeep[s] = 0u; a1k[s] = false; a2k[s] = false;
+            const int b = wv + kMtWgWaves * s;
             if (b >= kMtBlocks) break;
             const int q0 = 64 * b, nval = kMtN - q0 < 64 ? kMtN - q0 : 64;
             const bool valid = lane < nval;
@@ -394,16 +397,22 @@ __device__ void mt_draws_pair_wg(MtWgShared &sh, int cur, uint32_t W, uint32_t P
             }
         }
         __syncthreads();
-        // ---- combine (wave 0): chain the settled transfers, then the rest exactly
+        // ---- combine (wave 0): chain the settled transfers, then the rest exactly.  Lane b holds
+        // block b's summary; the chain reads it with readlane (no LDS round trip per block)
         if (wv == 0) {
             uint32_t st = sh.state[0], i1 = sh.state[1], i2 = sh.state[2];
+            uint32_t vs = 0u, vF = 0u, v10 = 0u, v11 = 0u, v20 = 0u, v21 = 0u;
+            if (lane < kMtBlocks) {
+                vs = sh.sum[lane][0];
+                if (vs) { vF = sh.sum[lane][1]; v10 = sh.sum[lane][2]; v11 = sh.sum[lane][3]; v20 = sh.sum[lane][4]; v21 = sh.sum[lane][5]; }
+            }
             int b = 0;
             for (; b < kMtBlocks; b++) {
                 if (lane == 0) { sh.start[b][0] = st; sh.start[b][1] = i1; sh.start[b][2] = i2; }
-                if (!sh.sum[b][0]) break;
-                i1 += sh.sum[b][2 + st];
-                i2 += sh.sum[b][4 + st];
-                st = role_apply(sh.sum[b][1], st);
+                if (!__builtin_amdgcn_readlane((int)vs, b)) break;
+                i1 += (uint32_t)__builtin_amdgcn_readlane((int)(st ? v11 : v10), b);
+                i2 += (uint32_t)__builtin_amdgcn_readlane((int)(st ? v21 : v20), b);
+                st = role_apply((uint32_t)__builtin_amdgcn_readlane((int)vF, b), st);
             }
             const int fu = b;
             for (; b < kMtBlocks && i2 < W; b++) {
@@ -417,8 +426,8 @@ __device__ void mt_draws_pair_wg(MtWgShared &sh, int cur, uint32_t W, uint32_t P
         // ---- emit the settled blocks before the first unsettled one
         const int fu = (int)sh.state[3];
 #pragma unroll
-        for (int s = 0; s < 3; s++) {
-            const int b = wv + 4 * s;
+        for (int s = 0; s < kMtPerWave; s++) {
+            const int b = wv + kMtWgWaves * s;
             if (b >= fu) break;
             const int q0 = 64 * b, nval = kMtN - q0 < 64 ? kMtN - q0 : 64;
             const bool valid = lane < nval;
