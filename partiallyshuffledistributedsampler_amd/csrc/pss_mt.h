@@ -145,6 +145,30 @@ __device__ __forceinline__ void mt_seed_int(uint32_t *mt, int64_t a) {
 // handed to emit(d, r).  Words come 64 at a time; lane l of a block assumes it serves draw
 // d0 + l - R_l (R_l = rejections among lower lanes) and the block iterates R to the fixed
 // point -- lane l is final after l passes, a block settles in ~5.  One wave.
+// One 64-word block of mt_draws at draw index d0 (the lanes = the block's words, nval of them):
+// the fixed point above; returns the draws the block made.
+template <class Bound, class Emit>
+__device__ __forceinline__ uint32_t draw_block(uint32_t word, int nval, uint32_t d0, uint32_t nd, Bound &bound,
+                                               Emit &emit) {
+    const int lane = threadIdx.x & 63;
+    uint32_t R = 0, d, r;
+    bool acc;
+    for (;;) {
+        d = d0 + (uint32_t)lane - R;
+        const bool valid = lane < nval && d < nd;
+        const uint32_t n = valid ? bound(d) : 2u;
+        const uint32_t k = 32u - (uint32_t)__builtin_clz(n);   // n.bit_length()
+        r = word >> (32u - k);
+        acc = valid && r < n;
+        const uint64_t rej = __ballot(valid && !acc);
+        const uint32_t Rn = (uint32_t)__popcll(rej & lanemask_lt());
+        if (__ballot(Rn != R) == 0) break;
+        R = Rn;
+    }
+    if (acc) emit(d, r);
+    return (uint32_t)__popcll(__ballot(acc));
+}
+
 template <class Bound, class Emit>
 __device__ void mt_draws(uint32_t *mt, uint32_t nd, Bound bound, Emit emit) {
     const int lane = threadIdx.x & 63;
@@ -154,22 +178,7 @@ __device__ void mt_draws(uint32_t *mt, uint32_t nd, Bound bound, Emit emit) {
         for (int q0 = 0; q0 < kMtN && d0 < nd; q0 += 64) {
             const int nval = kMtN - q0 < 64 ? kMtN - q0 : 64;
             const uint32_t word = lane < nval ? mt_temper(mt[q0 + lane]) : 0u;
-            uint32_t R = 0, d, r;
-            bool acc;
-            for (;;) {
-                d = d0 + (uint32_t)lane - R;
-                const bool valid = lane < nval && d < nd;
-                const uint32_t n = valid ? bound(d) : 2u;
-                const uint32_t k = 32u - (uint32_t)__builtin_clz(n);   // n.bit_length()
-                r = word >> (32u - k);
-                acc = valid && r < n;
-                const uint64_t rej = __ballot(valid && !acc);
-                const uint32_t Rn = (uint32_t)__popcll(rej & lanemask_lt());
-                if (__ballot(Rn != R) == 0) break;
-                R = Rn;
-            }
-            if (acc) emit(d, r);
-            d0 += (uint32_t)__popcll(__ballot(acc));
+            d0 += draw_block(word, nval, d0, nd, bound, emit);
         }
     }
 }
@@ -446,6 +455,100 @@ __device__ void mt_draws_pair_wg(MtWgShared &sh, int cur, uint32_t W, uint32_t P
                     if (j < W) emit(true, j, word >> (32u - (32u - (uint32_t)__builtin_clz(nhi))));
                 }
             }
+        }
+        __syncthreads();
+    }
+}
+
+// mt_draws on a workgroup per stream (V1 windows beyond LDS: ~12 windows per rank at C5), for a
+// non-increasing bound(d): the twist and the block transfers as in mt_draws_pair_wg -- a block
+// whose every verdict is fixed over the bounds of all draw indices it can see in this twist
+// ([d, d + 64 (b + 1)] for block b) makes exactly popc(accepted) draws wherever it starts.
+template <class Bound, class Emit>
+__device__ void mt_draws_wg(MtWgShared &sh, int cur, uint32_t nd, Bound bound, Emit emit) {
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const uint64_t below = lanemask_lt();
+    if (tid == 0) sh.state[0] = 0u;
+    __syncthreads();
+    for (;;) {
+        if (sh.state[0] >= nd) break;
+        const uint32_t *o = sh.mt[cur];
+        uint32_t *nw = sh.mt[cur ^ 1];
+        if (tid < kMtN - kMtM) {
+            const uint32_t v = mt_twist_word(o[tid], o[tid + 1], o[tid + kMtM]);
+            nw[tid] = v;
+            sh.tw[tid] = mt_temper(v);
+        }
+        __syncthreads();
+        if (tid < kMtN - kMtM) {
+            const int k = tid + (kMtN - kMtM);
+            const uint32_t v = mt_twist_word(o[k], o[k + 1], nw[k - (kMtN - kMtM)]);
+            nw[k] = v;
+            sh.tw[k] = mt_temper(v);
+        }
+        __syncthreads();
+        if (tid < kMtN - 2 * (kMtN - kMtM)) {
+            const int k = tid + 2 * (kMtN - kMtM);
+            const uint32_t v = k < kMtN - 1 ? mt_twist_word(o[k], o[k + 1], nw[k - (kMtN - kMtM)])
+                                            : mt_twist_word(o[kMtN - 1], nw[0], nw[kMtM - 1]);
+            nw[k] = v;
+            sh.tw[k] = mt_temper(v);
+        }
+        cur ^= 1;
+        __syncthreads();
+        const uint32_t d0 = sh.state[0];
+        bool acck[kMtPerWave];
+        uint32_t rk[kMtPerWave];
+#pragma unroll
+        for (int s = 0; s < kMtPerWave; s++) {
+            acck[s] = false; rk[s] = 0u;
+            const int b = wv + kMtWgWaves * s;
+            if (b >= kMtBlocks) break;
+            const int q0 = 64 * b, nval = kMtN - q0 < 64 ? kMtN - q0 : 64;
+            const bool valid = lane < nval;
+            const uint32_t word = valid ? sh.tw[q0 + lane] : 0u;
+            const uint32_t dlo = d0 < nd ? d0 : nd - 1u;
+            const uint32_t dhi = d0 + 64u * (uint32_t)(b + 1) < nd ? d0 + 64u * (uint32_t)(b + 1) : nd - 1u;
+            const uint32_t nhi = bound(dlo), nlo = bound(dhi);
+            const uint32_t kbh = 32u - (uint32_t)__builtin_clz(nhi);
+            const uint32_t r = word >> (32u - kbh);
+            const bool sure = kbh == 32u - (uint32_t)__builtin_clz(nlo) && (r < nlo || r >= nhi);
+            if (__ballot(valid && !sure) == 0) {
+                const bool acc = valid && r < nlo;
+                const uint32_t cnt = (uint32_t)__popcll(__ballot(acc));
+                if (lane == 0) { sh.sum[b][0] = 1u; sh.sum[b][1] = cnt; }
+                acck[s] = acc;
+                rk[s] = r;
+            } else if (lane == 0) {
+                sh.sum[b][0] = 0u;
+            }
+        }
+        __syncthreads();
+        if (wv == 0) {
+            uint32_t d = sh.state[0];
+            uint32_t vs = 0u, vc = 0u;
+            if (lane < kMtBlocks) { vs = sh.sum[lane][0]; vc = vs ? sh.sum[lane][1] : 0u; }
+            int b = 0;
+            for (; b < kMtBlocks; b++) {
+                if (lane == 0) sh.start[b][0] = d;
+                if (!__builtin_amdgcn_readlane((int)vs, b)) break;
+                d += (uint32_t)__builtin_amdgcn_readlane((int)vc, b);
+            }
+            const int fu = b;
+            for (; b < kMtBlocks && d < nd; b++) {
+                const int q0 = 64 * b, nval = kMtN - q0 < 64 ? kMtN - q0 : 64;
+                d += draw_block(lane < nval ? sh.tw[q0 + lane] : 0u, nval, d, nd, bound, emit);
+            }
+            if (lane == 0) { sh.state[0] = d; sh.state[3] = (uint32_t)fu; }
+        }
+        __syncthreads();
+        const int fu = (int)sh.state[3];
+#pragma unroll
+        for (int s = 0; s < kMtPerWave; s++) {
+            const int b = wv + kMtWgWaves * s;
+            if (b >= fu) break;
+            const uint32_t d = sh.start[b][0] + (uint32_t)__popcll(__ballot(acck[s]) & below);
+            if (acck[s] && d < nd) emit(d, rk[s]);
         }
         __syncthreads();
     }

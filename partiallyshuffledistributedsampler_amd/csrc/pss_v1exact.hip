@@ -173,6 +173,21 @@ __global__ __launch_bounds__(64) void k_v1x_draws32(Geometry g, V1xBig b, int64_
              [&](uint32_t d, uint32_t r) { jw[n - 1 - (int)d] = r; });
 }
 
+// The same draws with a workgroup per window (pss_mt.h mt_draws_wg): few, long windows (C5: 2^20
+// entries, ~12 per rank)
+__global__ __launch_bounds__(kMtWgThreads) void k_v1x_draws32_wg(Geometry g, V1xBig b, int64_t epoch) {
+    __shared__ MtWgShared sh;
+    const uint64_t job = b.j0 + blockIdx.x;
+    const int64_t w = b.w_lo + (int64_t)(job % (uint64_t)b.nw);
+    const int n = v1x_len(g, w);
+    if (n <= 1) return;
+    uint32_t *jw = b.J + (size_t)blockIdx.x * b.B;
+    if (threadIdx.x < 64) mt_seed_int(sh.mt[0], w == 0 ? epoch : epoch + w * 10000);
+    __syncthreads();
+    mt_draws_wg(sh, 0, (uint32_t)(n - 1), [&](uint32_t d) { return (uint32_t)n - d; },
+                [&](uint32_t d, uint32_t r) { jw[n - 1 - (int)d] = r; });
+}
+
 // blockIdx.y = slot of the pass, x-threads over the window's entries
 #define V1X_SLOT_PROLOGUE                                                          \
     const uint32_t slot = blockIdx.y;                                              \
@@ -337,7 +352,14 @@ static hipError_t launch_v1_exact_big(const Geometry &g, const RankDesc *ranks, 
         hipError_t e = hipMemsetAsync(b.CNT, 0, sizeof(uint32_t) * (size_t)b.nj * ((size_t)B + 1), s);
         if (e != hipSuccess) return e;
         const dim3 flat((B + 255) / 256, b.nj);
-        hipLaunchKernelGGL(k_v1x_draws32, dim3(b.nj), dim3(64), 0, s, g, b, epoch);
+        // few windows: a workgroup per window's MT stream (PSS_V1X_DRAWS_WG=0 / 1 forces a form)
+        static const int wg_env = [] {
+            const char *e = getenv("PSS_V1X_DRAWS_WG");
+            return e ? atoi(e) : -1;
+        }();
+        const bool wg = wg_env == 0 || wg_env == 1 ? wg_env == 1 : b.nj < 1024;
+        if (wg) hipLaunchKernelGGL(k_v1x_draws32_wg, dim3(b.nj), dim3(kMtWgThreads), 0, s, g, b, epoch);
+        else hipLaunchKernelGGL(k_v1x_draws32, dim3(b.nj), dim3(64), 0, s, g, b, epoch);
         hipLaunchKernelGGL(k_v1x_count, flat, dim3(256), 0, s, g, b);
         hipLaunchKernelGGL(k_v1x_scan, dim3(b.nj), dim3(kV1xScanNT), 0, s, g, b);
         hipLaunchKernelGGL(k_v1x_scatter, flat, dim3(256), 0, s, g, b);
