@@ -579,20 +579,56 @@ __global__ __launch_bounds__(64) void k_g_emit(Geometry g, GPlan pl, const RankD
 #pragma unroll
                 for (int j = 0; j < 4; j++) k[j] = scale32(slot_hash(tb + j * G64, s0, s1), S);
             }
+            uint32_t in[4];
+            bool nxt[4];
+            uint32_t pj[4];
 #pragma unroll
             for (int j = 0; j < 4; j++) {
-                uint32_t p = pa + c_lane + j * G64;
-                const bool nxt = p >= B;
-                if (nxt) p -= B;
-                uint32_t Kl[kFeistelRounds];
-#pragma unroll
-                for (int i = 0; i < kFeistelRounds; i++) Kl[i] = nxt ? Kn[i] : Kc[i];
-                const uint32_t in = ids.to_slot((wa + (nxt ? 1u : 0u)) * B + feistel_once(p, pl.hB, Kl));
-                uint32_t vv;
-                if constexpr (ORDERED) vv = atomicExch(&buf[k[j]], in);
-                else vv = xchg_unordered(buf, mark, k[j], in, true, lane);
-                put((int64_t)tb + j * G64, ids.from_slot(vv));
+                pj[j] = pa + c_lane + j * G64;
+                nxt[j] = pj[j] >= B;
+                if (nxt[j]) pj[j] -= B;
             }
+            if constexpr (PACKED) {
+                // the 16-bit round function, chains paired per register as in the runs, each
+                // half-word under its own window's key (per-lane selects of the two windows'
+                // key half-words)
+                const uint32_t h = pl.hB, mask = (1u << h) - 1u;
+                const pss_u16x2 M = {(unsigned short)kFeistelM16, (unsigned short)kFeistelM16};
+                const pss_u16x2 SH = {(unsigned short)(16u - h), (unsigned short)(16u - h)};
+                uint32_t L0 = (pj[0] >> h) | ((pj[1] >> h) << 16), R0 = (pj[0] & mask) | ((pj[1] & mask) << 16);
+                uint32_t L1 = (pj[2] >> h) | ((pj[3] >> h) << 16), R1 = (pj[2] & mask) | ((pj[3] & mask) << 16);
+#pragma unroll
+                for (int i = 0; i < kFeistelRounds; i++) {
+                    const uint32_t lo = Kc[i] & 0xFFFFu, lon = Kn[i] & 0xFFFFu, hi = Kc[i] << 16, hin = Kn[i] << 16;
+                    const uint32_t k0 = (nxt[0] ? lon : lo) | (nxt[1] ? hin : hi);
+                    const uint32_t k1 = (nxt[2] ? lon : lo) | (nxt[3] ? hin : hi);
+                    const uint32_t f0 = __builtin_bit_cast(uint32_t, (__builtin_bit_cast(pss_u16x2, R0 ^ k0) * M) >> SH);
+                    const uint32_t f1 = __builtin_bit_cast(uint32_t, (__builtin_bit_cast(pss_u16x2, R1 ^ k1) * M) >> SH);
+                    const uint32_t t0 = L0 ^ f0, t1 = L1 ^ f1;
+                    L0 = R0; R0 = t0;
+                    L1 = R1; R1 = t1;
+                }
+                const uint32_t y[4] = {((L0 & 0xFFFFu) << h) | (R0 & 0xFFFFu), ((L0 >> 16) << h) | (R0 >> 16),
+                                       ((L1 & 0xFFFFu) << h) | (R1 & 0xFFFFu), ((L1 >> 16) << h) | (R1 >> 16)};
+#pragma unroll
+                for (int j = 0; j < 4; j++) in[j] = ids.to_slot((wa + (nxt[j] ? 1u : 0u)) * B + y[j]);
+            } else {
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    uint32_t Kl[kFeistelRounds];
+#pragma unroll
+                    for (int i = 0; i < kFeistelRounds; i++) Kl[i] = nxt[j] ? Kn[i] : Kc[i];
+                    in[j] = ids.to_slot((wa + (nxt[j] ? 1u : 0u)) * B + feistel_once(pj[j], pl.hB, Kl));
+                }
+            }
+            uint32_t vv[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                if constexpr (ORDERED) vv[j] = atomicExch(&buf[k[j]], in[j]);
+                else vv[j] = xchg_unordered(buf, mark, k[j], in[j], true, lane);
+            }
+#pragma unroll
+            for (int j = 0; j < 4; j++) put((int64_t)tb + j * G64, ids.from_slot(vv[j]));
             t_first += G256;
             pa += G256;
             while (pa >= B) { pa -= B; wa++; }
