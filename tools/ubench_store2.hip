@@ -98,6 +98,26 @@ __global__ __launch_bounds__(64) void persist_rb(int64_t *o, uint64_t n, int64_t
     }
 }
 
+// canonical grid-stride fill: every iteration of the whole grid writes one contiguous band
+__global__ __launch_bounds__(256) void gridstride(int64_t *o, uint64_t n, int64_t salt) {
+    const uint64_t stride = (uint64_t)gridDim.x * 256;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) o[i] = (int64_t)i + salt;
+}
+// persistent one-wave runs, but each wave's run split into KB-sized pieces dealt round-robin
+// over the waves (wave w writes pieces w, w + G, ...), piece = P x 2 KB
+template <int P>
+__global__ __launch_bounds__(64) void persist_pieces(int64_t *o, uint64_t n, int64_t salt) {
+    extern __shared__ uint32_t pad[];
+    if (n == 0) pad[threadIdx.x] = 0;
+    const uint64_t piece = 256ull * P, np = n / piece;
+    for (uint64_t q = blockIdx.x; q < np; q += gridDim.x) {
+        int64_t *p = o + q * piece;
+        for (int c = 0; c < P; c++)
+#pragma unroll
+            for (int j = 0; j < 4; j++) p[256 * c + 64 * j + threadIdx.x] = (int64_t)(256 * c + 64 * j + threadIdx.x) + salt;
+    }
+}
+
 template <class F>
 void timeit(const char *name, F launch) {
     hipEvent_t a, b;
@@ -118,7 +138,8 @@ int main() {
     hipMalloc(&o, kIds * 8 + 4096);
     const uint64_t n = kIds;
     for (auto fn : {(const void *)persist_c, (const void *)persist_r<0>, (const void *)persist_r<1>, (const void *)persist_rb<0>,
-                    (const void *)persist_rb<1>, (const void *)persist_rb<2>, (const void *)persist_rb<3>})
+                    (const void *)persist_rb<1>, (const void *)persist_rb<2>, (const void *)persist_rb<3>,
+                    (const void *)persist_pieces<16>, (const void *)persist_pieces<128>})
         (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     for (int rep = 0; rep < 2; rep++) {
         timeit("oneshot4", [&](int s) { hipLaunchKernelGGL(oneshot4, dim3((uint32_t)((n / 4 + 255) / 256)), dim3(256), 0, 0, o, n, (int64_t)s); });
@@ -140,6 +161,10 @@ int main() {
         timeit("os_256x4", [&](int s) { hipLaunchKernelGGL((oneshot_ns<256, 4>), dim3((uint32_t)(n / 1024)), dim3(256), 0, 0, o, n, (int64_t)s); });
         timeit("os_256x16", [&](int s) { hipLaunchKernelGGL((oneshot_ns<256, 16>), dim3((uint32_t)(n / 4096)), dim3(256), 0, 0, o, n, (int64_t)s); });
         timeit("os_1024x4", [&](int s) { hipLaunchKernelGGL((oneshot_ns<1024, 4>), dim3((uint32_t)(n / 4096)), dim3(1024), 0, 0, o, n, (int64_t)s); });
+        timeit("grid_2048", [&](int s) { hipLaunchKernelGGL(gridstride, dim3(2048), dim3(256), 0, 0, o, n, (int64_t)s); });
+        timeit("grid_512", [&](int s) { hipLaunchKernelGGL(gridstride, dim3(512), dim3(256), 0, 0, o, n, (int64_t)s); });
+        timeit("pieces_32K", [&](int s) { hipLaunchKernelGGL(persist_pieces<16>, dim3(2048), dim3(64), 18220, 0, o, n, (int64_t)s); });
+        timeit("pieces_256K", [&](int s) { hipLaunchKernelGGL(persist_pieces<128>, dim3(2048), dim3(64), 18220, 0, o, n, (int64_t)s); });
         timeit("persist_r32x4", [&](int s) { hipLaunchKernelGGL(persist_r<1>, dim3(8192), dim3(64), 4000, 0, o, n, (int64_t)s); });
     }
     return 0;
