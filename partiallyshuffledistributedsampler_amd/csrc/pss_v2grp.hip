@@ -23,6 +23,12 @@ namespace pss {
 
 static inline int64_t gdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
+// cache-policy bits of the run stores (build-time A/B: -DPSS_G_STORE_AUX=1 sets sc0)
+#ifndef PSS_G_STORE_AUX
+#define PSS_G_STORE_AUX 0
+#endif
+constexpr int kGStoreAux = PSS_G_STORE_AUX;
+
 // key table layout per local rank (words): [0, 2) slot key, [8, 16) init keys,
 // [16 + 8 (w - 1), + 8) round keys of pool2 window w = 1 .. W
 constexpr int64_t kGKeySlot = 0, kGKeyInit = 8, kGKeyWin = 16;
@@ -531,7 +537,7 @@ __global__ __launch_bounds__(64) void k_g_emit(Geometry g, GPlan pl, const RankD
                         } else {
                             const uint64_t id = (uint64_t)ids.from_slot(v[j]);
                             const g_u32x2 d = {(uint32_t)id, (uint32_t)(id >> 32)};
-                            __builtin_amdgcn_raw_buffer_store_b64(d, orsrc, (int)voff, (int)(8u * (uint32_t)j * G64), 0);
+                            __builtin_amdgcn_raw_buffer_store_b64(d, orsrc, (int)voff, (int)(8u * (uint32_t)j * G64), kGStoreAux);
                         }
                     }
                     tb += G256;
