@@ -1006,6 +1006,15 @@ static int64_t keytab_windows(const V2Plan &pl, const Geometry &g) {
     return pl.T > 0 ? 1 + (pl.T - 1) / g.B : 0;
 }
 static size_t keytab_words(const V2Plan &pl, const Geometry &g, int32_t nr) {
+    // Off by default: the replay waves and last-occurrence workgroups derive their windows'
+    // keys with Philox themselves, which costs less than the extra kernel (and its boundary)
+    // on the lookahead stream -- C2 544 -> 548, C3 540 -> 544 G idx/s, same-box A/B
+    // (profiles/r03/ab_keytab).  PSS_V2_KEYTAB=1 restores the per-launch table.
+    static const bool off = [] {
+        const char *e = getenv("PSS_V2_KEYTAB");
+        return !(e && e[0] == '1');
+    }();
+    if (off) return 0;
     const size_t w = (size_t)nr * (size_t)(16 + kRoundKeyWords * keytab_windows(pl, g));
     return w <= ((size_t)64 << 20) ? w : 0;     // <= 256 MB
 }
