@@ -301,12 +301,12 @@ __device__ void mt_draws_pair(uint32_t *mt, uint32_t W, uint32_t P, Emit emit) {
     }
 }
 
-// The same draws on a workgroup of kMtWgThreads (8 waves) per stream, for long windows (C5's
+// The same draws on a workgroup of kMtWgThreads (10 waves) per stream, for long windows (C5's
 // pool2 windows are 2^20 steps and there are only ~11 per rank: one wave per stream left most of
 // the chip idle).  Per twist:
 //   twist   the 624 new words in three barrier-separated phases of <= 227 words (new[k] needs
 //           new[k - 227] from k = 227 on), double-buffered, tempered into tw[]
-//   blocks  the ten 64-word blocks, wave w takes blocks w and w + 8: where every k2 verdict
+//   blocks  the ten 64-word blocks, wave w takes block w: where every k2 verdict
 //           of a block is fixed over all k2 indices the block can see in this twist ([i2, i2 +
 //           32 (b + 1)] for block b), its transfer -- the composed role map and the k1 / k2
 //           acceptances for either start role -- comes from one role scan without knowing
@@ -314,18 +314,47 @@ __device__ void mt_draws_pair(uint32_t *mt, uint32_t W, uint32_t P, Emit emit) {
 //   combine wave 0 chains the transfers from the twist's start state up to the first block
 //           that was not settled, then runs that block and all after it exactly (pair_block)
 //   emit    each wave emits its settled blocks from their now known start states
-constexpr int kMtWgThreads = 512;
+constexpr int kMtWgThreads = 640;   // ten waves: one 64-word block each
 constexpr int kMtBlocks = (kMtN + 63) / 64;   // 10: nine of 64 words, one of 48
 constexpr int kMtWgWaves = kMtWgThreads / 64;
 constexpr int kMtPerWave = (kMtBlocks + kMtWgWaves - 1) / kMtWgWaves;
 
 struct MtWgShared {
     uint32_t mt[2][kMtN];           // state, double-buffered across the twist
-    uint32_t tw[kMtN];              // tempered words of the current twist
+    uint32_t tw[2][kMtN];           // tempered words: the current twist's and the next one's
     uint32_t sum[kMtBlocks][6];     // settled?, role map, c1(st = 0), c1(st = 1), c2(0), c2(1)
     uint32_t start[kMtBlocks][3];   // (st, i1, i2) at each block's start
     uint32_t state[4];              // st, i1, i2, first unsettled block
 };
+
+// Software pipeline of the workgroup draws: the twist that makes the NEXT 624 words runs on
+// waves 4.. beside the current twist's three phases (blocks | combine | emit), one of its three
+// dependent steps per phase, so a twist costs three barriers instead of six phases.  Step p
+// computes new[k], k in [227 p, 227 p + 227) (new[k] needs new[k - 227] from k = 227 on), by
+// thread tt = tid - kMtTwistLo; the tempered word goes to tw.
+constexpr int kMtTwistLo = 256;
+__device__ __forceinline__ void mt_twist_step(const uint32_t *o, uint32_t *nw, uint32_t *tw, int p,
+                                              int tid) {
+    constexpr int D = kMtN - kMtM;   // 227
+    const uint32_t tt = (uint32_t)(tid - kMtTwistLo);
+    const int k = (int)tt + D * p;
+    if (tt >= (uint32_t)D || k >= kMtN) return;
+    uint32_t v;
+    if (p == 0) v = mt_twist_word(o[k], o[k + 1], o[k + kMtM]);
+    else if (k < kMtN - 1) v = mt_twist_word(o[k], o[k + 1], nw[k - D]);
+    else v = mt_twist_word(o[kMtN - 1], nw[0], nw[kMtM - 1]);
+    nw[k] = v;
+    tw[k] = mt_temper(v);
+}
+
+// the first twist of a stream (the pipeline's prologue): old = mt[cur] -> mt[cur ^ 1], tw
+__device__ __forceinline__ void mt_twist_wg(MtWgShared &sh, int cur, uint32_t *tw) {
+#pragma unroll
+    for (int p = 0; p < 3; p++) {
+        mt_twist_step(sh.mt[cur], sh.mt[cur ^ 1], tw, p, threadIdx.x);
+        __syncthreads();
+    }
+}
 
 template <class Emit>
 __device__ void mt_draws_pair_wg(MtWgShared &sh, int cur, uint32_t W, uint32_t P, Emit emit) {
@@ -333,34 +362,16 @@ __device__ void mt_draws_pair_wg(MtWgShared &sh, int cur, uint32_t W, uint32_t P
     const uint32_t kb1 = 32u - (uint32_t)__builtin_clz(P);
     const uint64_t below = lanemask_lt();
     if (tid == 0) { sh.state[0] = 0u; sh.state[1] = 0u; sh.state[2] = 0u; }
-    __syncthreads();
-    for (;;) {
+    mt_twist_wg(sh, cur, sh.tw[0]);   // (its first barrier also publishes state)
+    cur ^= 1;
+    for (int tb = 0;; tb ^= 1) {
         if (sh.state[2] >= W) break;   // (uniform: read after a barrier)
-        // ---- twist: old = mt[cur] -> new = mt[cur ^ 1], tempered into tw
+        // tc: this twist's tempered words; the next twist (old = mt[cur] -> mt[cur ^ 1], into
+        // tw[tb ^ 1]) runs one step per phase beside it
+        const uint32_t *tc = sh.tw[tb];
         const uint32_t *o = sh.mt[cur];
-        uint32_t *nw = sh.mt[cur ^ 1];
-        if (tid < kMtN - kMtM) {                                   // k in [0, 227)
-            const uint32_t v = mt_twist_word(o[tid], o[tid + 1], o[tid + kMtM]);
-            nw[tid] = v;
-            sh.tw[tid] = mt_temper(v);
-        }
-        __syncthreads();
-        if (tid < kMtN - kMtM) {                                   // k in [227, 454)
-            const int k = tid + (kMtN - kMtM);
-            const uint32_t v = mt_twist_word(o[k], o[k + 1], nw[k - (kMtN - kMtM)]);
-            nw[k] = v;
-            sh.tw[k] = mt_temper(v);
-        }
-        __syncthreads();
-        if (tid < kMtN - 2 * (kMtN - kMtM)) {                      // k in [454, 624)
-            const int k = tid + 2 * (kMtN - kMtM);
-            const uint32_t v = k < kMtN - 1 ? mt_twist_word(o[k], o[k + 1], nw[k - (kMtN - kMtM)])
-                                            : mt_twist_word(o[kMtN - 1], nw[0], nw[kMtM - 1]);
-            nw[k] = v;
-            sh.tw[k] = mt_temper(v);
-        }
-        cur ^= 1;
-        __syncthreads();
+        uint32_t *nw = sh.mt[cur ^ 1], *tn = sh.tw[tb ^ 1];
+        mt_twist_step(o, nw, tn, 0, tid);
         // ---- blocks: transfers of the settled ones
         const uint32_t i2_0 = sh.state[2];
         uint32_t Fkeep[kMtPerWave];
@@ -372,7 +383,7 @@ __device__ void mt_draws_pair_wg(MtWgShared &sh, int cur, uint32_t W, uint32_t P
             if (b >= kMtBlocks) break;
             const int q0 = 64 * b, nval = kMtN - q0 < 64 ? kMtN - q0 : 64;
             const bool valid = lane < nval;
-            const uint32_t word = valid ? sh.tw[q0 + lane] : 0u;
+            const uint32_t word = valid ? tc[q0 + lane] : 0u;
             const bool a1 = valid && (word >> (32u - kb1)) < P;
             const uint32_t jhi = i2_0 + 32u * (uint32_t)(b + 1);
             const uint32_t nhi = i2_0 < W ? W - i2_0 : 1u, nlo = jhi < W ? W - jhi : 1u;
@@ -406,6 +417,7 @@ __device__ void mt_draws_pair_wg(MtWgShared &sh, int cur, uint32_t W, uint32_t P
             }
         }
         __syncthreads();
+        mt_twist_step(o, nw, tn, 1, tid);
         // ---- combine (wave 0): chain the settled transfers, then the rest exactly.  Lane b holds
         // block b's summary; the chain reads it with readlane (no LDS round trip per block)
         if (wv == 0) {
@@ -427,11 +439,13 @@ __device__ void mt_draws_pair_wg(MtWgShared &sh, int cur, uint32_t W, uint32_t P
             for (; b < kMtBlocks && i2 < W; b++) {
                 const int q0 = 64 * b, nval = kMtN - q0 < 64 ? kMtN - q0 : 64;
                 const bool valid = lane < nval;
-                pair_block(valid ? sh.tw[q0 + lane] : 0u, valid, W, P, kb1, st, i1, i2, emit);
+                pair_block(valid ? tc[q0 + lane] : 0u, valid, W, P, kb1, st, i1, i2, emit);
             }
             if (lane == 0) { sh.state[0] = st; sh.state[1] = i1; sh.state[2] = i2; sh.state[3] = (uint32_t)fu; }
         }
         __syncthreads();
+        mt_twist_step(o, nw, tn, 2, tid);
+        cur ^= 1;
         // ---- emit the settled blocks before the first unsettled one
         const int fu = (int)sh.state[3];
 #pragma unroll
@@ -440,7 +454,7 @@ __device__ void mt_draws_pair_wg(MtWgShared &sh, int cur, uint32_t W, uint32_t P
             if (b >= fu) break;
             const int q0 = 64 * b, nval = kMtN - q0 < 64 ? kMtN - q0 : 64;
             const bool valid = lane < nval;
-            const uint32_t word = valid ? sh.tw[q0 + lane] : 0u;
+            const uint32_t word = valid ? tc[q0 + lane] : 0u;
             const uint32_t st = sh.start[b][0], i1 = sh.start[b][1], i2 = sh.start[b][2];
             const uint32_t role = lane ? role_apply(Fkeep[s], st) : st;
             const bool acc = valid && (role ? a2k[s] : a1k[s]);
@@ -469,33 +483,14 @@ __device__ void mt_draws_wg(MtWgShared &sh, int cur, uint32_t nd, Bound bound, E
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const uint64_t below = lanemask_lt();
     if (tid == 0) sh.state[0] = 0u;
-    __syncthreads();
-    for (;;) {
+    mt_twist_wg(sh, cur, sh.tw[0]);   // pipelined as in mt_draws_pair_wg
+    cur ^= 1;
+    for (int tb = 0;; tb ^= 1) {
         if (sh.state[0] >= nd) break;
+        const uint32_t *tc = sh.tw[tb];
         const uint32_t *o = sh.mt[cur];
-        uint32_t *nw = sh.mt[cur ^ 1];
-        if (tid < kMtN - kMtM) {
-            const uint32_t v = mt_twist_word(o[tid], o[tid + 1], o[tid + kMtM]);
-            nw[tid] = v;
-            sh.tw[tid] = mt_temper(v);
-        }
-        __syncthreads();
-        if (tid < kMtN - kMtM) {
-            const int k = tid + (kMtN - kMtM);
-            const uint32_t v = mt_twist_word(o[k], o[k + 1], nw[k - (kMtN - kMtM)]);
-            nw[k] = v;
-            sh.tw[k] = mt_temper(v);
-        }
-        __syncthreads();
-        if (tid < kMtN - 2 * (kMtN - kMtM)) {
-            const int k = tid + 2 * (kMtN - kMtM);
-            const uint32_t v = k < kMtN - 1 ? mt_twist_word(o[k], o[k + 1], nw[k - (kMtN - kMtM)])
-                                            : mt_twist_word(o[kMtN - 1], nw[0], nw[kMtM - 1]);
-            nw[k] = v;
-            sh.tw[k] = mt_temper(v);
-        }
-        cur ^= 1;
-        __syncthreads();
+        uint32_t *nw = sh.mt[cur ^ 1], *tn = sh.tw[tb ^ 1];
+        mt_twist_step(o, nw, tn, 0, tid);
         const uint32_t d0 = sh.state[0];
         bool acck[kMtPerWave];
         uint32_t rk[kMtPerWave];
@@ -506,7 +501,7 @@ __device__ void mt_draws_wg(MtWgShared &sh, int cur, uint32_t nd, Bound bound, E
             if (b >= kMtBlocks) break;
             const int q0 = 64 * b, nval = kMtN - q0 < 64 ? kMtN - q0 : 64;
             const bool valid = lane < nval;
-            const uint32_t word = valid ? sh.tw[q0 + lane] : 0u;
+            const uint32_t word = valid ? tc[q0 + lane] : 0u;
             const uint32_t dlo = d0 < nd ? d0 : nd - 1u;
             const uint32_t dhi = d0 + 64u * (uint32_t)(b + 1) < nd ? d0 + 64u * (uint32_t)(b + 1) : nd - 1u;
             const uint32_t nhi = bound(dlo), nlo = bound(dhi);
@@ -524,6 +519,7 @@ __device__ void mt_draws_wg(MtWgShared &sh, int cur, uint32_t nd, Bound bound, E
             }
         }
         __syncthreads();
+        mt_twist_step(o, nw, tn, 1, tid);
         if (wv == 0) {
             uint32_t d = sh.state[0];
             uint32_t vs = 0u, vc = 0u;
@@ -537,11 +533,13 @@ __device__ void mt_draws_wg(MtWgShared &sh, int cur, uint32_t nd, Bound bound, E
             const int fu = b;
             for (; b < kMtBlocks && d < nd; b++) {
                 const int q0 = 64 * b, nval = kMtN - q0 < 64 ? kMtN - q0 : 64;
-                d += draw_block(lane < nval ? sh.tw[q0 + lane] : 0u, nval, d, nd, bound, emit);
+                d += draw_block(lane < nval ? tc[q0 + lane] : 0u, nval, d, nd, bound, emit);
             }
             if (lane == 0) { sh.state[0] = d; sh.state[3] = (uint32_t)fu; }
         }
         __syncthreads();
+        mt_twist_step(o, nw, tn, 2, tid);
+        cur ^= 1;
         const int fu = (int)sh.state[3];
 #pragma unroll
         for (int s = 0; s < kMtPerWave; s++) {
