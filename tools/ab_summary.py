@@ -1,4 +1,6 @@
-"""Summarise an A/B directory of bench lines: G idx/s and dominant-kernel launch time per run."""
+"""Summarise an A/B directory (tools/gpu_ab_lib.sh, gpu_ab_env.sh, gpu_ab_exact.sh): per tag,
+G idx/s and the dominant kernel's launch time (bench.py lines) or ms per epoch
+(tools/bench_configs.py lines), one column per run."""
 import glob
 import json
 import sys
@@ -12,7 +14,10 @@ for d in sys.argv[1:]:
             print(f, "unreadable")
             continue
         tag = f.rsplit("/", 1)[1].rsplit("_", 1)[0]
-        rows.setdefault(tag, []).append((j["value"], j["roofline"]["launch_ms"] * 1e3))
+        if "roofline" in j:
+            rows.setdefault(tag, []).append((j["value"], "launch us", j["roofline"]["launch_ms"] * 1e3))
+        else:
+            rows.setdefault(tag, []).append((j["G_idx_per_s"], "ms/epoch", j["ms_per_step"]))
     for tag, v in rows.items():
-        print("%-10s G idx/s %s   launch us %s" % (tag, " ".join("%.1f" % a for a, _ in v),
-                                                  " ".join("%.1f" % b for _, b in v)))
+        print("%-14s G idx/s %s   %s %s" % (tag, " ".join("%.2f" % a for a, _, _ in v), v[0][1],
+                                          " ".join("%.2f" % c for _, _, c in v)))
