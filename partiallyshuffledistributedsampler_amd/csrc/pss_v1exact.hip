@@ -154,7 +154,22 @@ struct V1xBig {
     uint32_t nj;            // jobs in the pass
     uint32_t B;             // slice length: min(shuffle_buffer, num_samples)
     uint32_t *J, *CNT, *LST, *NXT;
+    uint32_t xb;            // 256-entry blocks per window (the flat kernels' x extent)
+    uint32_t xcd;           // 1: XCD-major flat grid (v1x_flat_grid)
 };
+
+// The flat kernels (count, scatter, parent, out) make random accesses inside one window's
+// slices.  XCD-major grid: workgroup L runs on XCD L mod 8 (round-robin dispatch), so block L is
+// given window slot 8 (L / 8 / xb) + L mod 8 and entry block (L / 8) mod xb -- every window's
+// blocks then run on one XCD, which keeps its slices' lines in that XCD's L2 instead of
+// bouncing the atomics and reads of one window across all eight.  xcd = 0: blockIdx.y = slot.
+__device__ __forceinline__ bool v1x_block(const V1xBig &b, uint32_t &slot, uint32_t &xblk) {
+    if (!b.xcd) { slot = blockIdx.y; xblk = blockIdx.x; return true; }
+    const uint32_t L = blockIdx.x, q = L >> 3;
+    slot = 8u * (q / b.xb) + (L & 7u);
+    xblk = q % b.xb;
+    return slot < b.nj;
+}
 
 __device__ __forceinline__ int v1x_len(const Geometry &g, int64_t w) {
     const int64_t wb = w * g.B;
@@ -188,9 +203,10 @@ __global__ __launch_bounds__(kMtWgThreads) void k_v1x_draws32_wg(Geometry g, V1x
                 [&](uint32_t d, uint32_t r) { jw[n - 1 - (int)d] = r; });
 }
 
-// blockIdx.y = slot of the pass, x-threads over the window's entries
+// slot of the pass and block of the window's entries (v1x_block)
 #define V1X_SLOT_PROLOGUE                                                          \
-    const uint32_t slot = blockIdx.y;                                              \
+    uint32_t slot, xblk;                                                           \
+    if (!v1x_block(b, slot, xblk)) return;                                         \
     const uint64_t job = b.j0 + slot;                                              \
     const int64_t w = b.w_lo + (int64_t)(job % (uint64_t)b.nw);                    \
     const int n = v1x_len(g, w);                                                   \
@@ -200,7 +216,7 @@ __global__ __launch_bounds__(kMtWgThreads) void k_v1x_draws32_wg(Geometry g, V1x
 
 __global__ __launch_bounds__(256) void k_v1x_count(Geometry g, V1xBig b) {
     V1X_SLOT_PROLOGUE
-    const int k = (int)(blockIdx.x * 256 + threadIdx.x);
+    const int k = (int)(xblk * 256 + threadIdx.x);
     if (k >= 1 && k < n) atomicAdd(&CNT[J[k]], 1u);
 }
 
@@ -247,7 +263,7 @@ __global__ __launch_bounds__(kV1xScanNT) void k_v1x_scan(Geometry g, V1xBig b) {
 
 __global__ __launch_bounds__(256) void k_v1x_scatter(Geometry g, V1xBig b) {
     V1X_SLOT_PROLOGUE
-    const int k = (int)(blockIdx.x * 256 + threadIdx.x);
+    const int k = (int)(xblk * 256 + threadIdx.x);
     if (k >= 1 && k < n) b.LST[(size_t)slot * b.B + atomicAdd(&CNT[J[k]], 1u)] = (uint32_t)k;
 }
 
@@ -264,7 +280,7 @@ __device__ __forceinline__ int v1x_succ(const uint32_t *CNT, const uint32_t *LST
 
 __global__ __launch_bounds__(256) void k_v1x_parent(Geometry g, V1xBig b) {
     V1X_SLOT_PROLOGUE
-    const int k = (int)(blockIdx.x * 256 + threadIdx.x);
+    const int k = (int)(xblk * 256 + threadIdx.x);
     if (k >= n) return;
     const int pk = v1x_succ(CNT, b.LST + (size_t)slot * b.B, k, k);
     b.NXT[(size_t)slot * b.B + k] = (uint32_t)(pk < 0 ? k : pk);
@@ -275,7 +291,7 @@ __global__ __launch_bounds__(256) void k_v1x_out(Geometry g, V1xBig b, const Ran
                                                  int64_t *__restrict__ out) {
     V1X_SLOT_PROLOGUE
     const int64_t wb = w * g.B;
-    const int64_t p = wb + (int64_t)(blockIdx.x * 256 + threadIdx.x);
+    const int64_t p = wb + (int64_t)(xblk * 256 + threadIdx.x);
     const int i = (int)(p - wb);
     if (i >= n || p < pos_lo || p >= pos_lo + count) return;
     const uint32_t *LST = b.LST + (size_t)slot * b.B, *NXT = b.NXT + (size_t)slot * b.B;
@@ -351,7 +367,15 @@ static hipError_t launch_v1_exact_big(const Geometry &g, const RankDesc *ranks, 
         b.NXT = b.LST + (size_t)b.nj * B;
         hipError_t e = hipMemsetAsync(b.CNT, 0, sizeof(uint32_t) * (size_t)b.nj * ((size_t)B + 1), s);
         if (e != hipSuccess) return e;
-        const dim3 flat((B + 255) / 256, b.nj);
+        b.xb = (B + 255) / 256;
+        static const bool xcd_env = [] {   // A/B knob: PSS_V1X_XCD=0 keeps the (x, slot) grid
+            const char *e = getenv("PSS_V1X_XCD");
+            return !(e && e[0] == '0');
+        }();
+        // XCD-major only while the 1-D grid stays below 2^32 threads
+        b.xcd = xcd_env && (uint64_t)b.xb * (((uint64_t)b.nj + 7) / 8) * 8 < ((uint64_t)1 << 24) ? 1u : 0u;
+        const dim3 flat = b.xcd ? dim3((uint32_t)((uint64_t)b.xb * (((uint64_t)b.nj + 7) / 8) * 8))
+                                : dim3(b.xb, b.nj);
         // few windows: a workgroup per window's MT stream (PSS_V1X_DRAWS_WG=0 / 1 forces a form)
         static const int wg_env = [] {
             const char *e = getenv("PSS_V1X_DRAWS_WG");
