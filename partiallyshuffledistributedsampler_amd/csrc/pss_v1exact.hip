@@ -155,7 +155,8 @@ struct V1xBig {
     uint32_t B;             // slice length: min(shuffle_buffer, num_samples)
     uint32_t *J, *CNT, *LST, *NXT;
     uint32_t xb;            // 256-entry blocks per window (the flat kernels' x extent)
-    uint32_t xcd;           // 1: XCD-major flat grid (v1x_flat_grid)
+    uint32_t xcd;           // 1: XCD-major flat grid (v1x_block)
+    uint32_t fcount;        // 1: the draws count the buckets (no k_v1x_count)
 };
 
 // The flat kernels (count, scatter, parent, out) make random accesses inside one window's
@@ -176,6 +177,8 @@ __device__ __forceinline__ int v1x_len(const Geometry &g, int64_t w) {
     return (int)(g.ns - wb < g.B ? g.ns - wb : g.B);
 }
 
+// b.fcount: each draw also counts its bucket (CNT[j]++, a fire-and-forget atomic beside the
+// latency-bound draws) and k_v1x_count is skipped
 __global__ __launch_bounds__(64) void k_v1x_draws32(Geometry g, V1xBig b, int64_t epoch) {
     __shared__ uint32_t mt[kMtN];
     const uint64_t job = b.j0 + blockIdx.x;
@@ -183,9 +186,13 @@ __global__ __launch_bounds__(64) void k_v1x_draws32(Geometry g, V1xBig b, int64_
     const int n = v1x_len(g, w);
     if (n <= 1) return;
     uint32_t *jw = b.J + (size_t)blockIdx.x * b.B;
+    uint32_t *cnt = b.CNT + (size_t)blockIdx.x * ((size_t)b.B + 1);
     mt_seed_int(mt, w == 0 ? epoch : epoch + w * 10000);
     mt_draws(mt, (uint32_t)(n - 1), [&](uint32_t d) { return (uint32_t)n - d; },
-             [&](uint32_t d, uint32_t r) { jw[n - 1 - (int)d] = r; });
+             [&](uint32_t d, uint32_t r) {
+                 jw[n - 1 - (int)d] = r;
+                 if (b.fcount) atomicAdd(&cnt[r], 1u);
+             });
 }
 
 // The same draws with a workgroup per window (pss_mt.h mt_draws_wg): few, long windows (C5: 2^20
@@ -197,10 +204,14 @@ __global__ __launch_bounds__(kMtWgThreads) void k_v1x_draws32_wg(Geometry g, V1x
     const int n = v1x_len(g, w);
     if (n <= 1) return;
     uint32_t *jw = b.J + (size_t)blockIdx.x * b.B;
+    uint32_t *cnt = b.CNT + (size_t)blockIdx.x * ((size_t)b.B + 1);
     if (threadIdx.x < 64) mt_seed_int(sh.mt[0], w == 0 ? epoch : epoch + w * 10000);
     __syncthreads();
     mt_draws_wg(sh, 0, (uint32_t)(n - 1), [&](uint32_t d) { return (uint32_t)n - d; },
-                [&](uint32_t d, uint32_t r) { jw[n - 1 - (int)d] = r; });
+                [&](uint32_t d, uint32_t r) {
+                    jw[n - 1 - (int)d] = r;
+                    if (b.fcount) atomicAdd(&cnt[r], 1u);
+                });
 }
 
 // slot of the pass and block of the window's entries (v1x_block)
@@ -382,9 +393,14 @@ static hipError_t launch_v1_exact_big(const Geometry &g, const RankDesc *ranks, 
             return e ? atoi(e) : -1;
         }();
         const bool wg = wg_env == 0 || wg_env == 1 ? wg_env == 1 : b.nj < 1024;
+        static const bool fcount_env = [] {   // A/B knob: PSS_V1X_FUSED_COUNT=1 counts in the draws
+            const char *e = getenv("PSS_V1X_FUSED_COUNT");
+            return e && e[0] == '1';
+        }();
+        b.fcount = fcount_env ? 1u : 0u;
         if (wg) hipLaunchKernelGGL(k_v1x_draws32_wg, dim3(b.nj), dim3(kMtWgThreads), 0, s, g, b, epoch);
         else hipLaunchKernelGGL(k_v1x_draws32, dim3(b.nj), dim3(64), 0, s, g, b, epoch);
-        hipLaunchKernelGGL(k_v1x_count, flat, dim3(256), 0, s, g, b);
+        if (!b.fcount) hipLaunchKernelGGL(k_v1x_count, flat, dim3(256), 0, s, g, b);
         hipLaunchKernelGGL(k_v1x_scan, dim3(b.nj), dim3(kV1xScanNT), 0, s, g, b);
         hipLaunchKernelGGL(k_v1x_scatter, flat, dim3(256), 0, s, g, b);
         hipLaunchKernelGGL(k_v1x_parent, flat, dim3(256), 0, s, g, b);

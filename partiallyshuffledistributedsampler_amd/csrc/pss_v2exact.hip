@@ -395,10 +395,15 @@ __global__ __launch_bounds__(256) void k_v2x_gsplit(V2xGeo x, uint32_t nr, uint3
     SP[gi] = r;
 }
 
-// decoded pool2 windows (as sequences of B steps) -> Q2[window step] = its pool2 rank
-__global__ __launch_bounds__(256) void k_v2x_q2(uint64_t n, uint32_t B, const uint32_t *__restrict__ V,
+// decoded pool2 windows (as sequences of B steps) -> Q2[window step] = its pool2 rank.  The
+// writes are random inside one window, so the grid is XCD-major over chunks of xb blocks (about
+// a window; v1x_block in pss_v1exact.hip): workgroup L (on XCD L mod 8) takes block
+// xb (8 (L / 8 / xb) + L mod 8) + (L / 8) mod xb, and each window's lines stay in one L2.
+__global__ __launch_bounds__(256) void k_v2x_q2(uint64_t n, uint32_t B, uint32_t xb, const uint32_t *__restrict__ V,
                                                 const uint32_t *__restrict__ O, uint32_t *__restrict__ Q2) {
-    const uint64_t gi = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    const uint64_t L = blockIdx.x, q = L >> 3;
+    const uint64_t blk = xb ? (uint64_t)xb * (8u * (q / xb) + (L & 7u)) + q % xb : L;
+    const uint64_t gi = blk * 256 + threadIdx.x;
     if (gi >= n) return;
     const uint64_t seq = gi / B;
     Q2[seq * B + O[gi]] = V[gi];
@@ -822,9 +827,15 @@ static hipError_t v2x_pass(const Geometry &g, const V2xGeo &x, const RankDesc *r
         });
         uint32_t *wv = V, *wo = O, *wvd = Vd, *wod = Od;
         v2x_global_levels(xw, nseq, wv, wo, wvd, wod, SP, s);
-        const uint64_t nw = (uint64_t)nseq * x.B;
-        hipLaunchKernelGGL(k_v2x_q2, dim3((uint32_t)v2x_cdiv((int64_t)nw, 256)), dim3(256), 0, s, nw, x.B,
-                           wv, wo, Q2);
+        const uint64_t nw = (uint64_t)nseq * x.B, nblk = (uint64_t)v2x_cdiv((int64_t)nw, 256);
+        static const bool q2_xcd = [] {   // A/B knob: PSS_V2X_Q2_XCD=1 takes the XCD-major grid
+            const char *e = getenv("PSS_V2X_Q2_XCD");
+            return e && e[0] == '1';
+        }();
+        uint32_t xb = q2_xcd ? (uint32_t)v2x_cdiv((int64_t)x.B, 256) : 0u;
+        uint64_t grid = xb ? (uint64_t)xb * 8u * (uint64_t)v2x_cdiv((int64_t)v2x_cdiv((int64_t)nblk, xb), 8) : nblk;
+        if (grid >= ((uint64_t)1 << 24)) { xb = 0u; grid = nblk; }   // (threads below 2^32)
+        hipLaunchKernelGGL(k_v2x_q2, dim3((uint32_t)grid), dim3(256), 0, s, nw, x.B, xb, wv, wo, Q2);
     }
     // pool1 tiles (and, for B <= kTile, the windows in the same launch)
     const uint32_t per_rank = x.tiles1 + (big_windows ? 0u : x.S);
