@@ -188,35 +188,11 @@ __device__ __forceinline__ void tail_round_keys(const Geometry &g, uint32_t rank
     }
 }
 
-// Per-launch key table (k_v2_keys): for local rank rl at p + rl * stride:
-//   [0, 2) slot key, [8, 16) tail round keys, [16 + 8 (w - 1), +8) round keys of pool2 window w.
-// p == nullptr: the kernels derive the keys with Philox themselves.
-
-__device__ __forceinline__ SlotKey slot_key_t(const Geometry &g, uint32_t rank, const KeyTab &kt,
-                                              int32_t rl) {
-    if (!kt.p) return slot_key(g, rank);
-    const uint32_t *b = kt.p + rl * kt.stride;
-    return SlotKey{b[0], b[1]};
-}
-
-__device__ __forceinline__ void tail_keys_t(const Geometry &g, uint32_t rank, const KeyTab &kt,
-                                            int32_t rl, uint32_t k[kRoundKeyWords]) {
-    if (!kt.p) { tail_round_keys(g, rank, k); return; }
-    const uint32_t *b = kt.p + rl * kt.stride + 8;
-#pragma unroll
-    for (int i = 0; i < kRoundKeyWords; i++) k[i] = b[i];
-}
-
 // round keys of windows [w_lo, w_lo + nwin) into LDS (all threads of the block take part)
-__device__ __forceinline__ void stage_keys_t(const Geometry &g, uint32_t rank, int64_t w_lo, int nwin,
-                                             uint32_t *rk, const KeyTab &kt, int32_t rl) {
-    if (!kt.p) {
-        for (int j = threadIdx.x; j < nwin; j += blockDim.x)
-            window_round_keys(g, rank, w_lo + j, rk + kRoundKeyWords * j);
-        return;
-    }
-    const uint32_t *b = kt.p + rl * kt.stride + 16 + kRoundKeyWords * (w_lo - 1);
-    for (int i = threadIdx.x; i < nwin * kRoundKeyWords; i += blockDim.x) rk[i] = b[i];
+__device__ __forceinline__ void stage_keys(const Geometry &g, uint32_t rank, int64_t w_lo, int nwin,
+                                           uint32_t *rk) {
+    for (int j = threadIdx.x; j < nwin; j += blockDim.x)
+        window_round_keys(g, rank, w_lo + j, rk + kRoundKeyWords * j);
 }
 
 // virtual index inserted at step t (pool2 window w = 1 + t/B in Feistel order), given the

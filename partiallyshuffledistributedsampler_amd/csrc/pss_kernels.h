@@ -22,11 +22,6 @@ struct Geometry {       // per-epoch constants of one sampler
     uint32_t key0, key1;  // Philox key = epoch_key(seed, epoch)
 };
 
-struct KeyTab {         // per-launch table of Philox-derived keys (pss_device.h layout)
-    const uint32_t *p;  // nullptr: kernels derive the keys themselves
-    int64_t stride;     // words per local rank
-};
-
 struct V2Plan {         // slot-machine tiling of one V2 stream
     int64_t P1;         // slots = min(B, ns)
     int64_t T;          // replacement steps = ns - P1
@@ -152,7 +147,7 @@ size_t v2_val_bytes(const Geometry &g, int32_t nr);
 hipError_t launch_v2_tail_vals(const Geometry &g, const V2Plan &pl, const RankDesc *ranks,
                                int32_t rank_lo, int32_t nr, const uint32_t *VAL, int64_t pos_lo,
                                int64_t count, int64_t *out, hipStream_t s,
-                               KeyTab kt, const MapArgs *mapped = nullptr);
+                               const MapArgs *mapped = nullptr);
 // pools beyond LDS (P1 > kLdsSlotMax): the grouped slot machine (pss_v2grp.hip); its key
 // table and per-tile tables live in val_ws (v2_val_bytes)
 bool v2_grouped(const Geometry &g);

@@ -239,7 +239,7 @@ struct V1Plan {
     int64_t per_wave;          // super-blocks per wave
     int64_t w_lo, nw;          // windows of the key table
     uint32_t B, hB, walk_full, fast_ok;
-    uint32_t pairs;            // fast super-blocks in the 16-B pair layout (PSS_V1_PAIRS=0: off)
+    uint32_t pairs;            // fast super-blocks in the 16-B pair layout (on; 8-B stores measured slower)
 };
 
 // One wave per (rank, run of per_wave super-blocks).  Lane l computes positions p0 + 64 j + l,
@@ -251,7 +251,7 @@ __global__ __launch_bounds__(64) void k_v1_feistel(Geometry g, V1Plan vp, const 
                                                    int32_t rank_lo, const uint32_t *__restrict__ kt,
                                                    int64_t pos_lo, int64_t count,
                                                    int64_t *__restrict__ out, MapArgs ma) {
-    extern __shared__ uint32_t v1_pad[];   // occupancy limiter only (PSS_V1_WAVES_PER_CU)
+    extern __shared__ uint32_t v1_pad[];   // occupancy limiter only (8 waves per CU)
     if (vp.nsb < 0) v1_pad[threadIdx.x] = 0;
     const int lane = threadIdx.x;
     const int64_t waves_per_rank = (vp.nsb + vp.per_wave - 1) / vp.per_wave;
@@ -539,26 +539,13 @@ hipError_t launch_v1(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, 
     vp.walk_full = vp.B != (1u << (2 * vp.hB));
     // fast super-blocks: inside one full window that needs no cycle walking
     vp.fast_ok = g.shuffle && !vp.walk_full && (g.B % 256) == 0;
-    static const uint32_t pairs_env = [] {   // A/B knob: 16-byte pair stores on fast super-blocks
-        const char *e = getenv("PSS_V1_PAIRS");
-        return (uint32_t)!(e && e[0] == '0');
-    }();
-    vp.pairs = pairs_env;
-    // One round of waves: the stream is cut into exactly as many waves as the chip holds at
-    // PSS_V1_WAVES_PER_CU resident waves per CU (default 8: two per SIMD, an LDS claim caps it),
-    // each a run of consecutive super-blocks.  A round-1/2 shape of 16 super-blocks per wave at
-    // full occupancy (3 rounds of 8 waves per SIMD) stored at 4.3-4.6 TB/s (C2 V1: 184 us), one
-    // round of 2 per SIMD at 4.6 (175 us): fewer stores in flight, no tail round.
-    static const int64_t wpc = [] {
-        const char *e = getenv("PSS_V1_WAVES_PER_CU");
-        const long v = e ? atol(e) : 8;
-        return (int64_t)(v > 0 && v <= 32 ? v : 8);
-    }();
-    static const int64_t per_env = [] {   // A/B knob: super-blocks per wave (0: one round)
-        const char *e = getenv("PSS_V1_PER_WAVE");
-        const long v = e ? atol(e) : 0;
-        return (int64_t)(v > 0 && v <= 4096 ? v : 0);
-    }();
+    vp.pairs = 1;   // 16-byte pair stores on fast super-blocks
+    // One round of waves: the stream is cut into exactly as many waves as the chip holds at 8
+    // resident waves per CU (two per SIMD, an LDS claim caps it), each a run of consecutive
+    // super-blocks.  A round-1/2 shape of 16 super-blocks per wave at full occupancy (3 rounds
+    // of 8 waves per SIMD) stored at 4.3-4.6 TB/s (C2 V1: 184 us), one round of 2 per SIMD at
+    // 4.6 (175 us): fewer stores in flight, no tail round.
+    constexpr int64_t wpc = 8;
     // the mapped form reads the bucket index and the prefix for every id (dependent global
     // loads): it wants latency hiding, i.e. the full 32 waves per CU, where the plain form stores
     // best at one round of 8 (C2 V1 mapped: 0.55-0.63 ms at 8 per CU, round 2's 0.32-0.36 at
@@ -566,7 +553,7 @@ hipError_t launch_v1(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, 
     const int64_t wpc_run = mapped ? 32 : wpc;
     const int64_t slots_per_rank = wpc_run * gcus_v1() / nr;
     // (mapped: round 2's shape, runs of 16 super-blocks at full occupancy, several rounds)
-    int64_t per = per_env ? per_env : mapped ? 16 : cdiv(vp.nsb, slots_per_rank > 1 ? slots_per_rank : 1);
+    int64_t per = mapped ? 16 : cdiv(vp.nsb, slots_per_rank > 1 ? slots_per_rank : 1);
     if (per < 1) per = 1;
     vp.per_wave = per;
     const int64_t waves = (int64_t)nr * cdiv(vp.nsb, per);

@@ -576,20 +576,16 @@ int generate_v2_lookahead(pss_sampler *h, const pss::Geometry &g, int32_t rank_l
     if (!h->side) {
         int least = 0, greatest = 0;
         PSS_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
-        static const bool side_hi = [] {   // A/B knob: side stream at the greatest priority
-            const char *e = getenv("PSS_V2_LOOKAHEAD_PRIO");
-            return e && e[0] == 'h';
-        }();
-        PSS_HIP(hipStreamCreateWithPriority(&h->side, hipStreamNonBlocking, side_hi ? greatest : least));
+        // the lowest priority: at the highest the C2 step was slower (519 vs 526 G idx/s, round 2)
+        (void)greatest;
+        PSS_HIP(hipStreamCreateWithPriority(&h->side, hipStreamNonBlocking, least));
         for (hipEvent_t &e : h->ev_read) PSS_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         for (hipEvent_t &e : h->ev_done) PSS_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         PSS_HIP(hipEventCreateWithFlags(&h->ev_side, hipEventDisableTiming));
     }
-    static const int depth = [] {   // epochs queued ahead: 2 (default) keeps the wait for a pass
-        const char *e = getenv("PSS_V2_LOOKAHEAD_DEPTH");   // off the replay's critical path
-        const int d = e ? atoi(e) : 2;
-        return d < 1 ? 1 : (d > 2 ? 2 : d);
-    }();
+    // epochs queued ahead: 2 keeps the wait for a pass off the replay's critical path (one
+    // epoch ahead: the replay waits 33 us per step, 491 against 526 G idx/s, round 2)
+    constexpr int depth = 2;
     const pss_sampler::Shape shape{g.N, g.ns, g.B, pos_lo, count, g.R, rank_lo, nr, h->emit_path};
     auto held = [&](int b) {
         for (const auto &p : h->pend) if (p.valid && p.buf == b) return true;

@@ -156,7 +156,6 @@ struct V1xBig {
     uint32_t *J, *CNT, *LST, *NXT;
     uint32_t xb;            // 256-entry blocks per window (the flat kernels' x extent)
     uint32_t xcd;           // 1: XCD-major flat grid (v1x_block)
-    uint32_t fcount;        // 1: the draws count the buckets (no k_v1x_count)
 };
 
 // The flat kernels (count, scatter, parent, out) make random accesses inside one window's
@@ -177,8 +176,9 @@ __device__ __forceinline__ int v1x_len(const Geometry &g, int64_t w) {
     return (int)(g.ns - wb < g.B ? g.ns - wb : g.B);
 }
 
-// b.fcount: each draw also counts its bucket (CNT[j]++, a fire-and-forget atomic beside the
-// latency-bound draws) and k_v1x_count is skipped
+// Each draw also counts its bucket (CNT[j]++, a fire-and-forget atomic beside the latency-bound
+// draws), so no counting pass re-reads J: C5 V1 exact 17.3 -> 15.4 ms (round 4, same box,
+// profiles/r04/ab_v1x_fcount/)
 __global__ __launch_bounds__(64) void k_v1x_draws32(Geometry g, V1xBig b, int64_t epoch) {
     __shared__ uint32_t mt[kMtN];
     const uint64_t job = b.j0 + blockIdx.x;
@@ -191,7 +191,7 @@ __global__ __launch_bounds__(64) void k_v1x_draws32(Geometry g, V1xBig b, int64_
     mt_draws(mt, (uint32_t)(n - 1), [&](uint32_t d) { return (uint32_t)n - d; },
              [&](uint32_t d, uint32_t r) {
                  jw[n - 1 - (int)d] = r;
-                 if (b.fcount) atomicAdd(&cnt[r], 1u);
+                 atomicAdd(&cnt[r], 1u);
              });
 }
 
@@ -210,7 +210,7 @@ __global__ __launch_bounds__(kMtWgThreads) void k_v1x_draws32_wg(Geometry g, V1x
     mt_draws_wg(sh, 0, (uint32_t)(n - 1), [&](uint32_t d) { return (uint32_t)n - d; },
                 [&](uint32_t d, uint32_t r) {
                     jw[n - 1 - (int)d] = r;
-                    if (b.fcount) atomicAdd(&cnt[r], 1u);
+                    atomicAdd(&cnt[r], 1u);
                 });
 }
 
@@ -224,12 +224,6 @@ __global__ __launch_bounds__(kMtWgThreads) void k_v1x_draws32_wg(Geometry g, V1x
     const uint32_t *J = b.J + (size_t)slot * b.B;                                  \
     uint32_t *CNT = b.CNT + (size_t)slot * ((size_t)b.B + 1);                      \
     (void)J; (void)CNT;
-
-__global__ __launch_bounds__(256) void k_v1x_count(Geometry g, V1xBig b) {
-    V1X_SLOT_PROLOGUE
-    const int k = (int)(xblk * 256 + threadIdx.x);
-    if (k >= 1 && k < n) atomicAdd(&CNT[J[k]], 1u);
-}
 
 // exclusive scan of CNT[0, n) in place, one workgroup per window, in tiles of kV1xScanNT x 8
 // counts: coalesced loads into LDS (skewed one word per 32), each thread scans 8 consecutive
@@ -379,12 +373,9 @@ static hipError_t launch_v1_exact_big(const Geometry &g, const RankDesc *ranks, 
         hipError_t e = hipMemsetAsync(b.CNT, 0, sizeof(uint32_t) * (size_t)b.nj * ((size_t)B + 1), s);
         if (e != hipSuccess) return e;
         b.xb = (B + 255) / 256;
-        static const bool xcd_env = [] {   // A/B knob: PSS_V1X_XCD=0 keeps the (x, slot) grid
-            const char *e = getenv("PSS_V1X_XCD");
-            return !(e && e[0] == '0');
-        }();
-        // XCD-major only while the 1-D grid stays below 2^32 threads
-        b.xcd = xcd_env && (uint64_t)b.xb * (((uint64_t)b.nj + 7) / 8) * 8 < ((uint64_t)1 << 24) ? 1u : 0u;
+        // XCD-major only while the 1-D grid stays below 2^32 threads (round 3: the scatter's
+        // random LST writes 8.2 -> 5.2 ms at C5 against the (x, slot) grid)
+        b.xcd = (uint64_t)b.xb * (((uint64_t)b.nj + 7) / 8) * 8 < ((uint64_t)1 << 24) ? 1u : 0u;
         const dim3 flat = b.xcd ? dim3((uint32_t)((uint64_t)b.xb * (((uint64_t)b.nj + 7) / 8) * 8))
                                 : dim3(b.xb, b.nj);
         // few windows: a workgroup per window's MT stream (PSS_V1X_DRAWS_WG=0 / 1 forces a form)
@@ -393,14 +384,8 @@ static hipError_t launch_v1_exact_big(const Geometry &g, const RankDesc *ranks, 
             return e ? atoi(e) : -1;
         }();
         const bool wg = wg_env == 0 || wg_env == 1 ? wg_env == 1 : b.nj < 1024;
-        static const bool fcount_env = [] {   // A/B knob: PSS_V1X_FUSED_COUNT=1 counts in the draws
-            const char *e = getenv("PSS_V1X_FUSED_COUNT");
-            return e && e[0] == '1';
-        }();
-        b.fcount = fcount_env ? 1u : 0u;
         if (wg) hipLaunchKernelGGL(k_v1x_draws32_wg, dim3(b.nj), dim3(kMtWgThreads), 0, s, g, b, epoch);
         else hipLaunchKernelGGL(k_v1x_draws32, dim3(b.nj), dim3(64), 0, s, g, b, epoch);
-        if (!b.fcount) hipLaunchKernelGGL(k_v1x_count, flat, dim3(256), 0, s, g, b);
         hipLaunchKernelGGL(k_v1x_scan, dim3(b.nj), dim3(kV1xScanNT), 0, s, g, b);
         hipLaunchKernelGGL(k_v1x_scatter, flat, dim3(256), 0, s, g, b);
         hipLaunchKernelGGL(k_v1x_parent, flat, dim3(256), 0, s, g, b);

@@ -29,29 +29,6 @@ __device__ __forceinline__ void tile_bounds(const V2Plan &pl, int64_t tile, int6
     thi = tlo + pl.L < pl.T ? tlo + pl.L : pl.T;
 }
 
-// ---- key table: one thread per (local rank, item) --------------------------------------------
-__global__ __launch_bounds__(256) void k_v2_keys(Geometry g, int32_t rank_lo, int64_t nwin_tot,
-                                                 int64_t stride, uint32_t *__restrict__ kt) {
-    const int32_t rl = (int32_t)blockIdx.y;
-    const uint32_t rank = (uint32_t)(rank_lo + rl);
-    const int64_t item = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    uint32_t *b = kt + rl * stride;
-    if (item == 0) {
-        const SlotKey sk = slot_key(g, rank);
-        b[0] = sk.s0; b[1] = sk.s1;
-    } else if (item == 1) {
-        uint32_t k[kRoundKeyWords];
-        tail_round_keys(g, rank, k);
-#pragma unroll
-        for (int i = 0; i < kRoundKeyWords; i++) b[8 + i] = k[i];
-    } else if (item < nwin_tot + 2) {
-        uint32_t k[kRoundKeyWords];
-        window_round_keys(g, rank, item - 1, k);
-#pragma unroll
-        for (int i = 0; i < kRoundKeyWords; i++) b[16 + kRoundKeyWords * (item - 2) + i] = k[i];
-    }
-}
-
 #ifdef PSS_STAMPS   // diagnostic build only (tools/stamp_v2.hip): per-workgroup phase clocks
 __device__ uint64_t pss_stamps[1 << 16][8];
 #define PSS_STAMP(i) do { if (threadIdx.x == 0 && blockIdx.x < (1u << 16)) pss_stamps[blockIdx.x][i] = __builtin_amdgcn_s_memtime(); } while (0)
@@ -61,15 +38,11 @@ __device__ uint64_t pss_stamps[1 << 16][8];
 #endif
 
 // ---- pass A, LDS ----------------------------------------------------------------------------
-// Per tile: the last step (tile-local, +1) that drew each slot, then that step's inserted value.
-//   ORDERED (NT = 64, one wave per tile): the wave walks its steps in order with PLAIN stores
-//     -- a later instruction overwrites an earlier one and, inside one store, the highest lane
-//     wins (start-up check), so each slot ends with its last step.  No LDS atomics.
-//   otherwise (NT = 256): any order, ds_max.
-template <int NT, bool ORDERED, bool POW2>
+// Per tile: the last step (tile-local, +1) that drew each slot (ds_max in any order), then that
+// step's inserted value.
+template <int NT, bool POW2>
 __global__ __launch_bounds__(NT) void k_v2_lastocc(Geometry g, V2Plan pl, int32_t rank_lo,
-                                                   int64_t ng, uint32_t *__restrict__ VAL,
-                                                   KeyTab kt) {
+                                                   int64_t ng, uint32_t *__restrict__ VAL) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     PSS_STAMP(0);
     const int P1 = (int)pl.P1;
@@ -87,8 +60,8 @@ __global__ __launch_bounds__(NT) void k_v2_lastocc(Geometry g, V2Plan pl, int32_
     if (threadIdx.x == 0) pss_stamps[blockIdx.x][4] = __builtin_amdgcn_s_memrealtime();
 #endif
     for (int s = threadIdx.x; s < P1; s += NT) lastT[s] = 0;
-    stage_keys_t(g, rank, w_lo, nwin, rk, kt, rl);
-    const SlotKey sk = slot_key_t(g, rank, kt, rl);
+    stage_keys(g, rank, w_lo, nwin, rk);
+    const SlotKey sk = slot_key(g, rank);
     __syncthreads();
     PSS_STAMP(1);
     // whole blocks of 8*NT steps run branch-free with 8 independent hashes per thread
@@ -102,15 +75,12 @@ __global__ __launch_bounds__(NT) void k_v2_lastocc(Geometry g, V2Plan pl, int32_
     for (uint32_t base = 0; base < nfull; base += BLK) {
         pace.step(base);
         // thread -> 8 steps: (t, t + 64) pairs of 4 different 128-step groups, so that with
-        // a paired draw (POW2) one hash serves two steps.  ORDERED (one wave) keeps step order:
-        // j-th store covers steps base + 64 j + lane.
+        // a paired draw (POW2) one hash serves two steps
         uint32_t st[8], k[8];
 #pragma unroll
-        for (int j = 0; j < 8; j++) {
-            if (ORDERED) st[j] = base + 64u * j + threadIdx.x;
-            else st[j] = base + 128u * ((threadIdx.x >> 6) + (NT / 64) * (j >> 1)) + 64u * (j & 1) + (threadIdx.x & 63u);
-        }
-        if (POW2 && !ORDERED) {
+        for (int j = 0; j < 8; j++)
+            st[j] = base + 128u * ((threadIdx.x >> 6) + (NT / 64) * (j >> 1)) + 64u * (j & 1) + (threadIdx.x & 63u);
+        if (POW2) {
             // t0 + base is a multiple of 256, so the pair index of st[j] (j even) is
             // (t0 + base) / 2 + 64 (wave + NT/64 (j/2)) + lane: one add of a per-thread constant
             const uint32_t pb = (t0 + base) >> 1;
@@ -126,17 +96,13 @@ __global__ __launch_bounds__(NT) void k_v2_lastocc(Geometry g, V2Plan pl, int32_
             for (int j = 0; j < 8; j++) k[j] = slot_draw(t0 + st[j], sk.s0, sk.s1, (uint32_t)P1);
         }
 #pragma unroll
-        for (int j = 0; j < 8; j++) {
-            if (ORDERED) lastT[k[j]] = st[j] + 1u;
-            else atomicMax(&lastT[k[j]], st[j] + 1u);
-        }
+        for (int j = 0; j < 8; j++) atomicMax(&lastT[k[j]], st[j] + 1u);
     }
     for (uint32_t base = nfull; base < n; base += NT) {
         const uint32_t b = base + threadIdx.x;
         if (b < n) {
             const uint32_t kk = slot_draw(t0 + b, sk.s0, sk.s1, (uint32_t)P1);
-            if (ORDERED) lastT[kk] = b + 1u;
-            else atomicMax(&lastT[kk], b + 1u);
+            atomicMax(&lastT[kk], b + 1u);
         }
     }
     __syncthreads();
@@ -378,7 +344,7 @@ __global__ __launch_bounds__(64) void k_v2_emit(Geometry g, V2Plan pl,
             }
         }
     }
-    stage_keys_t(g, rank, w_lo, nwin, rk, KeyTab{nullptr, 0}, rl);
+    stage_keys(g, rank, w_lo, nwin, rk);
     __syncthreads();
     EmitCtx<FOLD> c;
     c.lane = lane;
@@ -462,8 +428,8 @@ __global__ __launch_bounds__(64) void k_v2_emit_x(Geometry g, V2Plan pl,
                                                   int32_t rank_lo, int64_t g_lo, int64_t ng,
                                                   const uint32_t *__restrict__ VAL,
                                                   int64_t pos_lo, int64_t count, int do_tail,
-                                                  int64_t *__restrict__ out, KeyTab kt, MapArgs ma,
-                                                  RankArgs ra, int use_ra) {
+                                                  int64_t *__restrict__ out, MapArgs ma, RankArgs ra,
+                                                  int use_ra) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     PSS_TWO_WAVES_PER_SIMD();
 #ifdef PSS_STAMPS
@@ -500,22 +466,7 @@ __global__ __launch_bounds__(64) void k_v2_emit_x(Geometry g, V2Plan pl,
     const uint32_t thi = pl.T32 - tlo < pl.L32 ? pl.T32 : tlo + pl.L32;
     const uint32_t w_lo = 1 + tlo / B;
     const int nwin = (int)(1 + (thi - 1) / B - w_lo + 1);
-    // the tile's window keys and the slot key are independent of the slot table: their loads
-    // are issued first and land while the table streams in
-    constexpr int kKeyPre = 3;                    // nwin <= L / B + 2 <= 18 windows of 8 words
-    const int nkw = nwin * kRoundKeyWords;
-    uint32_t kpre[kKeyPre];
-    SlotKey sk;
-    const bool key_pre = kt.p && nkw <= 64 * kKeyPre;
-    if (key_pre) {
-        const uint32_t *kb = kt.p + rl * kt.stride;
-        sk = SlotKey{kb[0], kb[1]};
-        kb += 16 + kRoundKeyWords * (w_lo - 1);
-#pragma unroll
-        for (int i = 0; i < kKeyPre; i++) kpre[i] = lane + 64 * i < nkw ? kb[lane + 64 * i] : 0u;
-    } else {
-        sk = slot_key_t(g, rank, kt, rl);
-    }
+    const SlotKey sk = slot_key(g, rank);
     {   // slot table at the tile's start: 16-byte loads, up to 16 per lane in flight (the whole
         // 16 KB table of P1 = 4096 in one round trip); slots the previous tile never drew walk
         // back further (probability e^-(L/P1))
@@ -555,13 +506,7 @@ __global__ __launch_bounds__(64) void k_v2_emit_x(Geometry g, V2Plan pl,
             }
         }
     }
-    if (key_pre) {
-#pragma unroll
-        for (int i = 0; i < kKeyPre; i++)
-            if (lane + 64 * i < nkw) rk[lane + 64 * i] = kpre[i];
-    } else {
-        stage_keys_t(g, rank, w_lo, nwin, rk, kt, rl);
-    }
+    stage_keys(g, rank, w_lo, nwin, rk);
     __syncthreads();
     // tile-local step tl = t - tlo (tlo is a multiple of 256); the tile emits tl in [e_lo, e_hi)
     const int64_t pos_hi = pos_lo + count;
@@ -784,7 +729,7 @@ __global__ __launch_bounds__(64) void k_v2_emit_x(Geometry g, V2Plan pl,
         __builtin_amdgcn_s_setprio(3);
         __syncthreads();
         uint32_t tk[kRoundKeyWords];
-        tail_keys_t(g, rank, kt, rl, tk);
+        tail_round_keys(g, rank, tk);
         const uint32_t hT = feistel_half_bits(P1);
         int64_t *ot = out + (int64_t)rl * count - pos_lo + pl.T;
         const int64_t etail = (int64_t)rl * count - pos_lo + pl.T;
@@ -888,13 +833,13 @@ __global__ __launch_bounds__(256) void k_v2_tail_f(Geometry g, V2Plan pl,
                                                   const RankDesc *__restrict__ ranks,
                                                   int32_t rank_lo, const uint32_t *__restrict__ VAL,
                                                   int64_t pos_lo, int64_t count,
-                                                  int64_t *__restrict__ out, KeyTab kt, MapArgs ma) {
+                                                  int64_t *__restrict__ out, MapArgs ma) {
     const int32_t rl = (int32_t)blockIdx.y;
     const uint32_t rank = (uint32_t)(rank_lo + rl);
     const RankDesc rd = ranks[rank];
     const uint32_t P1 = (uint32_t)pl.P1;
     uint32_t tk[kRoundKeyWords];
-    tail_keys_t(g, rank, kt, rl, tk);
+    tail_round_keys(g, rank, tk);
     const uint32_t hT = feistel_half_bits(P1);
     const uint32_t *VALr = VAL + (int64_t)rl * pl.G * pl.P1;
     int64_t *o = out + (int64_t)rl * count - pos_lo;
@@ -942,51 +887,24 @@ V2Plan v2_plan(const Geometry &g, int32_t nr) {
     p.P1 = g.B < g.ns ? g.B : g.ns;
     p.T = g.ns - p.P1;
     p.fold = g.ns <= (int64_t)1 << 24;
-    static const int64_t mult_env = [] {
-        const char *e = getenv("PSS_V2_TILE_MULT");   // tuning knob: tile = mult * P1 steps
-        const long v = e ? atol(e) : 0;
-        return (int64_t)(v > 0 ? (v < kMaxTileMult ? v : kMaxTileMult) : 0);
-    }();
-    static const int64_t wpc_env = [] {   // tuning knob: emit waves per CU the tiling targets
-        const char *e = getenv("PSS_V2_WPC");
-        const long v = e ? atol(e) : 0;
-        return (int64_t)(v > 0 ? v : 0);
-    }();
     // emit wave LDS: Feistel keys of up to kMaxTileMult + 2 windows, the slot table, the probe
     const int64_t keys = (int64_t)kRoundKeyWords * 4 * (kMaxTileMult + 2);
     const int64_t lds = keys + p.P1 * 4 + (p.fold ? 0 : kMarkBytes);
-    // waves per CU the LDS admits, rounded down to whole SIMD quads (balanced SIMDs), <= 16;
-    // the launch pads its LDS so that no CU takes more (dispatch would otherwise stack a 9th)
+    // waves per CU the LDS admits, rounded down to whole SIMD quads (balanced SIMDs), <= 16
     int64_t wpc = kCuLdsBytes / lds;
     wpc = wpc > 16 ? 16 : wpc;
     if (wpc >= 4) wpc &= ~3;
-    if (wpc_env && wpc_env < wpc) wpc = wpc_env;
-    p.emit_lds = lds;
     // No LDS padding: k_v2_emit_x claims VGPRs for two waves per SIMD (PSS_TWO_WAVES_PER_SIMD),
     // which caps a CU at eight replay waves, and the LDS left over (25 KB at P1 = 4096) takes a
-    // last-occurrence workgroup of the next epoch's lookahead beside them (C2 487-496 ->
-    // 511-516 G idx/s, same box).  PSS_V2_LDS_PAD=1 pads as round 1 did (A/B knob).
-    static const bool pad = [] {
-        const char *e = getenv("PSS_V2_LDS_PAD");
-        return e && e[0] == '1';
-    }();
-    if (pad && wpc >= 1 && kCuLdsBytes / (wpc + 1) >= lds) p.emit_lds = kCuLdsBytes / (wpc + 1) + 16;
-    static const int64_t lds_env = [] {   // experiment knob: explicit emit LDS bytes per wave
-        const char *e = getenv("PSS_V2_EMIT_LDS");
-        return (int64_t)(e ? atol(e) : 0);
-    }();
-    if (lds_env > lds) p.emit_lds = lds_env;
-    int64_t L;
-    if (mult_env) {
-        L = mult_env * p.P1;
-    } else {
-        // one round of waves: tiles = waves per CU x CUs spread over the nr streams
-        const int64_t waves = wpc * device_cus();
-        const int64_t per_rank = cdiv(waves, nr > 0 ? nr : 1);
-        L = p.T > 0 ? cdiv(p.T, per_rank) : p.P1;
-        const int64_t lo = kMinTileMult * p.P1, hi = kMaxTileMult * p.P1;
-        L = L < lo ? lo : (L > hi ? hi : L);
-    }
+    // last-occurrence workgroup of the next epoch's lookahead beside them (round 2: C2 487-496
+    // -> 511-516 G idx/s against round 1's LDS padding, same box).
+    p.emit_lds = lds;
+    // one round of waves: tiles = waves per CU x CUs spread over the nr streams
+    const int64_t waves = wpc * device_cus();
+    const int64_t per_rank = cdiv(waves, nr > 0 ? nr : 1);
+    int64_t L = p.T > 0 ? cdiv(p.T, per_rank) : p.P1;
+    const int64_t lo = kMinTileMult * p.P1, hi = kMaxTileMult * p.P1;
+    L = L < lo ? lo : (L > hi ? hi : L);
     p.L = cdiv(L, 256) * 256;
     p.G = p.T > 0 ? cdiv(p.T, p.L) : 0;
     p.B32 = (uint32_t)g.B;
@@ -1001,28 +919,10 @@ V2Plan v2_plan(const Geometry &g, int32_t nr) {
     return p;
 }
 
-// key table: pool2 windows 1..W of every rank + slot and tail keys; none when it would be big
-static int64_t keytab_windows(const V2Plan &pl, const Geometry &g) {
-    return pl.T > 0 ? 1 + (pl.T - 1) / g.B : 0;
-}
-static size_t keytab_words(const V2Plan &pl, const Geometry &g, int32_t nr) {
-    // Off by default: the replay waves and last-occurrence workgroups derive their windows'
-    // keys with Philox themselves, which costs less than the extra kernel (and its boundary)
-    // on the lookahead stream -- C2 544 -> 548, C3 540 -> 544 G idx/s, same-box A/B
-    // (profiles/r03/ab_keytab).  PSS_V2_KEYTAB=1 restores the per-launch table.
-    static const bool off = [] {
-        const char *e = getenv("PSS_V2_KEYTAB");
-        return !(e && e[0] == '1');
-    }();
-    if (off) return 0;
-    const size_t w = (size_t)nr * (size_t)(16 + kRoundKeyWords * keytab_windows(pl, g));
-    return w <= ((size_t)64 << 20) ? w : 0;     // <= 256 MB
-}
-
 size_t v2_val_bytes(const Geometry &g, int32_t nr) {
     if (v2_grouped(g)) return v2_grp_val_bytes(g, nr);
     const V2Plan p = v2_plan(g, nr);
-    return ((size_t)nr * (size_t)p.G * (size_t)p.P1 + keytab_words(p, g, nr)) * sizeof(uint32_t);
+    return (size_t)nr * (size_t)p.G * (size_t)p.P1 * sizeof(uint32_t);
 }
 
 size_t v2_buf_bytes(const Geometry &, int32_t) {
@@ -1046,12 +946,11 @@ size_t v2_sort_bytes(const Geometry &, int32_t) {
 
 hipError_t launch_v2_tail_vals(const Geometry &g, const V2Plan &pl, const RankDesc *ranks,
                                int32_t rank_lo, int32_t nr, const uint32_t *VAL, int64_t pos_lo,
-                               int64_t count, int64_t *out, hipStream_t s, KeyTab kt,
-                               const MapArgs *mapped) {
+                               int64_t count, int64_t *out, hipStream_t s, const MapArgs *mapped) {
     const dim3 grid((uint32_t)cdiv(pl.P1 < 65536 ? pl.P1 : 65536, 256), (uint32_t)nr);
     const MapArgs ma = mapped ? *mapped : MapArgs{};
     hipLaunchKernelGGL(k_v2_tail_f, grid, dim3(256), 0, s, g, pl, ranks, rank_lo, VAL, pos_lo,
-                       count, out, kt, ma);
+                       count, out, ma);
     return hipGetLastError();
 }
 
@@ -1063,15 +962,9 @@ bool v2_ranks_by_value(const Geometry &g, int32_t nr, int emit_path) {
 bool v2_stage_split(const Geometry &g, int32_t nr, int emit_path) {
     if (emit_path == EMIT_AUTO) emit_path = lds_xchg_ordered() ? EMIT_XCHG : EMIT_PROBE;
     // grouped pools always split: their pre-pass (key table, last occurrences of tiled
-    // streams) runs a step ahead on the side stream; in line (A/B knob PSS_V2_GRP_SPLIT=0) the
-    // C5 step is 0.264 ms against 0.233 ms split (profiles/r02/c5_split_ab.txt)
-    if (v2_grouped(g)) {
-        static const bool inline_pre = [] {
-            const char *e = getenv("PSS_V2_GRP_SPLIT");
-            return e && e[0] == '0';
-        }();
-        return !inline_pre;
-    }
+    // streams) runs a step ahead on the side stream; in line the C5 step was 0.264 ms against
+    // 0.233 ms split (round 2, profiles/r02/c5_split_ab.txt)
+    if (v2_grouped(g)) return true;
     return emit_path == EMIT_XCHG;
 }
 
@@ -1102,16 +995,6 @@ hipError_t launch_v2(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, 
     const size_t lds_keys = (size_t)kRoundKeyWords * nwin_max * sizeof(uint32_t);
     const bool need_tail = pos_hi > pl.T;
     bool tail_fused = false;   // drained by the last tile's k_v2_emit_x wave
-    KeyTab kt{nullptr, 0};
-    if (keytab_words(pl, g, nr)) {   // keys of every window once, after the VAL tables
-        uint32_t *ktp = VAL + (size_t)nr * (size_t)pl.G * (size_t)pl.P1;
-        kt.p = ktp;
-        kt.stride = 16 + kRoundKeyWords * keytab_windows(pl, g);
-        const int64_t items = keytab_windows(pl, g) + 2;
-        if (do_pre)
-            hipLaunchKernelGGL(k_v2_keys, dim3((uint32_t)cdiv(items, 256), (uint32_t)nr), dim3(256), 0, s,
-                               g, rank_lo, keytab_windows(pl, g), kt.stride, ktp);
-    }
     if (pl.G > 0) {
         // pass A over every tile up to the last one emitted (the tail needs all of them);
         // VAL is indexed (rl*G + tile), tile < g_need
@@ -1119,26 +1002,14 @@ hipError_t launch_v2(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, 
         const int64_t g_need = need_tail ? pl.G : last_emit + 1;
         if (g_need > 0 && do_pre) {
             mk(K_V2_LASTOCC, s);
-            {
-                static const int lo_mode = [] {   // A/B knob: "ordered" = one-wave plain-store kernel
-                    const char *e = getenv("PSS_V2_LASTOCC");  // (measured 15% slower than ds_max on C2)
-                    return e && e[0] == 'o' ? 1 : 0;
-                }();
-                const size_t lds = (size_t)pl.P1 * 4 + lds_keys;
-                static const int lo_nt = [] {   // A/B knob: threads per last-occurrence workgroup
-                    const char *e = getenv("PSS_V2_LASTOCC_NT");
-                    return e ? atoi(e) : 256;   // 512 shortens this pass (0.066 -> 0.060 ms) but the replay after it slows by as much (power-limited: interleaved A/B, tools/ab_lastocc_nt.sh)
-                }();
-                const bool pow2 = pl.P1 >= 2 && slot_paired((uint32_t)pl.P1);   // paired draws
-                const dim3 grid((uint32_t)(nr * g_need));
-#define PSS_LO(NT, ORD) do { if (pow2) hipLaunchKernelGGL((k_v2_lastocc<NT, ORD, true>), grid, dim3(NT), lds, s, g, pl, rank_lo, g_need, VAL, kt); \
-                             else hipLaunchKernelGGL((k_v2_lastocc<NT, ORD, false>), grid, dim3(NT), lds, s, g, pl, rank_lo, g_need, VAL, kt); } while (0)
-                if (lds_write_ordered() && lo_mode) PSS_LO(64, true);
-                else if (lo_nt == 1024) PSS_LO(1024, false);
-                else if (lo_nt == 512) PSS_LO(512, false);
-                else PSS_LO(256, false);
-#undef PSS_LO
-            }
+            // 256 threads per workgroup: 512 shortens this pass (0.066 -> 0.060 ms) but the
+            // replay beside it slows by as much (power-limited, same-box A/B in rounds 2 and 4);
+            // a one-wave pass with ordered plain stores instead of ds_max was 15 % slower
+            const size_t lds = (size_t)pl.P1 * 4 + lds_keys;
+            const bool pow2 = pl.P1 >= 2 && slot_paired((uint32_t)pl.P1);   // paired draws
+            const dim3 grid((uint32_t)(nr * g_need));
+            if (pow2) hipLaunchKernelGGL((k_v2_lastocc<256, true>), grid, dim3(256), lds, s, g, pl, rank_lo, g_need, VAL);
+            else hipLaunchKernelGGL((k_v2_lastocc<256, false>), grid, dim3(256), lds, s, g, pl, rank_lo, g_need, VAL);
         }
         if (do_pre && !do_emit) mk(-1, s);
         if (last_emit >= 0 && do_emit) {
@@ -1160,9 +1031,9 @@ hipError_t launch_v2(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, 
                 const int use_ra = rank_args ? 1 : 0;
                 if (rank_args) ra = *rank_args;
 #define PSS_EX(N, P2) do { if (mapped) hipLaunchKernelGGL((k_v2_emit_x<N, P2, true>), grid, dim3(64), lds, s, g, pl, ranks, rank_lo, \
-                                         g_lo, ng, (const uint32_t *)VAL, pos_lo, count, dt, out, kt, ma, ra, use_ra); \
+                                         g_lo, ng, (const uint32_t *)VAL, pos_lo, count, dt, out, ma, ra, use_ra); \
                            else hipLaunchKernelGGL((k_v2_emit_x<N, P2, false>), grid, dim3(64), lds, s, g, pl, ranks, rank_lo, \
-                                         g_lo, ng, (const uint32_t *)VAL, pos_lo, count, dt, out, kt, ma, ra, use_ra); } while (0)
+                                         g_lo, ng, (const uint32_t *)VAL, pos_lo, count, dt, out, ma, ra, use_ra); } while (0)
                 if (narrow && pow2) PSS_EX(true, true);
                 else if (narrow) PSS_EX(true, false);
                 else if (pow2) PSS_EX(false, true);
@@ -1191,7 +1062,7 @@ hipError_t launch_v2(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, 
             if (e != hipSuccess) return e;
         }
         mk(K_V2_TAIL, s);
-        hipError_t e = launch_v2_tail_vals(g, pl, ranks, rank_lo, nr, VAL, pos_lo, count, out, s, kt, mapped);
+        hipError_t e = launch_v2_tail_vals(g, pl, ranks, rank_lo, nr, VAL, pos_lo, count, out, s, mapped);
         if (e != hipSuccess) return e;
     }
     mk(-1, s);
@@ -1253,14 +1124,8 @@ hipError_t init_kernel_attributes_v2() {
     // handles never pay for it, V2 ones once per device per process
     hipError_t e = init_kernel_attributes_v2grp();
 #define PSS_ATTR(fn) { hipError_t x = hipFuncSetAttribute((const void *)(fn), hipFuncAttributeMaxDynamicSharedMemorySize, big); if (x != hipSuccess) e = x; }
-    PSS_ATTR((k_v2_lastocc<64, true, true>));
-    PSS_ATTR((k_v2_lastocc<64, true, false>));
-    PSS_ATTR((k_v2_lastocc<256, false, true>));
-    PSS_ATTR((k_v2_lastocc<256, false, false>));
-    PSS_ATTR((k_v2_lastocc<512, false, true>));
-    PSS_ATTR((k_v2_lastocc<512, false, false>));
-    PSS_ATTR((k_v2_lastocc<1024, false, true>));
-    PSS_ATTR((k_v2_lastocc<1024, false, false>));
+    PSS_ATTR((k_v2_lastocc<256, true>));
+    PSS_ATTR((k_v2_lastocc<256, false>));
     PSS_ATTR((k_v2_emit_x<true, true, false>));
     PSS_ATTR((k_v2_emit_x<true, false, false>));
     PSS_ATTR((k_v2_emit_x<false, true, false>));

@@ -395,15 +395,11 @@ __global__ __launch_bounds__(256) void k_v2x_gsplit(V2xGeo x, uint32_t nr, uint3
     SP[gi] = r;
 }
 
-// decoded pool2 windows (as sequences of B steps) -> Q2[window step] = its pool2 rank.  The
-// writes are random inside one window, so the grid is XCD-major over chunks of xb blocks (about
-// a window; v1x_block in pss_v1exact.hip): workgroup L (on XCD L mod 8) takes block
-// xb (8 (L / 8 / xb) + L mod 8) + (L / 8) mod xb, and each window's lines stay in one L2.
-__global__ __launch_bounds__(256) void k_v2x_q2(uint64_t n, uint32_t B, uint32_t xb, const uint32_t *__restrict__ V,
+// decoded pool2 windows (as sequences of B steps) -> Q2[window step] = its pool2 rank (random
+// writes inside one window; an XCD-major grid as v1x_block's measured neutral at C5, round 4)
+__global__ __launch_bounds__(256) void k_v2x_q2(uint64_t n, uint32_t B, const uint32_t *__restrict__ V,
                                                 const uint32_t *__restrict__ O, uint32_t *__restrict__ Q2) {
-    const uint64_t L = blockIdx.x, q = L >> 3;
-    const uint64_t blk = xb ? (uint64_t)xb * (8u * (q / xb) + (L & 7u)) + q % xb : L;
-    const uint64_t gi = blk * 256 + threadIdx.x;
+    const uint64_t gi = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (gi >= n) return;
     const uint64_t seq = gi / B;
     Q2[seq * B + O[gi]] = V[gi];
@@ -704,15 +700,8 @@ static bool v2x_draws_wg(uint64_t streams, uint32_t B) {
     return B > (uint32_t)kTile && streams < 1024;
 }
 
-// chain mode: pools of at most kTile entries (one decode tile's frame holds the whole pool);
-// PSS_V2X_CHAIN=0 keeps the global merge levels there too (A/B)
-static bool v2x_chain(const V2xGeo &x) {
-    static const bool on = [] {
-        const char *e = getenv("PSS_V2X_CHAIN");
-        return !(e && e[0] == '0');
-    }();
-    return on && x.P <= (uint32_t)kTile;
-}
+// chain mode: pools of at most kTile entries (one decode tile's frame holds the whole pool)
+static bool v2x_chain(const V2xGeo &x) { return x.P <= (uint32_t)kTile; }
 
 // chunks of tiles per rank: about two 1024-thread workgroups per CU over the pass's ranks
 static V2xChain v2x_chain_plan(const V2xGeo &x, int32_t nr) {
@@ -778,22 +767,12 @@ static hipError_t v2x_pass(const Geometry &g, const V2xGeo &x, const RankDesc *r
     });
     const uint32_t nru = (uint32_t)nr;
     const bool narrow = v2x_narrow(x.P, x.B);
-    static const int outk = [] {   // A/B knob: merge outputs per thread (4, 8 = default, 16)
-        const char *e = getenv("PSS_V2X_OUT");
-        const int v = e ? atoi(e) : kTileOut;
-        return v == 4 || v == 16 ? v : kTileOut;
-    }();
-    // one decode-tile launch of nb blocks from block b0 (the entry width and outputs per thread)
+    // one decode-tile launch of nb blocks from block b0 (the entry width; kTileOut merge outputs
+    // per thread -- 4 and 16 measured slower, 6.46 / 5.9 against 5.1-5.2 ms at C2, round 3)
     auto tile = [&](uint64_t b0, uint32_t nb, const V2xGeo &xg, uint32_t per, const uint32_t *k1,
                     const uint32_t *k2, uint32_t *v, uint32_t *o, uint32_t *q2, uint32_t *sv, size_t lds) {
-        if (narrow && outk == 16)
-            hipLaunchKernelGGL((k_v2x_tile<uint32_t, 16>), dim3(nb), dim3(kTile / 16), lds, s, xg, per, b0, k1, k2, v, o, q2, sv);
-        else if (narrow && outk == 4)
-            hipLaunchKernelGGL((k_v2x_tile<uint32_t, 4>), dim3(nb), dim3(kTile / 4), lds, s, xg, per, b0, k1, k2, v, o, q2, sv);
-        else if (narrow)
+        if (narrow)
             hipLaunchKernelGGL((k_v2x_tile<uint32_t, kTileOut>), dim3(nb), dim3(kTile / kTileOut), lds, s, xg, per, b0, k1, k2, v, o, q2, sv);
-        else if (outk == 16)
-            hipLaunchKernelGGL((k_v2x_tile<uint64_t, 16>), dim3(nb), dim3(kTile / 16), lds, s, xg, per, b0, k1, k2, v, o, q2, sv);
         else
             hipLaunchKernelGGL((k_v2x_tile<uint64_t, kTileOut>), dim3(nb), dim3(kTile / kTileOut), lds, s, xg, per, b0, k1, k2, v, o, q2, sv);
     };
@@ -828,14 +807,7 @@ static hipError_t v2x_pass(const Geometry &g, const V2xGeo &x, const RankDesc *r
         uint32_t *wv = V, *wo = O, *wvd = Vd, *wod = Od;
         v2x_global_levels(xw, nseq, wv, wo, wvd, wod, SP, s);
         const uint64_t nw = (uint64_t)nseq * x.B, nblk = (uint64_t)v2x_cdiv((int64_t)nw, 256);
-        static const bool q2_xcd = [] {   // A/B knob: PSS_V2X_Q2_XCD=1 takes the XCD-major grid
-            const char *e = getenv("PSS_V2X_Q2_XCD");
-            return e && e[0] == '1';
-        }();
-        uint32_t xb = q2_xcd ? (uint32_t)v2x_cdiv((int64_t)x.B, 256) : 0u;
-        uint64_t grid = xb ? (uint64_t)xb * 8u * (uint64_t)v2x_cdiv((int64_t)v2x_cdiv((int64_t)nblk, xb), 8) : nblk;
-        if (grid >= ((uint64_t)1 << 24)) { xb = 0u; grid = nblk; }   // (threads below 2^32)
-        hipLaunchKernelGGL(k_v2x_q2, dim3((uint32_t)grid), dim3(256), 0, s, nw, x.B, xb, wv, wo, Q2);
+        hipLaunchKernelGGL(k_v2x_q2, dim3((uint32_t)nblk), dim3(256), 0, s, nw, x.B, wv, wo, Q2);
     }
     // pool1 tiles (and, for B <= kTile, the windows in the same launch)
     const uint32_t per_rank = x.tiles1 + (big_windows ? 0u : x.S);
@@ -858,11 +830,8 @@ hipError_t launch_v2_exact(const Geometry &g, const RankDesc *ranks, int32_t ran
     const V2xGeo x = v2x_geo(g);
     static const hipError_t attr = [] {
         const int lds = 2 * (int)TileEntry<uint64_t>::kSlots * (int)sizeof(uint64_t);
-        hipError_t e = hipFuncSetAttribute((const void *)k_v2x_tile<uint64_t, kTileOut>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-        if (e == hipSuccess)
-            e = hipFuncSetAttribute((const void *)k_v2x_tile<uint64_t, 16>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-        return e;
+        return hipFuncSetAttribute((const void *)k_v2x_tile<uint64_t, kTileOut>,
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     }();
     if (attr != hipSuccess) return attr;
     const int32_t per = v2x_ranks_per_pass(g, nr);

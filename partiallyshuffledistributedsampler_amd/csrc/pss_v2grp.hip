@@ -23,11 +23,8 @@ namespace pss {
 
 static inline int64_t gdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
-// cache-policy bits of the run stores (build-time A/B: -DPSS_G_STORE_AUX=1 sets sc0)
-#ifndef PSS_G_STORE_AUX
-#define PSS_G_STORE_AUX 0
-#endif
-constexpr int kGStoreAux = PSS_G_STORE_AUX;
+// cache-policy bits of the run stores: none (sc0 measured neutral, 173.4 vs 173.1 us, round 3)
+constexpr int kGStoreAux = 0;
 
 // key table layout per local rank (words): [0, 2) slot key, [8, 16) init keys,
 // [16 + 8 (w - 1), + 8) round keys of pool2 window w = 1 .. W
@@ -41,7 +38,6 @@ struct GPlan {
     Groups gr;
     uint32_t Smax;           // largest group
     uint32_t B32, hB, walk_full, w_last, len_last, h_last, hP, twoB;
-    uint32_t straddle;       // window-straddling iterations on the run machinery (PSS_G_STRADDLE)
 };
 
 
@@ -71,11 +67,6 @@ static GPlan gplan(const Geometry &g, int32_t nr, int cus) {
     p.h_last = feistel_half_bits(p.len_last > 0 ? p.len_last : 1);
     p.hP = feistel_half_bits((uint32_t)p.P1);
     p.twoB = (uint32_t)(2 * g.B < g.ns ? 2 * g.B : g.ns);
-    static const uint32_t straddle = [] {
-        const char *e = getenv("PSS_G_STRADDLE");
-        return (uint32_t)!(e && e[0] == '0');
-    }();
-    p.straddle = straddle;
     return p;
 }
 
@@ -564,7 +555,7 @@ __global__ __launch_bounds__(64) void k_g_emit(Geometry g, GPlan pl, const RankD
         // one whole iteration straddling the boundary of two full windows wa, wa + 1 (both
         // non-walking): the run machinery with each lane's round keys picked from the two
         // windows' SGPR keys (one v_cndmask per key word) and the paired slot hashes
-        if (pl.straddle && runs_ok && wa + 1u < pl.w_last && pa < B && pa + span >= B && uhi - u0 >= 256u) {
+        if (runs_ok && wa + 1u < pl.w_last && pa < B && pa + span >= B && uhi - u0 >= 256u) {
             if (wa != wk) {
                 if (wa == wk + 1u) {
 #pragma unroll

@@ -135,10 +135,40 @@ def test_gpu_fuzz_exact_order_equals_cpu_mode(i, device=0):
     kw = dict(shuffle=g["shuffle"], seed=g["seed"], order="exact")
     gpu = pss.IndexEngine(*args, device=device, **kw)
     cpu = pss.IndexEngine(*args, device="cpu", **kw)
-    R = g["R"]
+    R, N, B = g["R"], g["N"], g["B"]
+    ns = gpu.num_samples
     for epoch in (g["epoch"], g["epoch"] + 1):
         gpu.init_iter(epoch)
         cpu.init_iter(epoch)
+        old, new = gpu.rank_starts()
         a = gpu.generate(0, R)
         gpu.check()
-        assert np.array_equal(a.cpu().numpy(), cpu.generate(0, R).numpy()), (i, epoch)
+        a = a.cpu().numpy()
+        assert np.array_equal(a, cpu.generate(0, R).numpy()), (i, epoch)
+        # and the exact oracle (the reference's algorithm restated, oracle/pss_oracle.c), which
+        # the golden fixtures pin to the reference itself (tests/test_oracle_golden.py)
+        for r in sorted({0, R - 1}):
+            if g["version"] == 1:
+                ref = O.v1_exact_stream(epoch, int(new[r]), ns, B, N, g["shuffle"])
+            else:
+                ref = O.v2_exact_stream_rs(epoch, int(old[r]), int(new[r]), ns, B, N)
+            assert np.array_equal(a[r], ref), (i, epoch, r)
+
+
+@pytest.mark.parametrize("i", range(N_EXACT_CASES))
+def test_cpu_mode_fuzz_exact_order_matches_exact_oracle(i):
+    """The CPU mode's exact order (CPythonMT windows, Fenwick-tree V2) == the exact oracle on
+    the same random geometries the GPU's exact order is checked on."""
+    g = _geometry(i)
+    cpu = pss.IndexEngine(g["lengths"], g["N"], g["R"], g["B"], g["version"], shuffle=g["shuffle"],
+                          seed=g["seed"], device="cpu", order="exact")
+    R, N, B, ns = g["R"], g["N"], g["B"], cpu.num_samples
+    cpu.init_iter(g["epoch"])
+    old, new = cpu.rank_starts()
+    for r in sorted({0, R // 2, R - 1}):
+        got = cpu.generate(r, r + 1).numpy()[0]
+        if g["version"] == 1:
+            ref = O.v1_exact_stream(g["epoch"], int(new[r]), ns, B, N, g["shuffle"])
+        else:
+            ref = O.v2_exact_stream_rs(g["epoch"], int(old[r]), int(new[r]), ns, B, N)
+        assert np.array_equal(got, ref), (i, r)

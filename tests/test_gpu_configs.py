@@ -239,3 +239,42 @@ def test_exact_order_launch_sizes_beyond_2_32_threads():
     a = _gen(gpu, 0, R).cpu().numpy()
     assert np.array_equal(a, cpu.generate(0, R).numpy())
     gpu.close()
+
+
+@pytest.mark.parametrize("cfg,version,pad", [("c2", 2, 0), ("c2", 2, 3), ("c2", 1, 3),
+                                             ("c5", 2, 0), ("c5", 2, 3), ("c5", 1, 3)])
+def test_exact_order_at_bench_shape_matches_exact_oracle(cfg, version, pad):
+    """order="exact" at the shapes bench.py reports it on: C2 (R = 8, ns = 12.5M, B = 4096: the
+    V2 chain mode, ~3000 chunks linked per rank) and C5 (B = 2^20: 12 pool2 windows through
+    the global merge levels; V1 windows through HBM).  pad = 3 drops three samples from the last
+    file so that ns * R - N = 3 and the block at 7 * ns wraps at N (V1:161-163, V2:113-114).
+    Two ranks per epoch (rank 0 and the wrapping / last block) == the exact oracle (V2: the
+    rank-select restatement), over two consecutive epochs; all 8 ranks are generated at once."""
+    from concurrent.futures import ThreadPoolExecutor
+    lengths, N, R, B, _ = W.shape(cfg)
+    lengths = lengths.copy()
+    lengths[-1] -= pad
+    N -= pad
+    eng = pss.IndexEngine(lengths, N, R, B, version, device=0, shuffle=True, order="exact")
+    ns = eng.num_samples
+    assert ns * R - N == pad
+    with ThreadPoolExecutor(4) as ex:           # the oracle calls release the GIL
+        for epoch in (0, 1):
+            eng.init_iter(epoch)
+            old, new = eng.rank_starts()
+            last = int(np.argmax(new))              # the block at 7 * ns: wraps when pad > 0
+            picks = sorted({0, last})
+            if version == 1:
+                futs = [ex.submit(O.v1_exact_stream, epoch, int(new[r]), ns, B, N) for r in picks]
+            else:
+                futs = [ex.submit(O.v2_exact_stream_rs, epoch, int(old[r]), int(new[r]), ns, B, N)
+                        for r in picks]
+            out = _gen(eng, 0, R).cpu().numpy()
+            for r, f in zip(picks, futs):
+                ref = f.result()
+                assert np.array_equal(out[r], ref), (cfg, version, pad, epoch, r,
+                                                     int(np.argmax(out[r] != ref)))
+            if pad:
+                assert int(out[last].min()) < pad <= ns   # wrapped ids present
+            del out
+    eng.close()
