@@ -82,54 +82,87 @@ def _host():
     return {"cores": len(os.sched_getaffinity(0)), "cpu_model": model}
 
 
-def cpu_baseline(seconds_budget=10.0):
-    """The reference algorithm on this box's host cores (the reference is not on the GPU box:
-    its restatements in oracle/, pinned by the goldens), bounded samples, one core each:
-      value       -- V2 (the bench workload C2): oracle's C port of get_index (CPython MT19937 +
-                     list.remove pools, V2:96-116) over whole rank streams, G idx/s;
-      c1_v1       -- C1 (BASELINE configs[0]): oracle/pyref.py's Python V1 __next__ loop
-                     (V1:151-259) with its per-batch gc.collect() on and off, 64 batches,
-                     extrapolated to the epoch;
-      c3_v2/c5_v2 -- Python get_index at B = 4096 / 2^20 (C3 / C5), a prefix, extrapolated;
+def _reference_processes(workload, version, nproc, batches, bs, use_gc):
+    """The reference's __next__ loop (oracle/pyref.py via oracle/cpu_ref.py) for logical ranks
+    0..nproc-1 of `workload`, one process per rank, all started together; aggregate ids/s =
+    all ids / (last end - first start).  Child processes of this one (fork + exec of a fresh
+    interpreter that never touches the GPU)."""
+    import subprocess
+    env = {k: v for k, v in os.environ.items() if not k.startswith("PSS_")}
+    env["OMP_NUM_THREADS"] = "1"
+    procs = [subprocess.Popen([sys.executable, "-m", "oracle.cpu_ref", workload, str(version),
+                               str(r), str(batches), str(bs), "1" if use_gc else "0"],
+                              cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                              text=True) for r in range(nproc)]
+    res = []
+    for p in procs:
+        o, e = p.communicate(timeout=300)
+        if p.returncode != 0:
+            raise RuntimeError("cpu_ref worker failed: %s" % e[-2000:])
+        res.append(json.loads(o.strip().splitlines()[-1]))
+    ids = sum(r["ids"] for r in res)
+    span = max(r["wall_end"] for r in res) - min(r["wall_start"] for r in res)
+    return {"idx_per_s": ids / span, "processes": nproc, "ids": ids, "seconds": span,
+            "per_process_idx_per_s": float(np.median([r["ids"] / r["seconds"] for r in res])),
+            "batches_per_rank": batches, "batch_size": bs, "gc_collect_per_batch": use_gc}
+
+
+def cpu_baseline():
+    """The reference's own per-batch loop on this box's host cores, as the reference runs: one
+    single-threaded process per logical rank (BASELINE.md "CPU-baseline plan"; the reference
+    is not on the GPU box -- oracle/pyref.py restates its loops and tests/test_oracle_golden.py
+    pins them to its recorded streams):
+      value   -- C2 (the bench workload): V2 __next__ (get_index draws with list.remove pools,
+                 V2:96-116; id -> (file, offset) walk and row gather, V2:181-248; the per-batch
+                 gc.collect() of V2:253) in 8 processes, ranks 0..7, a prefix of 64 batches of
+                 1024 each -- aggregate G idx/s (extrapolated to the epoch: the rate is flat);
+      gc_off  -- the same with gc.collect() stubbed;
+      c1_v1   -- C1 (BASELINE configs[0]): V1 __next__ (V1:151-259) in 2 processes, gc on / off;
+      c_port  -- the oracle's C port of get_index on whole C2 rank streams, one thread: the
+                 reference algorithm without the interpreter (labelled, not the headline);
+      c3_v2 / c5_v2 -- Python get_index prefixes at B = 4096 / 2^20, one process, extrapolated;
       c3_v2_set_epoch_to_first_batch_ms -- Python init_iter (100K-file shuffle, 1024 blocks) +
-                     the first 1024 get_index draws at C3.
+                 the first 1024 get_index draws at C3.
     """
     import gc
     import random
     from oracle import oracle as O
-    from oracle.pyref import V1Loop, V2Draws
+    from oracle.pyref import V2Draws
+    host = _host()
+    nproc = max(1, min(8, host["cores"], 16))
     lengths, N, R, B, _ = W.shape("c2")
     ns = O.num_samples(N, R)
+    on = _reference_processes("c2", 2, nproc, 64, 1024, True)
+    off = _reference_processes("c2", 2, nproc, 64, 1024, False)
+    out = {"value": on["idx_per_s"] / 1e9, "unit": "G idx/s", "cores": nproc,
+           "kind": "port",
+           "sample": "reference V2 __next__ loop (oracle/pyref.py: get_index + map + gather + "
+                     "per-batch gc.collect, V2:96-116,170-254) at C2, %d processes = logical "
+                     "ranks 0..%d, 64 batches x 1024 ids each, all concurrent; extrapolated "
+                     "(label: extrapolated) the C2 epoch (%d ids) takes %.0f s"
+                     % (nproc, nproc - 1, ns * R, ns * R / on["idx_per_s"]),
+           "gc_on": on, "gc_off": off, "host": host}
+    # C1, Python V1 loop, gc on / off, one process per rank (R = 2)
+    l1, N1, R1, B1, _ = W.shape("c1")
+    ns1 = O.num_samples(N1, R1)
+    c1 = {}
+    for use_gc in (True, False):
+        r = _reference_processes("c1", 1, min(R1, nproc), 64, 1024, use_gc)
+        r["epoch_s_extrapolated"] = ns1 * R1 / r["idx_per_s"]
+        c1["gc_on" if use_gc else "gc_off"] = r
+    out["c1_v1"] = c1
+    # the C port of the reference algorithm, one thread, whole rank streams (bounded)
     total, t0, r = 0, time.perf_counter(), 0
-    while r < R and time.perf_counter() - t0 < seconds_budget:
+    while r < R and time.perf_counter() - t0 < 6.0:
         hr = O.RefHistory(2, len(lengths), R, r, N)
         hr.init_iter(0)
         total += len(O.v2_exact_stream(0, hr.old_start, hr.start, ns, B, N))
         r += 1
     dt = time.perf_counter() - t0
-    out = {"value": total / dt / 1e9, "unit": "G idx/s", "cores": 1, "kind": "port",
-           "sample": "reference V2 algorithm (oracle C port: CPython MT19937 + list.remove "
-                     "pools, V2:96-116) over the full epoch streams of logical ranks 0..%d of "
-                     "the c2 workload (%d ids, %.1f s, 1 thread)" % (r - 1, total, dt),
-           "host": _host()}
-    # C1, Python V1 loop, gc on / off
-    l1, N1, R1, B1, _ = W.shape("c1")
-    ns1 = O.num_samples(N1, R1)
-    arr = np.arange(int(l1.max()), dtype=np.int64)
-    c1 = {}
-    for use_gc in (True, False):
-        loop = V1Loop(0, ns1, B1, N1, l1.tolist(), lambda f: {"x": arr[:l1[f]]}, bs=1024,
-                      use_gc=use_gc)
-        nb, t0 = 0, time.perf_counter()
-        while nb < 64 and loop.next_batch() is not None:
-            nb += 1
-        dt = time.perf_counter() - t0
-        per_batch = dt / nb
-        c1["gc_on" if use_gc else "gc_off"] = {
-            "idx_per_s": nb * 1024 / dt,
-            "epoch_s_extrapolated": per_batch * (-(-ns1 // 1024)) * R1,
-            "sample": "%d batches of 1024 of rank 0, extrapolated to both ranks' epoch" % nb}
-    out["c1_v1"] = c1
+    out["c_port"] = {"value": total / dt / 1e9, "unit": "G idx/s", "cores": 1,
+                     "sample": "oracle C port of get_index (CPython MT19937 + list.remove pools, "
+                               "V2:96-116), full epoch streams of C2 ranks 0..%d (%d ids, %.1f s)"
+                               % (r - 1, total, dt)}
     # C3 / C5 get_index prefixes
     for name, draws in (("c3", 65536), ("c5", 256)):
         ln, Nn, Rn, Bn, _ = W.shape(name)

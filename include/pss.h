@@ -41,6 +41,14 @@ typedef struct pss_sampler pss_sampler;
 const char *pss_last_error(void);
 int pss_abi_version(void);
 
+/* Version of the counter-order schedule (PSS_ORDER_COUNTER, DESIGN.md §3: the keyed
+ * bijections, the slot hash, the grouped-pool layout).  It changes whenever some geometry's
+ * counter-order id stream changes, so a resume position (find_ckpt_position) recorded under
+ * another version would not continue the same permutation: the facade's state_dict() records it
+ * and load_state_dict() refuses a mismatch.  The exact order is the reference's and never
+ * changes. */
+int pss_schedule_version(void);
+
 /* Constructor math of __init__ (V1:16-56, V2:16-52):
  *   files_len[F]  -- per-file sample counts in dataset.files order (files_len dict, or the
  *                    reader(path, get_data=False) probe, V1:186-189)
@@ -91,9 +99,10 @@ int pss_map(pss_sampler *h, const int64_t *ids_dev, int64_t n, int32_t *file_pos
  * ([r - rank_lo][pos - pos_lo]) and the same reflection flag as pss_map.  Counter order (V1,
  * and V2 on the exchange replays): one kernel, each id mapped where it is emitted (V2 pools up
  * to 16384 through a per-tile LDS map of the files its ids can come from, grouped pools
- * through the bucket-indexed map); the exact orders and the V2 collision-probe path:
- * generation into handle scratch, then the bucket-indexed map.  PSS_ENOTSUP if a file holds
- * 2^31 samples or more. */
+ * through the bucket-indexed map).  Exact order: the pipeline's output kernels map each id
+ * through the bucket-indexed map where they would write it (no id scratch).  Only the V2
+ * collision-probe path generates into handle scratch and then maps.  PSS_ENOTSUP if a file
+ * holds 2^31 samples or more. */
 int pss_generate_mapped(pss_sampler *h, int32_t rank_lo, int32_t rank_hi, int64_t pos_lo,
                         int64_t count, int32_t *file_pos_dev, int32_t *offset_dev, void *stream);
 
@@ -164,6 +173,10 @@ int pss_emit_path(pss_sampler *h, int32_t *path);
  *       shuffle(range(n))` (V1:102,114-115,165-171, shuffle_buffer < 2^31); V2 get_index's
  *       choice / remove / append with its per-window and per-tail-step reseeding (V2:96-116,
  *       num_samples < 2^31, shuffle_buffer < 2^30).  PSS_ENOTSUP outside those bounds.
+ *       Device workspace: V1 windows beyond 16000 entries take ~16 B per entry of the windows
+ *       one pass resolves (<= 2 GB up to 2^27-entry windows, one window per pass beyond:
+ *       ~16 GB at shuffle_buffer = 2^30); V2 ~28 B per position of the ranks of a pass.  A
+ *       workspace the device cannot hold makes pss_generate return PSS_EHIP.
  * Replaces nothing in the reference: its order IS the exact one. */
 #define PSS_ORDER_COUNTER 0
 #define PSS_ORDER_EXACT 1

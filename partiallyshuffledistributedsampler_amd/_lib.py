@@ -22,6 +22,7 @@ _i32, _i64, _u64 = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64
 SIGNATURES = {
     "pss_last_error": ([], ctypes.c_char_p),
     "pss_abi_version": ([], ctypes.c_int),
+    "pss_schedule_version": ([], ctypes.c_int),
     "pss_create": ([_c_i64p, _i64, _i64, _i32, _i64, _i32, _i32, _u64, _i32,
                     ctypes.POINTER(_vp)], ctypes.c_int),
     "pss_destroy": ([_vp], ctypes.c_int),

@@ -291,6 +291,21 @@ constexpr uint32_t kSegBuckets = 256, kSegBackWin = 40;
 constexpr uint32_t kSegLdsWords = 3 * kSegBuckets;
 constexpr uint32_t kSegMulti = 0xFFFFu;    // bucket with >= 2 boundaries: global path
 
+// exact orders (pss_v1exact.hip, pss_v2exact.hip): the id into out[e], or -- ma.fpos set, the
+// fused hand-off of pss_generate_mapped -- its (file position, offset) pair through the global
+// bucketed map, the same values pss_map gives
+__device__ __forceinline__ void put_id_or_pair(int64_t *out, const MapArgs &ma, int64_t e, int64_t id) {
+    if (ma.fpos) {
+        int32_t f;
+        int64_t o;
+        map_one_bucketed(ma.prefix, ma.F, ma.BT, ma.kb, ma.nb, id, f, o);
+        ma.fpos[e] = f;
+        ma.off[e] = (int32_t)o;
+    } else {
+        out[e] = id;
+    }
+}
+
 // the global map for the rare ids the LDS buckets miss
 __device__ __forceinline__ void seg_global_map(const MapArgs &ma, int64_t T, int64_t id,
                                                int32_t &f, int32_t &off) {

@@ -111,16 +111,18 @@ size_t v1_workspace_bytes(const Geometry &g, int32_t nr, int64_t pos_lo, int64_t
 constexpr int64_t kV1ExactMaxB = 16000;
 bool v1_exact_supported(const Geometry &g);
 size_t v1_exact_ws_bytes(const Geometry &g, int32_t nr, int64_t pos_lo, int64_t count);
+// mapped != nullptr (pss_generate_mapped): (file, offset) pairs into mapped->fpos / off in
+// place of the ids (out unused), through the global bucketed map -- same values as pss_map
 hipError_t launch_v1_exact(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, int32_t nr,
                            int64_t pos_lo, int64_t count, int64_t epoch, int64_t *out, void *ws,
-                           hipStream_t s);
+                           hipStream_t s, const MapArgs *mapped = nullptr);
 
 // V2 in the reference's exact order (pss_v2exact.hip): shuffle_buffer < 2^30, ns < 2^31
 bool v2_exact_supported(const Geometry &g);
 size_t v2_exact_ws_bytes(const Geometry &g, int32_t nr);
 hipError_t launch_v2_exact(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, int32_t nr,
                            int64_t pos_lo, int64_t count, int64_t epoch, int64_t *out, uint32_t *ws,
-                           hipStream_t s);
+                           hipStream_t s, const MapArgs *mapped = nullptr);
 
 // V2 replay kernel: EMIT_XCHG = one LDS exchange per step (needs the lane-ordered exchange the
 // start-up check confirms), EMIT_PROBE = collision probe + per-clash fix-up (any hardware)

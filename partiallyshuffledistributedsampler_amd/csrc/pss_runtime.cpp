@@ -399,6 +399,10 @@ extern "C" {
 const char *pss_last_error(void) { return g_err.c_str(); }
 int pss_abi_version(void) { return 2; }
 
+// counter-order schedule: 1 round 1, 2 round 2 (grouped pools, 24-bit slot hash), 3 round 3
+// (16-bit round function at 10-bit halves, 8 fmix32 rounds at halves <= 5 bits)
+int pss_schedule_version(void) { return 3; }
+
 int pss_create(const int64_t *files_len, int64_t num_files, int64_t total_size,
                int32_t num_replicas, int64_t shuffle_buffer, int32_t version, int32_t shuffle,
                uint64_t seed, int32_t device, pss_sampler **out) {
@@ -874,13 +878,32 @@ int pss_generate_mapped(pss_sampler *h, int32_t rank_lo, int32_t rank_hi, int64_
     if (rc) return rc;
     const pss::Geometry g = h->geometry();
     const pss::Marker mk = marker_of(h);
-    if (h->version == 1 && h->order_mode == PSS_ORDER_COUNTER) {
-        // fused: the V1 kernel maps each id as it computes it
-        auto words = [](size_t bytes) { return (bytes + sizeof(uint32_t) - 1) / sizeof(uint32_t); };
+    auto words = [](size_t bytes) { return (bytes + sizeof(uint32_t) - 1) / sizeof(uint32_t); };
+    const bool exact = h->order_mode == PSS_ORDER_EXACT && (h->version == 2 || g.shuffle);
+    if (h->version == 1 && !exact) {
+        // fused: the V1 kernel maps each id as it computes it (shuffle = false is the identity
+        // order of both modes)
         const size_t sb = pss::v1_workspace_bytes(g, nr, pos_lo, count);
         if (sb) PSS_HIP(h->d_sort.ensure(words(sb)));
         pss::MapArgs ma{h->d_prefix.p, h->F, h->d_bucket.p, h->kb, h->nb, file_pos_dev, offset_dev};
         PSS_HIP(pss::launch_v1(g, h->d_ranks.p, rank_lo, nr, pos_lo, count, nullptr, h->d_sort.p, s, mk, &ma));
+        return PSS_OK;
+    }
+    if (exact) {
+        // fused: the exact pipelines' output kernels map each id where they would write it
+        pss::MapArgs ma{h->d_prefix.p, h->F, h->d_bucket.p, h->kb, h->nb, file_pos_dev, offset_dev};
+        if (h->version == 1) {
+            PSS_HIP(h->d_sort.ensure(words(pss::v1_exact_ws_bytes(g, nr, pos_lo, count))));
+            mk(pss::K_V1, s);
+            PSS_HIP(pss::launch_v1_exact(g, h->d_ranks.p, rank_lo, nr, pos_lo, count, h->epoch, nullptr,
+                                         h->d_sort.p, s, &ma));
+        } else {
+            PSS_HIP(h->d_sort.ensure(words(pss::v2_exact_ws_bytes(g, nr))));
+            mk(pss::K_V2_EMIT, s);
+            PSS_HIP(pss::launch_v2_exact(g, h->d_ranks.p, rank_lo, nr, pos_lo, count, h->epoch, nullptr,
+                                         h->d_sort.p, s, &ma));
+        }
+        mk(-1, s);
         return PSS_OK;
     }
     if (h->version == 2 && h->order_mode == PSS_ORDER_COUNTER && pss::v2_mapped_fused(g, h->emit_path)) {
@@ -888,7 +911,7 @@ int pss_generate_mapped(pss_sampler *h, int32_t rank_lo, int32_t rank_hi, int64_
         pss::MapArgs ma{h->d_prefix.p, h->F, h->d_bucket.p, h->kb, h->nb, file_pos_dev, offset_dev};
         return generate_impl(h, rank_lo, rank_hi, pos_lo, count, nullptr, stream, &ma);
     }
-    // V2 grouped pools (and the exact orders): ids into the handle's scratch, then the bucket map
+    // the V2 collision-probe path: ids into the handle's scratch, then the bucket map
     if (!h->ids_free) PSS_HIP(hipEventCreateWithFlags(&h->ids_free, hipEventDisableTiming));
     if (h->d_ids.n < n) {
         PSS_HIP(hipEventSynchronize(h->ids_free));

@@ -52,7 +52,7 @@ __global__ __launch_bounds__(kExactNT) void k_v1_exact(Geometry g, const RankDes
                                                        int32_t rank_lo, int64_t w_lo, int64_t nw,
                                                        int64_t pos_lo, int64_t count, int64_t epoch,
                                                        const uint16_t *__restrict__ J,
-                                                       int64_t *__restrict__ out) {
+                                                       int64_t *__restrict__ out, MapArgs ma) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     const int32_t rl = (int32_t)(blockIdx.x / nw);
     const int64_t w = w_lo + (int64_t)(blockIdx.x % nw);
@@ -114,7 +114,7 @@ __global__ __launch_bounds__(kExactNT) void k_v1_exact(Geometry g, const RankDes
     }
     // ---- output: x[i] for the positions of this window inside [pos_lo, pos_lo + count) ----
     const int64_t base = ranks[rank].new_start + wb;
-    int64_t *o = out + (int64_t)rl * count - pos_lo;
+    const int64_t ebase = (int64_t)rl * count - pos_lo;   // element of stream position 0
     int64_t p0 = 0, p1 = n;
     if (wb < pos_lo) p0 = pos_lo - wb;
     if (wb + n > pos_lo + count) p1 = pos_lo + count - wb;
@@ -135,7 +135,7 @@ __global__ __launch_bounds__(kExactNT) void k_v1_exact(Geometry g, const RankDes
                 x = k < 0 ? pj : nxt[k];
             }
         }
-        o[wb + p] = wrap_id(base + x, g.N);
+        put_id_or_pair(out, ma, ebase + wb + p, wrap_id(base + x, g.N));
     }
 }
 
@@ -293,7 +293,7 @@ __global__ __launch_bounds__(256) void k_v1x_parent(Geometry g, V1xBig b) {
 
 __global__ __launch_bounds__(256) void k_v1x_out(Geometry g, V1xBig b, const RankDesc *__restrict__ ranks,
                                                  int32_t rank_lo, int64_t pos_lo, int64_t count,
-                                                 int64_t *__restrict__ out) {
+                                                 int64_t *__restrict__ out, MapArgs ma) {
     V1X_SLOT_PROLOGUE
     const int64_t wb = w * g.B;
     const int64_t p = wb + (int64_t)(xblk * 256 + threadIdx.x);
@@ -323,11 +323,13 @@ __global__ __launch_bounds__(256) void k_v1x_out(Geometry g, V1xBig b, const Ran
         }
     }
     const int32_t rl = (int32_t)(job / (uint64_t)b.nw);
-    out[(int64_t)rl * count + (p - pos_lo)] = wrap_id(ranks[rank_lo + rl].new_start + wb + x, g.N);
+    put_id_or_pair(out, ma, (int64_t)rl * count + (p - pos_lo), wrap_id(ranks[rank_lo + rl].new_start + wb + x, g.N));
 }
 
 namespace {
-// entries per pass of the HBM path (16 B each: a pass's workspace is <= 2 GB)
+// entries per pass of the HBM path (16 B each: a pass's workspace is <= 2 GB while windows have
+// at most 2^27 entries; a longer window is one job of ~16 B per entry, up to ~32 GB near 2^31 --
+// pss.h states the cost, and a workspace the device cannot hold fails pss_generate with PSS_EHIP)
 constexpr int64_t kV1xPassEntries = (int64_t)1 << 27;
 int64_t v1x_jobs_per_pass(int64_t B) {
     const int64_t j = kV1xPassEntries / B;
@@ -354,7 +356,7 @@ size_t v1_exact_ws_bytes(const Geometry &g, int32_t nr, int64_t pos_lo, int64_t 
 
 static hipError_t launch_v1_exact_big(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, int32_t nr,
                                       int64_t pos_lo, int64_t count, int64_t epoch, int64_t *out,
-                                      uint32_t *ws, hipStream_t s) {
+                                      uint32_t *ws, hipStream_t s, const MapArgs &ma) {
     const int64_t pos_hi = pos_lo + count < g.ns ? pos_lo + count : g.ns;
     const int64_t w_lo = pos_lo / g.B, w_hi = (pos_hi - 1) / g.B;
     const int64_t nw = w_hi - w_lo + 1;
@@ -389,7 +391,7 @@ static hipError_t launch_v1_exact_big(const Geometry &g, const RankDesc *ranks, 
         hipLaunchKernelGGL(k_v1x_scan, dim3(b.nj), dim3(kV1xScanNT), 0, s, g, b);
         hipLaunchKernelGGL(k_v1x_scatter, flat, dim3(256), 0, s, g, b);
         hipLaunchKernelGGL(k_v1x_parent, flat, dim3(256), 0, s, g, b);
-        hipLaunchKernelGGL(k_v1x_out, flat, dim3(256), 0, s, g, b, ranks, rank_lo, pos_lo, count, out);
+        hipLaunchKernelGGL(k_v1x_out, flat, dim3(256), 0, s, g, b, ranks, rank_lo, pos_lo, count, out, ma);
         e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
@@ -398,13 +400,14 @@ static hipError_t launch_v1_exact_big(const Geometry &g, const RankDesc *ranks, 
 
 hipError_t launch_v1_exact(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, int32_t nr,
                            int64_t pos_lo, int64_t count, int64_t epoch, int64_t *out, void *ws,
-                           hipStream_t s) {
+                           hipStream_t s, const MapArgs *mapped) {
+    const MapArgs ma = mapped ? *mapped : MapArgs{};
     const int64_t pos_hi = pos_lo + count < g.ns ? pos_lo + count : g.ns;
     if (nr <= 0 || pos_hi <= pos_lo) return hipSuccess;
     if (!v1_exact_supported(g)) return hipErrorInvalidValue;
     if ((g.B < g.ns ? g.B : g.ns) > kV1ExactMaxB) {
         if (!ws) return hipErrorInvalidValue;
-        return launch_v1_exact_big(g, ranks, rank_lo, nr, pos_lo, count, epoch, out, (uint32_t *)ws, s);
+        return launch_v1_exact_big(g, ranks, rank_lo, nr, pos_lo, count, epoch, out, (uint32_t *)ws, s, ma);
     }
     const int64_t w_lo = pos_lo / g.B, w_hi = (pos_hi - 1) / g.B;
     const int64_t nw = w_hi - w_lo + 1;
@@ -418,7 +421,7 @@ hipError_t launch_v1_exact(const Geometry &g, const RankDesc *ranks, int32_t ran
     // ahead of the resolution; without one, each workgroup's first wave does them in place
     if (ws) hipLaunchKernelGGL(k_v1x_draws, grid, dim3(64), 0, s, g, w_lo, nw, epoch, (uint16_t *)ws);
     hipLaunchKernelGGL(k_v1_exact, grid, dim3(kExactNT), lds, s, g, ranks, rank_lo, w_lo, nw, pos_lo,
-                       count, epoch, (const uint16_t *)ws, out);
+                       count, epoch, (const uint16_t *)ws, out, ma);
     return hipGetLastError();
 }
 

@@ -527,7 +527,7 @@ __global__ __launch_bounds__(kChainNT) void k_v2x_emit(Geometry g, V2xGeo x, V2x
                                                        const RankDesc *__restrict__ ranks, int32_t rank_lo,
                                                        const uint32_t *__restrict__ ANS,
                                                        const uint32_t *__restrict__ Q2, int64_t pos_lo,
-                                                       int64_t count, int64_t *__restrict__ out) {
+                                                       int64_t count, int64_t *__restrict__ out, MapArgs ma) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     uint32_t *A = smem, *An = smem + x.P;
     const uint32_t rl = blockIdx.x / ch.nch, c = blockIdx.x % ch.nch;
@@ -540,7 +540,7 @@ __global__ __launch_bounds__(kChainNT) void k_v2x_emit(Geometry g, V2xGeo x, V2x
     const RankDesc rd = ranks[rank_lo + (int32_t)rl];
     const uint32_t *ans = ANS + (size_t)rl * x.ns;
     const uint32_t *q2 = Q2 + (size_t)rl * x.T2;
-    int64_t *o = out + (int64_t)rl * count - pos_lo;
+    const int64_t ebase = (int64_t)rl * count - pos_lo;   // element of stream position 0
     // tile j's answers (q) and survivors (sr) of this thread: u = threadIdx.x + k * kChainNT
     auto load = [&](uint32_t j, uint32_t (&q)[kChainPer], uint32_t (&sr)[kChainPer]) {
         const uint32_t t0 = j * (uint32_t)kTile, n = x.ns - t0 < (uint32_t)kTile ? x.ns - t0 : (uint32_t)kTile;
@@ -600,7 +600,7 @@ __global__ __launch_bounds__(kChainNT) void k_v2x_emit(Geometry g, V2xGeo x, V2x
                 const int64_t wbase = s == 0 ? rd.old_start + x.B : rd.new_start + (int64_t)(s + 1) * x.B;
                 id = wbase + g2[k];
             }
-            o[t] = wrap_id(id, g.N);
+            put_id_or_pair(out, ma, ebase + t, wrap_id(id, g.N));
         }
         if (more) {
             __syncthreads();
@@ -616,7 +616,8 @@ __global__ __launch_bounds__(kChainNT) void k_v2x_emit(Geometry g, V2xGeo x, V2x
 __global__ __launch_bounds__(256) void k_v2x_out(Geometry g, V2xGeo x, uint32_t nr, const RankDesc *__restrict__ ranks,
                                                  int32_t rank_lo, const uint32_t *__restrict__ V,
                                                  const uint32_t *__restrict__ O, const uint32_t *__restrict__ Q2,
-                                                 int64_t pos_lo, int64_t count, int64_t *__restrict__ out) {
+                                                 int64_t pos_lo, int64_t count, int64_t *__restrict__ out,
+                                                 MapArgs ma) {
     const uint64_t gi = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     const uint32_t rl = (uint32_t)(gi / x.ns), i = (uint32_t)(gi % x.ns);
     if (rl >= nr) return;
@@ -633,7 +634,7 @@ __global__ __launch_bounds__(256) void k_v2x_out(Geometry g, V2xGeo x, uint32_t 
         const int64_t wbase = s == 0 ? rd.old_start + x.B : rd.new_start + (int64_t)(s + 1) * x.B;
         id = wbase + Q2[(size_t)rl * x.T2 + uu];
     }
-    out[(int64_t)rl * count + (t - pos_lo)] = wrap_id(id, g.N);
+    put_id_or_pair(out, ma, (int64_t)rl * count + (t - pos_lo), wrap_id(id, g.N));
 }
 
 static int64_t v2x_cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
@@ -745,7 +746,7 @@ static void v2x_global_levels(const V2xGeo &x, uint32_t nr, uint32_t *&V, uint32
 // one pass over nr ranks (nr * ns < 2^30)
 static hipError_t v2x_pass(const Geometry &g, const V2xGeo &x, const RankDesc *ranks, int32_t rank_lo,
                            int32_t nr, int32_t nr_plan, int64_t pos_lo, int64_t count, int64_t epoch,
-                           int64_t *out, uint32_t *ws, hipStream_t s) {
+                           int64_t *out, uint32_t *ws, hipStream_t s, const MapArgs &ma) {
     const size_t nsr = (size_t)nr * x.ns, tr = (size_t)nr * x.T2;
     // merge-levels layout: K1 | V | O | Vd | Od | K2 | Q2 | splits | tables
     // chain layout:        K1 | V (answers) | K2 | Q2 | survivors | chunk maps | chunk starts
@@ -792,7 +793,7 @@ static hipError_t v2x_pass(const Geometry &g, const V2xGeo &x, const RankDesc *r
         hipLaunchKernelGGL(k_v2x_compose, dim3(nru * ch.nch), dim3(kChainNT), lds, s, x, ch);
         hipLaunchKernelGGL(k_v2x_link, dim3(nru), dim3(kChainNT), lds, s, x, ch);
         hipLaunchKernelGGL(k_v2x_emit, dim3(nru * ch.nch), dim3(kChainNT), lds, s, g, x, ch, ranks, rank_lo, ANS,
-                           (const uint32_t *)Q2, pos_lo, count, out);
+                           (const uint32_t *)Q2, pos_lo, count, out, ma);
         return hipGetLastError();
     }
     uint32_t *SP = Q2 + tr;                    // merge-path splits: 2 words per tile
@@ -817,13 +818,13 @@ static hipError_t v2x_pass(const Geometry &g, const V2xGeo &x, const RankDesc *r
     v2x_global_levels(x, nru, V, O, Vd, Od, SP, s);
     const dim3 grid1((uint32_t)v2x_cdiv((int64_t)nsr, 256));   // one thread per (rank, step)
     hipLaunchKernelGGL(k_v2x_out, grid1, dim3(256), 0, s, g, x, nru, ranks, rank_lo, V, O, Q2,
-                       pos_lo, count, out);
+                       pos_lo, count, out, ma);
     return hipGetLastError();
 }
 
 hipError_t launch_v2_exact(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, int32_t nr,
                            int64_t pos_lo, int64_t count, int64_t epoch, int64_t *out, uint32_t *ws,
-                           hipStream_t s) {
+                           hipStream_t s, const MapArgs *mapped) {
     const int64_t pos_hi = pos_lo + count < g.ns ? pos_lo + count : g.ns;
     if (nr <= 0 || pos_hi <= pos_lo) return hipSuccess;
     if (!v2_exact_supported(g) || !ws) return hipErrorInvalidValue;
@@ -837,8 +838,10 @@ hipError_t launch_v2_exact(const Geometry &g, const RankDesc *ranks, int32_t ran
     const int32_t per = v2x_ranks_per_pass(g, nr);
     for (int32_t r0 = 0; r0 < nr; r0 += per) {
         const int32_t n = nr - r0 < per ? nr - r0 : per;
+        MapArgs ma = mapped ? *mapped : MapArgs{};
+        if (ma.fpos) { ma.fpos += (int64_t)r0 * count; ma.off += (int64_t)r0 * count; }
         const hipError_t e = v2x_pass(g, x, ranks, rank_lo + r0, n, per, pos_lo, count, epoch,
-                                      out + (int64_t)r0 * count, ws, s);
+                                      out ? out + (int64_t)r0 * count : nullptr, ws, s, ma);
         if (e != hipSuccess) return e;
     }
     return hipSuccess;

@@ -137,6 +137,7 @@ class _PartialShuffleSampler(Sampler):
         self._host = None      # host copies of (file_pos, offset) or (ids,) + per-chunk events
         self._err = None       # pinned int32: the device error word after this epoch's kernels
         self._scan = None      # lazy-length mode: the epoch's _LazyScan
+        self._history = []     # epochs of every init_iter so far (file order / blocks are cumulative)
         # every dataset file's length known up front -> device map; else lazy probing in scan
         # order (V1:186-190) with the library's host map over the scanned prefix
         self._lazy = any(p not in self.files_len for p in self.dataset.files)
@@ -169,6 +170,7 @@ class _PartialShuffleSampler(Sampler):
         self.dataset.reset()
         eng = self._get_engine()
         eng.init_iter(self.epoch)
+        self._history.append(int(self.epoch))
         self.files = _FileOrder(self.dataset.files, eng.file_order())
         self.blocks = eng.blocks().tolist()
         _, new = eng.rank_starts()
@@ -223,6 +225,47 @@ class _PartialShuffleSampler(Sampler):
         self.warm_start = True
         self.init_iter()
         self._pos = min(step * self.batch_size, self._end)
+
+    def state_dict(self):
+        """Resume point (extension; the reference only has find_ckpt_position(step)): the epochs
+        of every init_iter so far -- the file order and V1's blocks are cumulative over them
+        (V1:122-125, V2:149-152) -- the stream position reached, and what positions mean: the
+        order mode, and for the counter order the seed and libpss's schedule version."""
+        return {"history": list(self._history), "position": int(self._pos),
+                "sampler_version": self._VERSION, "num_replicas": self.num_replicas,
+                "rank": self.rank, "shuffle_buffer": self.shuffle_buffer,
+                "total_size": self.ori_total_size, "order": self.order, "seed": int(self.seed),
+                "schedule_version": _lib.load().pss_schedule_version()}
+
+    def load_state_dict(self, sd):
+        """Continue exactly where state_dict() was taken: the init_iter history is replayed on
+        the host (O(F) each, no generation), then the last epoch is generated and iteration
+        resumes at the recorded position -- the next __iter__ is a warm start.  A state of
+        another configuration, or of another counter schedule (pss_schedule_version), raises
+        ValueError: its positions would index a different permutation."""
+        mine = self.state_dict()
+        for k in ("sampler_version", "num_replicas", "rank", "shuffle_buffer", "total_size", "order"):
+            if sd[k] != mine[k]:
+                raise ValueError("state_dict was taken with %s=%r, this sampler has %r"
+                                 % (k, sd[k], mine[k]))
+        if self.order == "counter":
+            for k in ("seed", "schedule_version"):
+                if sd[k] != mine[k]:
+                    raise ValueError("state_dict was taken with %s=%r, this sampler has %r: the "
+                                     "counter-order positions would not continue the same "
+                                     "permutation" % (k, sd[k], mine[k]))
+        if not sd["history"]:
+            return
+        if self._history:
+            raise ValueError("load_state_dict needs a sampler that has not iterated yet")
+        eng = self._get_engine()
+        for e in sd["history"][:-1]:
+            eng.init_iter(e)
+        self._history = list(sd["history"][:-1])
+        self.epoch = sd["history"][-1]
+        self.warm_start = True
+        self.init_iter()
+        self._pos = min(int(sd["position"]), self._end)
 
     def __iter__(self):
         if not self.warm_start:

@@ -125,7 +125,7 @@ def test_pyref_loops_reproduce_reference_streams():
     """oracle/pyref.py (bench.py's cpu_baseline restatement of the reference loops) draws the
     reference's own id streams (tests/golden raw batches, captured at V1:178 / V2:181)."""
     import numpy as np
-    from oracle.pyref import V1Loop, V2Draws
+    from oracle.pyref import V1Loop, V2Draws, V2Loop
     for name in ("v1_small", "v1_c1_small", "v1_zipf"):
         fx = load(name)
         files, lengths, fl, N, R, B, bs, shuffle = fixture_params(fx)
@@ -152,6 +152,36 @@ def test_pyref_loops_reproduce_reference_streams():
             got = [d.get_index() for _ in range(len(want))]
             got = [x - N if x >= N else x for x in got]
             assert got == want, (name, rrec["rank"])
+            # the whole __next__ loop (draws + map + gather) on the same rank
+            lens = [fl.get(p, lengths[p]) for p in er["files"]]
+            loop = V2Loop(er["old_start"], er["start_num"], ns, B, N, lens,
+                          lambda f: {"x": np.arange(lens[f])}, epoch=er["epoch"], bs=bs,
+                          use_gc=False)
+            got = []
+            while loop.next_batch() is not None:
+                got.append(loop.last_indices)
+            assert got[:len(er["batches"])] == er["batches"], (name, rrec["rank"])
+    # bench-scale fixture (tests/golden/big): whole rank streams at B = 4096 / 400
+    from tests.golden_util import big_lengths, check_stream, load_big
+    for name in ("c1_v1", "c1_v2", "zipf_v2"):
+        fx = load_big(name)
+        lens_ds = big_lengths(fx)
+        N, B, bs = int(lens_ds.sum()), fx["B"], fx["bs"]
+        rr = fx["ranks"][0]
+        h = O.RefHistory(fx["version"], len(lens_ds), fx["R"], rr["rank"], N)
+        er = rr["epochs"][0]
+        h.init_iter(er["epoch"])
+        lens = lens_ds[h.order].tolist()
+        data = lambda f: {"x": np.arange(lens[f])}   # noqa: E731
+        if fx["version"] == 1:
+            loop = V1Loop(h.start, h.ns, B, N, lens, data, epoch=er["epoch"], bs=bs, use_gc=False)
+        else:
+            loop = V2Loop(h.old_start, h.start, h.ns, B, N, lens, data, epoch=er["epoch"], bs=bs,
+                          use_gc=False)
+        got = []
+        while loop.next_batch() is not None:
+            got.extend(loop.last_indices)
+        check_stream(got, er, fx, name)
 
 
 def _rs_cases():

@@ -316,3 +316,40 @@ def test_fused_mapping_and_device_gather(device):
     assert len(dev_batches) >= len(host)
     for (tg, _, rf), (rows, f, o) in zip(host, dev_batches):
         assert sorted(np.concatenate([d["off"] for d in tg]).tolist()) == sorted(rows.cpu().tolist())
+
+
+@pytest.mark.parametrize("device", DEVICES)
+@pytest.mark.parametrize("order", ["counter", "exact"])
+def test_state_dict_resume_continues_the_same_stream(device, order):
+    """state_dict() after some batches of the third epoch (init_iter history 0, 1, 1): a fresh
+    sampler's load_state_dict() replays the history, so file order, blocks and the remaining
+    batches equal the uninterrupted run's; a different schedule version or seed is refused."""
+    rng = np.random.default_rng(8)
+    lens = rng.integers(50, 400, 40)
+    files = ["f%02d" % i for i in range(40)]
+    lengths = dict(zip(files, lens.tolist()))
+    for mod in (V1mod, V2mod):
+        kw = dict(num_replicas=3, rank=2, shuffle_buffer=64, total_size=1, batch_size=32,
+                  files_len=lengths, device=device, order=order)
+        a = mod.DistributedSamplerViaLocallyShuffle(Dataset(files), reader_for(lengths), **kw)
+        for e in (0, 1):
+            a.set_epoch(e)
+            batches_of(iter(a))
+        it = iter(a)                       # epoch 1 again: a third, cumulative init_iter
+        head = [next(it) for _ in range(5)]
+        sd = a.state_dict()
+        tail = [b[2] for b in batches_of(it)]
+        assert sd["history"] == [0, 1, 1] and sd["position"] == 5 * 32 and head
+        b = mod.DistributedSamplerViaLocallyShuffle(Dataset(files), reader_for(lengths), **kw)
+        b.load_state_dict(sd)
+        it2 = iter(b)                      # warm start
+        assert b.files == a.files and b.blocks == a.blocks and b.start_num == a.start_num
+        assert [x[2] for x in batches_of(it2)] == tail
+        assert np.array_equal(b.indices(), a.indices())
+        if order == "counter":
+            bad = dict(sd, schedule_version=sd["schedule_version"] - 1)
+            c = mod.DistributedSamplerViaLocallyShuffle(Dataset(files), reader_for(lengths), **kw)
+            with pytest.raises(ValueError):
+                c.load_state_dict(bad)
+            with pytest.raises(ValueError):
+                c.load_state_dict(dict(sd, seed=sd["seed"] + 1))
