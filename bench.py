@@ -511,7 +511,7 @@ def main():
         syms = ["k_g_emit"]
     else:
         units = RG * ns
-        syms = ["k_v1_feistel"]
+        syms = ["k_v1_os"]           # the one-shot V1 kernel (k_v1_feistel serves the mapped form)
     achieved = units * BYTES_PER_ID / (per_launch_ms * 1e-3) / 1e9 if per_launch_ms > 0 else 0.0
     out_bytes = out.numel() * out.element_size()
     traffic = _pmc_traffic(args.workload, syms) if world == 1 else None

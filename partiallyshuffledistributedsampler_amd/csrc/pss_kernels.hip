@@ -389,6 +389,91 @@ __global__ __launch_bounds__(64) void k_v1_feistel(Geometry g, V1Plan vp, const 
     }
 }
 
+// One-shot V1 (unmapped ids): a grid of short-lived 256-thread workgroups, each 1024
+// consecutive positions of one rank -- 4 per lane, written as two 16-byte stores (the store
+// pattern of torch's fill_, which MI355X writes at 6.2-6.9 TB/s against 5.2-5.3 TB/s for waves
+// that loop over their own runs, tools/ubench_store2.hip).  Fast workgroups (inside one full
+// window that needs no cycle walking, inside the position range, 16-B aligned output) take the
+// packed Feistel on the window's SGPR keys; the others the per-position general path.  C2 V1:
+// 168 -> 150 us per epoch against the persistent k_v1_feistel, which now serves the mapped
+// hand-off only (same box, profiles/r04/ab_v1_oneshot/).
+constexpr int64_t kV1OsPos = 1024;
+struct V1OsPlan {
+    int64_t blk_lo;            // first 1024-position block of each rank
+    uint32_t bpr;              // blocks per rank
+    uint32_t b_log;            // B = 2^b_log when b_pow2
+    int64_t w_lo, nw;          // windows of the key table
+    uint32_t B, hB, fast_ok, b_pow2;
+};
+
+template <bool PACKED, bool NARROW>
+__global__ __launch_bounds__(256) void k_v1_os(Geometry g, V1OsPlan vp, const RankDesc *__restrict__ ranks,
+                                               int32_t rank_lo, const uint32_t *__restrict__ kt,
+                                               int64_t pos_lo, int64_t count, int64_t *__restrict__ out) {
+    const uint32_t rl = blockIdx.x / vp.bpr;
+    const int64_t p0 = (vp.blk_lo + (int64_t)(blockIdx.x - rl * vp.bpr)) * kV1OsPos;
+    const int64_t pos_hi = pos_lo + count < g.ns ? pos_lo + count : g.ns;
+    const int64_t start = ranks[rank_lo + (int32_t)rl].new_start;
+    int64_t *o = out + (int64_t)rl * count - pos_lo;
+    const uint32_t *ktr = kt + (int64_t)rl * vp.nw * kRoundKeyWords;
+    const int64_t B = vp.B;
+    const int64_t w = vp.b_pow2 ? (p0 >> vp.b_log) : p0 / B;
+    const int64_t wB = w * B;
+    const bool fast = vp.fast_ok && wB + B <= g.ns && p0 + kV1OsPos <= wB + B && p0 >= pos_lo &&
+                      p0 + kV1OsPos <= pos_hi && (((uintptr_t)(o + p0)) & 15u) == 0;
+    const uint32_t l4 = 4u * threadIdx.x;
+    if (fast) {
+        const uint32_t *kw = ktr + (w - vp.w_lo) * kRoundKeyWords;
+        uint32_t kp[kFeistelRounds];
+#pragma unroll
+        for (int i = 0; i < kFeistelRounds; i++) {
+            const uint32_t k = __builtin_amdgcn_readfirstlane(kw[i]);
+            kp[i] = PACKED ? (k & 0xFFFFu) * 0x10001u : k;
+        }
+        const uint32_t x0 = (uint32_t)(p0 - wB) + l4;
+        const uint32_t x[4] = {x0, x0 + 1u, x0 + 2u, x0 + 3u};
+        uint32_t y[4];
+        if constexpr (PACKED) {
+            feistel4_pk16(x, vp.hB, kp, y);
+        } else {
+#pragma unroll
+            for (int j = 0; j < 4; j++) y[j] = feistel_once(x[j], vp.hB, kp);
+        }
+        const int64_t base = start + wB;
+        int64_t id[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            if constexpr (NARROW) {
+                const uint32_t v = (uint32_t)base + y[j];
+                id[j] = (int64_t)__builtin_elementwise_min(v, v - (uint32_t)g.N);
+            } else {
+                id[j] = wrap_id(base + y[j], g.N);
+            }
+        }
+        longlong2 a, b;
+        a.x = id[0]; a.y = id[1]; b.x = id[2]; b.y = id[3];
+        *(longlong2 *)(o + p0 + l4) = a;
+        *(longlong2 *)(o + p0 + l4 + 2) = b;
+        return;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const int64_t p = p0 + l4 + j;
+        if (p < pos_lo || p >= pos_hi) continue;
+        int64_t y = p;
+        if (g.shuffle) {
+            const int64_t wp = p / B;
+            const int64_t len = g.ns - wp * B < B ? g.ns - wp * B : B;
+            const uint32_t *kw = ktr + (wp - vp.w_lo) * kRoundKeyWords;
+            uint32_t kk[kFeistelRounds];
+#pragma unroll
+            for (int i = 0; i < kFeistelRounds; i++) kk[i] = kw[i];
+            y = wp * B + feistel((uint32_t)(p - wp * B), (uint32_t)len, feistel_half_bits((uint32_t)len), kk);
+        }
+        o[p] = wrap_id(start + y, g.N);
+    }
+}
+
 // ------------------------------------------------------------------------------------------
 // launchers
 // ------------------------------------------------------------------------------------------
@@ -529,6 +614,34 @@ hipError_t launch_v1(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, 
     if (g.shuffle)
         hipLaunchKernelGGL(k_v1_keys, dim3((uint32_t)cdiv(nw, 256), (uint32_t)nr), dim3(256), 0, s,
                            g, rank_lo, w_lo, nw, key_ws);
+    if (!mapped) {
+        V1OsPlan op{};
+        op.blk_lo = pos_lo / kV1OsPos;
+        const int64_t bpr = (pos_hi - 1) / kV1OsPos - op.blk_lo + 1;
+        op.bpr = (uint32_t)bpr;
+        op.w_lo = w_lo;
+        op.nw = nw;
+        op.B = (uint32_t)g.B;
+        op.hB = feistel_half_bits(op.B);
+        op.b_pow2 = (g.B & (g.B - 1)) == 0 ? 1u : 0u;
+        op.b_log = (uint32_t)ceil_log2_u64((uint64_t)g.B);
+        op.fast_ok = g.shuffle && op.B == (1u << (2 * op.hB)) && (g.B % kV1OsPos) == 0;
+        const bool narrow = g.N + g.ns < (int64_t)UINT32_MAX;
+        const uint64_t blocks = (uint64_t)bpr * (uint64_t)nr;
+        if (blocks < ((uint64_t)1 << 31)) {
+            const dim3 grid((uint32_t)blocks);
+#define PSS_V1OS(PK, NA) hipLaunchKernelGGL((k_v1_os<PK, NA>), grid, dim3(256), 0, s, g, op, ranks, rank_lo, \
+                                            (const uint32_t *)key_ws, pos_lo, count, out)
+            const bool pk = feistel_packed_ok(op.hB);
+            if (pk && narrow) PSS_V1OS(true, true);
+            else if (pk) PSS_V1OS(true, false);
+            else if (narrow) PSS_V1OS(false, true);
+            else PSS_V1OS(false, false);
+#undef PSS_V1OS
+            mk(-1, s);
+            return hipGetLastError();
+        }
+    }
     V1Plan vp{};
     vp.sb_lo = pos_lo / 256;
     vp.nsb = (pos_hi - 1) / 256 - vp.sb_lo + 1;

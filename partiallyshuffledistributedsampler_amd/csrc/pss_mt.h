@@ -303,250 +303,427 @@ __device__ void mt_draws_pair(uint32_t *mt, uint32_t W, uint32_t P, Emit emit) {
 
 // The same draws on a workgroup of kMtWgThreads (10 waves) per stream, for long windows (C5's
 // pool2 windows are 2^20 steps and there are only ~11 per rank: one wave per stream left most of
-// the chip idle).  Per twist:
-//   twist   the 624 new words in three barrier-separated phases of <= 227 words (new[k] needs
-//           new[k - 227] from k = 227 on), double-buffered, tempered into tw[]
-//   blocks  the ten 64-word blocks, wave w takes block w: where every k2 verdict
-//           of a block is fixed over all k2 indices the block can see in this twist ([i2, i2 +
-//           32 (b + 1)] for block b), its transfer -- the composed role map and the k1 / k2
-//           acceptances for either start role -- comes from one role scan without knowing
-//           where the block starts
-//   combine wave 0 chains the transfers from the twist's start state up to the first block
-//           that was not settled, then runs that block and all after it exactly (pair_block)
-//   emit    each wave emits its settled blocks from their now known start states
-constexpr int kMtWgThreads = 640;   // ten waves: one 64-word block each
-constexpr int kMtBlocks = (kMtN + 63) / 64;   // 10: nine of 64 words, one of 48
+// the chip idle).  The stream is consumed in ROUNDS of kMtRound twists (kMtRound * 624 words);
+// one wave -- the generator, the last -- twists and tempers the NEXT round into the other half
+// of a double-buffered ring (three dependent 227-word steps per twist, in program order inside
+// the wave: no barrier), while the other nine consume the current round in three
+// barrier-separated phases:
+//   summaries  each 64-word block of the round, wave w taking blocks w, w + 9, ...: where every
+//              verdict of the block is fixed over the index window its start can lie in, its
+//              transfer -- V2: the composed role map and the k1 / k2 acceptances for either start
+//              role; V1: the draws it makes -- comes from one role scan (a popcount) without knowing
+//              where the block starts.  The window is the expected index at the block's word offset
+//              (the round's acceptance rate) +- 6 standard deviations, clipped to what is possible
+//              at all; a start outside it only costs the block its shortcut
+//   combine    wave 0 walks the round's blocks in order: a settled block whose true start lies in
+//              its window is one transfer, any other block runs exactly (pair_block / draw_block,
+//              which emit) -- where round 3 ran every block after the first unsettled one exactly
+//   emit       each wave emits its settled blocks from their now known start states.
+// Three barriers per round of 8 twists where round 3 took three per twist: C5 V2 exact draws
+// (profiles/r04/) against 14.2 ms.
+constexpr int kMtWgThreads = 640;   // nine consumer waves and the generator
+constexpr int kMtBlocks = (kMtN + 63) / 64;   // 10 per twist: nine of 64 words, one of 48
 constexpr int kMtWgWaves = kMtWgThreads / 64;
-constexpr int kMtPerWave = (kMtBlocks + kMtWgWaves - 1) / kMtWgWaves;
+constexpr int kMtRound = 8;                               // twists per round (even)
+constexpr int kMtRoundWords = kMtRound * kMtN;
+constexpr int kMtRoundBlocks = kMtRound * kMtBlocks;      // 80
+constexpr int kMtConsumers = kMtWgWaves - 1;
+constexpr int kMtPerWave = (kMtRoundBlocks + kMtConsumers - 1) / kMtConsumers;   // 9
+static_assert(kMtRound % 2 == 0, "the generator's state buffer returns to mt[cur] after a round");
+static_assert(kMtRoundBlocks <= 128, "the combiner keeps the summaries in two lanes sets");
 
 struct MtWgShared {
-    uint32_t mt[2][kMtN];           // state, double-buffered across the twist
-    uint32_t tw[2][kMtN];           // tempered words: the current twist's and the next one's
-    uint32_t sum[kMtBlocks][6];     // settled?, role map, c1(st = 0), c1(st = 1), c2(0), c2(1)
-    uint32_t start[kMtBlocks][3];   // (st, i1, i2) at each block's start
-    uint32_t state[4];              // st, i1, i2, first unsettled block
+    uint32_t mt[2][kMtN];                 // generator state, double-buffered across a twist
+    uint32_t tw[2][kMtRoundWords];        // tempered words: the round consumed, the next one
+    uint32_t sum[kMtRoundBlocks][6];      // settled?, role map | draws, c1(0), c1(1), c2(0), c2(1)
+    uint32_t win[kMtRoundBlocks][2];      // index window [lo, hi] the block's summary assumed
+    uint32_t start[kMtRoundBlocks][4];    // (st, i1, i2) or (d) at each block's start; [3] = 1:
+                                          // handled by the combiner (ran exactly, or past the end)
+    uint32_t state[4];                    // st, i1, i2 | d
 };
 
-// Software pipeline of the workgroup draws: the twist that makes the NEXT 624 words runs on
-// waves 4.. beside the current twist's three phases (blocks | combine | emit), one of its three
-// dependent steps per phase, so a twist costs three barriers instead of six phases.  Step p
-// computes new[k], k in [227 p, 227 p + 227) (new[k] needs new[k - 227] from k = 227 on), by
-// thread tt = tid - kMtTwistLo; the tempered word goes to tw.
-constexpr int kMtTwistLo = 256;
-__device__ __forceinline__ void mt_twist_step(const uint32_t *o, uint32_t *nw, uint32_t *tw, int p,
-                                              int tid) {
+// diagnostic build only (-DPSS_MT_STAMPS, tools/stamp_mt.hip): per-workgroup clock sums of the
+// round phases -- [0..2] summaries / combine / emit (wave 0, barrier to barrier), [3..5] the
+// generator's share of each phase, [6] blocks run exactly, [7] rounds
+#ifdef PSS_MT_STAMPS
+__device__ uint64_t pss_mt_stamps[4096][8];
+#define PSS_MT_T(v) const uint64_t v = __builtin_amdgcn_s_memtime()
+#define PSS_MT_ADD(slot_, val_) do { if ((threadIdx.x & 63) == 0 && blockIdx.x < 4096u) pss_mt_stamps[blockIdx.x][slot_] += (val_); } while (0)
+#else
+#define PSS_MT_T(v) do { } while (0)
+#define PSS_MT_ADD(slot_, val_) do { } while (0)
+#endif
+
+// generator wave: step p (0..2) of one twist, o -> nw, tempered words into tw: new[k] for k in
+// [227 p, 227 p + 227) (new[k] needs new[k - 227] from k = 227 on), 64 lanes x 4
+__device__ __forceinline__ void mt_gen_step(const uint32_t *o, uint32_t *nw, uint32_t *tw, int p, int lane) {
     constexpr int D = kMtN - kMtM;   // 227
-    const uint32_t tt = (uint32_t)(tid - kMtTwistLo);
-    const int k = (int)tt + D * p;
-    if (tt >= (uint32_t)D || k >= kMtN) return;
-    uint32_t v;
-    if (p == 0) v = mt_twist_word(o[k], o[k + 1], o[k + kMtM]);
-    else if (k < kMtN - 1) v = mt_twist_word(o[k], o[k + 1], nw[k - D]);
-    else v = mt_twist_word(o[kMtN - 1], nw[0], nw[kMtM - 1]);
-    nw[k] = v;
-    tw[k] = mt_temper(v);
+    uint32_t v[4];
+#pragma unroll
+    for (int it = 0; it < 4; it++) {
+        const int tt = lane + 64 * it, k = tt + D * p;
+        v[it] = 0u;
+        if (tt < D && k < kMtN) {
+            if (p == 0) v[it] = mt_twist_word(o[k], o[k + 1], o[k + kMtM]);
+            else if (k < kMtN - 1) v[it] = mt_twist_word(o[k], o[k + 1], nw[k - D]);
+            else v[it] = mt_twist_word(o[kMtN - 1], nw[0], nw[kMtM - 1]);
+        }
+    }
+#pragma unroll
+    for (int it = 0; it < 4; it++) {
+        const int tt = lane + 64 * it, k = tt + D * p;
+        if (tt < D && k < kMtN) {
+            nw[k] = v[it];
+            tw[k] = mt_temper(v[it]);
+        }
+    }
+    wave_lds_order();
 }
 
-// the first twist of a stream (the pipeline's prologue): old = mt[cur] -> mt[cur ^ 1], tw
-__device__ __forceinline__ void mt_twist_wg(MtWgShared &sh, int cur, uint32_t *tw) {
-#pragma unroll
-    for (int p = 0; p < 3; p++) {
-        mt_twist_step(sh.mt[cur], sh.mt[cur ^ 1], tw, p, threadIdx.x);
-        __syncthreads();
+// steps [s_lo, s_hi) of a round's 3 kMtRound twist steps, the round's words into tw (generator
+// wave only; the round starts from mt[cur] and, kMtRound being even, ends there)
+__device__ __forceinline__ void mt_gen_round(MtWgShared &sh, int cur, uint32_t *tw, int s_lo, int s_hi,
+                                             int lane) {
+    for (int s = s_lo; s < s_hi; s++) {
+        const int t = s / 3, p = s - 3 * t, c = cur ^ (t & 1);
+        mt_gen_step(sh.mt[c], sh.mt[c ^ 1], tw + t * kMtN, p, lane);
     }
+}
+
+// block b of a round: its first word and valid words
+__device__ __forceinline__ int mt_block_q0(int b) { return (b / kMtBlocks) * kMtN + 64 * (b % kMtBlocks); }
+__device__ __forceinline__ int mt_block_nval(int b) { return b % kMtBlocks == kMtBlocks - 1 ? kMtN - 64 * (kMtBlocks - 1) : 64; }
+
+// index window of a block's start: x0 + the expected count at word offset wb (rate per word) +-
+// 6 sd + 8 (var = the count's variance per word), clipped to [x0, x0 + cap(wb)] (what the words
+// before it can reach at all)
+__device__ __forceinline__ void mt_window(uint32_t x0, float rate, float var, uint32_t wb, uint32_t cap,
+                                          uint32_t &lo, uint32_t &hi) {
+    const float e = rate * (float)wb;
+    const float m = 6.0f * __builtin_sqrtf(var * (float)wb + 1.0f) + 8.0f;
+    const float l = e - m, h = e + m;
+    lo = x0 + (l > 0.0f ? (uint32_t)l : 0u);
+    const uint32_t hh = (uint32_t)h + 1u;
+    hi = x0 + (hh < cap ? hh : cap);
+    if (lo > hi) lo = hi;
 }
 
 template <class Emit>
 __device__ void mt_draws_pair_wg(MtWgShared &sh, int cur, uint32_t W, uint32_t P, Emit emit) {
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const bool gen = wv == kMtWgWaves - 1;
     const uint32_t kb1 = 32u - (uint32_t)__builtin_clz(P);
     const uint64_t below = lanemask_lt();
+    const float acc1 = (float)P / (float)(1ull << kb1);
     if (tid == 0) { sh.state[0] = 0u; sh.state[1] = 0u; sh.state[2] = 0u; }
-    mt_twist_wg(sh, cur, sh.tw[0]);   // (its first barrier also publishes state)
-    cur ^= 1;
-    for (int tb = 0;; tb ^= 1) {
+    if (gen) mt_gen_round(sh, cur, sh.tw[0], 0, 3 * kMtRound, lane);
+    __syncthreads();
+    for (int rs = 0;; rs ^= 1) {
         if (sh.state[2] >= W) break;   // (uniform: read after a barrier)
-        // tc: this twist's tempered words; the next twist (old = mt[cur] -> mt[cur ^ 1], into
-        // tw[tb ^ 1]) runs one step per phase beside it
-        const uint32_t *tc = sh.tw[tb];
-        const uint32_t *o = sh.mt[cur];
-        uint32_t *nw = sh.mt[cur ^ 1], *tn = sh.tw[tb ^ 1];
-        mt_twist_step(o, nw, tn, 0, tid);
-        // ---- blocks: transfers of the settled ones
+        PSS_MT_T(t0);
+        const uint32_t *tc = sh.tw[rs];
+        uint32_t *tn = sh.tw[rs ^ 1];
+        // ---- summaries (consumers) | the next round's first third (generator)
         const uint32_t i2_0 = sh.state[2];
+        const uint32_t n2_0 = i2_0 < W ? W - i2_0 : 1u;
+        const float acc2 = (float)n2_0 / (float)(1ull << (32u - (uint32_t)__builtin_clz(n2_0)));
+        // k2 draws per word: a step takes Geom(acc1) + Geom(acc2) words, so over w words the
+        // count has mean w / E and variance ~ w Var / E^3 (renewal process)
+        const float Ex = 1.0f / acc1 + 1.0f / acc2;
+        const float Vx = (1.0f - acc1) / (acc1 * acc1) + (1.0f - acc2) / (acc2 * acc2);
+        const float rate = 1.0f / Ex, var = Vx / (Ex * Ex * Ex);
         uint32_t Fkeep[kMtPerWave];
         bool a1k[kMtPerWave], a2k[kMtPerWave];
+        if (gen) {
+            mt_gen_round(sh, cur, tn, 0, kMtRound, lane);
+            PSS_MT_T(tg); PSS_MT_ADD(3, tg - t0);
+        } else {
 #pragma unroll
-        for (int s = 0; s < kMtPerWave; s++) {
-            Fkeep[s] = 0u; a1k[s] = false; a2k[s] = false;
-            const int b = wv + kMtWgWaves * s;
-            if (b >= kMtBlocks) break;
-            const int q0 = 64 * b, nval = kMtN - q0 < 64 ? kMtN - q0 : 64;
-            const bool valid = lane < nval;
-            const uint32_t word = valid ? tc[q0 + lane] : 0u;
-            const bool a1 = valid && (word >> (32u - kb1)) < P;
-            const uint32_t jhi = i2_0 + 32u * (uint32_t)(b + 1);
-            const uint32_t nhi = i2_0 < W ? W - i2_0 : 1u, nlo = jhi < W ? W - jhi : 1u;
-            const uint32_t kbh = 32u - (uint32_t)__builtin_clz(nhi);
-            const uint32_t rh = word >> (32u - kbh);
-            const bool sure = kbh == 32u - (uint32_t)__builtin_clz(nlo) && (rh < nlo || rh >= nhi);
-            const bool settled = __ballot(valid && !sure) == 0;
-            if (settled) {
-                const bool a2 = valid && rh < nlo;
-                const uint32_t Fx = wave_role_scan(((a1 != a2) ? 2u : 0u) | (a1 ? 1u : 0u));
-                const uint32_t Fp = (uint32_t)__shfl((int)Fx, lane > 0 ? lane - 1 : 0);
-                uint32_t c[4];
-#pragma unroll
-                for (uint32_t s0 = 0; s0 < 2; s0++) {
-                    const uint32_t role = lane ? role_apply(Fp, s0) : s0;
-                    const bool acc = valid && (role ? a2 : a1);
-                    c[s0] = (uint32_t)__popcll(__ballot(acc && role == 0u));
-                    c[2 + s0] = (uint32_t)__popcll(__ballot(acc && role == 1u));
-                }
-                const uint32_t F63 = (uint32_t)__shfl((int)Fx, 63);   // (all lanes: a shuffle reads active lanes)
-                if (lane == 0) {
-                    sh.sum[b][0] = 1u;
-                    sh.sum[b][1] = F63;
-                    sh.sum[b][2] = c[0]; sh.sum[b][3] = c[1]; sh.sum[b][4] = c[2]; sh.sum[b][5] = c[3];
-                }
-                Fkeep[s] = Fp;
-                a1k[s] = a1;
-                a2k[s] = a2;
-            } else if (lane == 0) {
-                sh.sum[b][0] = 0u;
-            }
-        }
-        __syncthreads();
-        mt_twist_step(o, nw, tn, 1, tid);
-        // ---- combine (wave 0): chain the settled transfers, then the rest exactly.  Lane b holds
-        // block b's summary; the chain reads it with readlane (no LDS round trip per block)
-        if (wv == 0) {
-            uint32_t st = sh.state[0], i1 = sh.state[1], i2 = sh.state[2];
-            uint32_t vs = 0u, vF = 0u, v10 = 0u, v11 = 0u, v20 = 0u, v21 = 0u;
-            if (lane < kMtBlocks) {
-                vs = sh.sum[lane][0];
-                if (vs) { vF = sh.sum[lane][1]; v10 = sh.sum[lane][2]; v11 = sh.sum[lane][3]; v20 = sh.sum[lane][4]; v21 = sh.sum[lane][5]; }
-            }
-            int b = 0;
-            for (; b < kMtBlocks; b++) {
-                if (lane == 0) { sh.start[b][0] = st; sh.start[b][1] = i1; sh.start[b][2] = i2; }
-                if (!__builtin_amdgcn_readlane((int)vs, b)) break;
-                i1 += (uint32_t)__builtin_amdgcn_readlane((int)(st ? v11 : v10), b);
-                i2 += (uint32_t)__builtin_amdgcn_readlane((int)(st ? v21 : v20), b);
-                st = role_apply((uint32_t)__builtin_amdgcn_readlane((int)vF, b), st);
-            }
-            const int fu = b;
-            for (; b < kMtBlocks && i2 < W; b++) {
-                const int q0 = 64 * b, nval = kMtN - q0 < 64 ? kMtN - q0 : 64;
+            for (int s = 0; s < kMtPerWave; s++) {
+                Fkeep[s] = 0u; a1k[s] = false; a2k[s] = false;
+                const int b = wv + kMtConsumers * s;
+                if (b >= kMtRoundBlocks) break;
+                const int q0 = mt_block_q0(b), nval = mt_block_nval(b);
                 const bool valid = lane < nval;
-                pair_block(valid ? tc[q0 + lane] : 0u, valid, W, P, kb1, st, i1, i2, emit);
-            }
-            if (lane == 0) { sh.state[0] = st; sh.state[1] = i1; sh.state[2] = i2; sh.state[3] = (uint32_t)fu; }
-        }
-        __syncthreads();
-        mt_twist_step(o, nw, tn, 2, tid);
-        cur ^= 1;
-        // ---- emit the settled blocks before the first unsettled one
-        const int fu = (int)sh.state[3];
+                const uint32_t word = valid ? tc[q0 + lane] : 0u;
+                const bool a1 = valid && (word >> (32u - kb1)) < P;
+                uint32_t jlo, jhi;   // the k2 index at the block's start (at most 1 per 2 words)
+                mt_window(i2_0, rate, var, (uint32_t)q0, (uint32_t)q0 / 2u + 1u, jlo, jhi);
+                const uint32_t jtop = jhi + 32u;
+                const uint32_t nhi = jlo < W ? W - jlo : 1u, nlo = jtop < W ? W - jtop : 1u;
+                const uint32_t kbh = 32u - (uint32_t)__builtin_clz(nhi);
+                const uint32_t rh = word >> (32u - kbh);
+                const bool sure = kbh == 32u - (uint32_t)__builtin_clz(nlo) && (rh < nlo || rh >= nhi);
+                const bool settled = __ballot(valid && !sure) == 0;
+                if (settled) {
+                    const bool a2 = valid && rh < nlo;
+                    const uint32_t Fx = wave_role_scan(((a1 != a2) ? 2u : 0u) | (a1 ? 1u : 0u));
+                    const uint32_t Fp = (uint32_t)__shfl((int)Fx, lane > 0 ? lane - 1 : 0);
+                    uint32_t c[4];
 #pragma unroll
-        for (int s = 0; s < kMtPerWave; s++) {
-            const int b = wv + kMtWgWaves * s;
-            if (b >= fu) break;
-            const int q0 = 64 * b, nval = kMtN - q0 < 64 ? kMtN - q0 : 64;
-            const bool valid = lane < nval;
-            const uint32_t word = valid ? tc[q0 + lane] : 0u;
-            const uint32_t st = sh.start[b][0], i1 = sh.start[b][1], i2 = sh.start[b][2];
-            const uint32_t role = lane ? role_apply(Fkeep[s], st) : st;
-            const bool acc = valid && (role ? a2k[s] : a1k[s]);
-            const uint64_t m1 = __ballot(acc && role == 0u), m2 = __ballot(acc && role == 1u);
-            if (acc) {
-                if (role == 0u) {
-                    const uint32_t i = i1 + (uint32_t)__popcll(m1 & below);
-                    if (i < W) emit(false, i, word >> (32u - kb1));
-                } else {
-                    const uint32_t j = i2 + (uint32_t)__popcll(m2 & below);
-                    const uint32_t nhi = i2_0 < W ? W - i2_0 : 1u;
-                    if (j < W) emit(true, j, word >> (32u - (32u - (uint32_t)__builtin_clz(nhi))));
+                    for (uint32_t s0 = 0; s0 < 2; s0++) {
+                        const uint32_t role = lane ? role_apply(Fp, s0) : s0;
+                        const bool acc = valid && (role ? a2 : a1);
+                        c[s0] = (uint32_t)__popcll(__ballot(acc && role == 0u));
+                        c[2 + s0] = (uint32_t)__popcll(__ballot(acc && role == 1u));
+                    }
+                    const uint32_t F63 = (uint32_t)__shfl((int)Fx, 63);   // (all lanes: a shuffle reads active lanes)
+                    if (lane == 0) {
+                        sh.sum[b][0] = 1u; sh.sum[b][1] = F63;
+                        sh.sum[b][2] = c[0]; sh.sum[b][3] = c[1]; sh.sum[b][4] = c[2]; sh.sum[b][5] = c[3];
+                        sh.win[b][0] = jlo; sh.win[b][1] = jhi;
+                    }
+                    Fkeep[s] = Fp; a1k[s] = a1; a2k[s] = a2;
+                } else if (lane == 0) {
+                    sh.sum[b][0] = 0u;
                 }
             }
         }
         __syncthreads();
+        PSS_MT_T(t1);
+        if (wv == 0) PSS_MT_ADD(0, t1 - t0);
+        // ---- combine (wave 0) | second third
+        if (gen) {
+            mt_gen_round(sh, cur, tn, kMtRound, 2 * kMtRound, lane);
+            PSS_MT_T(tg); PSS_MT_ADD(4, tg - t1);
+        } else if (wv == 0) {
+            // the round's blocks in order, 64 at a time (lane = block): an inclusive scan of the
+            // settled blocks' transfers from the first unresolved block f gives every block's
+            // start; the blocks up to the first one that is unsettled or whose start falls outside
+            // its window take their starts from it, that block runs exactly, and the scan resumes
+            // after it
+            uint32_t st = sh.state[0], i1 = sh.state[1], i2 = sh.state[2];
+            bool fin = false;   // past the stream's end
+            for (int h = 0; h < 2 && !fin; h++) {
+                const int b = 64 * h + lane;
+                const bool inb = b < kMtRoundBlocks;
+                const uint32_t vs = inb ? sh.sum[b][0] : 0u;
+                uint32_t F = 0u, a0 = 0u, a1 = 0u, c0 = 0u, c1 = 0u, lo = 0u, hi = 0u;
+                if (vs) {
+                    F = sh.sum[b][1]; a0 = sh.sum[b][2]; a1 = sh.sum[b][3];
+                    c0 = sh.sum[b][4]; c1 = sh.sum[b][5]; lo = sh.win[b][0]; hi = sh.win[b][1];
+                }
+                const int nb = kMtRoundBlocks - 64 * h < 64 ? kMtRoundBlocks - 64 * h : 64;
+                int f = 0;
+                while (f < nb) {
+                    // transfer of lane l (identity below f): (role map, k1 / k2 draws per start role)
+                    uint32_t tF = lane >= f && vs ? F : 0u;
+                    uint32_t t10 = lane >= f && vs ? a0 : 0u, t11 = lane >= f && vs ? a1 : 0u;
+                    uint32_t t20 = lane >= f && vs ? c0 : 0u, t21 = lane >= f && vs ? c1 : 0u;
+#pragma unroll
+                    for (int d = 1; d < 64; d <<= 1) {   // inclusive scan: (earlier) then (this)
+                        const uint32_t pF = (uint32_t)__shfl_up((int)tF, d), p10 = (uint32_t)__shfl_up((int)t10, d);
+                        const uint32_t p11 = (uint32_t)__shfl_up((int)t11, d), p20 = (uint32_t)__shfl_up((int)t20, d);
+                        const uint32_t p21 = (uint32_t)__shfl_up((int)t21, d);
+                        if (lane >= d) {
+                            const uint32_t q0 = role_apply(pF, 0u), q1 = role_apply(pF, 1u);
+                            const uint32_t n10 = p10 + (q0 ? t11 : t10), n11 = p11 + (q1 ? t11 : t10);
+                            const uint32_t n20 = p20 + (q0 ? t21 : t20), n21 = p21 + (q1 ? t21 : t20);
+                            tF = role_compose(tF, pF);
+                            t10 = n10; t11 = n11; t20 = n20; t21 = n21;
+                        }
+                    }
+                    // exclusive prefix -> each lane's start state
+                    const uint32_t eF = (uint32_t)__shfl_up((int)tF, 1), e10 = (uint32_t)__shfl_up((int)t10, 1);
+                    const uint32_t e11 = (uint32_t)__shfl_up((int)t11, 1), e20 = (uint32_t)__shfl_up((int)t20, 1);
+                    const uint32_t e21 = (uint32_t)__shfl_up((int)t21, 1);
+                    const bool first = lane == 0;
+                    const uint32_t sst = first ? st : role_apply(eF, st);
+                    const uint32_t si1 = i1 + (first ? 0u : (st ? e11 : e10));
+                    const uint32_t si2 = i2 + (first ? 0u : (st ? e21 : e20));
+                    const bool ok = lane >= f && lane < nb && vs && si2 < W && si2 >= lo && si2 <= hi;
+                    const uint64_t bad = __ballot(lane >= f && lane < nb && !ok);
+                    const int g = bad ? __ffsll((long long)bad) - 1 : nb;
+                    if (lane >= f && lane < g) {
+                        sh.start[b][0] = sst; sh.start[b][1] = si1; sh.start[b][2] = si2; sh.start[b][3] = 0u;
+                    }
+                    if (g >= nb) {   // every block through: the state after the set's last block
+                        const int e = nb - 1;
+                        const uint32_t lF = (uint32_t)__builtin_amdgcn_readlane((int)tF, e);
+                        const uint32_t l10 = (uint32_t)__builtin_amdgcn_readlane((int)t10, e);
+                        const uint32_t l11 = (uint32_t)__builtin_amdgcn_readlane((int)t11, e);
+                        const uint32_t l20 = (uint32_t)__builtin_amdgcn_readlane((int)t20, e);
+                        const uint32_t l21 = (uint32_t)__builtin_amdgcn_readlane((int)t21, e);
+                        i1 += st ? l11 : l10;
+                        i2 += st ? l21 : l20;
+                        st = role_apply(lF, st);
+                        break;
+                    }
+                    // the state at block g's start
+                    st = (uint32_t)__builtin_amdgcn_readlane((int)sst, g);
+                    i1 = (uint32_t)__builtin_amdgcn_readlane((int)si1, g);
+                    i2 = (uint32_t)__builtin_amdgcn_readlane((int)si2, g);
+                    // block g: past the stream's end (so is every block after it), or run exactly
+                    const int bg = 64 * h + g;
+                    if (i2 >= W) {
+                        for (int r = bg + lane; r < kMtRoundBlocks; r += 64) {
+                            sh.start[r][0] = st; sh.start[r][1] = i1; sh.start[r][2] = i2; sh.start[r][3] = 1u;
+                        }
+                        fin = true;
+                        break;
+                    }
+                    if (lane == 0) {
+                        sh.start[bg][0] = st; sh.start[bg][1] = i1; sh.start[bg][2] = i2; sh.start[bg][3] = 1u;
+                    }
+                    PSS_MT_ADD(6, 1);
+                    const int q0 = mt_block_q0(bg), nval = mt_block_nval(bg);
+                    const bool valid = lane < nval;
+                    pair_block(valid ? tc[q0 + lane] : 0u, valid, W, P, kb1, st, i1, i2, emit);
+                    f = g + 1;
+                }
+            }
+            if (lane == 0) { sh.state[0] = st; sh.state[1] = i1; sh.state[2] = i2; }
+        }
+        __syncthreads();
+        PSS_MT_T(t2);
+        if (wv == 0) PSS_MT_ADD(1, t2 - t1);
+        // ---- emit the settled blocks the combiner only chained | last third
+        if (gen) {
+            mt_gen_round(sh, cur, tn, 2 * kMtRound, 3 * kMtRound, lane);
+            PSS_MT_T(tg); PSS_MT_ADD(5, tg - t2);
+        } else {
+#pragma unroll
+            for (int s = 0; s < kMtPerWave; s++) {
+                const int b = wv + kMtConsumers * s;
+                if (b >= kMtRoundBlocks) break;
+                if (!sh.sum[b][0] || sh.start[b][3]) continue;
+                const int q0 = mt_block_q0(b), nval = mt_block_nval(b);
+                const bool valid = lane < nval;
+                const uint32_t word = valid ? tc[q0 + lane] : 0u;
+                const uint32_t st = sh.start[b][0], i1 = sh.start[b][1], i2 = sh.start[b][2];
+                const uint32_t role = lane ? role_apply(Fkeep[s], st) : st;
+                const bool acc = valid && (role ? a2k[s] : a1k[s]);
+                const uint64_t m1 = __ballot(acc && role == 0u), m2 = __ballot(acc && role == 1u);
+                if (acc) {
+                    if (role == 0u) {
+                        const uint32_t i = i1 + (uint32_t)__popcll(m1 & below);
+                        if (i < W) emit(false, i, word >> (32u - kb1));
+                    } else {
+                        const uint32_t j = i2 + (uint32_t)__popcll(m2 & below);
+                        const uint32_t jlo = sh.win[b][0];
+                        const uint32_t nhi = jlo < W ? W - jlo : 1u;
+                        if (j < W) emit(true, j, word >> (32u - (32u - (uint32_t)__builtin_clz(nhi))));
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        PSS_MT_T(t3);
+        if (wv == 0) { PSS_MT_ADD(2, t3 - t2); PSS_MT_ADD(7, 1); }
     }
 }
 
 // mt_draws on a workgroup per stream (V1 windows beyond LDS: ~12 windows per rank at C5), for a
-// non-increasing bound(d): the twist and the block transfers as in mt_draws_pair_wg -- a block
-// whose every verdict is fixed over the bounds of all draw indices it can see in this twist
-// ([d, d + 64 (b + 1)] for block b) makes exactly popc(accepted) draws wherever it starts.
+// non-increasing bound(d), in the rounds of mt_draws_pair_wg: a block whose every verdict is
+// fixed over the bounds of its window's draw indices ([lo, hi + 64]) makes exactly
+// popc(accepted) draws wherever in the window it starts.
 template <class Bound, class Emit>
 __device__ void mt_draws_wg(MtWgShared &sh, int cur, uint32_t nd, Bound bound, Emit emit) {
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const bool gen = wv == kMtWgWaves - 1;
     const uint64_t below = lanemask_lt();
     if (tid == 0) sh.state[0] = 0u;
-    mt_twist_wg(sh, cur, sh.tw[0]);   // pipelined as in mt_draws_pair_wg
-    cur ^= 1;
-    for (int tb = 0;; tb ^= 1) {
+    if (gen) mt_gen_round(sh, cur, sh.tw[0], 0, 3 * kMtRound, lane);
+    __syncthreads();
+    for (int rs = 0;; rs ^= 1) {
         if (sh.state[0] >= nd) break;
-        const uint32_t *tc = sh.tw[tb];
-        const uint32_t *o = sh.mt[cur];
-        uint32_t *nw = sh.mt[cur ^ 1], *tn = sh.tw[tb ^ 1];
-        mt_twist_step(o, nw, tn, 0, tid);
+        const uint32_t *tc = sh.tw[rs];
+        uint32_t *tn = sh.tw[rs ^ 1];
         const uint32_t d0 = sh.state[0];
+        const uint32_t n0 = bound(d0);
+        // draws per word: acceptance a; over w words the count is Binomial(w, a)
+        const float rate = (float)n0 / (float)(1ull << (32u - (uint32_t)__builtin_clz(n0)));
+        const float var = rate * (1.0f - rate);
         bool acck[kMtPerWave];
         uint32_t rk[kMtPerWave];
+        if (gen) {
+            mt_gen_round(sh, cur, tn, 0, kMtRound, lane);
+        } else {
 #pragma unroll
-        for (int s = 0; s < kMtPerWave; s++) {
-            acck[s] = false; rk[s] = 0u;
-            const int b = wv + kMtWgWaves * s;
-            if (b >= kMtBlocks) break;
-            const int q0 = 64 * b, nval = kMtN - q0 < 64 ? kMtN - q0 : 64;
-            const bool valid = lane < nval;
-            const uint32_t word = valid ? tc[q0 + lane] : 0u;
-            const uint32_t dlo = d0 < nd ? d0 : nd - 1u;
-            const uint32_t dhi = d0 + 64u * (uint32_t)(b + 1) < nd ? d0 + 64u * (uint32_t)(b + 1) : nd - 1u;
-            const uint32_t nhi = bound(dlo), nlo = bound(dhi);
-            const uint32_t kbh = 32u - (uint32_t)__builtin_clz(nhi);
-            const uint32_t r = word >> (32u - kbh);
-            const bool sure = kbh == 32u - (uint32_t)__builtin_clz(nlo) && (r < nlo || r >= nhi);
-            if (__ballot(valid && !sure) == 0) {
-                const bool acc = valid && r < nlo;
-                const uint32_t cnt = (uint32_t)__popcll(__ballot(acc));
-                if (lane == 0) { sh.sum[b][0] = 1u; sh.sum[b][1] = cnt; }
-                acck[s] = acc;
-                rk[s] = r;
-            } else if (lane == 0) {
-                sh.sum[b][0] = 0u;
+            for (int s = 0; s < kMtPerWave; s++) {
+                acck[s] = false; rk[s] = 0u;
+                const int b = wv + kMtConsumers * s;
+                if (b >= kMtRoundBlocks) break;
+                const int q0 = mt_block_q0(b), nval = mt_block_nval(b);
+                const bool valid = lane < nval;
+                const uint32_t word = valid ? tc[q0 + lane] : 0u;
+                uint32_t dlo, dhi;
+                mt_window(d0, rate, var, (uint32_t)q0, (uint32_t)q0, dlo, dhi);
+                const uint32_t dtop = dhi + 64u;
+                const uint32_t nhi = bound(dlo < nd ? dlo : nd - 1u), nlo = bound(dtop < nd ? dtop : nd - 1u);
+                const uint32_t kbh = 32u - (uint32_t)__builtin_clz(nhi);
+                const uint32_t r = word >> (32u - kbh);
+                const bool sure = kbh == 32u - (uint32_t)__builtin_clz(nlo) && (r < nlo || r >= nhi);
+                if (__ballot(valid && !sure) == 0) {
+                    const bool acc = valid && r < nlo;
+                    const uint32_t cnt = (uint32_t)__popcll(__ballot(acc));
+                    if (lane == 0) { sh.sum[b][0] = 1u; sh.sum[b][1] = cnt; sh.win[b][0] = dlo; sh.win[b][1] = dhi; }
+                    acck[s] = acc;
+                    rk[s] = r;
+                } else if (lane == 0) {
+                    sh.sum[b][0] = 0u;
+                }
             }
         }
         __syncthreads();
-        mt_twist_step(o, nw, tn, 1, tid);
-        if (wv == 0) {
+        if (gen) {
+            mt_gen_round(sh, cur, tn, kMtRound, 2 * kMtRound, lane);
+        } else if (wv == 0) {
+            // as in mt_draws_pair_wg: a prefix sum of the settled blocks' draw counts from the
+            // first unresolved block, up to the first block that is unsettled or out of its window
             uint32_t d = sh.state[0];
-            uint32_t vs = 0u, vc = 0u;
-            if (lane < kMtBlocks) { vs = sh.sum[lane][0]; vc = vs ? sh.sum[lane][1] : 0u; }
-            int b = 0;
-            for (; b < kMtBlocks; b++) {
-                if (lane == 0) sh.start[b][0] = d;
-                if (!__builtin_amdgcn_readlane((int)vs, b)) break;
-                d += (uint32_t)__builtin_amdgcn_readlane((int)vc, b);
+            bool fin = false;
+            for (int h = 0; h < 2 && !fin; h++) {
+                const int b = 64 * h + lane;
+                const bool inb = b < kMtRoundBlocks;
+                const uint32_t vs = inb ? sh.sum[b][0] : 0u;
+                uint32_t c = 0u, lo = 0u, hi = 0u;
+                if (vs) { c = sh.sum[b][1]; lo = sh.win[b][0]; hi = sh.win[b][1]; }
+                const int nb = kMtRoundBlocks - 64 * h < 64 ? kMtRoundBlocks - 64 * h : 64;
+                int f = 0;
+                while (f < nb) {
+                    uint32_t t = lane >= f && vs ? c : 0u;
+#pragma unroll
+                    for (int dd = 1; dd < 64; dd <<= 1) {
+                        const uint32_t p = (uint32_t)__shfl_up((int)t, dd);
+                        if (lane >= dd) t += p;
+                    }
+                    const uint32_t sd = d + (t - (lane >= f && vs ? c : 0u));   // exclusive prefix
+                    const bool ok = lane >= f && lane < nb && vs && sd < nd && sd >= lo && sd <= hi;
+                    const uint64_t bad = __ballot(lane >= f && lane < nb && !ok);
+                    const int g = bad ? __ffsll((long long)bad) - 1 : nb;
+                    if (lane >= f && lane < g) { sh.start[b][0] = sd; sh.start[b][3] = 0u; }
+                    if (g >= nb) {
+                        d += (uint32_t)__builtin_amdgcn_readlane((int)t, nb - 1);
+                        break;
+                    }
+                    d = (uint32_t)__builtin_amdgcn_readlane((int)sd, g);
+                    const int bg = 64 * h + g;
+                    if (d >= nd) {
+                        for (int r = bg + lane; r < kMtRoundBlocks; r += 64) { sh.start[r][0] = d; sh.start[r][3] = 1u; }
+                        fin = true;
+                        break;
+                    }
+                    if (lane == 0) { sh.start[bg][0] = d; sh.start[bg][3] = 1u; }
+                    const int q0 = mt_block_q0(bg), nval = mt_block_nval(bg);
+                    d += draw_block(lane < nval ? tc[q0 + lane] : 0u, nval, d, nd, bound, emit);
+                    f = g + 1;
+                }
             }
-            const int fu = b;
-            for (; b < kMtBlocks && d < nd; b++) {
-                const int q0 = 64 * b, nval = kMtN - q0 < 64 ? kMtN - q0 : 64;
-                d += draw_block(lane < nval ? tc[q0 + lane] : 0u, nval, d, nd, bound, emit);
-            }
-            if (lane == 0) { sh.state[0] = d; sh.state[3] = (uint32_t)fu; }
+            if (lane == 0) sh.state[0] = d;
         }
         __syncthreads();
-        mt_twist_step(o, nw, tn, 2, tid);
-        cur ^= 1;
-        const int fu = (int)sh.state[3];
+        if (gen) {
+            mt_gen_round(sh, cur, tn, 2 * kMtRound, 3 * kMtRound, lane);
+        } else {
 #pragma unroll
-        for (int s = 0; s < kMtPerWave; s++) {
-            const int b = wv + kMtWgWaves * s;
-            if (b >= fu) break;
-            const uint32_t d = sh.start[b][0] + (uint32_t)__popcll(__ballot(acck[s]) & below);
-            if (acck[s] && d < nd) emit(d, rk[s]);
+            for (int s = 0; s < kMtPerWave; s++) {
+                const int b = wv + kMtConsumers * s;
+                if (b >= kMtRoundBlocks) break;
+                if (!sh.sum[b][0] || sh.start[b][3]) continue;
+                const uint32_t d = sh.start[b][0] + (uint32_t)__popcll(__ballot(acck[s]) & below);
+                if (acck[s] && d < nd) emit(d, rk[s]);
+            }
         }
         __syncthreads();
     }

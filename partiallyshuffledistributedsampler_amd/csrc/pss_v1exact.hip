@@ -141,28 +141,37 @@ __global__ __launch_bounds__(kExactNT) void k_v1_exact(Geometry g, const RankDes
 
 // ---- windows beyond LDS (n > kV1ExactMaxB): the same resolution through HBM ----------------
 // One pass covers `nj` jobs (rank, window) of the launch, jobs j0 .. j0 + nj - 1 (job -> local
-// rank job / nw, window w_lo + job % nw), each with B-entry slices of four u32 arrays:
-//   J   the draws j_i (k_v1x_draws32, one wave per window: the MT stream is serial)
-//   CNT bucket counts of j -> exclusive offsets -> bucket ends (count, scan, scatter)
-//   LST the steps bucketed by j
-//   NXT parent(k) = the smallest k' > k with j_k' = k, else k
-// and the output walks each x[i]'s parent chain to its root (expected length O(1): parent(k)
-// is about k * U^-1 for a uniform U, so chains climb geometrically towards n).
+// rank job / nw, window w_lo + job % nw), each with slices of the window length W:
+//   J      the draws j_k, k = 1 .. n-1 (k_v1x_draws32[_wg]: the MT stream is serial); each draw
+//          also counts its bucket, j >> 11, in BCNT (nbk = ceil(W / 2048) counters per window)
+//   PART   the steps k partitioned by bucket (k_v1x_part: counts -> offsets by k_v1x_bscan, then
+//          per 8192-step chunk a local LDS sort and one coalesced run per bucket), PARTP their
+//          j & 2047
+//   S, H   per bucket in LDS (k_v1x_solve): the lists {k : j_k = p} of its 2048 values p,
+//          sorted; S[k] = the next element of k's list (none: ~0), H[p] = the first element of
+//          list p above p -- with x[0]'s list 0 taking 0 as its smallest element
+// and the output x[i] = S[i] ? root(S[i]) : j_i (x[0]: 0), root(k) = H[k] ? root(H[k]) : k
+// (k_v1x_out; the chains climb geometrically towards n, ~1-2 steps on average).  The resolution
+// of round 3 bucketed the steps by j with one random HBM atomic and one random store per step
+// (5.2 ms at C5) and read every answer back through them (3.3 ms).
+constexpr uint32_t kV1bShift = 11, kV1bBW = 1u << kV1bShift;   // bucket width in values of j
+constexpr uint32_t kV1bNone = 0xFFFFFFFFu;
 struct V1xBig {
     int64_t w_lo, nw;       // windows of the launch
     uint64_t j0;            // first job of the pass
     uint32_t nj;            // jobs in the pass
-    uint32_t B;             // slice length: min(shuffle_buffer, num_samples)
-    uint32_t *J, *CNT, *LST, *NXT;
-    uint32_t xb;            // 256-entry blocks per window (the flat kernels' x extent)
+    uint32_t B;             // slice length W: min(shuffle_buffer, num_samples)
+    uint32_t nbk;           // buckets per window: ceil(W / 2048)
+    uint32_t *J, *S, *H, *PART, *BCNT;   // BCNT: nbk counts -> offsets -> bucket ends per window
+    uint16_t *PARTP;
+    uint32_t xb;            // the flat kernel's x extent (blocks per window)
     uint32_t xcd;           // 1: XCD-major flat grid (v1x_block)
 };
 
-// The flat kernels (count, scatter, parent, out) make random accesses inside one window's
-// slices.  XCD-major grid: workgroup L runs on XCD L mod 8 (round-robin dispatch), so block L is
-// given window slot 8 (L / 8 / xb) + L mod 8 and entry block (L / 8) mod xb -- every window's
-// blocks then run on one XCD, which keeps its slices' lines in that XCD's L2 instead of
-// bouncing the atomics and reads of one window across all eight.  xcd = 0: blockIdx.y = slot.
+// The flat kernels make random accesses inside one window's slices.  XCD-major grid: workgroup
+// L runs on XCD L mod 8 (round-robin dispatch), so block L is given window slot 8 (L / 8 / xb) +
+// L mod 8 and block (L / 8) mod xb -- every window's blocks then run on one XCD, one window after
+// another, which keeps its slices' lines in that XCD's L2.  xcd = 0: blockIdx.y = slot.
 __device__ __forceinline__ bool v1x_block(const V1xBig &b, uint32_t &slot, uint32_t &xblk) {
     if (!b.xcd) { slot = blockIdx.y; xblk = blockIdx.x; return true; }
     const uint32_t L = blockIdx.x, q = L >> 3;
@@ -176,9 +185,8 @@ __device__ __forceinline__ int v1x_len(const Geometry &g, int64_t w) {
     return (int)(g.ns - wb < g.B ? g.ns - wb : g.B);
 }
 
-// Each draw also counts its bucket (CNT[j]++, a fire-and-forget atomic beside the latency-bound
-// draws), so no counting pass re-reads J: C5 V1 exact 17.3 -> 15.4 ms (round 4, same box,
-// profiles/r04/ab_v1x_fcount/)
+// Each draw also counts its bucket (a fire-and-forget atomic on a small, L2-resident table beside
+// the latency-bound draws)
 __global__ __launch_bounds__(64) void k_v1x_draws32(Geometry g, V1xBig b, int64_t epoch) {
     __shared__ uint32_t mt[kMtN];
     const uint64_t job = b.j0 + blockIdx.x;
@@ -186,12 +194,12 @@ __global__ __launch_bounds__(64) void k_v1x_draws32(Geometry g, V1xBig b, int64_
     const int n = v1x_len(g, w);
     if (n <= 1) return;
     uint32_t *jw = b.J + (size_t)blockIdx.x * b.B;
-    uint32_t *cnt = b.CNT + (size_t)blockIdx.x * ((size_t)b.B + 1);
+    uint32_t *cnt = b.BCNT + (size_t)blockIdx.x * b.nbk;
     mt_seed_int(mt, w == 0 ? epoch : epoch + w * 10000);
     mt_draws(mt, (uint32_t)(n - 1), [&](uint32_t d) { return (uint32_t)n - d; },
              [&](uint32_t d, uint32_t r) {
                  jw[n - 1 - (int)d] = r;
-                 atomicAdd(&cnt[r], 1u);
+                 atomicAdd(&cnt[r >> kV1bShift], 1u);
              });
 }
 
@@ -204,38 +212,24 @@ __global__ __launch_bounds__(kMtWgThreads) void k_v1x_draws32_wg(Geometry g, V1x
     const int n = v1x_len(g, w);
     if (n <= 1) return;
     uint32_t *jw = b.J + (size_t)blockIdx.x * b.B;
-    uint32_t *cnt = b.CNT + (size_t)blockIdx.x * ((size_t)b.B + 1);
+    uint32_t *cnt = b.BCNT + (size_t)blockIdx.x * b.nbk;
     if (threadIdx.x < 64) mt_seed_int(sh.mt[0], w == 0 ? epoch : epoch + w * 10000);
     __syncthreads();
     mt_draws_wg(sh, 0, (uint32_t)(n - 1), [&](uint32_t d) { return (uint32_t)n - d; },
                 [&](uint32_t d, uint32_t r) {
                     jw[n - 1 - (int)d] = r;
-                    atomicAdd(&cnt[r], 1u);
+                    atomicAdd(&cnt[r >> kV1bShift], 1u);
                 });
 }
 
-// slot of the pass and block of the window's entries (v1x_block)
-#define V1X_SLOT_PROLOGUE                                                          \
-    uint32_t slot, xblk;                                                           \
-    if (!v1x_block(b, slot, xblk)) return;                                         \
-    const uint64_t job = b.j0 + slot;                                              \
-    const int64_t w = b.w_lo + (int64_t)(job % (uint64_t)b.nw);                    \
-    const int n = v1x_len(g, w);                                                   \
-    const uint32_t *J = b.J + (size_t)slot * b.B;                                  \
-    uint32_t *CNT = b.CNT + (size_t)slot * ((size_t)b.B + 1);                      \
-    (void)J; (void)CNT;
-
-// exclusive scan of CNT[0, n) in place, one workgroup per window, in tiles of kV1xScanNT x 8
-// counts: coalesced loads into LDS (skewed one word per 32), each thread scans 8 consecutive
-// counts, one block scan, coalesced stores.  (A thread per 1/1024 of the window, reading its
-// stretch serially, had every load of a wave touch 64 cache lines: 2.2 ms at C5's windows.)
+// exclusive scan of a window's nbk bucket counts in place, one workgroup per window, in tiles of
+// kV1xScanNT x 8 counts: coalesced loads into LDS (skewed one word per 32), each thread scans 8
+// consecutive counts, one block scan, coalesced stores
 constexpr int kV1xScanNT = 1024, kV1xScanPer = 8, kV1xScanTile = kV1xScanNT * kV1xScanPer;
-__global__ __launch_bounds__(kV1xScanNT) void k_v1x_scan(Geometry g, V1xBig b) {
+__global__ __launch_bounds__(kV1xScanNT) void k_v1x_bscan(Geometry g, V1xBig b) {
     const uint32_t slot = blockIdx.x;
-    const uint64_t job = b.j0 + slot;
-    const int64_t w = b.w_lo + (int64_t)(job % (uint64_t)b.nw);
-    const int n = v1x_len(g, w);
-    uint32_t *CNT = b.CNT + (size_t)slot * ((size_t)b.B + 1);
+    const int n = (int)b.nbk;
+    uint32_t *CNT = b.BCNT + (size_t)slot * b.nbk;
     __shared__ uint32_t tot[kV1xScanNT / 64];
     __shared__ uint32_t st[kV1xScanTile + kV1xScanTile / 32];
     auto ix = [](int e) { return e + (e >> 5); };
@@ -266,60 +260,217 @@ __global__ __launch_bounds__(kV1xScanNT) void k_v1x_scan(Geometry g, V1xBig b) {
     }
 }
 
-__global__ __launch_bounds__(256) void k_v1x_scatter(Geometry g, V1xBig b) {
-    V1X_SLOT_PROLOGUE
-    const int k = (int)(xblk * 256 + threadIdx.x);
-    if (k >= 1 && k < n) b.LST[(size_t)slot * b.B + atomicAdd(&CNT[J[k]], 1u)] = (uint32_t)k;
-}
-
-// smallest k > above in bucket p (bucket p = LST[p ? CNT[p-1] : 0, CNT[p])), or -1
-__device__ __forceinline__ int v1x_succ(const uint32_t *CNT, const uint32_t *LST, int p, int above) {
-    const int b0 = p ? (int)CNT[p - 1] : 0, b1 = (int)CNT[p];
-    int best = -1;
-    for (int x = b0; x < b1; x++) {
-        const int k = (int)LST[x];
-        if (k > above && (best < 0 || k < best)) best = k;
+// ---- partition: steps k -> PART by bucket j_k >> 11 ------------------------------------------
+// A workgroup per 4096-step chunk of a window: the chunk's steps are counted and ranked per
+// bucket in LDS, every bucket present reserves its run of the window's bucket region with one
+// global atomic on BCNT (offsets -> ends), the chunk is sorted by bucket in LDS and written as
+// those runs (C5: ~8 consecutive steps per bucket and chunk).  Windows of more than
+// kV1pLocal buckets (W > 4M) take one global atomic per step instead.
+constexpr int kV1pNT = 256, kV1pPer = 16, kV1pChunk = kV1pNT * kV1pPer, kV1pLocal = 2048;
+__global__ __launch_bounds__(kV1pNT) void k_v1x_part(Geometry g, V1xBig b) {
+    uint32_t slot, xblk;
+    if (!v1x_block(b, slot, xblk)) return;
+    const uint64_t job = b.j0 + slot;
+    const int64_t w = b.w_lo + (int64_t)(job % (uint64_t)b.nw);
+    const int n = v1x_len(g, w);
+    const uint32_t *J = b.J + (size_t)slot * b.B;
+    uint32_t *BC = b.BCNT + (size_t)slot * b.nbk;
+    uint32_t *PART = b.PART + (size_t)slot * b.B;
+    uint16_t *PARTP = b.PARTP + (size_t)slot * b.B;
+    const int k0 = (int)xblk * kV1pChunk, tid = (int)threadIdx.x;
+    if (k0 >= n) return;
+    const int k1 = k0 + kV1pChunk < n ? k0 + kV1pChunk : n;
+    if (b.nbk > (uint32_t)kV1pLocal) {
+        for (int k = k0 + tid; k < k1; k += kV1pNT) {
+            if (k < 1) continue;
+            const uint32_t v = J[k];
+            const uint32_t pos = atomicAdd(&BC[v >> kV1bShift], 1u);
+            PART[pos] = (uint32_t)k;
+            PARTP[pos] = (uint16_t)(v & (kV1bBW - 1u));
+        }
+        return;
     }
-    return best;
+    __shared__ uint32_t hist[kV1pLocal], loff[kV1pLocal], gbase[kV1pLocal];
+    __shared__ uint32_t stk[kV1pChunk];
+    __shared__ uint16_t stp[kV1pChunk], stb[kV1pChunk];
+    __shared__ uint32_t tot[kV1pNT / 64];
+    const int nb = (int)b.nbk;
+    for (int i = tid; i < nb; i += kV1pNT) hist[i] = 0u;
+    __syncthreads();
+    uint32_t val[kV1pPer], rk[kV1pPer];
+#pragma unroll
+    for (int i = 0; i < kV1pPer; i++) {
+        const int k = k0 + tid + kV1pNT * i;
+        val[i] = (k >= 1 && k < k1) ? J[k] : kV1bNone;
+    }
+#pragma unroll
+    for (int i = 0; i < kV1pPer; i++)
+        rk[i] = val[i] != kV1bNone ? atomicAdd(&hist[val[i] >> kV1bShift], 1u) : 0u;
+    __syncthreads();
+    {   // exclusive scan of hist -> loff (nb <= 2048: 8 per thread), and each bucket's reservation
+        constexpr int per = kV1pLocal / kV1pNT;
+        uint32_t c[per], sum = 0;
+#pragma unroll
+        for (int i = 0; i < per; i++) {
+            const int bb = tid * per + i;
+            c[i] = bb < nb ? hist[bb] : 0u;
+            sum += c[i];
+        }
+        uint32_t total;
+        uint32_t run = block_excl_scan<kV1pNT>(sum, tot, total);
+#pragma unroll
+        for (int i = 0; i < per; i++) {
+            const int bb = tid * per + i;
+            if (bb < nb) {
+                loff[bb] = run;
+                if (c[i]) gbase[bb] = atomicAdd(&BC[bb], c[i]);
+            }
+            run += c[i];
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < kV1pPer; i++) {
+        if (val[i] == kV1bNone) continue;
+        const uint32_t bb = val[i] >> kV1bShift, pos = loff[bb] + rk[i];
+        stk[pos] = (uint32_t)(k0 + tid + kV1pNT * i);
+        stp[pos] = (uint16_t)(val[i] & (kV1bBW - 1u));
+        stb[pos] = (uint16_t)bb;
+    }
+    __syncthreads();
+    const int m = k1 - (k0 < 1 ? 1 : k0);
+    for (int e = tid; e < m; e += kV1pNT) {
+        const uint32_t bb = stb[e];
+        const uint32_t pos = gbase[bb] + ((uint32_t)e - loff[bb]);
+        PART[pos] = stk[e];
+        PARTP[pos] = stp[e];
+    }
 }
 
-__global__ __launch_bounds__(256) void k_v1x_parent(Geometry g, V1xBig b) {
-    V1X_SLOT_PROLOGUE
-    const int k = (int)(xblk * 256 + threadIdx.x);
-    if (k >= n) return;
-    const int pk = v1x_succ(CNT, b.LST + (size_t)slot * b.B, k, k);
-    b.NXT[(size_t)slot * b.B + k] = (uint32_t)(pk < 0 ? k : pk);
+// ---- solve: per bucket, its lists sorted in LDS -> S (successors) and H (first above p) ------
+// A workgroup per (window, bucket of 2048 values p): counts its steps per p in LDS, scans them,
+// places the steps list by list in LDS (as many p at a time as kV1sCap entries hold: the first
+// buckets of long windows hold up to ~2048 (ln(W / 2048) + 1) steps), sorts each list (a thread
+// per p; lists are short, ~ln(n / p)) and writes H[p] and the successors S[k].
+constexpr int kV1sNT = 256, kV1sCap = 8192;
+__global__ __launch_bounds__(kV1sNT) void k_v1x_solve(Geometry g, V1xBig b) {
+    uint32_t slot, bk;
+    if (!v1x_block(b, slot, bk)) return;
+    const uint64_t job = b.j0 + slot;
+    const int64_t w = b.w_lo + (int64_t)(job % (uint64_t)b.nw);
+    const int n = v1x_len(g, w);
+    const uint32_t pbase = bk << kV1bShift;
+    if ((int64_t)pbase >= (int64_t)n) return;
+    const int plen = n - (int)pbase < (int)kV1bBW ? n - (int)pbase : (int)kV1bBW;
+    const uint32_t *BC = b.BCNT + (size_t)slot * b.nbk;
+    const uint32_t e0 = bk ? BC[bk - 1] : 0u, e1 = BC[bk];   // (after k_v1x_part: bucket ends)
+    const uint32_t *PART = b.PART + (size_t)slot * b.B;
+    const uint16_t *PARTP = b.PARTP + (size_t)slot * b.B;
+    uint32_t *S = b.S + (size_t)slot * b.B, *H = b.H + (size_t)slot * b.B;
+    __shared__ uint32_t off[kV1bBW + 1], cur[kV1bBW], L[kV1sCap];
+    __shared__ uint32_t tot[kV1sNT / 64];
+    __shared__ int bounds[2];
+    const int tid = (int)threadIdx.x;
+    for (int p = tid; p <= plen; p += kV1sNT) off[p] = 0u;
+    __syncthreads();
+    for (uint32_t e = e0 + tid; e < e1; e += kV1sNT) atomicAdd(&off[PARTP[e]], 1u);
+    __syncthreads();
+    {   // exclusive scan of off[0, plen), 8 per thread; off[plen] = the bucket's steps
+        constexpr int per = (int)kV1bBW / kV1sNT;
+        uint32_t c[per], sum = 0;
+#pragma unroll
+        for (int i = 0; i < per; i++) {
+            const int p = tid * per + i;
+            c[i] = p < plen ? off[p] : 0u;
+            sum += c[i];
+        }
+        uint32_t total;
+        uint32_t run = block_excl_scan<kV1sNT>(sum, tot, total);
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < per; i++) {
+            const int p = tid * per + i;
+            if (p < plen) off[p] = run;
+            run += c[i];
+        }
+        if (tid == 0) off[plen] = total;
+    }
+    __syncthreads();
+    int plo = 0;
+    while (plo < plen) {
+        if (tid == 0) {   // the longest run of lists from plo that fits kV1sCap entries
+            int lo = plo + 1, hi = plen;
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (off[mid] - off[plo] <= (uint32_t)kV1sCap) lo = mid; else hi = mid - 1;
+            }
+            bounds[0] = lo;
+        }
+        __syncthreads();
+        const int phi = bounds[0];
+        const uint32_t ob = off[plo];
+        for (int p = plo + tid; p < phi; p += kV1sNT) cur[p] = off[p] - ob;
+        __syncthreads();
+        for (uint32_t e = e0 + tid; e < e1; e += kV1sNT) {
+            const int p = (int)PARTP[e];
+            if (p >= plo && p < phi) {
+                const uint32_t pos = atomicAdd(&cur[p], 1u);
+                if (pos < (uint32_t)kV1sCap) L[pos] = PART[e];   // (one list of > kV1sCap steps: never)
+            }
+        }
+        __syncthreads();
+        for (int p = plo + tid; p < phi; p += kV1sNT) {
+            const int s0 = (int)(off[p] - ob), s1 = (int)(off[p + 1] - ob);
+            for (int a = s0 + 1; a < s1; a++) {   // insertion sort of the list (short)
+                const uint32_t v = L[a];
+                int c = a - 1;
+                while (c >= s0 && L[c] > v) { L[c + 1] = L[c]; c--; }
+                L[c + 1] = v;
+            }
+            const uint32_t pa = pbase + (uint32_t)p;
+            uint32_t first = kV1bNone;
+            for (int a = s0; a < s1; a++) {
+                const uint32_t k = L[a];
+                if (first == kV1bNone && k > pa) first = k;
+                S[k] = a + 1 < s1 ? L[a + 1] : kV1bNone;
+            }
+            H[pa] = first;
+            if (pa == 0u) S[0] = first;   // step 0 heads list 0 (x[0] = its successor's root)
+        }
+        __syncthreads();
+        plo = phi;
+    }
 }
 
+// ---- output: x[i] = S[i] ? root(S[i]) : j_i (x[0]: 0) -----------------------------------------
 __global__ __launch_bounds__(256) void k_v1x_out(Geometry g, V1xBig b, const RankDesc *__restrict__ ranks,
                                                  int32_t rank_lo, int64_t pos_lo, int64_t count,
                                                  int64_t *__restrict__ out, MapArgs ma) {
-    V1X_SLOT_PROLOGUE
+    uint32_t slot, xblk;
+    if (!v1x_block(b, slot, xblk)) return;
+    const uint64_t job = b.j0 + slot;
+    const int64_t w = b.w_lo + (int64_t)(job % (uint64_t)b.nw);
+    const int n = v1x_len(g, w);
     const int64_t wb = w * g.B;
     const int64_t p = wb + (int64_t)(xblk * 256 + threadIdx.x);
     const int i = (int)(p - wb);
     if (i >= n || p < pos_lo || p >= pos_lo + count) return;
-    const uint32_t *LST = b.LST + (size_t)slot * b.B, *NXT = b.NXT + (size_t)slot * b.B;
-    auto root = [&](int k) {
-        for (;;) {
-            const int nk = (int)NXT[k];
-            if (nk == k) return k;
-            k = nk;
-        }
-    };
-    int x;
+    const uint32_t *J = b.J + (size_t)slot * b.B;
+    const uint32_t *S = b.S + (size_t)slot * b.B, *H = b.H + (size_t)slot * b.B;
+    uint32_t x;
     if (n <= 1) {
-        x = 0;
-    } else if (i == 0) {
-        const int k = v1x_succ(CNT, LST, 0, 0);
-        x = k < 0 ? 0 : root(k);
+        x = 0u;
     } else {
-        const int pj = (int)J[i];
-        if (pj == i) {
-            x = root(i);
+        uint32_t k = S[i];
+        if (k == kV1bNone) {
+            x = i == 0 ? 0u : J[i];
         } else {
-            const int k = v1x_succ(CNT, LST, pj, i);
-            x = k < 0 ? pj : root(k);
+            for (;;) {
+                const uint32_t h = H[k];
+                if (h == kV1bNone) break;
+                k = h;
+            }
+            x = k;
         }
     }
     const int32_t rl = (int32_t)(job / (uint64_t)b.nw);
@@ -327,14 +478,18 @@ __global__ __launch_bounds__(256) void k_v1x_out(Geometry g, V1xBig b, const Ran
 }
 
 namespace {
-// entries per pass of the HBM path (16 B each: a pass's workspace is <= 2 GB while windows have
-// at most 2^27 entries; a longer window is one job of ~16 B per entry, up to ~32 GB near 2^31 --
-// pss.h states the cost, and a workspace the device cannot hold fails pss_generate with PSS_EHIP)
+// entries per pass of the HBM path (~18 B each: a pass's workspace is <= 2.3 GB while windows
+// have at most 2^27 entries; a longer window is one job of ~18 B per entry, up to ~39 GB near
+// 2^31 -- pss.h states the cost, and a workspace the device cannot hold fails pss_generate with
+// PSS_EHIP)
 constexpr int64_t kV1xPassEntries = (int64_t)1 << 27;
 int64_t v1x_jobs_per_pass(int64_t B) {
     const int64_t j = kV1xPassEntries / B;
     return j < 1 ? 1 : (j > 65535 ? 65535 : j);
 }
+uint32_t v1x_nbk(int64_t W) { return (uint32_t)((W + kV1bBW - 1) / kV1bBW); }
+// words per job: J, S, H, PART (W each), PARTP (W u16), BCNT (nbk)
+size_t v1x_job_words(int64_t W) { return (size_t)4 * W + (size_t)(W + 1) / 2 + v1x_nbk(W); }
 }  // namespace
 
 size_t v1_exact_lds_bytes(int64_t n) {
@@ -351,7 +506,7 @@ size_t v1_exact_ws_bytes(const Geometry &g, int32_t nr, int64_t pos_lo, int64_t 
     const int64_t W = g.B < g.ns ? g.B : g.ns;   // the longest window
     if (W <= kV1ExactMaxB) return (size_t)jobs * (size_t)W * sizeof(uint16_t);
     const int64_t pj = jobs < v1x_jobs_per_pass(W) ? jobs : v1x_jobs_per_pass(W);
-    return (size_t)pj * ((size_t)4 * W + 1) * sizeof(uint32_t);
+    return (size_t)pj * v1x_job_words(W) * sizeof(uint32_t);
 }
 
 static hipError_t launch_v1_exact_big(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, int32_t nr,
@@ -364,22 +519,24 @@ static hipError_t launch_v1_exact_big(const Geometry &g, const RankDesc *ranks, 
     const int64_t W = g.B < g.ns ? g.B : g.ns;   // the longest window: the slice length
     const uint64_t per = (uint64_t)v1x_jobs_per_pass(W);
     const uint32_t B = (uint32_t)W;
+    const uint32_t nbk = v1x_nbk(W);
+    // the flat grids: XCD-major while they stay below 2^32 threads
+    auto grid = [&](const V1xBig &b, uint32_t xb) {
+        const uint64_t flat = (uint64_t)xb * (((uint64_t)b.nj + 7) / 8) * 8;
+        return flat < ((uint64_t)1 << 24) ? dim3((uint32_t)flat) : dim3(xb, b.nj);
+    };
     for (uint64_t j0 = 0; j0 < jobs; j0 += per) {
         V1xBig b{};
-        b.w_lo = w_lo; b.nw = nw; b.j0 = j0; b.B = B;
+        b.w_lo = w_lo; b.nw = nw; b.j0 = j0; b.B = B; b.nbk = nbk;
         b.nj = (uint32_t)(jobs - j0 < per ? jobs - j0 : per);
         b.J = ws;
-        b.CNT = b.J + (size_t)b.nj * B;
-        b.LST = b.CNT + (size_t)b.nj * ((size_t)B + 1);
-        b.NXT = b.LST + (size_t)b.nj * B;
-        hipError_t e = hipMemsetAsync(b.CNT, 0, sizeof(uint32_t) * (size_t)b.nj * ((size_t)B + 1), s);
+        b.S = b.J + (size_t)b.nj * B;
+        b.H = b.S + (size_t)b.nj * B;
+        b.PART = b.H + (size_t)b.nj * B;
+        b.BCNT = b.PART + (size_t)b.nj * B;
+        b.PARTP = (uint16_t *)(b.BCNT + (size_t)b.nj * nbk);
+        hipError_t e = hipMemsetAsync(b.BCNT, 0, sizeof(uint32_t) * (size_t)b.nj * nbk, s);
         if (e != hipSuccess) return e;
-        b.xb = (B + 255) / 256;
-        // XCD-major only while the 1-D grid stays below 2^32 threads (round 3: the scatter's
-        // random LST writes 8.2 -> 5.2 ms at C5 against the (x, slot) grid)
-        b.xcd = (uint64_t)b.xb * (((uint64_t)b.nj + 7) / 8) * 8 < ((uint64_t)1 << 24) ? 1u : 0u;
-        const dim3 flat = b.xcd ? dim3((uint32_t)((uint64_t)b.xb * (((uint64_t)b.nj + 7) / 8) * 8))
-                                : dim3(b.xb, b.nj);
         // few windows: a workgroup per window's MT stream (PSS_V1X_DRAWS_WG=0 / 1 forces a form)
         static const int wg_env = [] {
             const char *e = getenv("PSS_V1X_DRAWS_WG");
@@ -388,10 +545,22 @@ static hipError_t launch_v1_exact_big(const Geometry &g, const RankDesc *ranks, 
         const bool wg = wg_env == 0 || wg_env == 1 ? wg_env == 1 : b.nj < 1024;
         if (wg) hipLaunchKernelGGL(k_v1x_draws32_wg, dim3(b.nj), dim3(kMtWgThreads), 0, s, g, b, epoch);
         else hipLaunchKernelGGL(k_v1x_draws32, dim3(b.nj), dim3(64), 0, s, g, b, epoch);
-        hipLaunchKernelGGL(k_v1x_scan, dim3(b.nj), dim3(kV1xScanNT), 0, s, g, b);
-        hipLaunchKernelGGL(k_v1x_scatter, flat, dim3(256), 0, s, g, b);
-        hipLaunchKernelGGL(k_v1x_parent, flat, dim3(256), 0, s, g, b);
-        hipLaunchKernelGGL(k_v1x_out, flat, dim3(256), 0, s, g, b, ranks, rank_lo, pos_lo, count, out, ma);
+        hipLaunchKernelGGL(k_v1x_bscan, dim3(b.nj), dim3(kV1xScanNT), 0, s, g, b);
+        V1xBig bp = b;
+        bp.xb = (B + kV1pChunk - 1) / kV1pChunk;
+        dim3 gp = grid(bp, bp.xb);
+        bp.xcd = gp.y == 1 ? 1u : 0u;
+        hipLaunchKernelGGL(k_v1x_part, gp, dim3(kV1pNT), 0, s, g, bp);
+        V1xBig bs = b;
+        bs.xb = nbk;
+        dim3 gs = grid(bs, bs.xb);
+        bs.xcd = gs.y == 1 ? 1u : 0u;
+        hipLaunchKernelGGL(k_v1x_solve, gs, dim3(kV1sNT), 0, s, g, bs);
+        V1xBig bo = b;
+        bo.xb = (B + 255) / 256;
+        dim3 go = grid(bo, bo.xb);
+        bo.xcd = go.y == 1 ? 1u : 0u;
+        hipLaunchKernelGGL(k_v1x_out, go, dim3(256), 0, s, g, bo, ranks, rank_lo, pos_lo, count, out, ma);
         e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
