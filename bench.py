@@ -407,6 +407,8 @@ def main():
     ap.add_argument("--no-exact", action="store_true", help="skip the exact-order figures")
     ap.add_argument("--no-kernel-timing", action="store_true",
                     help="time the steps without the per-launch HIP events (roofline omitted)")
+    ap.add_argument("--pipeline", type=int, default=1,
+                    help="epochs in flight: 2 alternates two streams and output buffers")
     ap.add_argument("--timing-every", type=int, default=4,
                     help="HIP-event timing of the generation kernel on every n-th timed step")
     args = ap.parse_args()
@@ -445,12 +447,18 @@ def main():
     ns = eng.num_samples
     r_lo, r_hi = shard(R, world, rank)
     RG = r_hi - r_lo
-    out = torch.empty((RG, ns), dtype=torch.int64, device=dev)
-    stream = torch.cuda.current_stream(dev)
+    # --pipeline 2: consecutive epochs alternate between two streams and two output buffers (a
+    # data pipeline consuming epoch e while e + 1 is generated), so one epoch's generation may
+    # start while the previous one drains; 1: every epoch on one stream into one buffer
+    npipe = max(1, args.pipeline)
+    outs = [torch.empty((RG, ns), dtype=torch.int64, device=dev) for _ in range(npipe)]
+    streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(npipe - 1)]
+    out = outs[0]
+    stream = streams[0]
 
     def step(epoch):
         eng.init_iter(epoch)
-        eng.generate(r_lo, r_hi, out=out, stream=stream)
+        eng.generate(r_lo, r_hi, out=outs[epoch % npipe], stream=streams[epoch % npipe])
 
     for e in range(args.warmup):
         step(e)
@@ -478,6 +486,7 @@ def main():
     eng.check()
 
     # coverage of the last epoch across all GPUs: (count, digest) all-gather over RCCL
+    out = outs[(args.warmup + args.steps - 1) % npipe]     # the last epoch's ids
     pairs = gather_pairs(out.numel(), as_u64(digest(out.view(-1))), device=cdev)
     coverage = None
     if rank == 0:
@@ -537,7 +546,8 @@ def main():
                    "name": args.workload, "version": ver, "files": len(lengths), "samples": N,
                    "logical_ranks": R, "ranks_per_gpu": RG, "shuffle_buffer": B,
                    "ids_per_step": ids_total // args.steps,
-                   "parallelism": "logical ranks sharded over %d GPU(s)" % world},
+                   "parallelism": "logical ranks sharded over %d GPU(s)" % world,
+                   "epochs_in_flight": npipe},
         "roofline": {"bound": "hbm", "kernel": kname, "symbols": syms, "achieved": achieved,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                      "traffic": traffic, "launch_ms": per_launch_ms,
@@ -553,7 +563,7 @@ def main():
         "collective": (dist.get_backend() if distributed else None),
     }
     eng.close()
-    del out
+    del out, outs
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline()
         line["cpu_mode"] = cpu_mode_figure()

@@ -397,7 +397,12 @@ __global__ __launch_bounds__(64) void k_v1_feistel(Geometry g, V1Plan vp, const 
 // packed Feistel on the window's SGPR keys; the others the per-position general path.  C2 V1:
 // 168 -> 150 us per epoch against the persistent k_v1_feistel, which now serves the mapped
 // hand-off only (same box, profiles/r04/ab_v1_oneshot/).
-constexpr int64_t kV1OsPos = 1024;
+#ifndef PSS_V1OS_PER
+#define PSS_V1OS_PER 4
+#endif
+constexpr int kV1OsPer = PSS_V1OS_PER;             // positions per lane (2, 4 or 8)
+static_assert(kV1OsPer == 2 || kV1OsPer == 4 || kV1OsPer == 8, "one or more 16-byte pair stores per lane");
+constexpr int64_t kV1OsPos = 256 * kV1OsPer;
 struct V1OsPlan {
     int64_t blk_lo;            // first 1024-position block of each rank
     uint32_t bpr;              // blocks per rank
@@ -421,7 +426,7 @@ __global__ __launch_bounds__(256) void k_v1_os(Geometry g, V1OsPlan vp, const Ra
     const int64_t wB = w * B;
     const bool fast = vp.fast_ok && wB + B <= g.ns && p0 + kV1OsPos <= wB + B && p0 >= pos_lo &&
                       p0 + kV1OsPos <= pos_hi && (((uintptr_t)(o + p0)) & 15u) == 0;
-    const uint32_t l4 = 4u * threadIdx.x;
+    const uint32_t l4 = (uint32_t)kV1OsPer * threadIdx.x;
     if (fast) {
         const uint32_t *kw = ktr + (w - vp.w_lo) * kRoundKeyWords;
         uint32_t kp[kFeistelRounds];
@@ -431,18 +436,22 @@ __global__ __launch_bounds__(256) void k_v1_os(Geometry g, V1OsPlan vp, const Ra
             kp[i] = PACKED ? (k & 0xFFFFu) * 0x10001u : k;
         }
         const uint32_t x0 = (uint32_t)(p0 - wB) + l4;
-        const uint32_t x[4] = {x0, x0 + 1u, x0 + 2u, x0 + 3u};
-        uint32_t y[4];
-        if constexpr (PACKED) {
-            feistel4_pk16(x, vp.hB, kp, y);
+        uint32_t x[kV1OsPer], y[kV1OsPer];
+#pragma unroll
+        for (int j = 0; j < kV1OsPer; j++) x[j] = x0 + (uint32_t)j;
+        if constexpr (PACKED && kV1OsPer == 2) {
+            feistel2_pk16(x[0], x[1], vp.hB, kp, y[0], y[1]);
+        } else if constexpr (PACKED) {
+#pragma unroll
+            for (int j = 0; j < kV1OsPer; j += 4) feistel4_pk16(x + j, vp.hB, kp, y + j);
         } else {
 #pragma unroll
-            for (int j = 0; j < 4; j++) y[j] = feistel_once(x[j], vp.hB, kp);
+            for (int j = 0; j < kV1OsPer; j++) y[j] = feistel_once(x[j], vp.hB, kp);
         }
         const int64_t base = start + wB;
-        int64_t id[4];
+        int64_t id[kV1OsPer];
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
+        for (int j = 0; j < kV1OsPer; j++) {
             if constexpr (NARROW) {
                 const uint32_t v = (uint32_t)base + y[j];
                 id[j] = (int64_t)__builtin_elementwise_min(v, v - (uint32_t)g.N);
@@ -450,14 +459,16 @@ __global__ __launch_bounds__(256) void k_v1_os(Geometry g, V1OsPlan vp, const Ra
                 id[j] = wrap_id(base + y[j], g.N);
             }
         }
-        longlong2 a, b;
-        a.x = id[0]; a.y = id[1]; b.x = id[2]; b.y = id[3];
-        *(longlong2 *)(o + p0 + l4) = a;
-        *(longlong2 *)(o + p0 + l4 + 2) = b;
+#pragma unroll
+        for (int j = 0; j < kV1OsPer; j += 2) {
+            longlong2 a;
+            a.x = id[j]; a.y = id[j + 1];
+            *(longlong2 *)(o + p0 + l4 + j) = a;
+        }
         return;
     }
 #pragma unroll
-    for (int j = 0; j < 4; j++) {
+    for (int j = 0; j < kV1OsPer; j++) {
         const int64_t p = p0 + l4 + j;
         if (p < pos_lo || p >= pos_hi) continue;
         int64_t y = p;

@@ -319,16 +319,26 @@ __device__ void mt_draws_pair(uint32_t *mt, uint32_t W, uint32_t P, Emit emit) {
 //              its window is one transfer, any other block runs exactly (pair_block / draw_block,
 //              which emit) -- where round 3 ran every block after the first unsettled one exactly
 //   emit       each wave emits its settled blocks from their now known start states.
-// Three barriers per round of 8 twists where round 3 took three per twist: C5 V2 exact draws
-// (profiles/r04/) against 14.2 ms.
+// Three barriers per round where round 3 took three per twist, and the combine a prefix scan per
+// run of settled blocks: C5 V2 exact draws 14.2 -> 11.5 ms.  Rounds of 4 / 6 / 8 / 10 twists and
+// window margins of 4 / 6 sd, same box: 11.75 / 11.5 / 11.75 / 15.8 ms at 4 sd, 12.4 ms at 6 sd
+// with 8 twists (profiles/r04/mt_ab/, tools/stamp_mt.hip): what is left is per-block work on
+// the stream's one CU -- ~160 clocks per 64-word block in the summaries, ~135 in the combine
+// (the blocks run exactly: the last ~3 % of a window, where k2's bound is small), ~115 in emit.
 constexpr int kMtWgThreads = 640;   // nine consumer waves and the generator
 constexpr int kMtBlocks = (kMtN + 63) / 64;   // 10 per twist: nine of 64 words, one of 48
 constexpr int kMtWgWaves = kMtWgThreads / 64;
-constexpr int kMtRound = 8;                               // twists per round (even)
+#ifndef PSS_MT_ROUND
+#define PSS_MT_ROUND 6
+#endif
+#ifndef PSS_MT_SD
+#define PSS_MT_SD 4
+#endif
+constexpr int kMtRound = PSS_MT_ROUND;                    // twists per round (even)
 constexpr int kMtRoundWords = kMtRound * kMtN;
-constexpr int kMtRoundBlocks = kMtRound * kMtBlocks;      // 80
+constexpr int kMtRoundBlocks = kMtRound * kMtBlocks;      // 60
 constexpr int kMtConsumers = kMtWgWaves - 1;
-constexpr int kMtPerWave = (kMtRoundBlocks + kMtConsumers - 1) / kMtConsumers;   // 9
+constexpr int kMtPerWave = (kMtRoundBlocks + kMtConsumers - 1) / kMtConsumers;   // 7
 static_assert(kMtRound % 2 == 0, "the generator's state buffer returns to mt[cur] after a round");
 static_assert(kMtRoundBlocks <= 128, "the combiner keeps the summaries in two lanes sets");
 
@@ -400,7 +410,7 @@ __device__ __forceinline__ int mt_block_nval(int b) { return b % kMtBlocks == kM
 __device__ __forceinline__ void mt_window(uint32_t x0, float rate, float var, uint32_t wb, uint32_t cap,
                                           uint32_t &lo, uint32_t &hi) {
     const float e = rate * (float)wb;
-    const float m = 6.0f * __builtin_sqrtf(var * (float)wb + 1.0f) + 8.0f;
+    const float m = (float)PSS_MT_SD * __builtin_sqrtf(var * (float)wb + 1.0f) + 8.0f;
     const float l = e - m, h = e + m;
     lo = x0 + (l > 0.0f ? (uint32_t)l : 0u);
     const uint32_t hh = (uint32_t)h + 1u;

@@ -77,27 +77,6 @@ __global__ __launch_bounds__(64) void k_v2x_draws(V2xGeo x, int64_t epoch, uint3
     }
 }
 
-// The same draws with a workgroup per window (pss_mt.h mt_draws_pair_wg): long windows, few
-// streams (C5: 2^20 steps each, ~11 per rank).
-__global__ __launch_bounds__(kMtWgThreads) void k_v2x_draws_wg(V2xGeo x, int64_t epoch, uint32_t jobs, uint64_t blk0,
-                                                              uint32_t *__restrict__ K1, uint32_t *__restrict__ K2) {
-    __shared__ MtWgShared sh;
-    const uint64_t b = blk0 + blockIdx.x;
-    const uint32_t rl = (uint32_t)(b / jobs), job = (uint32_t)(b % jobs);
-    if (job >= x.S) return;
-    uint32_t *k1 = K1 + (size_t)rl * x.ns;
-    uint32_t *k2 = K2 + (size_t)rl * x.T2;
-    const uint32_t s = job;
-    const uint32_t W = x.T - s * x.B < x.B ? x.T - s * x.B : x.B, t0 = s * x.B;
-    if (threadIdx.x < 64) mt_seed_int(sh.mt[0], s == 0 ? epoch + 2 : epoch + (int64_t)(s - 1) * 10000);
-    __syncthreads();
-    mt_draws_pair_wg(sh, 0, W, x.P, [&](bool second, uint32_t i, uint32_t r) {
-        if (second) k2[t0 + i] = r;
-        else k1[t0 + i] = r;
-    });
-    for (uint32_t u = W + threadIdx.x; u < x.B; u += kMtWgThreads) k2[t0 + u] = 0;   // padding steps
-}
-
 // seed of tail step j (pool2 stays empty: every step reseeds first, V2:107-109)
 __device__ __forceinline__ int64_t v2x_tail_seed(const V2xGeo &x, int64_t epoch, uint32_t j) {
     return x.S >= 1 ? epoch + (int64_t)(x.S - 1 + j) * 10000
@@ -106,14 +85,12 @@ __device__ __forceinline__ int64_t v2x_tail_seed(const V2xGeo &x, int64_t epoch,
 
 // ---- tail draws: one lane per tail step (its own reseeded stream's first draw) ---------------
 // 64 tail steps per wave, each lane seeding its own MT (mt_first_draw_lane); the rare lane whose
-// first kFirstWords words are all rejected is redone by the whole wave (mt_seed + mt_draws).
-__global__ __launch_bounds__(64) void k_v2x_tail_draws(V2xGeo x, int64_t epoch, uint32_t per_rank,
-                                                       uint64_t blk0, uint32_t *__restrict__ K1) {
-    __shared__ uint32_t mt[kMtN];
-    const uint64_t b = blk0 + blockIdx.x;
-    const uint32_t rl = (uint32_t)(b / per_rank), j0 = (uint32_t)(b % per_rank) * 64u;
+// first kFirstWords words are all rejected is redone by the whole wave (mt_seed + mt_draws, in
+// the wave's 624 words of LDS at mt).
+__device__ __forceinline__ void v2x_tail_block(const V2xGeo &x, int64_t epoch, uint32_t rl, uint32_t j0,
+                                               uint32_t *__restrict__ K1, uint32_t *mt) {
     uint32_t *k1 = K1 + (size_t)rl * x.ns;
-    const int lane = threadIdx.x;
+    const int lane = threadIdx.x & 63;
     const uint32_t j = j0 + (uint32_t)lane;
     const bool valid = j < x.P;
     const int64_t seed = v2x_tail_seed(x, epoch, valid ? j : 0u);
@@ -133,6 +110,46 @@ __global__ __launch_bounds__(64) void k_v2x_tail_draws(V2xGeo x, int64_t epoch, 
         mt_draws(mt, 1u, [&](uint32_t) { return nl; }, [&](uint32_t, uint32_t rr) { k1[t] = rr; });
         wave_lds_order();
     }
+}
+
+__global__ __launch_bounds__(64) void k_v2x_tail_draws(V2xGeo x, int64_t epoch, uint32_t per_rank,
+                                                       uint64_t blk0, uint32_t *__restrict__ K1) {
+    __shared__ uint32_t mt[kMtN];
+    const uint64_t b = blk0 + blockIdx.x;
+    v2x_tail_block(x, epoch, (uint32_t)(b / per_rank), (uint32_t)(b % per_rank) * 64u, K1, mt);
+}
+
+// The same draws with a workgroup per window (pss_mt.h mt_draws_pair_wg): long windows, few
+// streams (C5: 2^20 steps each, ~11 per rank), which leave most of the chip idle for ~11 ms --
+// so the launch also carries the tail draws: blocks past the windows' run ten tail blocks each
+// (one per wave) on the CUs the streams do not use (C5: 1.96 ms of k_v2x_tail_draws hidden).
+__global__ __launch_bounds__(kMtWgThreads) void k_v2x_draws_wg(V2xGeo x, int64_t epoch, uint32_t jobs, uint64_t blk0,
+                                                              uint32_t nr, uint32_t tail_blocks,
+                                                              uint32_t *__restrict__ K1, uint32_t *__restrict__ K2) {
+    __shared__ MtWgShared sh;
+    const uint64_t b = blk0 + blockIdx.x;
+    if (b >= (uint64_t)jobs * nr) {   // tail mode: wave w takes tail block 10 (b - windows) + w
+        const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));   // (uniform)
+        const uint64_t tb = (b - (uint64_t)jobs * nr) * (uint64_t)kMtWgWaves + wv;
+        const uint32_t rl = (uint32_t)(tb / tail_blocks);
+        if (rl >= nr) return;
+        static_assert(sizeof(sh.tw) >= sizeof(uint32_t) * kMtN * kMtWgWaves, "a tail wave's MT state in tw");
+        v2x_tail_block(x, epoch, rl, (uint32_t)(tb % tail_blocks) * 64u, K1, (uint32_t *)sh.tw + kMtN * wv);
+        return;
+    }
+    const uint32_t rl = (uint32_t)(b / jobs), job = (uint32_t)(b % jobs);
+    if (job >= x.S) return;
+    uint32_t *k1 = K1 + (size_t)rl * x.ns;
+    uint32_t *k2 = K2 + (size_t)rl * x.T2;
+    const uint32_t s = job;
+    const uint32_t W = x.T - s * x.B < x.B ? x.T - s * x.B : x.B, t0 = s * x.B;
+    if (threadIdx.x < 64) mt_seed_int(sh.mt[0], s == 0 ? epoch + 2 : epoch + (int64_t)(s - 1) * 10000);
+    __syncthreads();
+    mt_draws_pair_wg(sh, 0, W, x.P, [&](bool second, uint32_t i, uint32_t r) {
+        if (second) k2[t0 + i] = r;
+        else k1[t0 + i] = r;
+    });
+    for (uint32_t u = W + threadIdx.x; u < x.B; u += kMtWgThreads) k2[t0 + u] = 0;   // padding steps
 }
 
 // ---- decode tiles in LDS: pool1 tiles of kTile steps and whole pool2 windows ---------------
@@ -405,11 +422,16 @@ __global__ __launch_bounds__(256) void k_v2x_q2(uint64_t n, uint32_t B, const ui
     Q2[seq * B + O[gi]] = V[gi];
 }
 
-// merge sibling blocks (sorted by position, carrying the step of each entry)
+// merge sibling blocks (sorted by position, carrying the step of each entry).  The LDS copies are
+// swizzled inside each 32-word row (entry e at e ^ ((e / 32) mod 8)): a thread's merge walk reads
+// and writes its own kPer consecutive entries, so unswizzled the 32 lanes of a half-wave hit every
+// 8th bank -- 2/3 of the kernel's LDS cycles were bank conflicts (profiles/r04/pmc_exact/)
+__device__ __forceinline__ uint32_t gsk(uint32_t e) { return e ^ ((e >> 5) & 7u); }
+constexpr uint32_t kGTileSk = kGTile;
 __global__ __launch_bounds__(kGNT) void k_v2x_gmerge(V2xGeo x, uint32_t w, const uint32_t *__restrict__ V,
                                                     const uint32_t *__restrict__ O, uint32_t *__restrict__ Vd,
                                                     uint32_t *__restrict__ Od, const uint32_t *__restrict__ SP) {
-    __shared__ uint32_t sv[kGTile], so[kGTile], tv[kGTile], to[kGTile];
+    __shared__ uint32_t sv[kGTileSk], so[kGTileSk], tv[kGTileSk], to[kGTileSk];
     const uint32_t tpr = (x.ns + kGTile - 1) / kGTile;
     const uint32_t rl = blockIdx.x / tpr, o0 = (blockIdx.x % tpr) * kGTile;
     const size_t base = (size_t)rl * x.ns;
@@ -421,35 +443,36 @@ __global__ __launch_bounds__(kGNT) void k_v2x_gmerge(V2xGeo x, uint32_t w, const
         for (uint32_t u = threadIdx.x; u < on; u += kGNT) { vd[o0 + u] = v[o0 + u]; od[o0 + u] = o[o0 + u]; }
         return;
     }
-    const uint32_t e = m + w < x.ns ? m + w : x.ns, nL = m - a, nR = e - m;
-    const uint32_t *L = v + a, *R = v + m;
-    (void)nL; (void)nR;
     const uint32_t i0 = SP[2 * blockIdx.x], i1 = SP[2 * blockIdx.x + 1], dA = o0 - a;   // merge-path splits
     const uint32_t j0 = dA - i0, j1 = dA + on - i1;
     const uint32_t sL = i1 - i0, sR = j1 - j0;   // sL + sR == on
-    for (uint32_t u = threadIdx.x; u < sL; u += kGNT) { sv[u] = L[i0 + u]; so[u] = o[a + i0 + u]; }
-    for (uint32_t u = threadIdx.x; u < sR; u += kGNT) { sv[sL + u] = R[j0 + u]; so[sL + u] = o[m + j0 + u]; }
+    // (all kPer loads of a thread issued before its LDS stores measured slower: C5 exact 24.5 ->
+    // 26.1 ms together with the same change in k_v2x_tile, profiles/r04/ab_gmerge_batch/)
+    const uint32_t *L = v + a, *R = v + m;
+    for (uint32_t u = threadIdx.x; u < sL; u += kGNT) { sv[gsk(u)] = L[i0 + u]; so[gsk(u)] = o[a + i0 + u]; }
+    for (uint32_t u = threadIdx.x; u < sR; u += kGNT) { sv[gsk(sL + u)] = R[j0 + u]; so[gsk(sL + u)] = o[m + j0 + u]; }
     __syncthreads();
     const uint32_t p0 = threadIdx.x * kPer;
     if (p0 < on) {
         // the fused map-and-merge of k_v2x_tile: E_i = D_i - i against the right values (frame
         // m), a right entry after i0 + i left ones becomes q + i0 + i (frame a)
-        const uint32_t *lv = sv, *rv = sv + sL;
+        auto lv = [&](uint32_t i) { return sv[gsk(i)]; };
+        auto rv = [&](uint32_t j) { return sv[gsk(sL + j)]; };
         uint32_t lo = p0 > sR ? p0 - sR : 0u, hi = p0 < sL ? p0 : sL;
         while (lo < hi) {
             const uint32_t mid = (lo + hi) >> 1;
-            if (lv[mid] - (i0 + mid) <= rv[p0 - mid - 1]) lo = mid + 1; else hi = mid;
+            if (lv(mid) - (i0 + mid) <= rv(p0 - mid - 1)) lo = mid + 1; else hi = mid;
         }
         uint32_t i = lo, j = p0 - lo;
         const uint32_t pe = p0 + kPer < on ? p0 + kPer : on;
         for (uint32_t p = p0; p < pe; p++) {
-            const bool takeL = j >= sR || (i < sL && lv[i] - (i0 + i) <= rv[j]);
-            if (takeL) { tv[p] = lv[i]; to[p] = so[i]; i++; }
-            else { tv[p] = rv[j] + i0 + i; to[p] = so[sL + j]; j++; }
+            const bool takeL = j >= sR || (i < sL && lv(i) - (i0 + i) <= rv(j));
+            if (takeL) { tv[gsk(p)] = lv(i); to[gsk(p)] = so[gsk(i)]; i++; }
+            else { tv[gsk(p)] = rv(j) + i0 + i; to[gsk(p)] = so[gsk(sL + j)]; j++; }
         }
     }
     __syncthreads();
-    for (uint32_t u = threadIdx.x; u < on; u += kGNT) { vd[o0 + u] = tv[u]; od[o0 + u] = to[u]; }
+    for (uint32_t u = threadIdx.x; u < on; u += kGNT) { vd[o0 + u] = tv[gsk(u)]; od[o0 + u] = to[gsk(u)]; }
 }
 
 // ---- chain mode (pools of <= kTile entries): tiles linked by their survivor lists ----------
@@ -754,18 +777,25 @@ static hipError_t v2x_pass(const Geometry &g, const V2xGeo &x, const RankDesc *r
     uint32_t *K1 = ws, *V = K1 + nsr;
     uint32_t *O = chain ? nullptr : V + nsr, *Vd = chain ? nullptr : O + nsr, *Od = chain ? nullptr : Vd + nsr;
     uint32_t *K2 = chain ? V + nsr : Od + nsr, *Q2 = K2 + tr;
+    const uint32_t tail_blocks = (x.P + 63u) / 64u;
+    bool tail_done = false;
     if (x.S) {
-        // few long windows (the streams alone do not fill the chip): a workgroup per stream
+        // few long windows (the streams alone do not fill the chip): a workgroup per stream, the
+        // tail draws riding along on the idle CUs
         const bool wg = v2x_draws_wg((uint64_t)x.S * (uint64_t)nr, x.B);
-        v2x_launch_blocks((uint64_t)x.S * (uint64_t)nr, [&](uint64_t b0, uint32_t nb) {
-            if (wg) hipLaunchKernelGGL(k_v2x_draws_wg, dim3(nb), dim3(kMtWgThreads), 0, s, x, epoch, x.S, b0, K1, K2);
+        const uint64_t wblocks = (uint64_t)x.S * (uint64_t)nr;
+        const uint64_t tblocks = wg ? ((uint64_t)tail_blocks * (uint64_t)nr + kMtWgWaves - 1) / kMtWgWaves : 0u;
+        v2x_launch_blocks(wblocks + tblocks, [&](uint64_t b0, uint32_t nb) {
+            if (wg) hipLaunchKernelGGL(k_v2x_draws_wg, dim3(nb), dim3(kMtWgThreads), 0, s, x, epoch, x.S, b0,
+                                       (uint32_t)nr, tail_blocks, K1, K2);
             else hipLaunchKernelGGL(k_v2x_draws, dim3(nb), dim3(64), 0, s, x, epoch, x.S, b0, K1, K2);
         });
+        tail_done = wg;
     }
-    const uint32_t tail_blocks = (x.P + 63u) / 64u;
-    v2x_launch_blocks((uint64_t)tail_blocks * (uint64_t)nr, [&](uint64_t b0, uint32_t nb) {
-        hipLaunchKernelGGL(k_v2x_tail_draws, dim3(nb), dim3(64), 0, s, x, epoch, tail_blocks, b0, K1);
-    });
+    if (!tail_done)
+        v2x_launch_blocks((uint64_t)tail_blocks * (uint64_t)nr, [&](uint64_t b0, uint32_t nb) {
+            hipLaunchKernelGGL(k_v2x_tail_draws, dim3(nb), dim3(64), 0, s, x, epoch, tail_blocks, b0, K1);
+        });
     const uint32_t nru = (uint32_t)nr;
     const bool narrow = v2x_narrow(x.P, x.B);
     // one decode-tile launch of nb blocks from block b0 (the entry width; kTileOut merge outputs

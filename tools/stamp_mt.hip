@@ -29,9 +29,9 @@ __global__ __launch_bounds__(kMtWgThreads) void k_stamp_v1(uint32_t n, uint32_t 
 }
 
 int main() {
-    const uint32_t W = 1u << 20, P = 1u << 20, nb = 88;
+    const uint32_t W = 1u << 20, P = 1u << 20, nb = 88, nb1 = 96;
     uint32_t *K1, *K2;
-    hipMalloc(&K1, (size_t)nb * W * 4);
+    hipMalloc(&K1, (size_t)nb1 * W * 4);   // (the V1 run below takes 96 windows)
     hipMalloc(&K2, (size_t)nb * W * 4);
     hipEvent_t a, b;
     hipEventCreate(&a); hipEventCreate(&b);
@@ -57,7 +57,7 @@ int main() {
     }
     {   // V1 windows: 96 streams of 2^20 - 1 draws
         hipEventRecord(a);
-        hipLaunchKernelGGL(k_stamp_v1, dim3(96), dim3(kMtWgThreads), 0, 0, W, K1);
+        hipLaunchKernelGGL(k_stamp_v1, dim3(nb1), dim3(kMtWgThreads), 0, 0, W, K1);
         hipEventRecord(b);
         hipEventSynchronize(b);
         float ms = 0;
