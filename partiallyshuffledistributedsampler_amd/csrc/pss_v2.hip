@@ -33,6 +33,12 @@ __device__ __forceinline__ void tile_bounds(const V2Plan &pl, int64_t tile, int6
 __device__ uint64_t pss_stamps[1 << 16][8];
 #define PSS_STAMP(i) do { if (threadIdx.x == 0 && blockIdx.x < (1u << 16)) pss_stamps[blockIdx.x][i] = __builtin_amdgcn_s_memtime(); } while (0)
 #define PSS_STAMPW(i) do { if ((threadIdx.x & 63) == 0 && blockIdx.x < (1u << 16)) pss_stamps[blockIdx.x][i] = __builtin_amdgcn_s_memtime(); } while (0)
+#ifndef PSS_STAMPS_EMIT_ONLY   // (a pass running beside the replay would overwrite its slots)
+#define PSS_PASS_STAMPS 1
+#else
+#undef PSS_STAMP
+#define PSS_STAMP(i) do { } while (0)
+#endif
 #else
 #define PSS_STAMP(i) do { } while (0)
 #endif
@@ -56,7 +62,7 @@ __global__ __launch_bounds__(NT) void k_v2_lastocc(Geometry g, V2Plan pl, int32_
     const uint32_t thi = pl.T32 - tlo < pl.L32 ? pl.T32 : tlo + pl.L32;
     const uint32_t w_lo = 1 + tlo / B;
     const int nwin = (int)(1 + (thi - 1) / B - w_lo + 1);
-#ifdef PSS_STAMPS
+#ifdef PSS_PASS_STAMPS
     if (threadIdx.x == 0) pss_stamps[blockIdx.x][4] = __builtin_amdgcn_s_memrealtime();
 #endif
     for (int s = threadIdx.x; s < P1; s += NT) lastT[s] = 0;
@@ -150,7 +156,7 @@ __global__ __launch_bounds__(NT) void k_v2_lastocc(Geometry g, V2Plan pl, int32_
         }
     }
     PSS_STAMP(3);
-#ifdef PSS_STAMPS
+#ifdef PSS_PASS_STAMPS
     if (threadIdx.x == 0) {
         pss_stamps[blockIdx.x][5] = __builtin_amdgcn_s_memrealtime();
         pss_stamps[blockIdx.x][6] = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));

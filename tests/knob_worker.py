@@ -75,9 +75,10 @@ def check_exact(device):
 
 
 def check_counter(device):
-    shapes = [  # (F, L, R, B, version): small pools (lookahead ring), grouped pools, V1
-        (1000, 10_000, 8, 4096, 2), (300, 7_001, 5, 1000, 2), (500, 20_000, 4, 1 << 17, 2),
-        (1000, 10_000, 8, 4096, 1)]
+    shapes = [  # (F, L, R, B, version): small pools (lookahead ring; tiles of 4 pools: walks
+        # back over several tiles), grouped pools, V1
+        (1000, 10_000, 8, 4096, 2), (300, 7_001, 5, 1000, 2), (200, 3_001, 3, 100, 2),
+        (20, 10_000, 1, 4096, 2), (500, 20_000, 4, 1 << 17, 2), (1000, 10_000, 8, 4096, 1)]
     for F, L, R, B, version in shapes:
         lens = np.full(F, L, dtype=np.int64)
         N = int(lens.sum())
@@ -92,6 +93,10 @@ def check_counter(device):
                 ref = (O.v1_philox_stream(key, r, int(new[r]), ns, B, N) if version == 1 else
                        O.v2_philox_stream(key, r, int(old[r]), int(new[r]), ns, B, N))
                 assert np.array_equal(out[r], ref), ("counter", F, R, B, version, epoch, r)
+                if r == R - 1:   # a position range of the same stream
+                    lo = ns // 3
+                    part = _gen(eng, r, r + 1, pos_lo=lo, count=ns // 2)[0]
+                    assert np.array_equal(part, ref[lo:lo + ns // 2]), ("range", F, R, B, epoch)
         eng.close()
 
 
