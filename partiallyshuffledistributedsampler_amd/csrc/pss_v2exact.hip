@@ -412,26 +412,48 @@ __global__ __launch_bounds__(256) void k_v2x_gsplit(V2xGeo x, uint32_t nr, uint3
     SP[gi] = r;
 }
 
-// decoded pool2 windows (as sequences of B steps) -> Q2[window step] = its pool2 rank (random
-// writes inside one window; an XCD-major grid as v1x_block's measured neutral at C5, round 4)
-__global__ __launch_bounds__(256) void k_v2x_q2(uint64_t n, uint32_t B, const uint32_t *__restrict__ V,
-                                                const uint32_t *__restrict__ O, uint32_t *__restrict__ Q2) {
-    const uint64_t gi = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    if (gi >= n) return;
-    const uint64_t seq = gi / B;
-    Q2[seq * B + O[gi]] = V[gi];
-}
-
 // merge sibling blocks (sorted by position, carrying the step of each entry).  The LDS copies are
 // swizzled inside each 32-word row (entry e at e ^ ((e / 32) mod 8)): a thread's merge walk reads
 // and writes its own kPer consecutive entries, so unswizzled the 32 lanes of a half-wave hit every
 // 8th bank -- 2/3 of the kernel's LDS cycles were bank conflicts (profiles/r04/pmc_exact/)
 __device__ __forceinline__ uint32_t gsk(uint32_t e) { return e ^ ((e >> 5) & 7u); }
 constexpr uint32_t kGTileSk = kGTile;
+// The merge walk keeps a thread's kPer outputs in registers and stores them itself (two 16-byte
+// stores per array when the output rows are 16-byte aligned; the lanes of a wave then write 2 KB
+// contiguous): no LDS output staging, 16 KB of LDS per workgroup instead of 32 KB
+// The last level writes what the lists are for instead of the lists themselves: the decoded pool2
+// windows' ranks Q2[window][step] (FIN 1, a scatter inside one window), or the pool1 decode's
+// ids / (file, offset) pairs (FIN 2, position p < P is old_start + p, P + u the element step u
+// moved over from pool2: its window's base + its decoded pool2 rank)
+struct V2xFin {
+    Geometry g;
+    const RankDesc *ranks;
+    int32_t rank_lo;
+    uint32_t *Q2;                 // FIN 1: written ([seq][B]); FIN 2: read ([rank][T2])
+    int64_t pos_lo, count;
+    int64_t *out;
+    MapArgs ma;
+};
+__device__ __forceinline__ void v2x_put(const V2xFin &f, const V2xGeo &x, uint32_t rl, const RankDesc &rd,
+                                        uint32_t q, uint32_t t) {
+    if ((int64_t)t < f.pos_lo || (int64_t)t >= f.pos_lo + f.count) return;
+    int64_t id;
+    if (q < x.P) {
+        id = rd.old_start + q;
+    } else {
+        const uint32_t uu = q - x.P, s = uu / x.B;
+        const int64_t wbase = s == 0 ? rd.old_start + x.B : rd.new_start + (int64_t)(s + 1) * x.B;
+        id = wbase + f.Q2[(size_t)rl * x.T2 + uu];
+    }
+    put_id_or_pair(f.out, f.ma, (int64_t)rl * f.count + ((int64_t)t - f.pos_lo), wrap_id(id, f.g.N));
+}
+
+template <int FIN>
 __global__ __launch_bounds__(kGNT) void k_v2x_gmerge(V2xGeo x, uint32_t w, const uint32_t *__restrict__ V,
                                                     const uint32_t *__restrict__ O, uint32_t *__restrict__ Vd,
-                                                    uint32_t *__restrict__ Od, const uint32_t *__restrict__ SP) {
-    __shared__ uint32_t sv[kGTileSk], so[kGTileSk], tv[kGTileSk], to[kGTileSk];
+                                                    uint32_t *__restrict__ Od, const uint32_t *__restrict__ SP,
+                                                    V2xFin fin) {
+    __shared__ uint32_t sv[kGTileSk], so[kGTileSk];
     const uint32_t tpr = (x.ns + kGTile - 1) / kGTile;
     const uint32_t rl = blockIdx.x / tpr, o0 = (blockIdx.x % tpr) * kGTile;
     const size_t base = (size_t)rl * x.ns;
@@ -439,8 +461,15 @@ __global__ __launch_bounds__(kGNT) void k_v2x_gmerge(V2xGeo x, uint32_t w, const
     uint32_t *vd = Vd + base, *od = Od + base;
     const uint32_t on = x.ns - o0 < kGTile ? x.ns - o0 : kGTile;
     const uint32_t a = (o0 / (2 * w)) * (2 * w), m = a + w;
+    RankDesc rd{};
+    if constexpr (FIN == 2) rd = fin.ranks[fin.rank_lo + (int32_t)rl];
+    auto emit = [&](uint32_t p, uint32_t val, uint32_t st) {   // output p (of the tile) = (val, st)
+        if constexpr (FIN == 0) { vd[o0 + p] = val; od[o0 + p] = st; }
+        else if constexpr (FIN == 1) fin.Q2[(size_t)rl * x.ns + st] = val;
+        else v2x_put(fin, x, rl, rd, val, st);
+    };
     if (m >= x.ns) {                           // lone left block: already merged
-        for (uint32_t u = threadIdx.x; u < on; u += kGNT) { vd[o0 + u] = v[o0 + u]; od[o0 + u] = o[o0 + u]; }
+        for (uint32_t u = threadIdx.x; u < on; u += kGNT) emit(u, v[o0 + u], o[o0 + u]);
         return;
     }
     const uint32_t i0 = SP[2 * blockIdx.x], i1 = SP[2 * blockIdx.x + 1], dA = o0 - a;   // merge-path splits
@@ -453,26 +482,38 @@ __global__ __launch_bounds__(kGNT) void k_v2x_gmerge(V2xGeo x, uint32_t w, const
     for (uint32_t u = threadIdx.x; u < sR; u += kGNT) { sv[gsk(sL + u)] = R[j0 + u]; so[gsk(sL + u)] = o[m + j0 + u]; }
     __syncthreads();
     const uint32_t p0 = threadIdx.x * kPer;
-    if (p0 < on) {
-        // the fused map-and-merge of k_v2x_tile: E_i = D_i - i against the right values (frame
-        // m), a right entry after i0 + i left ones becomes q + i0 + i (frame a)
-        auto lv = [&](uint32_t i) { return sv[gsk(i)]; };
-        auto rv = [&](uint32_t j) { return sv[gsk(sL + j)]; };
-        uint32_t lo = p0 > sR ? p0 - sR : 0u, hi = p0 < sL ? p0 : sL;
-        while (lo < hi) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (lv(mid) - (i0 + mid) <= rv(p0 - mid - 1)) lo = mid + 1; else hi = mid;
-        }
-        uint32_t i = lo, j = p0 - lo;
-        const uint32_t pe = p0 + kPer < on ? p0 + kPer : on;
-        for (uint32_t p = p0; p < pe; p++) {
+    if (p0 >= on) return;
+    // the fused map-and-merge of k_v2x_tile: E_i = D_i - i against the right values (frame
+    // m), a right entry after i0 + i left ones becomes q + i0 + i (frame a)
+    auto lv = [&](uint32_t i) { return sv[gsk(i)]; };
+    auto rv = [&](uint32_t j) { return sv[gsk(sL + j)]; };
+    uint32_t lo = p0 > sR ? p0 - sR : 0u, hi = p0 < sL ? p0 : sL;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (lv(mid) - (i0 + mid) <= rv(p0 - mid - 1)) lo = mid + 1; else hi = mid;
+    }
+    uint32_t i = lo, j = p0 - lo;
+    const uint32_t pn = on - p0 < kPer ? on - p0 : kPer;
+    uint32_t tv[kPer], to[kPer];
+#pragma unroll
+    for (uint32_t k = 0; k < kPer; k++) {
+        tv[k] = 0; to[k] = 0;
+        if (k < pn) {
             const bool takeL = j >= sR || (i < sL && lv(i) - (i0 + i) <= rv(j));
-            if (takeL) { tv[gsk(p)] = lv(i); to[gsk(p)] = so[gsk(i)]; i++; }
-            else { tv[gsk(p)] = rv(j) + i0 + i; to[gsk(p)] = so[gsk(sL + j)]; j++; }
+            if (takeL) { tv[k] = lv(i); to[k] = so[gsk(i)]; i++; }
+            else { tv[k] = rv(j) + i0 + i; to[k] = so[gsk(sL + j)]; j++; }
         }
     }
-    __syncthreads();
-    for (uint32_t u = threadIdx.x; u < on; u += kGNT) { vd[o0 + u] = tv[gsk(u)]; od[o0 + u] = to[gsk(u)]; }
+    static_assert(kPer == 8, "two 16-byte stores per array");
+    if (FIN == 0 && pn == kPer && ((((uintptr_t)(vd + o0)) | ((uintptr_t)(od + o0))) & 15u) == 0) {
+        uint4 *v4 = (uint4 *)(vd + o0 + p0), *o4 = (uint4 *)(od + o0 + p0);
+        v4[0] = make_uint4(tv[0], tv[1], tv[2], tv[3]); v4[1] = make_uint4(tv[4], tv[5], tv[6], tv[7]);
+        o4[0] = make_uint4(to[0], to[1], to[2], to[3]); o4[1] = make_uint4(to[4], to[5], to[6], to[7]);
+    } else {
+#pragma unroll
+        for (uint32_t k = 0; k < kPer; k++)
+            if (k < pn) emit(p0 + k, tv[k], to[k]);
+    }
 }
 
 // ---- chain mode (pools of <= kTile entries): tiles linked by their survivor lists ----------
@@ -635,31 +676,6 @@ __global__ __launch_bounds__(kChainNT) void k_v2x_emit(Geometry g, V2xGeo x, V2x
     }
 }
 
-// ---- ids of the decoded positions ------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_v2x_out(Geometry g, V2xGeo x, uint32_t nr, const RankDesc *__restrict__ ranks,
-                                                 int32_t rank_lo, const uint32_t *__restrict__ V,
-                                                 const uint32_t *__restrict__ O, const uint32_t *__restrict__ Q2,
-                                                 int64_t pos_lo, int64_t count, int64_t *__restrict__ out,
-                                                 MapArgs ma) {
-    const uint64_t gi = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    const uint32_t rl = (uint32_t)(gi / x.ns), i = (uint32_t)(gi % x.ns);
-    if (rl >= nr) return;
-    const size_t base = (size_t)rl * x.ns;
-    const int64_t t = O[base + i];
-    if (t < pos_lo || t >= pos_lo + count) return;
-    const RankDesc rd = ranks[rank_lo + (int32_t)rl];
-    const uint32_t q = V[base + i];
-    int64_t id;
-    if (q < x.P) {
-        id = rd.old_start + q;
-    } else {
-        const uint32_t uu = q - x.P, s = uu / x.B;
-        const int64_t wbase = s == 0 ? rd.old_start + x.B : rd.new_start + (int64_t)(s + 1) * x.B;
-        id = wbase + Q2[(size_t)rl * x.T2 + uu];
-    }
-    put_id_or_pair(out, ma, (int64_t)rl * count + (t - pos_lo), wrap_id(id, g.N));
-}
-
 static int64_t v2x_cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
 static V2xGeo v2x_geo(const Geometry &g) {
@@ -752,15 +768,18 @@ size_t v2_exact_ws_bytes(const Geometry &g, int32_t nr_all) {
     return ((size_t)nr * ((size_t)5 * x.ns + (size_t)2 * x.T2) + v2x_split_words(x, nr)) * sizeof(uint32_t);
 }
 
-// global merge levels w = kTile, 2 kTile, ... of nr sequences of x.ns steps (V, O sorted per
-// block of w on entry); returns the buffers holding the result
-static void v2x_global_levels(const V2xGeo &x, uint32_t nr, uint32_t *&V, uint32_t *&O, uint32_t *&Vd,
-                              uint32_t *&Od, uint32_t *SP, hipStream_t s) {
+// global merge levels w = kTile, 2 kTile, ... of nr sequences of x.ns > kTile steps (V, O sorted
+// per block of w on entry); the last level writes what `fin_mode` asks (k_v2x_gmerge's FIN)
+static void v2x_global_levels(const V2xGeo &x, uint32_t nr, uint32_t *V, uint32_t *O, uint32_t *Vd,
+                              uint32_t *Od, uint32_t *SP, int fin_mode, const V2xFin &fin, hipStream_t s) {
     const int64_t tiles = (int64_t)nr * v2x_cdiv(x.ns, kGTile);
     const dim3 gridt((uint32_t)tiles), grids((uint32_t)v2x_cdiv(2 * tiles, 256));
     for (uint32_t w = kTile; w < x.ns; w <<= 1) {   // each level: fused map-and-merge
         hipLaunchKernelGGL(k_v2x_gsplit, grids, dim3(256), 0, s, x, nr, w, V, SP);
-        hipLaunchKernelGGL(k_v2x_gmerge, gridt, dim3(kGNT), 0, s, x, w, V, O, Vd, Od, SP);
+        const bool last = (uint64_t)2 * w >= x.ns;
+        if (!last) hipLaunchKernelGGL(k_v2x_gmerge<0>, gridt, dim3(kGNT), 0, s, x, w, V, O, Vd, Od, SP, fin);
+        else if (fin_mode == 1) hipLaunchKernelGGL(k_v2x_gmerge<1>, gridt, dim3(kGNT), 0, s, x, w, V, O, Vd, Od, SP, fin);
+        else hipLaunchKernelGGL(k_v2x_gmerge<2>, gridt, dim3(kGNT), 0, s, x, w, V, O, Vd, Od, SP, fin);
         uint32_t *t = V; V = Vd; Vd = t;
         t = O; O = Od; Od = t;
     }
@@ -835,20 +854,19 @@ static hipError_t v2x_pass(const Geometry &g, const V2xGeo &x, const RankDesc *r
         v2x_launch_blocks((uint64_t)xw.tiles1 * nseq, [&](uint64_t b0, uint32_t nb) {
             tile(b0, nb, xw, xw.tiles1, K2, K2, V, O, Q2, (uint32_t *)nullptr, kTileLds);
         });
-        uint32_t *wv = V, *wo = O, *wvd = Vd, *wod = Od;
-        v2x_global_levels(xw, nseq, wv, wo, wvd, wod, SP, s);
-        const uint64_t nw = (uint64_t)nseq * x.B, nblk = (uint64_t)v2x_cdiv((int64_t)nw, 256);
-        hipLaunchKernelGGL(k_v2x_q2, dim3((uint32_t)nblk), dim3(256), 0, s, nw, x.B, wv, wo, Q2);
+        V2xFin fw{};
+        fw.Q2 = Q2;   // [seq][B] == [rank][T2] (T2 = S * B)
+        v2x_global_levels(xw, nseq, V, O, Vd, Od, SP, 1, fw, s);
     }
     // pool1 tiles (and, for B <= kTile, the windows in the same launch)
     const uint32_t per_rank = x.tiles1 + (big_windows ? 0u : x.S);
     v2x_launch_blocks((uint64_t)per_rank * nru, [&](uint64_t b0, uint32_t nb) {
         tile(b0, nb, x, per_rank, K1, K2, V, O, Q2, (uint32_t *)nullptr, kTileLds);
     });
-    v2x_global_levels(x, nru, V, O, Vd, Od, SP, s);
-    const dim3 grid1((uint32_t)v2x_cdiv((int64_t)nsr, 256));   // one thread per (rank, step)
-    hipLaunchKernelGGL(k_v2x_out, grid1, dim3(256), 0, s, g, x, nru, ranks, rank_lo, V, O, Q2,
-                       pos_lo, count, out, ma);
+    V2xFin f{};
+    f.g = g; f.ranks = ranks; f.rank_lo = rank_lo; f.Q2 = Q2;
+    f.pos_lo = pos_lo; f.count = count; f.out = out; f.ma = ma;
+    v2x_global_levels(x, nru, V, O, Vd, Od, SP, 2, f, s);
     return hipGetLastError();
 }
 
