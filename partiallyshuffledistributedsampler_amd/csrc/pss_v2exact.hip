@@ -174,21 +174,25 @@ template <typename EW> struct TileEntry {
     static constexpr uint32_t kSlots = kTile + (kTile >> SKEW);
 };
 // The first three merge levels (blocks of 1, 2, 4 -> 8) of a thread's 8 consecutive entries in
-// registers, 32-bit entries: the same fused map-and-merge as the LDS levels, as a sorting network.
+// registers: the same fused map-and-merge as the LDS levels, as a sorting network (frame
+// positions below 2^28, so that a key fits 32 bits; 64-bit entries since round 4).
 // A left entry i gets key (E_i << 4) | i with E_i = D_i - i, a right entry j key (q_j << 4) | 8 | j:
 // left-before-right exactly when E_i <= q_j (left first on ties), lefts keep their order on equal E
 // (the index below), rights are distinct.  Batcher's odd-even merge of the two sorted halves, then a
 // right entry landing at k gains k - j (the left entries now before it).
-__device__ __forceinline__ void tile_ce(uint32_t &ka, uint32_t &kb, uint32_t &ea, uint32_t &eb) {
+template <typename EW>
+__device__ __forceinline__ void tile_ce(uint32_t &ka, uint32_t &kb, EW &ea, EW &eb) {
     const bool sw = ka > kb;
-    const uint32_t k0 = sw ? kb : ka, k1 = sw ? ka : kb, e0 = sw ? eb : ea, e1 = sw ? ea : eb;
+    const uint32_t k0 = sw ? kb : ka, k1 = sw ? ka : kb;
+    const EW e0 = sw ? eb : ea, e1 = sw ? ea : eb;
     ka = k0; kb = k1; ea = e0; eb = e1;
 }
-__device__ __forceinline__ void tile_merge8_regs(uint32_t (&e)[8]) {
-    using TE = TileEntry<uint32_t>;
+template <typename EW>
+__device__ __forceinline__ void tile_merge8_regs(EW (&e)[8]) {
+    using TE = TileEntry<EW>;
 #pragma unroll
     for (int p = 0; p < 4; p++) {   // blocks of 1
-        const uint32_t l = e[2 * p], r = e[2 * p + 1];
+        const EW l = e[2 * p], r = e[2 * p + 1];
         const bool take = TE::val(l) <= TE::val(r);
         e[2 * p] = take ? l : r;
         e[2 * p + 1] = take ? TE::add(r, 1u) : l;
@@ -259,12 +263,14 @@ __global__ __launch_bounds__(kTile / OUT) void k_v2x_tile(V2xGeo x, uint32_t per
         src = K2 + (size_t)rl * x.T2 + (size_t)s * x.B;
     }
     uint32_t w0 = 1;
-    if constexpr (sizeof(EW) == 4 && OUT == 8) {
-        if (n == (uint32_t)kTile) {   // full tile: a thread's 8 entries merged in registers first
+    // (the register levels' keys hold a frame position in 28 bits)
+    const bool regs = sizeof(EW) == 4 || ((uint64_t)x.P + kTile < ((uint64_t)1 << 28) && x.B < (1u << 28));
+    if constexpr (OUT == 8) {
+        if (n == (uint32_t)kTile && regs) {   // full tile: a thread's 8 entries merged in registers first
             const uint32_t b = threadIdx.x * 8u;
-            uint32_t e[8];
+            EW e[8];
 #pragma unroll
-            for (int i = 0; i < 8; i++) e[i] = (uint32_t)TE::make(src[b + i], b + (uint32_t)i);
+            for (int i = 0; i < 8; i++) e[i] = TE::make(src[b + i], b + (uint32_t)i);
             tile_merge8_regs(e);
 #pragma unroll
             for (int i = 0; i < 8; i++) va[TE::ix(b + (uint32_t)i)] = e[i];
