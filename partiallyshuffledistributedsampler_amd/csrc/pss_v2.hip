@@ -452,7 +452,11 @@ __global__ __launch_bounds__(64) void k_v2_emit_x(Geometry g, V2Plan pl,
     // 32-bit tile arithmetic from the plan's host-computed constants (T < 2^32)
     const uint32_t ngu = (uint32_t)ng;
     const int32_t rl = (int32_t)(blockIdx.x / ngu);
+#ifdef PSS_DIAG_TILE_SWAP   // (diagnostic build, tools/stamp_v2x.hip: adjacent tiles trade XCDs)
+    const uint32_t tile = (uint32_t)g_lo + ((blockIdx.x - (uint32_t)rl * ngu) ^ 1u);
+#else
     const uint32_t tile = (uint32_t)g_lo + (blockIdx.x - (uint32_t)rl * ngu);
+#endif
     const uint32_t rank = (uint32_t)(rank_lo + rl);
     const RankDesc rd = use_ra ? ra.r[rl] : ranks[rank];   // (kernel argument: a scalar load)
     const uint32_t twoB = pl.twoB;

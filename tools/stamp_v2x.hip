@@ -5,6 +5,8 @@
 //   stamp_v2x pass    each replay beside the next epoch's last-occurrence pass on a second
 //                     stream (the bench's steady state)
 //   stamp_v2x alone   the replays only
+//   stamp_v2x alone <shift>   ... into the output buffer shifted by <shift> ids (address effects)
+// (-DPSS_DIAG_TILE_SWAP: block b replays tile b ^ 1, so that tile parity and XCD trade places)
 // Build (from the repo root; -DPSS_V2_SRC='"<path>"' stamps another copy of pss_v2.hip):
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -DPSS_STAMPS -DPSS_STAMPS_EMIT_ONLY \
 //     -Ipartiallyshuffledistributedsampler_amd/csrc -o build/stamp_v2x tools/stamp_v2x.hip \
@@ -29,6 +31,7 @@ static void pct(const char *what, std::vector<double> v) {
 int main(int argc, char **argv) {
     using namespace pss;
     const bool pass = argc < 2 || std::string(argv[1]) == "pass";
+    const int64_t shift = argc > 2 ? atoll(argv[2]) : 0;
     Geometry g{};
     g.N = 100000000; g.R = 8; g.ns = 12500000; g.B = 4096; g.version = 2; g.shuffle = 1;
     g.key0 = 0x12345678u; g.key1 = 0x9abcdef0u;
@@ -37,7 +40,8 @@ int main(int argc, char **argv) {
     RankDesc *d_rd; hipMalloc(&d_rd, sizeof(RankDesc) * 8);
     hipMemcpy(d_rd, rd.data(), sizeof(RankDesc) * 8, hipMemcpyHostToDevice);
     init_kernel_attributes_v2();
-    int64_t *out; hipMalloc(&out, sizeof(int64_t) * 8 * g.ns);
+    int64_t *out0; hipMalloc(&out0, sizeof(int64_t) * (8 * g.ns + shift));
+    int64_t *out = out0 + shift;
     uint32_t *val[2]; hipMalloc(&val[0], v2_val_bytes(g, 8)); hipMalloc(&val[1], v2_val_bytes(g, 8));
     hipStream_t s1, s2; hipStreamCreate(&s1); hipStreamCreate(&s2);
     const V2Plan pl = v2_plan(g, 8);
@@ -86,6 +90,24 @@ int main(int argc, char **argv) {
         byx[(uint32_t)s[7] & 0xFu].push_back((s[5] - r0) / 100.0);
     }
     for (auto &kv : byx) { char nm[32]; snprintf(nm, sizeof nm, "end, XCC %u", kv.first); pct(nm, kv.second); }
+    printf("block -> XCC:");
+    for (int b = 0; b < 16; b++) printf(" %u", (uint32_t)st[(size_t)b * 8 + 7] & 0xFu);
+    printf("\n");
+    // by tile parity (the tile's output region) within each XCC parity
+    for (int xp = 0; xp < 2; xp++)
+        for (int tp = 0; tp < 2; tp++) {
+            std::vector<double> v;
+            for (int b = 0; b < nwg; b++) {
+                const uint64_t *s = &st[(size_t)b * 8];
+#ifdef PSS_DIAG_TILE_SWAP
+                const int tile = (int)((b % pl.G) ^ 1);
+#else
+                const int tile = (int)(b % pl.G);
+#endif
+                if ((int)(((uint32_t)s[7] & 0xFu) & 1u) == xp && (tile & 1) == tp) v.push_back((s[5] - r0) / 100.0);
+            }
+            char nm[40]; snprintf(nm, sizeof nm, "XCC%%2=%d tile%%2=%d", xp, tp); pct(nm, v);
+        }
     return 0;
 }
 
