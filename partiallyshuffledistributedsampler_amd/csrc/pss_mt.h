@@ -301,14 +301,14 @@ __device__ void mt_draws_pair(uint32_t *mt, uint32_t W, uint32_t P, Emit emit) {
     }
 }
 
-// The same draws on a workgroup of kMtWgThreads (10 waves) per stream, for long windows (C5's
+// The same draws on a workgroup of kMtWgThreads (16 waves) per stream, for long windows (C5's
 // pool2 windows are 2^20 steps and there are only ~11 per rank: one wave per stream left most of
 // the chip idle).  The stream is consumed in ROUNDS of kMtRound twists (kMtRound * 624 words);
 // one wave -- the generator, the last -- twists and tempers the NEXT round into the other half
 // of a double-buffered ring (three dependent 227-word steps per twist, in program order inside
-// the wave: no barrier), while the other nine consume the current round in three
+// the wave: no barrier), while the other fifteen consume the current round in three
 // barrier-separated phases:
-//   summaries  each 64-word block of the round, wave w taking blocks w, w + 9, ...: where every
+//   summaries  each 64-word block of the round, wave w taking blocks w, w + 15, ...: where every
 //              verdict of the block is fixed over the index window its start can lie in, its
 //              transfer -- V2: the composed role map and the k1 / k2 acceptances for either start
 //              role; V1: the draws it makes -- comes from one role scan (a popcount) without knowing
@@ -325,7 +325,12 @@ __device__ void mt_draws_pair(uint32_t *mt, uint32_t W, uint32_t P, Emit emit) {
 // with 8 twists (profiles/r04/mt_ab/, tools/stamp_mt.hip): what is left is per-block work on
 // the stream's one CU -- ~160 clocks per 64-word block in the summaries, ~135 in the combine
 // (the blocks run exactly: the last ~3 % of a window, where k2's bound is small), ~115 in emit.
-constexpr int kMtWgThreads = 640;   // nine consumer waves and the generator
+// 16 waves (15 consumers, 4 blocks each per round) against 10 (9, 7): C5 exact V2 24.6 -> 22.5 ms,
+// 12 waves 23.3 ms, same box (round 4, profiles/r04/ab_mt_waves/).
+#ifndef PSS_MT_WG_THREADS
+#define PSS_MT_WG_THREADS 1024
+#endif
+constexpr int kMtWgThreads = PSS_MT_WG_THREADS;   // consumer waves and the generator (the last)
 constexpr int kMtBlocks = (kMtN + 63) / 64;   // 10 per twist: nine of 64 words, one of 48
 constexpr int kMtWgWaves = kMtWgThreads / 64;
 #ifndef PSS_MT_ROUND
@@ -342,9 +347,11 @@ constexpr int kMtPerWave = (kMtRoundBlocks + kMtConsumers - 1) / kMtConsumers;  
 static_assert(kMtRound % 2 == 0, "the generator's state buffer returns to mt[cur] after a round");
 static_assert(kMtRoundBlocks <= 128, "the combiner keeps the summaries in two lanes sets");
 
+constexpr int kMtTwPad = kMtN * kMtWgWaves > 2 * kMtRoundWords ? kMtN * kMtWgWaves - 2 * kMtRoundWords : 1;
 struct MtWgShared {
     uint32_t mt[2][kMtN];                 // generator state, double-buffered across a twist
     uint32_t tw[2][kMtRoundWords];        // tempered words: the round consumed, the next one
+    uint32_t tw_pad[kMtTwPad];            // (V2 tail blocks: one MT state per wave from tw on)
     uint32_t sum[kMtRoundBlocks][6];      // settled?, role map | draws, c1(0), c1(1), c2(0), c2(1)
     uint32_t win[kMtRoundBlocks][2];      // index window [lo, hi] the block's summary assumed
     uint32_t start[kMtRoundBlocks][4];    // (st, i1, i2) or (d) at each block's start; [3] = 1:

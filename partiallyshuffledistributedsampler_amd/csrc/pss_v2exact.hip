@@ -133,7 +133,8 @@ __global__ __launch_bounds__(kMtWgThreads) void k_v2x_draws_wg(V2xGeo x, int64_t
         const uint64_t tb = (b - (uint64_t)jobs * nr) * (uint64_t)kMtWgWaves + wv;
         const uint32_t rl = (uint32_t)(tb / tail_blocks);
         if (rl >= nr) return;
-        static_assert(sizeof(sh.tw) >= sizeof(uint32_t) * kMtN * kMtWgWaves, "a tail wave's MT state in tw");
+        static_assert(sizeof(sh.tw) + sizeof(sh.tw_pad) >= sizeof(uint32_t) * kMtN * kMtWgWaves,
+                      "a tail wave's MT state in tw");
         v2x_tail_block(x, epoch, rl, (uint32_t)(tb % tail_blocks) * 64u, K1, (uint32_t *)sh.tw + kMtN * wv);
         return;
     }
