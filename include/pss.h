@@ -13,6 +13,11 @@
  *   - `*_dev` arguments are device pointers on the sampler's device; `stream` is a
  *     hipStream_t (NULL = default stream).  Device work is stream-ordered and asynchronous;
  *     nothing on the per-epoch path allocates once workspaces have grown to their size.
+ *     Calls of one handle may use different streams without host synchronisation (e.g. epoch
+ *     e + 1 generated on a second stream while epoch e is consumed): work that uses the
+ *     handle's device tables and workspaces waits on the device for the last such call on
+ *     another stream; whole-stream V2 counter-order generation (ranks as kernel arguments)
+ *     uses none of them and overlaps with the previous epoch's.
  *   - a handle is not thread-safe; distinct handles share no state.
  *   - CPU mode: a handle created with device = PSS_DEVICE_CPU runs the same schedule on host
  *     threads (bit-identical to the GPU); every `*_dev` pointer is then a HOST pointer, `stream`

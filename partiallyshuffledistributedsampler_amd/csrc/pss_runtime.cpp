@@ -260,6 +260,14 @@ struct pss_sampler {
     };
     struct Pending { bool valid; Shape shape; uint32_t key0, key1; int buf; };
     Pending pend[2] = {};        // queued lookahead passes (epochs e+1, e+2)
+    // Calls on different streams share the handle's device state (rank / order / prefix tables,
+    // the V1 key table and exact-order workspace, the map scratch): a call that uses it first
+    // waits for the last such call when that one ran on another stream (SharedUse).  The V2
+    // counter-order replays of whole streams with their ranks as kernel arguments use none of it
+    // (their VAL ring orders itself with events), so consecutive epochs on two streams overlap.
+    hipEvent_t ev_shared = nullptr;
+    hipStream_t last_shared = nullptr;
+    bool shared_used = false;
     bool last_valid = false;     // shape and epoch of the previous V2 generate
     Shape last_shape{};
     int64_t last_epoch = 0;
@@ -381,6 +389,26 @@ int cpu_prefix(pss_sampler *h) {
     return PSS_OK;
 }
 
+// RAII: device work on stream s that uses the handle's shared device state (see pss_sampler)
+struct SharedUse {
+    pss_sampler *h;
+    hipStream_t s;
+    SharedUse(pss_sampler *h_, hipStream_t s_) : h(h_), s(s_) {
+        if (h->shared_used && h->last_shared != s && h->ev_shared)
+            (void)hipStreamWaitEvent(s, h->ev_shared, 0);
+    }
+    ~SharedUse() {
+        if (!h->ev_shared && hipEventCreateWithFlags(&h->ev_shared, hipEventDisableTiming) != hipSuccess) {
+            h->ev_shared = nullptr;
+            return;
+        }
+        if (hipEventRecord(h->ev_shared, s) == hipSuccess) {
+            h->last_shared = s;
+            h->shared_used = true;
+        }
+    }
+};
+
 struct CpuTimer {   // pss_profile in CPU mode: wall milliseconds per kernel kind
     pss_sampler *h;
     int kind;
@@ -466,6 +494,7 @@ int pss_destroy(pss_sampler *h) {
         if (h->ev_side) (void)hipEventDestroy(h->ev_side);
         for (hipEvent_t e : h->ev_read) if (e) (void)hipEventDestroy(e);
         for (hipEvent_t e : h->ev_done) if (e) (void)hipEventDestroy(e);
+        if (h->ev_shared) (void)hipEventDestroy(h->ev_shared);
         h->d_val2.release(); h->d_buf2.release(); h->d_val3.release(); h->d_buf3.release();
     }
     delete h;
@@ -540,6 +569,7 @@ int pss_prepare(pss_sampler *h, void *stream) {
     if (!h) return fail(PSS_EINVAL, "NULL handle");
     if (h->cpu) return cpu_prefix(h);
     DeviceGuard dg(h->device);
+    SharedUse su(h, (hipStream_t)stream);
     return prepare_prefix(h, (hipStream_t)stream);
 }
 
@@ -694,6 +724,11 @@ int generate_impl(pss_sampler *h, int32_t rank_lo, int32_t rank_hi, int64_t pos_
     // ahead of it on the epoch path (the device table is refreshed on first other use)
     const bool by_value = h->version == 2 && h->order_mode == PSS_ORDER_COUNTER && nr > 0 &&
                           pss::v2_ranks_by_value(g, nr, h->emit_path);
+    // whole V2 streams, ranks by value, the lookahead ring: no shared device state (pss_sampler)
+    const bool own_state = by_value && !ma && pos_lo == 0 && count >= h->ns && lookahead_on() &&
+                           pss::v2_stage_split(g, nr, h->emit_path);
+    std::unique_ptr<SharedUse> su;
+    if (!own_state) su.reset(new SharedUse(h, s));
     pss::RankArgs ra;
     if (by_value) {
         for (int32_t i = 0; i < nr; i++) ra.r[i] = h->ranks[rank_lo + i];
@@ -839,6 +874,7 @@ int pss_map(pss_sampler *h, const int64_t *ids_dev, int64_t n, int32_t *file_pos
     }
     DeviceGuard dg(h->device);
     hipStream_t s = (hipStream_t)stream;
+    SharedUse su(h, s);
     int rc = prepare_prefix(h, s);
     if (rc) return rc;
     PSS_HIP(pss::launch_map(h->d_prefix.p, h->F, h->d_bucket.p, h->kb, h->nb, ids_dev, n, file_pos_dev,
@@ -874,6 +910,7 @@ int pss_generate_mapped(pss_sampler *h, int32_t rank_lo, int32_t rank_hi, int64_
     }
     DeviceGuard dg(h->device);
     hipStream_t s = (hipStream_t)stream;
+    SharedUse su(h, s);
     int rc = prepare_prefix(h, s);
     if (rc) return rc;
     const pss::Geometry g = h->geometry();
@@ -951,6 +988,7 @@ int pss_gather(pss_sampler *h, const void *data_dev, int64_t row_bytes, const in
     }
     DeviceGuard dg(h->device);
     hipStream_t s = (hipStream_t)stream;
+    SharedUse su(h, s);
     const int rc = prepare_order(h, s);
     if (rc) return rc;
     PSS_HIP(pss::launch_gather(data_dev, row_bytes, base_rows_dev, h->d_order.p, file_pos_dev, offset_dev, n,
@@ -976,6 +1014,7 @@ int pss_partition(pss_sampler *h, int32_t rank_lo, int32_t rank_hi, int64_t *seg
     }
     DeviceGuard dg(h->device);
     hipStream_t s = (hipStream_t)stream;
+    SharedUse su(h, s);
     int rc = prepare_prefix(h, s);
     if (rc) return rc;
     PSS_HIP(pss::launch_partition(h->geometry(), h->d_ranks.p, rank_lo, rank_hi - rank_lo,

@@ -1,0 +1,78 @@
+"""Consecutive epochs generated on two streams without a host sync between them (a data pipeline
+consuming epoch e while e + 1 is generated, bench.py --pipeline 2) give every epoch exactly the
+ids of a one-stream run (of a second handle: init_iter's history is cumulative, V1:122-125).
+The handle's shared device state (rank / order / prefix tables, the V1 key table, the
+exact-order workspace) is ordered across streams by the runtime (pss_sampler SharedUse); the V2
+whole-stream replays order their VAL ring with events."""
+import numpy as np
+import pytest
+import torch
+
+from partiallyshuffledistributedsampler_amd.engine import IndexEngine
+
+EPOCHS = 6
+
+
+def _shape(F, L):
+    lens = np.full(F, L, dtype=np.int64)
+    lens[::7] += 13
+    return lens, int(lens.sum())
+
+
+def _one_stream(eng, R, mapped=False):
+    res = []
+    for e in range(EPOCHS):
+        eng.init_iter(e)
+        if mapped:
+            f, o = eng.generate_mapped(0, R)
+            res.append((f.cpu().numpy(), o.cpu().numpy()))
+        else:
+            res.append(eng.generate(0, R).cpu().numpy())
+    return res
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("version,order,B", [(1, "counter", 4096), (2, "counter", 4096), (2, "counter", 1 << 17),
+                                             (1, "exact", 4096), (2, "exact", 4096)],
+                         ids=lambda x: str(x))
+def test_epochs_on_two_streams_equal_one_stream(version, order, B):
+    F = 300 if order == "exact" else 2000
+    lens, N = _shape(F, 10_000)
+    R = 8
+    ref = _one_stream(IndexEngine(lens, N, R, B, version, device=0, order=order, seed=11), R)
+    eng = IndexEngine(lens, N, R, B, version, device=0, order=order, seed=11)
+    ns = eng.num_samples
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    outs = [torch.empty((R, ns), dtype=torch.int64, device="cuda") for _ in range(EPOCHS)]
+    torch.cuda.synchronize()
+    for e in range(EPOCHS):            # no host sync between the epochs
+        eng.init_iter(e)
+        eng.generate(0, R, out=outs[e], stream=streams[e % 2])
+    torch.cuda.synchronize()
+    eng.check()
+    for e in range(EPOCHS):
+        assert np.array_equal(outs[e].cpu().numpy(), ref[e]), (version, order, B, e)
+    eng.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("version", [1, 2])
+def test_mapped_epochs_on_two_streams_equal_one_stream(version):
+    lens, N = _shape(1000, 10_000)
+    R = 8
+    ref = _one_stream(IndexEngine(lens, N, R, 4096, version, device=0, seed=12), R, mapped=True)
+    eng = IndexEngine(lens, N, R, 4096, version, device=0, seed=12)
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    got = []
+    torch.cuda.synchronize()
+    for e in range(EPOCHS):
+        eng.init_iter(e)
+        with torch.cuda.stream(streams[e % 2]):
+            got.append(eng.generate_mapped(0, R, stream=streams[e % 2]))
+    torch.cuda.synchronize()
+    eng.check()
+    for e in range(EPOCHS):
+        f, o = got[e]
+        assert np.array_equal(f.cpu().numpy(), ref[e][0]), (version, e)
+        assert np.array_equal(o.cpu().numpy(), ref[e][1]), (version, e)
+    eng.close()
