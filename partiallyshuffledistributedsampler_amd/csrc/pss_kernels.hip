@@ -400,9 +400,16 @@ __global__ __launch_bounds__(64) void k_v1_feistel(Geometry g, V1Plan vp, const 
 #ifndef PSS_V1OS_PER
 #define PSS_V1OS_PER 4
 #endif
-constexpr int kV1OsPer = PSS_V1OS_PER;             // positions per lane (2, 4 or 8)
+#ifndef PSS_V1OS_ITERS
+#define PSS_V1OS_ITERS 2
+#endif
+constexpr int kV1OsPer = PSS_V1OS_PER;             // positions per lane (2, 4 or 8) per iteration
 static_assert(kV1OsPer == 2 || kV1OsPer == 4 || kV1OsPer == 8, "one or more 16-byte pair stores per lane");
-constexpr int64_t kV1OsPos = 256 * kV1OsPer;
+constexpr int kV1OsIters = PSS_V1OS_ITERS;         // iterations per workgroup (one prologue):
+                                                   // 2 against 1: C2 V1 639-656 vs 637-641 G idx/s,
+                                                   // 4: 601-612 (profiles/r04/ab_v1os_iters/)
+constexpr int64_t kV1OsPos = 256 * kV1OsPer;       // positions per iteration
+constexpr int64_t kV1OsSpan = kV1OsPos * kV1OsIters;   // positions per workgroup
 struct V1OsPlan {
     int64_t blk_lo;            // first 1024-position block of each rank
     uint32_t bpr;              // blocks per rank
@@ -416,7 +423,7 @@ __global__ __launch_bounds__(256) void k_v1_os(Geometry g, V1OsPlan vp, const Ra
                                                int32_t rank_lo, const uint32_t *__restrict__ kt,
                                                int64_t pos_lo, int64_t count, int64_t *__restrict__ out) {
     const uint32_t rl = blockIdx.x / vp.bpr;
-    const int64_t p0 = (vp.blk_lo + (int64_t)(blockIdx.x - rl * vp.bpr)) * kV1OsPos;
+    const int64_t p0 = (vp.blk_lo + (int64_t)(blockIdx.x - rl * vp.bpr)) * kV1OsSpan;
     const int64_t pos_hi = pos_lo + count < g.ns ? pos_lo + count : g.ns;
     const int64_t start = ranks[rank_lo + (int32_t)rl].new_start;
     int64_t *o = out + (int64_t)rl * count - pos_lo;
@@ -424,8 +431,8 @@ __global__ __launch_bounds__(256) void k_v1_os(Geometry g, V1OsPlan vp, const Ra
     const int64_t B = vp.B;
     const int64_t w = vp.b_pow2 ? (p0 >> vp.b_log) : p0 / B;
     const int64_t wB = w * B;
-    const bool fast = vp.fast_ok && wB + B <= g.ns && p0 + kV1OsPos <= wB + B && p0 >= pos_lo &&
-                      p0 + kV1OsPos <= pos_hi && (((uintptr_t)(o + p0)) & 15u) == 0;
+    const bool fast = vp.fast_ok && wB + B <= g.ns && p0 + kV1OsSpan <= wB + B && p0 >= pos_lo &&
+                      p0 + kV1OsSpan <= pos_hi && (((uintptr_t)(o + p0)) & 15u) == 0;
     const uint32_t l4 = (uint32_t)kV1OsPer * threadIdx.x;
     if (fast) {
         const uint32_t *kw = ktr + (w - vp.w_lo) * kRoundKeyWords;
@@ -435,7 +442,10 @@ __global__ __launch_bounds__(256) void k_v1_os(Geometry g, V1OsPlan vp, const Ra
             const uint32_t k = __builtin_amdgcn_readfirstlane(kw[i]);
             kp[i] = PACKED ? (k & 0xFFFFu) * 0x10001u : k;
         }
-        const uint32_t x0 = (uint32_t)(p0 - wB) + l4;
+        const int64_t base = start + wB;
+#pragma unroll
+        for (int it = 0; it < kV1OsIters; it++) {
+        const uint32_t x0 = (uint32_t)(p0 - wB) + (uint32_t)(it * kV1OsPos) + l4;
         uint32_t x[kV1OsPer], y[kV1OsPer];
 #pragma unroll
         for (int j = 0; j < kV1OsPer; j++) x[j] = x0 + (uint32_t)j;
@@ -448,7 +458,6 @@ __global__ __launch_bounds__(256) void k_v1_os(Geometry g, V1OsPlan vp, const Ra
 #pragma unroll
             for (int j = 0; j < kV1OsPer; j++) y[j] = feistel_once(x[j], vp.hB, kp);
         }
-        const int64_t base = start + wB;
         int64_t id[kV1OsPer];
 #pragma unroll
         for (int j = 0; j < kV1OsPer; j++) {
@@ -463,13 +472,15 @@ __global__ __launch_bounds__(256) void k_v1_os(Geometry g, V1OsPlan vp, const Ra
         for (int j = 0; j < kV1OsPer; j += 2) {
             longlong2 a;
             a.x = id[j]; a.y = id[j + 1];
-            *(longlong2 *)(o + p0 + l4 + j) = a;
+            *(longlong2 *)(o + p0 + it * kV1OsPos + l4 + j) = a;
+        }
         }
         return;
     }
 #pragma unroll
-    for (int j = 0; j < kV1OsPer; j++) {
-        const int64_t p = p0 + l4 + j;
+    for (int q = 0; q < kV1OsPer * kV1OsIters; q++) {
+        const int j = q % kV1OsPer;
+        const int64_t p = p0 + (q / kV1OsPer) * kV1OsPos + l4 + j;
         if (p < pos_lo || p >= pos_hi) continue;
         int64_t y = p;
         if (g.shuffle) {
@@ -627,8 +638,8 @@ hipError_t launch_v1(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, 
                            g, rank_lo, w_lo, nw, key_ws);
     if (!mapped) {
         V1OsPlan op{};
-        op.blk_lo = pos_lo / kV1OsPos;
-        const int64_t bpr = (pos_hi - 1) / kV1OsPos - op.blk_lo + 1;
+        op.blk_lo = pos_lo / kV1OsSpan;
+        const int64_t bpr = (pos_hi - 1) / kV1OsSpan - op.blk_lo + 1;
         op.bpr = (uint32_t)bpr;
         op.w_lo = w_lo;
         op.nw = nw;
@@ -636,7 +647,7 @@ hipError_t launch_v1(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, 
         op.hB = feistel_half_bits(op.B);
         op.b_pow2 = (g.B & (g.B - 1)) == 0 ? 1u : 0u;
         op.b_log = (uint32_t)ceil_log2_u64((uint64_t)g.B);
-        op.fast_ok = g.shuffle && op.B == (1u << (2 * op.hB)) && (g.B % kV1OsPos) == 0;
+        op.fast_ok = g.shuffle && op.B == (1u << (2 * op.hB)) && (g.B % kV1OsSpan) == 0;
         const bool narrow = g.N + g.ns < (int64_t)UINT32_MAX;
         const uint64_t blocks = (uint64_t)bpr * (uint64_t)nr;
         if (blocks < ((uint64_t)1 << 31)) {
