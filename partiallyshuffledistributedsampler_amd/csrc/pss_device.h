@@ -137,6 +137,27 @@ __device__ __forceinline__ void feistel2_pk16(uint32_t x0, uint32_t x1, uint32_t
     y1 = ((L >> 16) << h) | (R >> 16);
 }
 
+// feistel2_pk16 with each chain's own round keys (k0: the low half-word's chain, k1: the high's)
+__device__ __forceinline__ void feistel2_pk16_k2(uint32_t x0, uint32_t x1, uint32_t h, const uint32_t *k0,
+                                                 const uint32_t *k1, uint32_t &y0, uint32_t &y1) {
+    const uint32_t mask = (1u << h) - 1u;
+    uint32_t L = (x0 >> h) | ((x1 >> h) << 16);
+    uint32_t R = (x0 & mask) | ((x1 & mask) << 16);
+    const pss_u16x2 M = {(unsigned short)kFeistelM16, (unsigned short)kFeistelM16};
+    const pss_u16x2 SH = {(unsigned short)(16u - h), (unsigned short)(16u - h)};
+#pragma unroll
+    for (int i = 0; i < kFeistelRounds; i++) {
+        const uint32_t kp = (k0[i] & 0xFFFFu) | (k1[i] << 16);
+        const pss_u16x2 a = __builtin_bit_cast(pss_u16x2, R ^ kp);
+        const pss_u16x2 f = (a * M) >> SH;
+        const uint32_t t = L ^ __builtin_bit_cast(uint32_t, f);
+        L = R;
+        R = t;
+    }
+    y0 = ((L & 0xFFFFu) << h) | (R & 0xFFFFu);
+    y1 = ((L >> 16) << h) | (R >> 16);
+}
+
 // Four chains in two registers, rounds interleaved so that neither packed multiply waits on
 // the other's result (no dependency stalls between the pk ops).  Same values as feistel2_pk16.
 __device__ __forceinline__ void feistel4_pk16(const uint32_t x[4], uint32_t h, const uint32_t *kp,

@@ -139,7 +139,12 @@ __global__ __launch_bounds__(NT) void k_v2_lastocc(Geometry g, V2Plan pl, int32_
 #pragma unroll
         for (int u = 0; u < 4; u++) slow |= lt[u] && (uint32_t)w_lo + dw[u] == w_last;
         uint32_t x[4];
-        if (!slow) {
+        if (!slow && feistel_packed_ok(hB)) {
+            // two chains per register on the packed 16-bit round function, each with its own
+            // window's keys (the slots' last steps lie in different windows)
+            feistel2_pk16_k2(pp[0], pp[1], hB, rk + kRoundKeyWords * dw[0], rk + kRoundKeyWords * dw[1], x[0], x[1]);
+            feistel2_pk16_k2(pp[2], pp[3], hB, rk + kRoundKeyWords * dw[2], rk + kRoundKeyWords * dw[3], x[2], x[3]);
+        } else if (!slow) {
 #pragma unroll
             for (int u = 0; u < 4; u++) x[u] = feistel_once(pp[u], hB, rk + kRoundKeyWords * dw[u]);
         } else {
