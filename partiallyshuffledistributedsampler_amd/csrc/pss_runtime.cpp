@@ -613,9 +613,15 @@ int generate_v2_lookahead(pss_sampler *h, const pss::Geometry &g, int32_t rank_l
         // the lowest priority: at the highest the C2 step was slower (519 vs 526 G idx/s, round 2)
         (void)greatest;
         PSS_HIP(hipStreamCreateWithPriority(&h->side, hipStreamNonBlocking, least));
-        for (hipEvent_t &e : h->ev_read) PSS_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-        for (hipEvent_t &e : h->ev_done) PSS_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-        PSS_HIP(hipEventCreateWithFlags(&h->ev_side, hipEventDisableTiming));
+        // these events only order device work on this device (never inspected by the host):
+        // without the system-scope fence a step takes 176 against 179 us at C2, same box
+        // (profiles/r04/ab_evflags; device-scope release alone: 179)
+#ifndef PSS_LA_EVENT_FLAGS
+#define PSS_LA_EVENT_FLAGS (hipEventDisableTiming | hipEventDisableSystemFence)
+#endif
+        for (hipEvent_t &e : h->ev_read) PSS_HIP(hipEventCreateWithFlags(&e, PSS_LA_EVENT_FLAGS));
+        for (hipEvent_t &e : h->ev_done) PSS_HIP(hipEventCreateWithFlags(&e, PSS_LA_EVENT_FLAGS));
+        PSS_HIP(hipEventCreateWithFlags(&h->ev_side, PSS_LA_EVENT_FLAGS));
     }
     // epochs queued ahead: 2 keeps the wait for a pass off the replay's critical path (one
     // epoch ahead: the replay waits 33 us per step, 491 against 526 G idx/s, round 2)
@@ -633,7 +639,10 @@ int generate_v2_lookahead(pss_sampler *h, const pss::Geometry &g, int32_t rank_l
         }
     if (buf >= 0 && small(buf)) buf = -1;   // (cannot happen: queued passes had their size)
     if (buf >= 0) {
+#if !defined(PSS_DIAG_NO_STREAM_EVENTS) && !defined(PSS_DIAG_NO_STREAM_WAIT)
+        // (diagnostics: the replay stream's gaps without its wait and/or record; racy)
         PSS_HIP(hipStreamWaitEvent(s, h->ev_done[buf], 0));
+#endif
         PSS_HIP(pss::launch_v2(g, h->d_ranks.p, rank_lo, nr, pos_lo, count, out_dev, V[buf]->p,
                                bwords ? W[buf]->p : nullptr, nullptr, h->d_err.p, s, mk, h->emit_path,
                                pss::V2_STAGE_EMIT, ma, ra));
@@ -647,7 +656,9 @@ int generate_v2_lookahead(pss_sampler *h, const pss::Geometry &g, int32_t rank_l
                                bwords ? W[buf]->p : nullptr, nullptr, h->d_err.p, s, mk, h->emit_path,
                                pss::V2_STAGE_ALL, ma, ra));
     }
+#if !defined(PSS_DIAG_NO_STREAM_EVENTS) && !defined(PSS_DIAG_NO_STREAM_RECORD)
     PSS_HIP(hipEventRecord(h->ev_read[buf], s));
+#endif
     const bool sequential = h->last_valid && h->last_shape == shape && h->last_epoch == h->epoch - 1;
     h->last_valid = true;
     h->last_shape = shape;
