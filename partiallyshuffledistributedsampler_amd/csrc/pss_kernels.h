@@ -99,10 +99,13 @@ struct MapArgs {
 
 // V1: ids of positions [pos_lo, pos_lo+count) of ranks [rank_lo, rank_lo+nr) -> out[r][count];
 // each window ordered by its keyed Feistel bijection (key table of the windows in key_ws).
-// mapped != nullptr: (file position, offset) into mapped->fpos / off instead (out unused)
+// mapped != nullptr: (file position, offset) into mapped->fpos / off instead (out unused).
+// rank_args != nullptr (nr <= kArgRanks): ranks [rank_lo, rank_lo+nr)'s descriptors by value;
+// the device table `ranks` is then refreshed from them only where a kernel reads it
 hipError_t launch_v1(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, int32_t nr,
                      int64_t pos_lo, int64_t count, int64_t *out, uint32_t *key_ws,
-                     hipStream_t s, const Marker &mk = Marker(), const MapArgs *mapped = nullptr);
+                     hipStream_t s, const Marker &mk = Marker(), const MapArgs *mapped = nullptr,
+                     const RankArgs *rank_args = nullptr);
 size_t v1_workspace_bytes(const Geometry &g, int32_t nr, int64_t pos_lo, int64_t count);
 
 // V1 in the reference's exact order (CPython MT19937 per window, pss_v1exact.hip): windows up

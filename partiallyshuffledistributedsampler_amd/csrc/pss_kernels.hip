@@ -421,11 +421,13 @@ struct V1OsPlan {
 template <bool PACKED, bool NARROW>
 __global__ __launch_bounds__(256) void k_v1_os(Geometry g, V1OsPlan vp, const RankDesc *__restrict__ ranks,
                                                int32_t rank_lo, const uint32_t *__restrict__ kt,
-                                               int64_t pos_lo, int64_t count, int64_t *__restrict__ out) {
+                                               int64_t pos_lo, int64_t count, int64_t *__restrict__ out,
+                                               RankArgs ra, int use_ra) {
     const uint32_t rl = blockIdx.x / vp.bpr;
     const int64_t p0 = (vp.blk_lo + (int64_t)(blockIdx.x - rl * vp.bpr)) * kV1OsSpan;
     const int64_t pos_hi = pos_lo + count < g.ns ? pos_lo + count : g.ns;
-    const int64_t start = ranks[rank_lo + (int32_t)rl].new_start;
+    // (use_ra: the rank's descriptor from the kernel arguments, no upload kernel ahead)
+    const int64_t start = use_ra ? ra.r[rl].new_start : ranks[rank_lo + (int32_t)rl].new_start;
     int64_t *o = out + (int64_t)rl * count - pos_lo;
     const uint32_t *ktr = kt + (int64_t)rl * vp.nw * kRoundKeyWords;
     const int64_t B = vp.B;
@@ -628,9 +630,10 @@ size_t v1_workspace_bytes(const Geometry &g, int32_t nr, int64_t pos_lo, int64_t
 
 hipError_t launch_v1(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, int32_t nr,
                      int64_t pos_lo, int64_t count, int64_t *out, uint32_t *key_ws,
-                     hipStream_t s, const Marker &mk, const MapArgs *mapped) {
+                     hipStream_t s, const Marker &mk, const MapArgs *mapped, const RankArgs *rank_args) {
     int64_t w_lo, nw;
     if (nr <= 0 || !v1_window_range(g, pos_lo, count, w_lo, nw)) return hipSuccess;
+    if (rank_args && nr > kArgRanks) return hipErrorInvalidValue;
     const int64_t pos_hi = pos_lo + count < g.ns ? pos_lo + count : g.ns;
     mk(K_V1, s);
     if (g.shuffle)
@@ -652,8 +655,11 @@ hipError_t launch_v1(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, 
         const uint64_t blocks = (uint64_t)bpr * (uint64_t)nr;
         if (blocks < ((uint64_t)1 << 31)) {
             const dim3 grid((uint32_t)blocks);
+            RankArgs ra;
+            if (rank_args) ra = *rank_args;
+            const int use_ra = rank_args ? 1 : 0;
 #define PSS_V1OS(PK, NA) hipLaunchKernelGGL((k_v1_os<PK, NA>), grid, dim3(256), 0, s, g, op, ranks, rank_lo, \
-                                            (const uint32_t *)key_ws, pos_lo, count, out)
+                                            (const uint32_t *)key_ws, pos_lo, count, out, ra, use_ra)
             const bool pk = feistel_packed_ok(op.hB);
             if (pk && narrow) PSS_V1OS(true, true);
             else if (pk) PSS_V1OS(true, false);
@@ -663,6 +669,10 @@ hipError_t launch_v1(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, 
             mk(-1, s);
             return hipGetLastError();
         }
+    }
+    if (rank_args) {   // the kernels below read the device table
+        const hipError_t e = launch_put_ranks(rank_args->r, nr, const_cast<RankDesc *>(ranks) + rank_lo, s);
+        if (e != hipSuccess) return e;
     }
     V1Plan vp{};
     vp.sb_lo = pos_lo / 256;

@@ -398,7 +398,10 @@ struct SharedUse {
             (void)hipStreamWaitEvent(s, h->ev_shared, 0);
     }
     ~SharedUse() {
-        if (!h->ev_shared && hipEventCreateWithFlags(&h->ev_shared, hipEventDisableTiming) != hipSuccess) {
+#ifndef PSS_SHARED_EVENT_FLAGS
+#define PSS_SHARED_EVENT_FLAGS hipEventDisableTiming
+#endif
+        if (!h->ev_shared && hipEventCreateWithFlags(&h->ev_shared, PSS_SHARED_EVENT_FLAGS) != hipSuccess) {
             h->ev_shared = nullptr;
             return;
         }
@@ -733,10 +736,11 @@ int generate_impl(pss_sampler *h, int32_t rank_lo, int32_t rank_hi, int64_t pos_
     const pss::Geometry g = h->geometry();
     // the V2 exchange replay takes its ranks' descriptors as kernel arguments: no upload kernel
     // ahead of it on the epoch path (the device table is refreshed on first other use)
-    const bool by_value = h->version == 2 && h->order_mode == PSS_ORDER_COUNTER && nr > 0 &&
-                          pss::v2_ranks_by_value(g, nr, h->emit_path);
+    // (so does V1's one-shot kernel, counter order, up to kArgRanks ranks per call)
+    const bool by_value = h->order_mode == PSS_ORDER_COUNTER && nr > 0 &&
+                          (h->version == 2 ? pss::v2_ranks_by_value(g, nr, h->emit_path) : nr <= pss::kArgRanks);
     // whole V2 streams, ranks by value, the lookahead ring: no shared device state (pss_sampler)
-    const bool own_state = by_value && !ma && pos_lo == 0 && count >= h->ns && lookahead_on() &&
+    const bool own_state = h->version == 2 && by_value && !ma && pos_lo == 0 && count >= h->ns && lookahead_on() &&
                            pss::v2_stage_split(g, nr, h->emit_path);
     std::unique_ptr<SharedUse> su;
     if (!own_state) su.reset(new SharedUse(h, s));
@@ -760,7 +764,8 @@ int generate_impl(pss_sampler *h, int32_t rank_lo, int32_t rank_hi, int64_t pos_
     } else if (h->version == 1) {
         const size_t sb = pss::v1_workspace_bytes(g, nr, pos_lo, count);
         if (sb) PSS_HIP(h->d_sort.ensure(words(sb)));
-        PSS_HIP(pss::launch_v1(g, h->d_ranks.p, rank_lo, nr, pos_lo, count, out_dev, h->d_sort.p, s, mk));
+        PSS_HIP(pss::launch_v1(g, h->d_ranks.p, rank_lo, nr, pos_lo, count, out_dev, h->d_sort.p, s, mk,
+                               nullptr, rap));
     } else if (h->order_mode == PSS_ORDER_EXACT) {
         PSS_HIP(h->d_sort.ensure(words(pss::v2_exact_ws_bytes(g, nr))));
         mk(pss::K_V2_EMIT, s);
