@@ -437,13 +437,23 @@ __global__ __launch_bounds__(256) void k_v1_os(Geometry g, V1OsPlan vp, const Ra
                       p0 + kV1OsSpan <= pos_hi && (((uintptr_t)(o + p0)) & 15u) == 0;
     const uint32_t l4 = (uint32_t)kV1OsPer * threadIdx.x;
     if (fast) {
-        const uint32_t *kw = ktr + (w - vp.w_lo) * kRoundKeyWords;
         uint32_t kp[kFeistelRounds];
+#ifdef PSS_V1OS_INKEYS   // the window's keys computed here (wave-uniform) instead of the key table
+        uint32_t kr[8];
+        round_keys8(g.key0, g.key1, (uint32_t)w, (uint32_t)(rank_lo + (int32_t)rl), DOM_V1_WIN, kr);
+#pragma unroll
+        for (int i = 0; i < kFeistelRounds; i++) {
+            const uint32_t k = __builtin_amdgcn_readfirstlane(kr[i]);
+            kp[i] = PACKED ? (k & 0xFFFFu) * 0x10001u : k;
+        }
+#else
+        const uint32_t *kw = ktr + (w - vp.w_lo) * kRoundKeyWords;
 #pragma unroll
         for (int i = 0; i < kFeistelRounds; i++) {
             const uint32_t k = __builtin_amdgcn_readfirstlane(kw[i]);
             kp[i] = PACKED ? (k & 0xFFFFu) * 0x10001u : k;
         }
+#endif
         const int64_t base = start + wB;
 #pragma unroll
         for (int it = 0; it < kV1OsIters; it++) {
@@ -488,10 +498,14 @@ __global__ __launch_bounds__(256) void k_v1_os(Geometry g, V1OsPlan vp, const Ra
         if (g.shuffle) {
             const int64_t wp = p / B;
             const int64_t len = g.ns - wp * B < B ? g.ns - wp * B : B;
+            uint32_t kk[8];
+#ifdef PSS_V1OS_INKEYS
+            round_keys8(g.key0, g.key1, (uint32_t)wp, (uint32_t)(rank_lo + (int32_t)rl), DOM_V1_WIN, kk);
+#else
             const uint32_t *kw = ktr + (wp - vp.w_lo) * kRoundKeyWords;
-            uint32_t kk[kFeistelRounds];
 #pragma unroll
             for (int i = 0; i < kFeistelRounds; i++) kk[i] = kw[i];
+#endif
             y = wp * B + feistel((uint32_t)(p - wp * B), (uint32_t)len, feistel_half_bits((uint32_t)len), kk);
         }
         o[p] = wrap_id(start + y, g.N);
@@ -636,7 +650,11 @@ hipError_t launch_v1(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, 
     if (rank_args && nr > kArgRanks) return hipErrorInvalidValue;
     const int64_t pos_hi = pos_lo + count < g.ns ? pos_lo + count : g.ns;
     mk(K_V1, s);
+#ifdef PSS_V1OS_INKEYS
+    if (g.shuffle && (mapped || (uint64_t)((pos_hi - 1) / kV1OsSpan - pos_lo / kV1OsSpan + 1) * (uint64_t)nr >= ((uint64_t)1 << 31)))
+#else
     if (g.shuffle)
+#endif
         hipLaunchKernelGGL(k_v1_keys, dim3((uint32_t)cdiv(nw, 256), (uint32_t)nr), dim3(256), 0, s,
                            g, rank_lo, w_lo, nw, key_ws);
     if (!mapped) {
