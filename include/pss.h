@@ -178,9 +178,10 @@ int pss_emit_path(pss_sampler *h, int32_t *path);
  *       shuffle(range(n))` (V1:102,114-115,165-171, shuffle_buffer < 2^31); V2 get_index's
  *       choice / remove / append with its per-window and per-tail-step reseeding (V2:96-116,
  *       num_samples < 2^31, shuffle_buffer < 2^30).  PSS_ENOTSUP outside those bounds.
- *       Device workspace: V1 windows beyond 16000 entries take ~16 B per entry of the windows
- *       one pass resolves (<= 2 GB up to 2^27-entry windows, one window per pass beyond:
- *       ~16 GB at shuffle_buffer = 2^30); V2 ~28 B per position of the ranks of a pass.  A
+ *       Device workspace: V1 windows beyond 16000 entries take ~18 B per entry of the windows
+ *       one pass resolves (J, S, H, PART as u32 and PARTP as u16: <= 2.3 GB up to 2^27-entry
+ *       windows, one window per pass beyond: ~19 GB at shuffle_buffer = 2^30, ~39 GB near
+ *       2^31); V2 ~28 B per position of the ranks of a pass.  A
  *       workspace the device cannot hold makes pss_generate return PSS_EHIP.
  * Replaces nothing in the reference: its order IS the exact one. */
 #define PSS_ORDER_COUNTER 0

@@ -152,7 +152,7 @@ size_t v2_val_bytes(const Geometry &g, int32_t nr);
 hipError_t launch_v2_tail_vals(const Geometry &g, const V2Plan &pl, const RankDesc *ranks,
                                int32_t rank_lo, int32_t nr, const uint32_t *VAL, int64_t pos_lo,
                                int64_t count, int64_t *out, hipStream_t s,
-                               const MapArgs *mapped = nullptr);
+                               const MapArgs *mapped = nullptr, const RankArgs *rank_args = nullptr);
 // pools beyond LDS (P1 > kLdsSlotMax): the grouped slot machine (pss_v2grp.hip); its key
 // table and per-tile tables live in val_ws (v2_val_bytes)
 bool v2_grouped(const Geometry &g);

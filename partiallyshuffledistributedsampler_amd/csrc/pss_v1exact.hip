@@ -520,10 +520,18 @@ static hipError_t launch_v1_exact_big(const Geometry &g, const RankDesc *ranks, 
     const uint64_t per = (uint64_t)v1x_jobs_per_pass(W);
     const uint32_t B = (uint32_t)W;
     const uint32_t nbk = v1x_nbk(W);
-    // the flat grids: XCD-major while they stay below 2^32 threads
-    auto grid = [&](const V1xBig &b, uint32_t xb) {
+    // the flat grids: XCD-major while they stay below 2^24 workgroups, else 2-D (blockIdx.y = the
+    // window slot).  The layout is decided here and handed to the kernels in b.xcd, never inferred
+    // from the dim3 (a 2-D grid of one job also has y == 1).  PSS_V1X_GRID2D=1 forces the 2-D form.
+    static const bool force2d = [] {
+        const char *e = getenv("PSS_V1X_GRID2D");
+        return e && atoi(e) == 1;
+    }();
+    auto grid = [&](V1xBig &b, uint32_t xb) {
+        b.xb = xb;
         const uint64_t flat = (uint64_t)xb * (((uint64_t)b.nj + 7) / 8) * 8;
-        return flat < ((uint64_t)1 << 24) ? dim3((uint32_t)flat) : dim3(xb, b.nj);
+        b.xcd = !force2d && flat < ((uint64_t)1 << 24) ? 1u : 0u;
+        return b.xcd ? dim3((uint32_t)flat) : dim3(xb, b.nj);
     };
     for (uint64_t j0 = 0; j0 < jobs; j0 += per) {
         V1xBig b{};
@@ -547,19 +555,13 @@ static hipError_t launch_v1_exact_big(const Geometry &g, const RankDesc *ranks, 
         else hipLaunchKernelGGL(k_v1x_draws32, dim3(b.nj), dim3(64), 0, s, g, b, epoch);
         hipLaunchKernelGGL(k_v1x_bscan, dim3(b.nj), dim3(kV1xScanNT), 0, s, g, b);
         V1xBig bp = b;
-        bp.xb = (B + kV1pChunk - 1) / kV1pChunk;
-        dim3 gp = grid(bp, bp.xb);
-        bp.xcd = gp.y == 1 ? 1u : 0u;
+        const dim3 gp = grid(bp, (B + kV1pChunk - 1) / kV1pChunk);
         hipLaunchKernelGGL(k_v1x_part, gp, dim3(kV1pNT), 0, s, g, bp);
         V1xBig bs = b;
-        bs.xb = nbk;
-        dim3 gs = grid(bs, bs.xb);
-        bs.xcd = gs.y == 1 ? 1u : 0u;
+        const dim3 gs = grid(bs, nbk);
         hipLaunchKernelGGL(k_v1x_solve, gs, dim3(kV1sNT), 0, s, g, bs);
         V1xBig bo = b;
-        bo.xb = (B + 255) / 256;
-        dim3 go = grid(bo, bo.xb);
-        bo.xcd = go.y == 1 ? 1u : 0u;
+        const dim3 go = grid(bo, (B + 255) / 256);
         hipLaunchKernelGGL(k_v1x_out, go, dim3(256), 0, s, g, bo, ranks, rank_lo, pos_lo, count, out, ma);
         e = hipGetLastError();
         if (e != hipSuccess) return e;

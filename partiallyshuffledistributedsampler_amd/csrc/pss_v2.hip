@@ -848,10 +848,12 @@ __global__ __launch_bounds__(256) void k_v2_tail_f(Geometry g, V2Plan pl,
                                                   const RankDesc *__restrict__ ranks,
                                                   int32_t rank_lo, const uint32_t *__restrict__ VAL,
                                                   int64_t pos_lo, int64_t count,
-                                                  int64_t *__restrict__ out, MapArgs ma) {
+                                                  int64_t *__restrict__ out, MapArgs ma,
+                                                  RankArgs ra, int use_ra) {
     const int32_t rl = (int32_t)blockIdx.y;
     const uint32_t rank = (uint32_t)(rank_lo + rl);
-    const RankDesc rd = ranks[rank];
+    // ranks by value (the whole-stream calls that touch no shared device table) or the table
+    const RankDesc rd = use_ra ? ra.r[rl] : ranks[rank];
     const uint32_t P1 = (uint32_t)pl.P1;
     uint32_t tk[kRoundKeyWords];
     tail_round_keys(g, rank, tk);
@@ -961,11 +963,14 @@ size_t v2_sort_bytes(const Geometry &, int32_t) {
 
 hipError_t launch_v2_tail_vals(const Geometry &g, const V2Plan &pl, const RankDesc *ranks,
                                int32_t rank_lo, int32_t nr, const uint32_t *VAL, int64_t pos_lo,
-                               int64_t count, int64_t *out, hipStream_t s, const MapArgs *mapped) {
+                               int64_t count, int64_t *out, hipStream_t s, const MapArgs *mapped,
+                               const RankArgs *rank_args) {
     const dim3 grid((uint32_t)cdiv(pl.P1 < 65536 ? pl.P1 : 65536, 256), (uint32_t)nr);
     const MapArgs ma = mapped ? *mapped : MapArgs{};
+    RankArgs ra;
+    if (rank_args) ra = *rank_args;
     hipLaunchKernelGGL(k_v2_tail_f, grid, dim3(256), 0, s, g, pl, ranks, rank_lo, VAL, pos_lo,
-                       count, out, ma);
+                       count, out, ma, ra, rank_args ? 1 : 0);
     return hipGetLastError();
 }
 
@@ -1070,14 +1075,11 @@ hipError_t launch_v2(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, 
     }
     if (!do_emit) return hipGetLastError();
     if (need_tail && !tail_fused) {
-        // the tail kernel reads the device rank table: this launch's ranks first, when they came
-        // by value (the runtime uploads the whole table later, on first other use)
-        if (rank_args) {
-            hipError_t e = launch_put_ranks(rank_args->r, nr, const_cast<RankDesc *>(ranks) + rank_lo, s);
-            if (e != hipSuccess) return e;
-        }
+        // ranks that came by value go to the tail kernel by value too: a whole-stream call
+        // touches no shared device table (the runtime skips its cross-stream ordering for it)
         mk(K_V2_TAIL, s);
-        hipError_t e = launch_v2_tail_vals(g, pl, ranks, rank_lo, nr, VAL, pos_lo, count, out, s, mapped);
+        hipError_t e = launch_v2_tail_vals(g, pl, ranks, rank_lo, nr, VAL, pos_lo, count, out, s, mapped,
+                                           rank_args);
         if (e != hipSuccess) return e;
     }
     mk(-1, s);

@@ -235,6 +235,9 @@ class _PartialShuffleSampler(Sampler):
                 "sampler_version": self._VERSION, "num_replicas": self.num_replicas,
                 "rank": self.rank, "shuffle_buffer": self.shuffle_buffer,
                 "total_size": self.ori_total_size, "order": self.order, "seed": int(self.seed),
+                # V2 always shuffles (its shuffle flag is ignored, V2:142-152)
+                "shuffle": bool(self.shuffle) if self._VERSION == 1 else True,
+                "num_files": len(self.files),
                 "schedule_version": _lib.load().pss_schedule_version()}
 
     def load_state_dict(self, sd):
@@ -244,7 +247,10 @@ class _PartialShuffleSampler(Sampler):
         another configuration, or of another counter schedule (pss_schedule_version), raises
         ValueError: its positions would index a different permutation."""
         mine = self.state_dict()
-        for k in ("sampler_version", "num_replicas", "rank", "shuffle_buffer", "total_size", "order"):
+        for k in ("sampler_version", "num_replicas", "rank", "shuffle_buffer", "total_size", "order",
+                  "shuffle", "num_files"):
+            if k not in sd:
+                raise ValueError("state_dict has no %r: it was taken by another build" % k)
             if sd[k] != mine[k]:
                 raise ValueError("state_dict was taken with %s=%r, this sampler has %r"
                                  % (k, sd[k], mine[k]))

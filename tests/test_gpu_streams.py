@@ -32,12 +32,15 @@ def _one_stream(eng, R, mapped=False):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("version,order,B", [(1, "counter", 4096), (2, "counter", 4096), (2, "counter", 1 << 17),
-                                             (1, "exact", 4096), (2, "exact", 4096)],
-                         ids=lambda x: str(x))
-def test_epochs_on_two_streams_equal_one_stream(version, order, B):
-    F = 300 if order == "exact" else 2000
-    lens, N = _shape(F, 10_000)
+@pytest.mark.parametrize("version,order,B,F,L", [
+    (1, "counter", 4096, 2000, 10_000), (2, "counter", 4096, 2000, 10_000),
+    (2, "counter", 1 << 17, 2000, 10_000), (1, "exact", 4096, 300, 10_000), (2, "exact", 4096, 300, 10_000),
+    # ns <= B: the whole stream is one pool (no tile, the unfused tail kernel) -- its ranks
+    # must come by value, not through the handle's table
+    (2, "counter", 4096, 30, 1000), (2, "counter", 1 << 17, 100, 10_000)],
+    ids=lambda x: str(x))
+def test_epochs_on_two_streams_equal_one_stream(version, order, B, F, L):
+    lens, N = _shape(F, L)
     R = 8
     ref = _one_stream(IndexEngine(lens, N, R, B, version, device=0, order=order, seed=11), R)
     eng = IndexEngine(lens, N, R, B, version, device=0, order=order, seed=11)

@@ -5,6 +5,8 @@ tests/knob_worker.py in a child interpreter with the variable set before any GPU
 
   PSS_V1X_DRAWS_WG / PSS_V2X_DRAWS_WG  0 / 1 force the one-wave / workgroup MT draws of the
                                        exact orders (by default chosen by geometry)
+  PSS_V1X_GRID2D=1                     the exact V1 HBM path's kernels on their 2-D grids (window
+                                       slot in blockIdx.y) instead of the XCD-major flat grids
   PSS_V2_LOOKAHEAD=0                   no epoch lookahead: the V2 last-occurrence passes run in
                                        line on the caller's stream
   PSS_CPU_THREADS=1 / 3                host threads of the CPU mode
@@ -24,6 +26,7 @@ CSRC = os.path.join(ROOT, "partiallyshuffledistributedsampler_amd", "csrc")
 GPU_CASES = [
     ("exact", {"PSS_V1X_DRAWS_WG": "0", "PSS_V2X_DRAWS_WG": "0"}),
     ("exact", {"PSS_V1X_DRAWS_WG": "1", "PSS_V2X_DRAWS_WG": "1"}),
+    ("exact", {"PSS_V1X_GRID2D": "1"}),
     ("counter", {"PSS_V2_LOOKAHEAD": "0"}),
 ]
 CPU_CASES = [("cpu", {"PSS_CPU_THREADS": "1"}), ("cpu", {"PSS_CPU_THREADS": "3"})]

@@ -353,3 +353,13 @@ def test_state_dict_resume_continues_the_same_stream(device, order):
                 c.load_state_dict(bad)
             with pytest.raises(ValueError):
                 c.load_state_dict(dict(sd, seed=sd["seed"] + 1))
+        c = mod.DistributedSamplerViaLocallyShuffle(Dataset(files), reader_for(lengths), **kw)
+        with pytest.raises(ValueError):    # another file count
+            c.load_state_dict(dict(sd, num_files=sd["num_files"] + 1))
+        if mod is V1mod:                   # V1 with shuffle=False is another permutation
+            with pytest.raises(ValueError):
+                c.load_state_dict(dict(sd, shuffle=False))
+            c = mod.DistributedSamplerViaLocallyShuffle(Dataset(files), reader_for(lengths),
+                                                        **dict(kw, shuffle=False))
+            with pytest.raises(ValueError):
+                c.load_state_dict(sd)
