@@ -136,6 +136,9 @@ def cpu_baseline():
     off = _reference_processes("c2", 2, nproc, 64, 1024, False)
     out = {"value": on["idx_per_s"] / 1e9, "unit": "G idx/s", "cores": nproc,
            "kind": "port",
+           "port_of": "the reference's Python __next__ loop restated line for line in Python "
+                      "(oracle/pyref.py, pinned to the reference's recorded streams), run by the "
+                      "CPython interpreter -- not a compiled port",
            "sample": "reference V2 __next__ loop (oracle/pyref.py: get_index + map + gather + "
                      "per-batch gc.collect, V2:96-116,170-254) at C2, %d processes = logical "
                      "ranks 0..%d, 64 batches x 1024 ids each, all concurrent; extrapolated "
@@ -266,6 +269,20 @@ def latency_dropin(device, reps=5):
             if e:
                 times.append((t1 - t0) * 1e3)
         res[key] = float(np.median(times))
+        if not kw:
+            # cold: a resume at an epoch the host prefetcher has not prepared (it computes the
+            # coming epochs' file permutations, V2:143-144, on worker threads): the O(F) CPython-MT
+            # shuffle of 100K files runs inside set_epoch -> first batch
+            cold = []
+            for e in (57, 113, 171, 229, 287):
+                torch.cuda.synchronize(device)
+                t0 = time.perf_counter()
+                s.set_epoch(e)
+                b = next(iter(s))
+                cold.append((time.perf_counter() - t0) * 1e3)
+                assert sum(len(d["x"]) for d in b[0]) == 1024
+            res["cold_set_epoch_to_first_batch_ms"] = float(np.median(cold))
+            res["cold_epochs"] = "57, 113, 171, 229, 287 after 0..%d (prefetcher misses), median" % reps
     # engine only: init_iter + generate + map + D2H of the first batch
     eng = IndexEngine(lengths, N, R, B, 2, seed=0, device=device)
     ns = eng.num_samples
@@ -396,6 +413,33 @@ def exact_order_figures(device):
 
 
 # ---- main ------------------------------------------------------------------------------------
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def launch_ranks(n):
+    """`python bench.py --gpus N` outside a launcher: start one process per GPU through
+    torch.distributed.run (127.0.0.1 rendezvous) as a CHILD of this process, which has not
+    touched the GPU (no HIP call before this point; torch.cuda.device_count does not
+    initialise it), relay rank 0's output and exit with the launcher's code.  The reference's
+    only multi-rank harness loops its ranks in one process (V1:344-355); here every logical-rank
+    shard is its own process on its own GPU."""
+    import subprocess
+    if os.environ.get("PSS_BENCH_SAME_GPU") != "1" and torch.cuda.device_count() < n:
+        sys.stderr.write("bench.py: --gpus %d but only %d GPU(s) visible\n" % (n, torch.cuda.device_count()))
+        return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "1")
+    return subprocess.call(cmd, env=env)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -413,7 +457,12 @@ def main():
                     help="HIP-event timing of the generation kernel on every n-th timed step")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        sys.stderr.write("bench.py: --gpus %d but WORLD_SIZE=%d\n" % (args.gpus, world))
+        sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # rehearsal of the multi-process path on a one-GPU box: every rank on cuda:0, gloo for the
@@ -476,11 +525,16 @@ def main():
         step(args.warmup + i)
     torch.cuda.synchronize(dev)
     dt = time.perf_counter() - t0
+    rank_ms = [dt / args.steps * 1e3]
+    pg_world = 1
     if distributed:
         dist.barrier()
+        pg_world = dist.get_world_size()
         t = torch.tensor([dt], dtype=torch.float64, device=cdev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
+        ts = [torch.zeros_like(t) for _ in range(pg_world)]
+        dist.all_gather(ts, t)
+        rank_ms = [float(x.item()) / args.steps * 1e3 for x in ts]
+        dt = max(float(x.item()) for x in ts)          # the slowest rank's time
     prof = eng.profile_read()
     eng.profile(False)
     eng.check()
@@ -561,6 +615,8 @@ def main():
         "timed_launches": k_n,
         "coverage_ok": coverage,
         "collective": (dist.get_backend() if distributed else None),
+        "process_group_world_size": pg_world,
+        "ms_per_step_by_rank": rank_ms,
     }
     eng.close()
     del out, outs

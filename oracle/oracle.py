@@ -10,7 +10,9 @@ Contents:
     block shuffle (V1:118-121), V2's reset-then-shuffle blocks and old/new start (V2:135-148);
   * `ref_batches`: restatement of the reference __next__ mapping/grouping semantics
     (V1:178-259, V2:181-254) on top of an id stream: lazy exclusive scan, reflection,
-    grouping by first appearance, the `tmp_count == 1` StopIteration quirk.
+    grouping by first appearance, the `tmp_count == 1` StopIteration quirk;
+  * `rank_id_ranges` / `partition_segments`: a rank's id ranges (V1:158-163, V2:110-114,135-138)
+    cut at the shuffled files' exclusive prefix sums (V1:181-214) -- the checker of pss_partition.
 """
 import ctypes
 import os
@@ -248,6 +250,52 @@ def map_ids(prefix, ids):
     off = np.empty(len(ids), dtype=np.int64)
     lib().orc_map(_p64(prefix), len(prefix) - 1, _p64(ids), len(ids), _p32(fpos), _p64(off))
     return fpos, off
+
+
+def rank_id_ranges(version, old_start, new_start, ns, B, N, T=None):
+    """The id ranges a rank's epoch draws from, in stream order: V1 its block [new, new + ns)
+    (V1:158-163); V2 the first two pools from the previous start [old, old + min(2B, ns))
+    (V2:135-138) and the later windows of the new one [new + min(2B, ns), new + ns)
+    (V2:110-112).  Each range wraps at N (V1:161-163, V2:113-114) and is clipped to the scanned
+    total T (ids past it are reflected by the map, V1:191-196, and own no file segment)."""
+    T = N if T is None else T
+    if version == 1:
+        parts = [(int(new_start), ns)]
+    else:
+        a = min(2 * B, ns)
+        parts = [(int(old_start), a)] + ([(int(new_start) + a, ns - a)] if ns > a else [])
+    out = []
+    for lo, ln in parts:
+        lo %= N
+        while ln > 0:
+            take = min(N - lo, ln)
+            hi = min(lo + take, T)
+            if lo < hi:
+                out.append((lo, hi))
+            ln -= take
+            lo = 0
+    return out
+
+
+def partition_segments(version, prefix, old_start, new_start, ns, B, N):
+    """(file position, lo, hi) segments of the shuffled files a rank's epoch reads, in stream
+    order of its id ranges (rank_id_ranges): each range cut at the exclusive prefix sums of the
+    shuffled file order (V1:181-190's past_files_samples, here complete); empty files own no
+    segment.  Offsets are within the file, as V1:210-214's `i - past_files_samples[...]`."""
+    prefix = np.asarray(prefix, dtype=np.int64)
+    F = len(prefix) - 1
+    sf, sl, sh = [], [], []
+    for a, b in rank_id_ranges(version, old_start, new_start, ns, B, N, int(prefix[-1])):
+        f0 = int(np.searchsorted(prefix, a, side="right")) - 1
+        f1 = min(int(np.searchsorted(prefix, b - 1, side="right")) - 1, F - 1)
+        fs = np.arange(f0, f1 + 1)
+        fs = fs[prefix[fs + 1] > prefix[fs]]
+        sf.append(fs.astype(np.int32))
+        sl.append(np.maximum(a, prefix[fs]) - prefix[fs])
+        sh.append(np.minimum(b, prefix[fs + 1]) - prefix[fs])
+    if not sf:
+        return np.zeros(0, np.int32), np.zeros(0, np.int64), np.zeros(0, np.int64)
+    return np.concatenate(sf), np.concatenate(sl), np.concatenate(sh)
 
 
 def digest(ids):

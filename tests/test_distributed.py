@@ -116,3 +116,40 @@ def test_rccl_group_of_one_gpu_runs_the_multi_gpu_bench_path():
     assert line["collective"] == "nccl"
     assert line["coverage_ok"] is True
     assert line["n_gpus"] == 1
+
+
+def _bench(args, env_extra, timeout):
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env.update(env_extra)
+    return subprocess.run([sys.executable, "bench.py"] + args, cwd=root, env=env,
+                          capture_output=True, text=True, timeout=timeout)
+
+
+def test_bench_refuses_a_world_that_is_not_gpus():
+    """bench.py exits non-zero, before any GPU call, when --gpus disagrees with the launcher's
+    WORLD_SIZE, or when --gpus N asks for more GPUs than are visible."""
+    r = _bench(["--gpus", "2"], {"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"}, 120)
+    assert r.returncode == 2 and "WORLD_SIZE=1" in r.stderr
+    r = _bench(["--gpus", "64"], {}, 120)
+    assert r.returncode == 2 and "GPU(s) visible" in r.stderr
+
+
+@pytest.mark.gpu
+def test_bench_gpus_2_launches_its_own_ranks():
+    """`python bench.py --gpus 2` with no launcher starts its two ranks itself
+    (torch.distributed.run as a child); on a one-GPU box both run on cuda:0
+    (PSS_BENCH_SAME_GPU=1, gloo for the (count, digest) exchange).  The line reports the world
+    the process group saw, each rank's ms per step and exact coverage over both shards."""
+    import json
+    r = _bench(["--gpus", "2", "--steps", "3", "--warmup", "1", "--no-latency", "--no-exact",
+                "--no-cpu-baseline"], {"PSS_BENCH_SAME_GPU": "1"}, 300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["n_gpus"] == 2 and line["process_group_world_size"] == 2
+    assert len(line["ms_per_step_by_rank"]) == 2
+    assert line["coverage_ok"] is True
+    assert line["config"]["logical_ranks"] == 16

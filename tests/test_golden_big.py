@@ -117,3 +117,50 @@ def test_cpu_mode_counter_order_has_reference_multiset(name):
     for r, er in _walk(fx, eng):
         check_multiset(eng.generate(r, r + 1).numpy()[0], er, "%s r%d e%d" % (name, r, er["epoch"]))
     eng.close()
+
+
+def test_partition_oracle_reads_what_the_reference_streams_read():
+    """oracle.partition_segments (the checker of pss_partition) against the reference itself:
+    for every rank-epoch of the Zipf fixtures (whole reference streams, both versions), the
+    segments' per-file lengths == the per-file counts of the reference stream mapped through the
+    reference's own file order (RefHistory, pinned above) and V1:181-221's map."""
+    for name in ("zipf_v1", "zipf_v2"):
+        fx = load_big(name)
+        lens = big_lengths(fx)
+        N, R, B = int(lens.sum()), fx["R"], fx["B"]
+        ns = O.num_samples(N, R)
+        full = load_big_streams(name)
+        for rr in fx["ranks"]:
+            h = O.RefHistory(fx["version"], len(lens), R, rr["rank"], N)
+            for er in rr["epochs"]:
+                h.init_iter(er["epoch"])
+                prefix = np.concatenate([[0], np.cumsum(lens[h.order])]).astype(np.int64)
+                f, _ = O.map_ids(prefix, full["r%d_e%d" % (rr["rank"], er["epoch"])])
+                sf, sl, sh = O.partition_segments(fx["version"], prefix, h.old_start, h.start, ns, B, N)
+                seg = np.zeros(len(lens), dtype=np.int64)
+                np.add.at(seg, sf, sh - sl)
+                assert np.array_equal(np.bincount(f, minlength=len(lens)), seg), (name, rr["rank"])
+
+
+@pytest.mark.parametrize("version", [2, 1])
+def test_cpu_mode_partition_at_c4_matches_oracle(version):
+    """pss_partition (CPU mode) of all 4096 ranks at C4 (Zipf, N > 2^31) == the oracle's
+    segments, over the reference-pinned file order (assign_c4)."""
+    import workloads as W
+    lengths, N, R, B, _ = W.shape("c4")
+    fx = load_big("assign_c4")
+    eng = pss.IndexEngine(lengths, N, R, B, version, device="cpu")
+    ns = eng.num_samples
+    rec = fx["versions"]["v%d" % version][1]
+    eng.init_iter(0)
+    eng.init_iter(rec["epoch"])
+    order = eng.file_order()
+    assert sha256_i64(order.astype(np.int64)) == rec["order_sha256"]
+    prefix = np.concatenate([[0], np.cumsum(lengths[order])]).astype(np.int64)
+    old, new = eng.rank_starts()
+    seg_off, sf, sl, sh = eng.partition(0, R)
+    for r in range(R):
+        a, b = int(seg_off[r]), int(seg_off[r + 1])
+        wf, wl, wh = O.partition_segments(version, prefix, int(old[r]), int(new[r]), ns, B, N)
+        assert np.array_equal(sf[a:b], wf) and np.array_equal(sl[a:b], wl) and np.array_equal(sh[a:b], wh), r
+    eng.close()

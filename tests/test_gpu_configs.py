@@ -158,6 +158,36 @@ def test_c5_big_pool_consecutive_epochs():
     eng.close()
 
 
+def test_c5_hundred_consecutive_epochs_cover_exactly():
+    """BASELINE configs[4] as stated: B = 2^20 pools with the per-epoch set_epoch reseed over 100
+    epochs.  Epochs 0..99 run back to back through the lookahead ring (each epoch's key table /
+    pre-pass queued on the side stream during the previous replay); every epoch's (count,
+    digest) over all 8 ranks equals [0, N)'s, and two epochs' rank streams equal the twin."""
+    lengths, N, R, B, ver = W.shape("c5")
+    eng = _engine(lengths, N, R, B, ver, seed=0)
+    ns = eng.num_samples
+    want = O.digest_range(0, N) & 0xFFFFFFFFFFFFFFFF       # N = ns * R: no pad
+    out = torch.empty((R, ns), dtype=torch.int64, device="cuda")
+    accs = torch.zeros(100, dtype=torch.int64, device="cuda")
+    twin_at = {37: None, 99: None}
+    for epoch in range(100):
+        eng.init_iter(epoch)
+        if epoch in twin_at:
+            twin_at[epoch] = eng.rank_starts()
+        eng.generate(0, R, out=out)
+        pss.digest(out.view(-1), accs[epoch:epoch + 1])
+        if epoch in twin_at:
+            twin_at[epoch] = (twin_at[epoch], out[epoch % R].cpu().numpy())
+    eng.check()
+    got = [int(x) & 0xFFFFFFFFFFFFFFFF for x in accs.cpu().tolist()]
+    bad = [e for e in range(100) if got[e] != want]
+    assert not bad, "epochs whose digest differs: %s" % bad
+    for epoch, ((old, new), row) in twin_at.items():
+        key = O.epoch_key(0, epoch)
+        assert np.array_equal(row, _twin(ver, key, epoch % R, old, new, ns, B, N)), epoch
+    eng.close()
+
+
 def test_c5_fused_mapping_equals_generate_then_map():
     """pss_generate_mapped at C5 (B = 2^20, the grouped replay maps each id in-kernel): equal to
     generate + pss_map over all 8 ranks, for two consecutive epochs (the second replay takes the

@@ -63,10 +63,11 @@ def test_gpu_counter_order_has_reference_multiset(name):
     eng.close()
 
 
-@pytest.mark.parametrize("name", ["c1_v1", "c1_v2", "zipf_v2", "v2_b65536_r0_e5"])
+@pytest.mark.parametrize("name", ["c1_v1", "c1_v2", "zipf_v2", "v2_b65536_r0_e5", "v1_c5_r0"])
 def test_gpu_exact_order_mapped_hand_off(name):
     """(file, offset) of the exact streams: pss_generate_mapped == pss_generate + pss_map, for
-    all recorded ranks at once and for a ragged position range."""
+    all recorded ranks at once and for a ragged position range.  v1_c5_r0: V1 windows of 2^20
+    entries, beyond LDS -- the HBM path's k_v1x_out maps each id where it writes it."""
     fx = load_big(name)
     eng = _engine(fx, "exact")
     for r, er in _walk(fx, eng):

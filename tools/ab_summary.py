@@ -1,4 +1,4 @@
-"""Summarise an A/B directory (tools/gpu_ab_lib.sh, gpu_ab_env.sh, gpu_ab_exact.sh): per tag,
+"""Summarise an A/B directory (tools/gpu_run.sh ab:/env: steps): per tag,
 G idx/s and the dominant kernel's launch time (bench.py lines) or ms per epoch
 (tools/bench_configs.py lines), one column per run."""
 import glob

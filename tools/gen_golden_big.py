@@ -26,8 +26,12 @@ Fixtures (tests/golden/big/):
   v2_c5_prefix_r*   C5 (V2, B = 2^20): the first 20480 draws of a rank
   assign_c3, assign_c4   file order / blocks / start_num history over init_iter(0,1,1,9) at
                          C3 (100K files, R=1024) and C4 (Zipf, R=4096), V1 and V2
+  v2_c2_r*, v2_c3_r*, v2_c4_r*   whole V2 rank streams at the true BASELINE shapes (B = 4096):
+                         C2 ranks 0 and 7 (12.5M ids each, epoch 0); C3 rank 0 and the ranks
+                         whose block wraps at N, epochs 0 and 1; C4 rank 0, the wrapping rank
+                         and two ranks with every id above 2^31, epoch 0
 
-Usage:  python tools/gen_golden_big.py [job ...]   (default: every job, 6 processes)
+Usage:  python tools/gen_golden_big.py [job ... | bench_shapes]   (default: every job, 6 processes)
 """
 import hashlib
 import importlib.util
@@ -270,6 +274,46 @@ def job_assign(cfg):
     write("assign_%s" % cfg, out)
 
 
+def _v2_blocks(cfg, epochs):
+    """blocks of each epoch as the reference's V2 sets them (V2:142-148), from rank 0's sampler."""
+    import workloads as W
+    lens, N, R, B, _ = W.shape(cfg)
+    s = sampler(2, lens, R, 0, B, 1)
+    out = {}
+    for e in epochs:
+        s.set_epoch(e)
+        iter(s)
+        out[e] = list(s.blocks)
+    return out, N, R, B
+
+
+def bench_shape_ranks(cfg):
+    """(ranks, epochs) recorded at a true BASELINE shape: rank 0 plus
+    the ranks whose block wraps at N (block R-1; C3 has pad 512) and, at C4, two ranks whose
+    ids all lie above 2^31 (old start ns*rank and new start ns*block both past 2^31)."""
+    if cfg == "c2":
+        return [0, 7], [0]
+    epochs = [0, 1] if cfg == "c3" else [0]
+    blocks, N, R, B = _v2_blocks(cfg, epochs)
+    ranks = {0} | {blocks[e].index(R - 1) for e in epochs}
+    if cfg == "c4":
+        ns = -(-N // R)
+        hi = [r for r in range(R) if r * ns > 2 ** 31 and blocks[0][r] * ns > 2 ** 31]
+        ranks |= {hi[0], hi[len(hi) // 2]}
+    return sorted(ranks), epochs
+
+
+def job_bench_shape(cfg, rank):
+    """Whole V2 rank streams at the true C2 / C3 / C4 shape (B = 4096), straight from the
+    reference's get_index (V2:96-116) over the init_iter history of `epochs`."""
+    import workloads as W
+    lens, N, R, B, _ = W.shape(cfg)
+    _, epochs = bench_shape_ranks(cfg)
+    recs, _ = run_stream(2, lens, R, B, 1024, [rank], epochs)
+    write("v2_%s_r%d" % (cfg, rank), {"kind": "stream", "version": 2, "R": R, "B": B, "bs": 1024,
+                                      "config": cfg, **lens_rec(lens), "ranks": recs})
+
+
 JOBS = {
     "c1_v1": (job_c1, 1), "c1_v2": (job_c1, 2),
     "zipf_v1": (job_zipf, 1), "zipf_v2": (job_zipf, 2),
@@ -281,17 +325,27 @@ JOBS = {
 }
 
 
+def bench_shape_jobs():
+    jobs = {}
+    for cfg in ("c2", "c3", "c4"):
+        for r in bench_shape_ranks(cfg)[0]:
+            jobs["v2_%s_r%d" % (cfg, r)] = (job_bench_shape, cfg, r)
+    return jobs
+
+
 def run_job(name):
     t = time.time()
-    fn, *args = JOBS[name]
+    fn, *args = JOBS[name] if name in JOBS else bench_shape_jobs()[name]
     fn(*args)
     return name, time.time() - t
 
 
 def main(argv):
-    todo = argv or list(JOBS)
+    if argv == ["bench_shapes"]:
+        argv = sorted(bench_shape_jobs())
+    todo = argv or list(JOBS) + sorted(bench_shape_jobs())
     # the longest jobs first
-    order = sorted(todo, key=lambda n: ("c5_prefix" not in n, "b65536" not in n, n))
+    order = sorted(todo, key=lambda n: ("_c2_" not in n, "c5_prefix" not in n, "b65536" not in n, n))
     with ProcessPoolExecutor(6) as ex:
         for name, dt in ex.map(run_job, order):
             print("wrote %-18s %7.1f s" % (name, dt), flush=True)
