@@ -35,9 +35,10 @@ for s in "$@"; do
     xstats) run 300 xstats_$a.log rocprofv3 --kernel-trace --stats --output-format csv -d $O/xstats_$a -o run -- python3 tools/bench_configs.py $a ;;
     pmc) run 600 pmc_$a.log bash tools/pmc_kernel.sh $a ${O#gpurun_out/}/pmc_$a ;;
     gpus2) run 300 gpus2.json env PSS_BENCH_SAME_GPU=1 python bench.py --gpus 2 --steps 10 --warmup 2 --no-latency --no-exact ;;
-    ab) for i in 1 2 3; do
-          run 240 ab_cur_${b}_$i.json python bench.py --steps 100 --workload $b $BN
-          run 240 ab_alt_${b}_$i.json env PSS_LIB=$a python bench.py --steps 100 --workload $b $BN
+    ab) t=$(basename $(dirname $a))
+        for i in 1 2 3; do
+          run 240 ab_${t}_cur_${b}_$i.json python bench.py --steps 100 --workload $b $BN
+          run 240 ab_${t}_alt_${b}_$i.json env PSS_LIB=$a python bench.py --steps 100 --workload $b $BN
         done ;;
     env) for i in 1 2 3; do
            run 240 env_cur_${b}_$i.json python bench.py --steps 100 --workload $b $BN

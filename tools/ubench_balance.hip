@@ -1,0 +1,170 @@
+// ubench_balance.hip -- is the persistent-kernel write gap (own runs ~5.3 TB/s against one-shot
+// ~6.3 TB/s for the same 800 MB) a per-XCD imbalance that dynamic work claiming removes?
+//   oneshot4      fill-like reference: 256-thread blocks, 4 int64 per thread, one pass
+//   persist_r     2048 one-wave blocks, each its own contiguous run (the replay's layout)
+//   queue_<C>     2048 one-wave blocks claiming chunks of C x 2 KB from one agent-scope counter
+//                 (vector atomic from lane 0, readfirstlane of the result) until none is left
+//   guided        2048 one-wave blocks: chunk = max(2 KB, remaining / (2 x 2048)) (guided
+//                 self-scheduling: big chunks first, small ones at the end)
+// Each variant also reports the bytes every XCC wrote (per-wave XCC_ID) and the spread of wave
+// end times (s_memrealtime, 100 MHz).
+// Build: hipcc --offload-arch=gfx950 -O3 -o build/ubench_balance tools/ubench_balance.hip
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdint>
+#include <vector>
+#include <algorithm>
+
+constexpr uint64_t kIds = 100000000ull;
+constexpr int kWaves = 2048;
+
+struct Stats { unsigned long long xcc_bytes[8]; unsigned long long end[kWaves]; unsigned long long t0; };
+
+__device__ __forceinline__ uint32_t xcc_id() { return __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (15 << 11)) & 7u; }
+
+__global__ __launch_bounds__(256) void oneshot4(int64_t *o, uint64_t n, int64_t salt) {
+    const uint64_t i = ((uint64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+    if (i + 3 < n) {
+        longlong2 a, b;
+        a.x = (int64_t)i + salt; a.y = (int64_t)i + 1 + salt;
+        b.x = (int64_t)i + 2 + salt; b.y = (int64_t)i + 3 + salt;
+        *(longlong2 *)(o + i) = a;
+        *(longlong2 *)(o + i + 2) = b;
+    }
+}
+
+__device__ __forceinline__ void fill_chunk(int64_t *o, uint64_t c0, uint64_t c1, int64_t salt) {
+    for (uint64_t c = c0; c < c1; c++) {
+        int64_t *p = o + c * 256;
+#pragma unroll
+        for (int j = 0; j < 4; j++) p[64 * j + threadIdx.x] = (int64_t)(c * 256 + 64 * j + threadIdx.x) + salt;
+    }
+}
+
+__device__ __forceinline__ void record(Stats *st, uint64_t chunks_done) {
+    if (threadIdx.x == 0) {
+        atomicAdd(&st->xcc_bytes[xcc_id()], (unsigned long long)chunks_done * 2048ull);
+        st->end[blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+    }
+}
+
+__global__ __launch_bounds__(64) void persist_r(int64_t *o, uint64_t n, int64_t salt, Stats *st) {
+    extern __shared__ uint32_t pad[];
+    if (n == 0) pad[threadIdx.x] = 0;
+    const uint64_t chunks = n / 256, per = chunks / gridDim.x;
+    fill_chunk(o, blockIdx.x * per, blockIdx.x * per + per, salt);
+    record(st, per);
+}
+
+// claim `k` chunks; returns the first (>= total: nothing left)
+__device__ __forceinline__ uint64_t claim(unsigned long long *ctr, uint64_t k) {
+    unsigned long long got = 0;
+    if (threadIdx.x == 0) got = atomicAdd(ctr, (unsigned long long)k);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)got);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(got >> 32));
+    return ((uint64_t)hi << 32) | lo;
+}
+
+template <int C>
+__global__ __launch_bounds__(64) void queue(int64_t *o, uint64_t n, int64_t salt, Stats *st,
+                                            unsigned long long *ctr) {
+    extern __shared__ uint32_t pad[];
+    if (n == 0) pad[threadIdx.x] = 0;
+    const uint64_t chunks = n / 256;
+    uint64_t done = 0;
+    for (;;) {
+        const uint64_t c0 = claim(ctr, C);
+        if (c0 >= chunks) break;
+        const uint64_t c1 = c0 + C < chunks ? c0 + C : chunks;
+        fill_chunk(o, c0, c1, salt);
+        done += c1 - c0;
+    }
+    record(st, done);
+}
+
+__global__ __launch_bounds__(64) void guided(int64_t *o, uint64_t n, int64_t salt, Stats *st,
+                                             unsigned long long *ctr) {
+    extern __shared__ uint32_t pad[];
+    if (n == 0) pad[threadIdx.x] = 0;
+    const uint64_t chunks = n / 256;
+    uint64_t done = 0;
+    for (;;) {
+        // guess of what is left from a plain read (racy but only a size hint), then claim
+        unsigned long long seen = 0;
+        if (threadIdx.x == 0) seen = __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint64_t s = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(seen >> 32)) << 32) |
+                           __builtin_amdgcn_readfirstlane((uint32_t)seen);
+        const uint64_t left = s < chunks ? chunks - s : 0;
+        uint64_t k = left / (2 * kWaves);
+        if (k < 1) k = 1;
+        const uint64_t c0 = claim(ctr, k);
+        if (c0 >= chunks) break;
+        const uint64_t c1 = c0 + k < chunks ? c0 + k : chunks;
+        fill_chunk(o, c0, c1, salt);
+        done += c1 - c0;
+    }
+    record(st, done);
+}
+
+__global__ void stamp_t0(Stats *st) { if (threadIdx.x == 0) st->t0 = __builtin_amdgcn_s_memrealtime(); }
+
+template <class F>
+void timeit(const char *name, Stats *st, unsigned long long *ctr, F launch) {
+    hipEvent_t a, b;
+    hipEventCreate(&a); hipEventCreate(&b);
+    hipMemset(ctr, 0, 8);
+    launch(1);
+    float best = 1e9, sum = 0;
+    Stats h{};
+    for (int r = 0; r < 10; r++) {
+        hipMemset(st, 0, sizeof(Stats));
+        hipMemset(ctr, 0, 8);
+        hipLaunchKernelGGL(stamp_t0, dim3(1), dim3(64), 0, 0, st);
+        hipEventRecord(a);
+        launch(2 + r);
+        hipEventRecord(b);
+        hipEventSynchronize(b);
+        float ms = 0;
+        hipEventElapsedTime(&ms, a, b);
+        sum += ms;
+        if (ms < best) { best = ms; hipMemcpy(&h, st, sizeof(Stats), hipMemcpyDeviceToHost); }
+    }
+    printf("%-12s mean %7.1f us best %7.1f us  %.2f TB/s (mean)", name, sum / 10 * 1e3, best * 1e3,
+           (double)kIds * 8 / (sum / 10 * 1e-3) / 1e12);
+    if (h.t0) {
+        std::vector<double> e;
+        for (int i = 0; i < kWaves; i++) if (h.end[i]) e.push_back((h.end[i] - h.t0) / 100.0);
+        std::sort(e.begin(), e.end());
+        if (!e.empty())
+            printf("  wave end us p10 %.1f p50 %.1f p90 %.1f max %.1f", e[e.size() / 10], e[e.size() / 2],
+                   e[e.size() * 9 / 10], e.back());
+        printf("\n   XCC MB:");
+        for (int x = 0; x < 8; x++) printf(" %6.1f", h.xcc_bytes[x] / 1e6);
+    }
+    printf("\n");
+}
+
+int main() {
+    int64_t *o;
+    Stats *st;
+    unsigned long long *ctr;
+    hipMalloc(&o, kIds * 8 + 4096);
+    hipMalloc(&st, sizeof(Stats));
+    hipMalloc(&ctr, 64);
+    const uint64_t n = kIds;
+    for (auto fn : {(const void *)persist_r, (const void *)queue<8>, (const void *)queue<32>, (const void *)queue<128>,
+                    (const void *)guided})
+        (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    const size_t lds = 18220;   // 8 one-wave blocks per CU, as the replay
+    for (int rep = 0; rep < 2; rep++) {
+        timeit("oneshot4", st, ctr, [&](int s) { hipLaunchKernelGGL(oneshot4, dim3((uint32_t)((n / 4 + 255) / 256)), dim3(256), 0, 0, o, n, (int64_t)s); });
+        timeit("persist_r", st, ctr, [&](int s) { hipLaunchKernelGGL(persist_r, dim3(kWaves), dim3(64), lds, 0, o, n, (int64_t)s, st); });
+        timeit("queue_16K", st, ctr, [&](int s) { hipLaunchKernelGGL(queue<8>, dim3(kWaves), dim3(64), lds, 0, o, n, (int64_t)s, st, ctr); });
+        timeit("queue_64K", st, ctr, [&](int s) { hipLaunchKernelGGL(queue<32>, dim3(kWaves), dim3(64), lds, 0, o, n, (int64_t)s, st, ctr); });
+        timeit("queue_256K", st, ctr, [&](int s) { hipLaunchKernelGGL(queue<128>, dim3(kWaves), dim3(64), lds, 0, o, n, (int64_t)s, st, ctr); });
+        timeit("guided", st, ctr, [&](int s) { hipLaunchKernelGGL(guided, dim3(kWaves), dim3(64), lds, 0, o, n, (int64_t)s, st, ctr); });
+    }
+    hipError_t e = hipDeviceSynchronize();
+    printf("status %s\n", hipGetErrorString(e));
+    return 0;
+}
