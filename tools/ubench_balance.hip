@@ -18,7 +18,7 @@
 constexpr uint64_t kIds = 100000000ull;
 constexpr int kWaves = 2048;
 
-struct Stats { unsigned long long xcc_bytes[8]; unsigned long long end[kWaves]; unsigned long long t0; };
+struct Stats { unsigned long long xcc_bytes[8]; unsigned long long end[kWaves]; unsigned long long t0; unsigned int xcc[kWaves]; };
 
 __device__ __forceinline__ uint32_t xcc_id() { return __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (15 << 11)) & 7u; }
 
@@ -44,7 +44,17 @@ __device__ __forceinline__ void fill_chunk(int64_t *o, uint64_t c0, uint64_t c1,
 __device__ __forceinline__ void record(Stats *st, uint64_t chunks_done) {
     if (threadIdx.x == 0) {
         atomicAdd(&st->xcc_bytes[xcc_id()], (unsigned long long)chunks_done * 2048ull);
-        st->end[blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+        const uint32_t w = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
+        st->end[w] = __builtin_amdgcn_s_memrealtime();
+        st->xcc[w] = xcc_id();
+    }
+}
+__device__ __forceinline__ void record_w(Stats *st, uint64_t chunks_done) {   // every wave of a block
+    if ((threadIdx.x & 63) == 0) {
+        atomicAdd(&st->xcc_bytes[xcc_id()], (unsigned long long)chunks_done * 2048ull);
+        const uint32_t w = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
+        st->end[w] = __builtin_amdgcn_s_memrealtime();
+        st->xcc[w] = xcc_id();
     }
 }
 
@@ -106,6 +116,40 @@ __global__ __launch_bounds__(64) void guided(int64_t *o, uint64_t n, int64_t sal
     record(st, done);
 }
 
+// NW waves per block, each its own contiguous run; the block's waves re-align every K chunks
+// (s_barrier), so no wave of a CU runs ahead of its partners
+template <int NW, int K>
+__global__ __launch_bounds__(64 * NW) void persist_bar(int64_t *o, uint64_t n, int64_t salt, Stats *st) {
+    const uint64_t chunks = n / 256, nwaves = (uint64_t)gridDim.x * NW, per = chunks / nwaves;
+    const uint64_t w = (uint64_t)blockIdx.x * NW + threadIdx.x / 64;
+    const int lane = threadIdx.x & 63;
+    int64_t *p = o + w * per * 256;
+    for (uint64_t c = 0; c < per; c++) {
+#pragma unroll
+        for (int j = 0; j < 4; j++) p[c * 256 + 64 * j + lane] = (int64_t)(c * 256 + 64 * j + lane) + salt;
+        if (K && (c % K) == K - 1) __syncthreads();
+    }
+    record_w(st, per);
+}
+
+// own runs sized by block parity: the blocks dispatched to the slow XCCs (block b on XCC
+// (b + 7) mod 8 on every box seen: even b -> odd XCC) get F/16 of the others' share.  The
+// partition depends on blockIdx only (always a partition); the balance on that mapping.
+template <int F>
+__global__ __launch_bounds__(64) void persist_x(int64_t *o, uint64_t n, int64_t salt, Stats *st) {
+    extern __shared__ uint32_t pad[];
+    if (n == 0) pad[threadIdx.x] = 0;
+    const uint64_t chunks = n / 256, pairs = gridDim.x / 2;
+    const uint64_t per2 = chunks / pairs;                       // chunks per (even, odd) pair
+    const uint64_t short_ = per2 * F / (16 + F), long_ = per2 - short_;
+    const uint64_t pr = blockIdx.x / 2;
+    const bool slow = (blockIdx.x & 1) == 0;
+    const uint64_t c0 = pr * per2 + (slow ? 0 : short_);
+    const uint64_t c1 = slow ? c0 + short_ : pr * per2 + per2;
+    fill_chunk(o, c0, c1, salt);
+    record(st, c1 - c0);
+}
+
 __global__ void stamp_t0(Stats *st) { if (threadIdx.x == 0) st->t0 = __builtin_amdgcn_s_memrealtime(); }
 
 template <class F>
@@ -132,14 +176,22 @@ void timeit(const char *name, Stats *st, unsigned long long *ctr, F launch) {
     printf("%-12s mean %7.1f us best %7.1f us  %.2f TB/s (mean)", name, sum / 10 * 1e3, best * 1e3,
            (double)kIds * 8 / (sum / 10 * 1e-3) / 1e12);
     if (h.t0) {
-        std::vector<double> e;
-        for (int i = 0; i < kWaves; i++) if (h.end[i]) e.push_back((h.end[i] - h.t0) / 100.0);
+        std::vector<double> e, ex[8];
+        for (int i = 0; i < kWaves; i++) if (h.end[i]) {
+            e.push_back((h.end[i] - h.t0) / 100.0);
+            ex[h.xcc[i] & 7].push_back((h.end[i] - h.t0) / 100.0);
+        }
         std::sort(e.begin(), e.end());
         if (!e.empty())
             printf("  wave end us p10 %.1f p50 %.1f p90 %.1f max %.1f", e[e.size() / 10], e[e.size() / 2],
                    e[e.size() * 9 / 10], e.back());
         printf("\n   XCC MB:");
         for (int x = 0; x < 8; x++) printf(" %6.1f", h.xcc_bytes[x] / 1e6);
+        printf("\n   XCC p50 end us:");
+        for (int x = 0; x < 8; x++) {
+            std::sort(ex[x].begin(), ex[x].end());
+            printf(" %6.1f", ex[x].empty() ? 0.0 : ex[x][ex[x].size() / 2]);
+        }
     }
     printf("\n");
 }
@@ -153,16 +205,22 @@ int main() {
     hipMalloc(&ctr, 64);
     const uint64_t n = kIds;
     for (auto fn : {(const void *)persist_r, (const void *)queue<8>, (const void *)queue<32>, (const void *)queue<128>,
-                    (const void *)guided})
+                    (const void *)guided, (const void *)persist_bar<4, 8>, (const void *)persist_bar<8, 8>,
+                    (const void *)persist_bar<8, 1>, (const void *)persist_bar<8, 0>, (const void *)persist_x<14>,
+                    (const void *)persist_x<13>, (const void *)persist_x<12>})
         (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     const size_t lds = 18220;   // 8 one-wave blocks per CU, as the replay
     for (int rep = 0; rep < 2; rep++) {
         timeit("oneshot4", st, ctr, [&](int s) { hipLaunchKernelGGL(oneshot4, dim3((uint32_t)((n / 4 + 255) / 256)), dim3(256), 0, 0, o, n, (int64_t)s); });
         timeit("persist_r", st, ctr, [&](int s) { hipLaunchKernelGGL(persist_r, dim3(kWaves), dim3(64), lds, 0, o, n, (int64_t)s, st); });
-        timeit("queue_16K", st, ctr, [&](int s) { hipLaunchKernelGGL(queue<8>, dim3(kWaves), dim3(64), lds, 0, o, n, (int64_t)s, st, ctr); });
-        timeit("queue_64K", st, ctr, [&](int s) { hipLaunchKernelGGL(queue<32>, dim3(kWaves), dim3(64), lds, 0, o, n, (int64_t)s, st, ctr); });
         timeit("queue_256K", st, ctr, [&](int s) { hipLaunchKernelGGL(queue<128>, dim3(kWaves), dim3(64), lds, 0, o, n, (int64_t)s, st, ctr); });
-        timeit("guided", st, ctr, [&](int s) { hipLaunchKernelGGL(guided, dim3(kWaves), dim3(64), lds, 0, o, n, (int64_t)s, st, ctr); });
+        timeit("xsplit_14", st, ctr, [&](int s) { hipLaunchKernelGGL(persist_x<14>, dim3(kWaves), dim3(64), lds, 0, o, n, (int64_t)s, st); });
+        timeit("xsplit_13", st, ctr, [&](int s) { hipLaunchKernelGGL(persist_x<13>, dim3(kWaves), dim3(64), lds, 0, o, n, (int64_t)s, st); });
+        timeit("xsplit_12", st, ctr, [&](int s) { hipLaunchKernelGGL(persist_x<12>, dim3(kWaves), dim3(64), lds, 0, o, n, (int64_t)s, st); });
+        timeit("bar4_k8", st, ctr, [&](int s) { hipLaunchKernelGGL((persist_bar<4, 8>), dim3(kWaves / 4), dim3(256), lds * 4, 0, o, n, (int64_t)s, st); });
+        timeit("bar8_k8", st, ctr, [&](int s) { hipLaunchKernelGGL((persist_bar<8, 8>), dim3(kWaves / 8), dim3(512), lds * 8, 0, o, n, (int64_t)s, st); });
+        timeit("bar8_k1", st, ctr, [&](int s) { hipLaunchKernelGGL((persist_bar<8, 1>), dim3(kWaves / 8), dim3(512), lds * 8, 0, o, n, (int64_t)s, st); });
+        timeit("bar8_k0", st, ctr, [&](int s) { hipLaunchKernelGGL((persist_bar<8, 0>), dim3(kWaves / 8), dim3(512), lds * 8, 0, o, n, (int64_t)s, st); });
     }
     hipError_t e = hipDeviceSynchronize();
     printf("status %s\n", hipGetErrorString(e));
