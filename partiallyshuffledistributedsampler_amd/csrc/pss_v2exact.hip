@@ -44,7 +44,13 @@ namespace pss {
 
 namespace {
 constexpr int kTile = 4096;       // steps per LDS decode tile; pool2 windows up to this size decode in one
-constexpr int kTileOut = 8;     // consecutive merge outputs per thread (one search each per level)
+// consecutive merge outputs per thread (one search each per level; the first log2 of them
+// merge levels run in registers)
+#ifndef PSS_TILE_OUT
+#define PSS_TILE_OUT 16
+#endif
+constexpr int kTileOut = PSS_TILE_OUT;
+static_assert(kTileOut == 8 || kTileOut == 16, "tile outputs per thread: 8 or 16");
 
 struct V2xGeo {                   // one rank's stream, host-computed
     uint32_t P, T, S, B;          // pool1 size, main steps, pool2 windows, shuffle_buffer
@@ -231,6 +237,44 @@ __device__ __forceinline__ void tile_merge8_regs(EW (&e)[8]) {
     }
 }
 
+// ... and four: two sorted blocks of 8 (tile_merge8_regs on each half) merged in registers by
+// Batcher's odd-even merge of 8 + 8 (25 compare-exchanges), same keys (an index and the right
+// flag fit the key's low 4 bits).
+template <typename EW>
+__device__ __forceinline__ void tile_merge16_regs(EW (&e)[16]) {
+    using TE = TileEntry<EW>;
+    EW lo[8], hi[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) { lo[i] = e[i]; hi[i] = e[8 + i]; }
+    tile_merge8_regs(lo);
+    tile_merge8_regs(hi);
+    uint32_t k[16];
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        e[i] = lo[i];
+        e[8 + i] = hi[i];
+        k[i] = ((TE::val(lo[i]) - (uint32_t)i) << 4) | (uint32_t)i;
+        k[8 + i] = (TE::val(hi[i]) << 4) | 8u | (uint32_t)i;
+    }
+#pragma unroll
+    for (int i = 0; i < 8; i++) tile_ce(k[i], k[i + 8], e[i], e[i + 8]);
+#pragma unroll
+    for (int i = 0; i < 4; i++) tile_ce(k[i + 4], k[i + 8], e[i + 4], e[i + 8]);
+    tile_ce(k[2], k[4], e[2], e[4]);
+    tile_ce(k[3], k[5], e[3], e[5]);
+    tile_ce(k[6], k[8], e[6], e[8]);
+    tile_ce(k[7], k[9], e[7], e[9]);
+    tile_ce(k[10], k[12], e[10], e[12]);
+    tile_ce(k[11], k[13], e[11], e[13]);
+#pragma unroll
+    for (int i = 0; i < 7; i++) tile_ce(k[2 * i + 1], k[2 * i + 2], e[2 * i + 1], e[2 * i + 2]);
+#pragma unroll
+    for (int q = 0; q < 16; q++) {   // a right entry j landing at q has q - j left entries before it
+        const uint32_t d = (k[q] & 8u) ? (uint32_t)q - (k[q] & 7u) : 0u;
+        e[q] = TE::add(e[q], d);
+    }
+}
+
 // largest frame position a launch can produce: pool1 tiles P + kTile, windows B
 static bool v2x_narrow(uint32_t P, uint32_t B) {
     return (uint64_t)P + kTile <= ((uint64_t)1 << (32 - kStepBits)) && (uint64_t)B <= ((uint64_t)1 << (32 - kStepBits));
@@ -277,6 +321,17 @@ __global__ __launch_bounds__(kTile / OUT) void k_v2x_tile(V2xGeo x, uint32_t per
             for (int i = 0; i < 8; i++) va[TE::ix(b + (uint32_t)i)] = e[i];
             w0 = 8;
         }
+    } else if constexpr (OUT == 16) {
+        if (n == (uint32_t)kTile && regs) {   // full tile: a thread's 16 entries merged in registers first
+            const uint32_t b = threadIdx.x * 16u;
+            EW e[16];
+#pragma unroll
+            for (int i = 0; i < 16; i++) e[i] = TE::make(src[b + i], b + (uint32_t)i);
+            tile_merge16_regs(e);
+#pragma unroll
+            for (int i = 0; i < 16; i++) va[TE::ix(b + (uint32_t)i)] = e[i];
+            w0 = 16;
+        }
     }
     if (w0 == 1)
         for (uint32_t u = threadIdx.x; u < n; u += NT) va[TE::ix(u)] = TE::make(src[u], u);
@@ -290,6 +345,55 @@ __global__ __launch_bounds__(kTile / OUT) void k_v2x_tile(V2xGeo x, uint32_t per
     // right block's own insertions: every E_i <= q there, and q + nL is their frame-a position.)
     const uint32_t p0 = threadIdx.x * (uint32_t)OUT;
     for (uint32_t w = w0; w < n; w <<= 1) {
+        if (w >= (uint32_t)OUT) {
+            // (wave-uniform) a thread's OUT outputs lie inside one pair: a binary-lifting
+            // merge-path search of log2(w) + 1 uniform rounds, then a branch-free walk
+            // (both candidates' next entry chosen by select, one LDS read per output)
+            const uint32_t q = p0;
+            if (q < n) {
+                const uint32_t a = q & ~(2u * w - 1u), m = a + w;
+                const uint32_t pe = q + (uint32_t)OUT < n ? q + (uint32_t)OUT : n;
+                if (m >= n) {
+#pragma unroll
+                    for (int t = 0; t < OUT; t++)
+                        if (q + (uint32_t)t < pe) vb[TE::ix(q + t)] = va[TE::ix(q + t)];
+                } else {
+                    const uint32_t e = m + w < n ? m + w : n, nL = w, nR = e - m, d = q - a;
+                    const uint32_t lo = d > nR ? d - nR : 0u, hi = d < nL ? d : nL;
+                    // i = lo + #{consecutive i >= lo : E_L(i) <= R(d - i - 1)} (monotone)
+                    uint32_t i = lo;
+                    for (uint32_t sp = w; sp; sp >>= 1) {
+                        const uint32_t c = i + sp;
+                        if (c <= hi) {
+                            const uint32_t mid = c - 1u;
+                            if (TE::val(va[TE::ix(a + mid)]) - mid <= TE::val(va[TE::ix(m + d - mid - 1u)])) i = c;
+                        }
+                    }
+                    // (exhausted sides read a clamped, valid entry that is never taken; bools
+                    // combined bitwise so that no lane takes a branch)
+                    const uint32_t lL = nL - 1u, lR = nR - 1u;
+                    uint32_t j = d - i;
+                    EW xl = va[TE::ix(a + min(i, lL))], xr = va[TE::ix(m + min(j, lR))];
+#pragma unroll
+                    for (int t = 0; t < OUT; t++) {
+                        const bool takeL = (j >= nR) | ((i < nL) & (TE::val(xl) - i <= TE::val(xr)));
+                        const EW o = takeL ? xl : TE::add(xr, i);
+                        if (q + (uint32_t)t < pe) vb[TE::ix(q + t)] = o;
+                        i += (uint32_t)takeL;
+                        j = d + (uint32_t)t + 1u - i;
+                        if (t + 1 < OUT) {
+                            const uint32_t ni = takeL ? a + min(i, lL) : m + min(j, lR);
+                            const EW nx = va[TE::ix(ni)];
+                            xl = takeL ? nx : xl;
+                            xr = takeL ? xr : nx;
+                        }
+                    }
+                }
+            }
+            __syncthreads();
+            EW *t = va; va = vb; vb = t;
+            continue;
+        }
         // a thread's outputs may span several pairs while 2w < OUT: one walk per pair
         for (uint32_t q = p0; q < p0 + (uint32_t)OUT && q < n;) {
             const uint32_t a = (q / (2 * w)) * (2 * w), m = a + w;
@@ -501,14 +605,28 @@ __global__ __launch_bounds__(kGNT) void k_v2x_gmerge(V2xGeo x, uint32_t w, const
     }
     uint32_t i = lo, j = p0 - lo;
     const uint32_t pn = on - p0 < kPer ? on - p0 : kPer;
+    // branch-free walk: the current entry of each side in registers (an exhausted side holds a
+    // clamped, valid LDS entry that is never taken), one LDS read pair per output for the side
+    // just consumed
+    const uint32_t lL = sL ? sL - 1u : 0u, lR = sR ? sR - 1u : 0u;
+    uint32_t xl, ol, xr, orr;
+    {
+        const uint32_t ia = gsk(min(i, lL)), ib = gsk(sL + min(j, lR));
+        xl = sv[ia]; ol = so[ia]; xr = sv[ib]; orr = so[ib];
+    }
     uint32_t tv[kPer], to[kPer];
 #pragma unroll
     for (uint32_t k = 0; k < kPer; k++) {
-        tv[k] = 0; to[k] = 0;
-        if (k < pn) {
-            const bool takeL = j >= sR || (i < sL && lv(i) - (i0 + i) <= rv(j));
-            if (takeL) { tv[k] = lv(i); to[k] = so[gsk(i)]; i++; }
-            else { tv[k] = rv(j) + i0 + i; to[k] = so[gsk(sL + j)]; j++; }
+        const bool takeL = (j >= sR) | ((i < sL) & (xl - (i0 + i) <= xr));
+        tv[k] = takeL ? xl : xr + i0 + i;
+        to[k] = takeL ? ol : orr;
+        i += (uint32_t)takeL;
+        j = p0 + k + 1u - i;
+        if (k + 1 < kPer) {
+            const uint32_t ix = gsk(takeL ? min(i, lL) : sL + min(j, lR));
+            const uint32_t nv = sv[ix], no = so[ix];
+            xl = takeL ? nv : xl; ol = takeL ? no : ol;
+            xr = takeL ? xr : nv; orr = takeL ? orr : no;
         }
     }
     static_assert(kPer == 8, "two 16-byte stores per array");

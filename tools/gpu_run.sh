@@ -13,6 +13,7 @@
 #   pmc:<w>            the counter passes of workload w (tools/pmc_kernel.sh)
 #   gpus2              bench.py --gpus 2 with no launcher (2 ranks on cuda:0, gloo)
 #   ab:<lib>:<w>       3 interleaved runs of bench workload w: in-tree library vs <lib> (PSS_LIB)
+#   abx:<lib>:<cfg>    the same for a tools/bench_configs.py config (c2x, c5x, c2v1x, ...)
 #   env:<K=V>:<w>      3 interleaved runs of bench workload w: as is vs with K=V
 cd "$GRAFT_REPO_ROOT"; O=gpurun_out/$1; shift; mkdir -p $O; export TMPDIR=/tmp
 BN="--no-cpu-baseline --no-latency --no-exact"
@@ -40,6 +41,11 @@ for s in "$@"; do
           run 240 ab_${t}_cur_${b}_$i.json python bench.py --steps 100 --workload $b $BN
           run 240 ab_${t}_alt_${b}_$i.json env PSS_LIB=$a python bench.py --steps 100 --workload $b $BN
         done ;;
+    abx) t=$(basename $(dirname $a))
+         for i in 1 2 3; do
+           run 300 abx_${t}_cur_${b}_$i.json python tools/bench_configs.py $b
+           run 300 abx_${t}_alt_${b}_$i.json env PSS_LIB=$a python tools/bench_configs.py $b
+         done ;;
     env) for i in 1 2 3; do
            run 240 env_cur_${b}_$i.json python bench.py --steps 100 --workload $b $BN
            run 240 env_alt_${b}_$i.json env "$a" python bench.py --steps 100 --workload $b $BN
