@@ -29,13 +29,23 @@ def short(name):
 
 
 def load(pass_dir):
-    acc = defaultdict(lambda: defaultdict(list))
+    """Per kernel, the counters of its dispatches of the LARGEST grid only: a process may launch
+    one kernel name at several sizes (torch's fill_ on the 800 MB output and on tiny buffers),
+    and averaging them together describes neither."""
+    acc = defaultdict(lambda: defaultdict(lambda: defaultdict(list)))
     for p in glob.glob(os.path.join(pass_dir, "**", "*counter_collection*.csv"), recursive=True):
         with open(p) as f:
             for row in csv.DictReader(f):
                 k = short(row.get("Kernel_Name", ""))
-                acc[k][row["Counter_Name"]].append(float(row["Counter_Value"]))
-    return acc
+                grid = int(float(row.get("Grid_Size", 0) or 0))
+                acc[k][grid][row["Counter_Name"]].append(float(row["Counter_Value"]))
+    out = {}
+    for k, grids in acc.items():
+        g = max(grids)
+        out[k] = grids[g]
+        if len(grids) > 1:
+            print("%s: counters of grid %d only (other grids: %s)" % (k, g, sorted(x for x in grids if x != g)))
+    return out
 
 
 def main():
