@@ -2,9 +2,12 @@
 // PSS_ORDER_EXACT): window 0 is `seed(epoch); shuffle(range(len))` (V1:102,114-115), window
 // b >= 1 is `seed(epoch + b*10000); shuffle(range(len))` (V1:165-171), both with CPython
 // 3.10's MT19937 (`random.py:128-168` seeding, `:239-249` _randbelow, `:380-396` shuffle).
-// Every window reseeds, so windows are independent: one 256-thread workgroup per
-// (rank, window), three phases, for windows up to kV1ExactMaxB entries (LDS-resident); larger
-// windows run the same three phases through HBM (k_v1x_*, below).
+// Every window reseeds, so windows are independent -- and the same for every rank: the seed is
+// the epoch and the window index, the shuffled list range(len) (V1:165-171), and every rank has
+// num_samples positions.  A window's permutation is resolved once per call; its output stage
+// writes id = new_start + w B + x for each rank of the call (kV1FanRanks per workgroup row).
+// One 256-thread workgroup per window, three phases, for windows up to kV1ExactMaxB entries
+// (LDS-resident); larger windows run the same three phases through HBM (k_v1x_*, below).
 //
 //   1. seeding (wave 0, uniform/scalar code): init_by_array over the compile-time
 //      init_genrand(19650218) table -- two serial chains of 624 + 623 steps.
@@ -30,10 +33,11 @@ namespace pss {
 
 namespace {
 constexpr int kExactNT = 256;
+constexpr int32_t kV1FanRanks = 8;   // ranks whose ids one workgroup writes
 }  // namespace
 
 // Phases 1-2 alone, one wave per window (2.5 KB of LDS, so a CU holds 32 of them): the draws
-// j_i of every window go to HBM (u16, B per window) for k_v1_exact's resolution.
+// j_i of every window go to HBM (u16, B per window) for k_v1_exact's resolution.  Grid: nw.
 __global__ __launch_bounds__(64) void k_v1x_draws(Geometry g, int64_t w_lo, int64_t nw, int64_t epoch,
                                                   uint16_t *__restrict__ J) {
     __shared__ uint32_t mt[kMtN];
@@ -47,16 +51,18 @@ __global__ __launch_bounds__(64) void k_v1x_draws(Geometry g, int64_t w_lo, int6
              [&](uint32_t d, uint32_t r) { jw[n - 1 - (int)d] = (uint16_t)r; });
 }
 
-// One workgroup per (local rank, window) of [w_lo, w_lo + nw).
+// One workgroup per (rank group, window) of [w_lo, w_lo + nw): the window's permutation, then
+// the ids of ranks [group * kV1FanRanks, ...) of the call (nout ranks from rank_lo).
 __global__ __launch_bounds__(kExactNT) void k_v1_exact(Geometry g, const RankDesc *__restrict__ ranks,
-                                                       int32_t rank_lo, int64_t w_lo, int64_t nw,
+                                                       int32_t rank_lo, int32_t nout, int64_t w_lo, int64_t nw,
                                                        int64_t pos_lo, int64_t count, int64_t epoch,
                                                        const uint16_t *__restrict__ J,
                                                        int64_t *__restrict__ out, MapArgs ma) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-    const int32_t rl = (int32_t)(blockIdx.x / nw);
-    const int64_t w = w_lo + (int64_t)(blockIdx.x % nw);
-    const int32_t rank = rank_lo + rl;
+    const int32_t r_a = (int32_t)(blockIdx.x / nw) * kV1FanRanks;
+    const int32_t r_b = r_a + kV1FanRanks < nout ? r_a + kV1FanRanks : nout;
+    const uint32_t wslot = (uint32_t)(blockIdx.x % nw);
+    const int64_t w = w_lo + (int64_t)wslot;
     const int64_t wb = w * g.B;
     const int n = (int)(g.ns - wb < g.B ? g.ns - wb : g.B);
     const int tid = threadIdx.x, wid = tid >> 6;
@@ -68,7 +74,7 @@ __global__ __launch_bounds__(kExactNT) void k_v1_exact(Geometry g, const RankDes
     __shared__ uint32_t tot[kExactNT / 64];
 
     if (J) {                 // draws already made by k_v1x_draws
-        const uint16_t *jw = J + (size_t)blockIdx.x * (size_t)(g.B < g.ns ? g.B : g.ns);
+        const uint16_t *jw = J + (size_t)wslot * (size_t)(g.B < g.ns ? g.B : g.ns);
         for (int i = tid; i < n; i += kExactNT) jv[i] = jw[i];
     } else if (wid == 0 && n > 1) {
         // ---- 1. seed(a): key = 32-bit words of abs(a) (random_seed) ----
@@ -113,8 +119,6 @@ __global__ __launch_bounds__(kExactNT) void k_v1_exact(Geometry g, const RankDes
         __syncthreads();
     }
     // ---- output: x[i] for the positions of this window inside [pos_lo, pos_lo + count) ----
-    const int64_t base = ranks[rank].new_start + wb;
-    const int64_t ebase = (int64_t)rl * count - pos_lo;   // element of stream position 0
     int64_t p0 = 0, p1 = n;
     if (wb < pos_lo) p0 = pos_lo - wb;
     if (wb + n > pos_lo + count) p1 = pos_lo + count - wb;
@@ -135,13 +139,14 @@ __global__ __launch_bounds__(kExactNT) void k_v1_exact(Geometry g, const RankDes
                 x = k < 0 ? pj : nxt[k];
             }
         }
-        put_id_or_pair(out, ma, ebase + wb + p, wrap_id(base + x, g.N));
+        for (int32_t r = r_a; r < r_b; r++)   // (wave-uniform rank: scalar descriptor loads)
+            put_id_or_pair(out, ma, (int64_t)r * count - pos_lo + wb + p, wrap_id(ranks[rank_lo + r].new_start + wb + x, g.N));
     }
 }
 
 // ---- windows beyond LDS (n > kV1ExactMaxB): the same resolution through HBM ----------------
-// One pass covers `nj` jobs (rank, window) of the launch, jobs j0 .. j0 + nj - 1 (job -> local
-// rank job / nw, window w_lo + job % nw), each with slices of the window length W:
+// One pass covers `nj` jobs (windows) of the launch, jobs j0 .. j0 + nj - 1 (job -> window
+// w_lo + job % nw: every rank of the call shares it), each with slices of the window length W:
 //   J      the draws j_k, k = 1 .. n-1 (k_v1x_draws32[_wg]: the MT stream is serial); each draw
 //          also counts its bucket, j >> 11, in BCNT (nbk = ceil(W / 2048) counters per window)
 //   PART   the steps k partitioned by bucket (k_v1x_part: counts -> offsets by k_v1x_bscan, then
@@ -443,8 +448,9 @@ __global__ __launch_bounds__(kV1sNT) void k_v1x_solve(Geometry g, V1xBig b) {
 }
 
 // ---- output: x[i] = S[i] ? root(S[i]) : j_i (x[0]: 0) -----------------------------------------
+// (the window's x[i] once, then the ids of the call's nout ranks from rank_lo)
 __global__ __launch_bounds__(256) void k_v1x_out(Geometry g, V1xBig b, const RankDesc *__restrict__ ranks,
-                                                 int32_t rank_lo, int64_t pos_lo, int64_t count,
+                                                 int32_t rank_lo, int32_t nout, int64_t pos_lo, int64_t count,
                                                  int64_t *__restrict__ out, MapArgs ma) {
     uint32_t slot, xblk;
     if (!v1x_block(b, slot, xblk)) return;
@@ -473,8 +479,8 @@ __global__ __launch_bounds__(256) void k_v1x_out(Geometry g, V1xBig b, const Ran
             x = k;
         }
     }
-    const int32_t rl = (int32_t)(job / (uint64_t)b.nw);
-    put_id_or_pair(out, ma, (int64_t)rl * count + (p - pos_lo), wrap_id(ranks[rank_lo + rl].new_start + wb + x, g.N));
+    for (int32_t r = 0; r < nout; r++)   // (wave-uniform rank: scalar descriptor loads)
+        put_id_or_pair(out, ma, (int64_t)r * count + (p - pos_lo), wrap_id(ranks[rank_lo + r].new_start + wb + x, g.N));
 }
 
 namespace {
@@ -502,7 +508,7 @@ size_t v1_exact_ws_bytes(const Geometry &g, int32_t nr, int64_t pos_lo, int64_t 
     const int64_t pos_hi = pos_lo + count < g.ns ? pos_lo + count : g.ns;
     if (nr <= 0 || pos_hi <= pos_lo || !v1_exact_supported(g)) return 0;
     const int64_t nw = (pos_hi - 1) / g.B - pos_lo / g.B + 1;
-    const int64_t jobs = (int64_t)nr * nw;
+    const int64_t jobs = nw;   // a window's draws and resolution serve every rank of the call
     const int64_t W = g.B < g.ns ? g.B : g.ns;   // the longest window
     if (W <= kV1ExactMaxB) return (size_t)jobs * (size_t)W * sizeof(uint16_t);
     const int64_t pj = jobs < v1x_jobs_per_pass(W) ? jobs : v1x_jobs_per_pass(W);
@@ -515,7 +521,7 @@ static hipError_t launch_v1_exact_big(const Geometry &g, const RankDesc *ranks, 
     const int64_t pos_hi = pos_lo + count < g.ns ? pos_lo + count : g.ns;
     const int64_t w_lo = pos_lo / g.B, w_hi = (pos_hi - 1) / g.B;
     const int64_t nw = w_hi - w_lo + 1;
-    const uint64_t jobs = (uint64_t)nr * (uint64_t)nw;
+    const uint64_t jobs = (uint64_t)nw;   // one per window: shared by every rank of the call
     const int64_t W = g.B < g.ns ? g.B : g.ns;   // the longest window: the slice length
     const uint64_t per = (uint64_t)v1x_jobs_per_pass(W);
     const uint32_t B = (uint32_t)W;
@@ -562,7 +568,7 @@ static hipError_t launch_v1_exact_big(const Geometry &g, const RankDesc *ranks, 
         hipLaunchKernelGGL(k_v1x_solve, gs, dim3(kV1sNT), 0, s, g, bs);
         V1xBig bo = b;
         const dim3 go = grid(bo, (B + 255) / 256);
-        hipLaunchKernelGGL(k_v1x_out, go, dim3(256), 0, s, g, bo, ranks, rank_lo, pos_lo, count, out, ma);
+        hipLaunchKernelGGL(k_v1x_out, go, dim3(256), 0, s, g, bo, ranks, rank_lo, nr, pos_lo, count, out, ma);
         e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
@@ -587,12 +593,12 @@ hipError_t launch_v1_exact(const Geometry &g, const RankDesc *ranks, int32_t ran
         (const void *)k_v1_exact, hipFuncAttributeMaxDynamicSharedMemorySize,
         (int)v1_exact_lds_bytes(kV1ExactMaxB));
     if (attr != hipSuccess) return attr;
-    const dim3 grid((uint32_t)(nr * nw));
+    const uint32_t ngrp = (uint32_t)((nr + kV1FanRanks - 1) / kV1FanRanks);
     // with a workspace, the serial MT phases run one wave per window (many windows in flight)
     // ahead of the resolution; without one, each workgroup's first wave does them in place
-    if (ws) hipLaunchKernelGGL(k_v1x_draws, grid, dim3(64), 0, s, g, w_lo, nw, epoch, (uint16_t *)ws);
-    hipLaunchKernelGGL(k_v1_exact, grid, dim3(kExactNT), lds, s, g, ranks, rank_lo, w_lo, nw, pos_lo,
-                       count, epoch, (const uint16_t *)ws, out, ma);
+    if (ws) hipLaunchKernelGGL(k_v1x_draws, dim3((uint32_t)nw), dim3(64), 0, s, g, w_lo, nw, epoch, (uint16_t *)ws);
+    hipLaunchKernelGGL(k_v1_exact, dim3((uint32_t)(ngrp * nw)), dim3(kExactNT), lds, s, g, ranks, rank_lo, nr,
+                       w_lo, nw, pos_lo, count, epoch, (const uint16_t *)ws, out, ma);
     return hipGetLastError();
 }
 

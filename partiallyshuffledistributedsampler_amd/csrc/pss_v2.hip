@@ -15,6 +15,7 @@
 // Pools beyond LDS (P1 > kLdsSlotMax) take the grouped schedule of pss_v2grp.hip.
 #include <cstdlib>
 #include <type_traits>
+#include <vector>
 
 #include "pss_device.h"
 
@@ -1090,6 +1091,53 @@ static signed char g_xchg_ordered[64];   // per device: 0 unknown, 1 ordered, -1
 static signed char g_write_ordered[64];
 static signed char g_add_ordered[64];
 
+// The exchange replay (k_v2_emit_x, one lane-ordered exchange per step) against the
+// collision-probe replay (k_v2_emit: probe bytes + ballots, no ordering assumption) on small real
+// geometries -- a power-of-two pool (paired draws, the C2 kernel) and a multiply-shift one, 3 ranks,
+// several tiles, a wrapping block, the tail.  Run once per device after the synthetic pattern
+// check passes: the ordering is then confirmed on the kernel and the shapes it serves, and a
+// difference anywhere sends every replay down the probe path.  same = every id equal.
+static hipError_t xchg_replay_crosscheck(bool &same) {
+    same = false;
+    struct Shape { int64_t ns, B; };
+    const Shape shapes[2] = {{6 * 4 * 4096 + 4096 + 777, 4096}, {5 * 4 * 3000 + 3000 + 321, 3000}};
+    const int32_t R = 3;
+    for (const Shape &sh : shapes) {
+        Geometry g{};
+        g.ns = sh.ns; g.R = R; g.N = sh.ns * R - 2; g.B = sh.B; g.version = 2; g.shuffle = 1;
+        g.key0 = 0x9E3779B9u; g.key1 = 0x7F4A7C15u;
+        RankDesc hr[R];
+        for (int32_t r = 0; r < R; r++) hr[r] = {(int64_t)r * g.ns, (int64_t)((r + 2) % R) * g.ns};
+        const size_t nval = v2_val_bytes(g, R), nbuf = v2_buf_bytes(g, R), nsort = v2_sort_bytes(g, R);
+        const size_t nout = (size_t)R * (size_t)g.ns * sizeof(int64_t);
+        char *mem = nullptr;
+        const size_t total = sizeof(hr) + 16 + nval + nbuf + nsort + 2 * nout + 64;
+        hipError_t e = hipMalloc((void **)&mem, total);
+        if (e != hipSuccess) return e;
+        auto at = [&](size_t off) { return mem + ((off + 15) & ~(size_t)15); };
+        size_t off = 0;
+        RankDesc *dr = (RankDesc *)at(off); off = (size_t)((char *)dr - mem) + sizeof(hr);
+        int32_t *err = (int32_t *)at(off); off = (size_t)((char *)err - mem) + 16;
+        uint32_t *val = (uint32_t *)at(off); off = (size_t)((char *)val - mem) + nval;
+        uint32_t *buf = nbuf ? (uint32_t *)at(off) : nullptr; off = (size_t)((char *)at(off) - mem) + nbuf;
+        uint32_t *srt = nsort ? (uint32_t *)at(off) : nullptr; off = (size_t)((char *)at(off) - mem) + nsort;
+        int64_t *o1 = (int64_t *)at(off); off = (size_t)((char *)o1 - mem) + nout;
+        int64_t *o2 = (int64_t *)at(off);
+        std::vector<int64_t> h1((size_t)R * g.ns), h2((size_t)R * g.ns);
+        e = hipMemcpy(dr, hr, sizeof(hr), hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = hipMemset(err, 0, 16);
+        if (e == hipSuccess) e = launch_v2(g, dr, 0, R, 0, g.ns, o1, val, buf, srt, err, 0, Marker(), EMIT_XCHG, V2_STAGE_ALL);
+        if (e == hipSuccess) e = launch_v2(g, dr, 0, R, 0, g.ns, o2, val, buf, srt, err, 0, Marker(), EMIT_PROBE, V2_STAGE_ALL);
+        if (e == hipSuccess) e = hipMemcpy(h1.data(), o1, nout, hipMemcpyDeviceToHost);
+        if (e == hipSuccess) e = hipMemcpy(h2.data(), o2, nout, hipMemcpyDeviceToHost);
+        (void)hipFree(mem);
+        if (e != hipSuccess) return e;
+        if (h1 != h2) return hipSuccess;   // same stays false
+    }
+    same = true;
+    return hipSuccess;
+}
+
 hipError_t check_lds_xchg_order() {
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
@@ -1108,9 +1156,18 @@ hipError_t check_lds_xchg_order() {
     if (e == hipSuccess) e = hipMemcpy(hbad, bad, sizeof(hbad), hipMemcpyDeviceToHost);
     (void)hipFree(bad);
     if (e != hipSuccess) return e;
-    g_xchg_ordered[dev] = (hbad[0] == 0 && hbad[1] == 0) ? 1 : -1;
     g_write_ordered[dev] = (hbad[2] == 0 && hbad[3] == 0) ? 1 : -1;
     g_add_ordered[dev] = (hbad[4] == 0 && hbad[5] == 0) ? 1 : -1;
+    if (hbad[0] != 0 || hbad[1] != 0) {
+        g_xchg_ordered[dev] = -1;
+        return hipSuccess;
+    }
+    // the pattern check passed: confirm it on the replay kernels themselves (the cross-check
+    // launches explicit paths, so it does not recurse into this function)
+    bool same = false;
+    e = xchg_replay_crosscheck(same);
+    if (e != hipSuccess) return e;
+    g_xchg_ordered[dev] = same ? 1 : -1;
     return hipSuccess;
 }
 

@@ -493,6 +493,10 @@ __global__ __launch_bounds__(kTile / OUT) void k_v2x_tile(V2xGeo x, uint32_t per
 // HBM), stages those sub-ranges in LDS with coalesced loads, works from LDS (kPer entries per
 // thread: one LDS search, then a sequential walk) and writes its tile back coalesced.
 constexpr uint32_t kGNT = 256, kPer = 8, kGTile = kGNT * kPer;   // w >= kTile is a multiple
+// ranks one output block writes: the decode is shared by every rank of a call, its last stage
+// writes each position's id for up to kFanRanks ranks (more ranks: more block rows, each
+// re-reading the same decoded entries)
+constexpr int32_t kFanRanks = 8;
 
 // Merge-path splits of every gmerge tile's first and end output, all at once (one thread per
 // tile boundary, so the binary searches' HBM latency overlaps).
@@ -540,23 +544,31 @@ struct V2xFin {
     Geometry g;
     const RankDesc *ranks;
     int32_t rank_lo;
+    int32_t nout;                 // FIN 2: ranks of the call (groups of kFanRanks per grid row y)
     uint32_t *Q2;                 // FIN 1: written ([seq][B]); FIN 2: read ([rank][T2])
     int64_t pos_lo, count;
     int64_t *out;
     MapArgs ma;
 };
-__device__ __forceinline__ void v2x_put(const V2xFin &f, const V2xGeo &x, uint32_t rl, const RankDesc &rd,
+// the decoded sequence (rl) is every rank's: ranks [r_a, r_b) of the call get its ids
+__device__ __forceinline__ void v2x_put(const V2xFin &f, const V2xGeo &x, uint32_t rl, int32_t r_a, int32_t r_b,
                                         uint32_t q, uint32_t t) {
     if ((int64_t)t < f.pos_lo || (int64_t)t >= f.pos_lo + f.count) return;
-    int64_t id;
+    bool old_side;
+    int64_t v;
     if (q < x.P) {
-        id = rd.old_start + q;
+        v = q;
+        old_side = true;
     } else {
-        const uint32_t uu = q - x.P, s = uu / x.B;
-        const int64_t wbase = s == 0 ? rd.old_start + x.B : rd.new_start + (int64_t)(s + 1) * x.B;
-        id = wbase + f.Q2[(size_t)rl * x.T2 + uu];
+        const uint32_t uu = q - x.P, sw = uu / x.B;
+        v = (int64_t)(sw + 1) * x.B + f.Q2[(size_t)rl * x.T2 + uu];
+        old_side = sw == 0;
     }
-    put_id_or_pair(f.out, f.ma, (int64_t)rl * f.count + ((int64_t)t - f.pos_lo), wrap_id(id, f.g.N));
+    for (int32_t r = r_a; r < r_b; r++) {
+        const RankDesc rd = f.ranks[f.rank_lo + r];
+        put_id_or_pair(f.out, f.ma, (int64_t)r * f.count + ((int64_t)t - f.pos_lo),
+                       wrap_id((old_side ? rd.old_start : rd.new_start) + v, f.g.N));
+    }
 }
 
 template <int FIN>
@@ -572,12 +584,12 @@ __global__ __launch_bounds__(kGNT) void k_v2x_gmerge(V2xGeo x, uint32_t w, const
     uint32_t *vd = Vd + base, *od = Od + base;
     const uint32_t on = x.ns - o0 < kGTile ? x.ns - o0 : kGTile;
     const uint32_t a = (o0 / (2 * w)) * (2 * w), m = a + w;
-    RankDesc rd{};
-    if constexpr (FIN == 2) rd = fin.ranks[fin.rank_lo + (int32_t)rl];
+    const int32_t r_a = (int32_t)blockIdx.y * kFanRanks;
+    const int32_t r_b = r_a + kFanRanks < fin.nout ? r_a + kFanRanks : fin.nout;
     auto emit = [&](uint32_t p, uint32_t val, uint32_t st) {   // output p (of the tile) = (val, st)
         if constexpr (FIN == 0) { vd[o0 + p] = val; od[o0 + p] = st; }
         else if constexpr (FIN == 1) fin.Q2[(size_t)rl * x.ns + st] = val;
-        else v2x_put(fin, x, rl, rd, val, st);
+        else v2x_put(fin, x, rl, r_a, r_b, val, st);
     };
     if (m >= x.ns) {                           // lone left block: already merged
         for (uint32_t u = threadIdx.x; u < on; u += kGNT) emit(u, v[o0 + u], o[o0 + u]);
@@ -712,24 +724,26 @@ __global__ __launch_bounds__(kChainNT) void k_v2x_link(V2xGeo x, V2xChain ch) {
 constexpr int kChainPer = kTile / kChainNT;
 static_assert(kChainPer * kChainNT == kTile, "a tile's steps and survivors: kChainPer per thread");
 
+// The decoded sequence is every rank's (the draws depend on the epoch and the window only,
+// V2:108,147): block (chunk c, group) writes the ids of ranks [group * kFanRanks, ...) of the call.
 __global__ __launch_bounds__(kChainNT) void k_v2x_emit(Geometry g, V2xGeo x, V2xChain ch,
                                                        const RankDesc *__restrict__ ranks, int32_t rank_lo,
-                                                       const uint32_t *__restrict__ ANS,
+                                                       int32_t nout, const uint32_t *__restrict__ ANS,
                                                        const uint32_t *__restrict__ Q2, int64_t pos_lo,
                                                        int64_t count, int64_t *__restrict__ out, MapArgs ma) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     uint32_t *A = smem, *An = smem + x.P;
-    const uint32_t rl = blockIdx.x / ch.nch, c = blockIdx.x % ch.nch;
+    const uint32_t rl = 0, c = blockIdx.x % ch.nch;
+    const int32_t r_a = (int32_t)(blockIdx.x / ch.nch) * kFanRanks;
+    const int32_t r_b = r_a + kFanRanks < nout ? r_a + kFanRanks : nout;
     const uint32_t j0 = c * ch.tpc, j1 = j0 + ch.tpc < x.tiles1 ? j0 + ch.tpc : x.tiles1;
     const int64_t pos_hi = pos_lo + count;
     if ((int64_t)j0 * kTile >= pos_hi) return;   // every step of the chunk past the range
     const uint32_t Ba0 = alive_at(x.P, x.T, j0 * (uint32_t)kTile);
     const uint32_t *aa = ch.AA + ((size_t)rl * ch.nch + c) * x.P;
     for (uint32_t r = threadIdx.x; r < Ba0; r += kChainNT) A[r] = aa[r];
-    const RankDesc rd = ranks[rank_lo + (int32_t)rl];
     const uint32_t *ans = ANS + (size_t)rl * x.ns;
     const uint32_t *q2 = Q2 + (size_t)rl * x.T2;
-    const int64_t ebase = (int64_t)rl * count - pos_lo;   // element of stream position 0
     // tile j's answers (q) and survivors (sr) of this thread: u = threadIdx.x + k * kChainNT
     auto load = [&](uint32_t j, uint32_t (&q)[kChainPer], uint32_t (&sr)[kChainPer]) {
         const uint32_t t0 = j * (uint32_t)kTile, n = x.ns - t0 < (uint32_t)kTile ? x.ns - t0 : (uint32_t)kTile;
@@ -781,15 +795,23 @@ __global__ __launch_bounds__(kChainNT) void k_v2x_emit(Geometry g, V2xGeo x, V2x
             const int64_t t = (int64_t)t0 + u;
             if (u >= n || t < pos_lo || t >= pos_hi) continue;
             const uint32_t a = av[k];
-            int64_t id;
+            // virtual index: a < P the initial pool1 position, else the element's window base +
+            // its pool2 rank (window 0 is the old start's second window, V2:135-138)
+            bool old_side;
+            int64_t v;
             if (a < x.P) {
-                id = rd.old_start + a;
+                v = a;
+                old_side = true;
             } else {
-                const uint32_t s = (a - x.P) / x.B;
-                const int64_t wbase = s == 0 ? rd.old_start + x.B : rd.new_start + (int64_t)(s + 1) * x.B;
-                id = wbase + g2[k];
+                const uint32_t sw = (a - x.P) / x.B;
+                v = (int64_t)(sw + 1) * x.B + g2[k];
+                old_side = sw == 0;
             }
-            put_id_or_pair(out, ma, ebase + t, wrap_id(id, g.N));
+            for (int32_t r = r_a; r < r_b; r++) {   // (wave-uniform rank: scalar descriptor loads)
+                const RankDesc rd = ranks[rank_lo + r];
+                put_id_or_pair(out, ma, (int64_t)r * count + (t - pos_lo),
+                               wrap_id((old_side ? rd.old_start : rd.new_start) + v, g.N));
+            }
         }
         if (more) {
             __syncthreads();
@@ -841,10 +863,6 @@ bool v2_exact_supported(const Geometry &g) {
 // Ranks decoded per pass: every flat kernel of the decode launches one thread per (rank, step)
 // and the draw / tile launches one block per (rank, job), so a pass keeps ranks x steps below
 // 2^30 (thread counts below 2^32) and the workspace is sized for one pass, reused by the next.
-static int32_t v2x_ranks_per_pass(const Geometry &g, int32_t nr) {
-    const int64_t cap = ((int64_t)1 << 30) / (g.ns > 0 ? g.ns : 1);
-    return (int32_t)(nr < cap ? nr : (cap > 1 ? cap : 1));
-}
 
 // launches of one block per job, cut into pieces of at most 2^20 blocks (2^30 threads)
 template <class F>
@@ -881,7 +899,7 @@ static V2xChain v2x_chain_plan(const V2xGeo &x, int32_t nr) {
 
 size_t v2_exact_ws_bytes(const Geometry &g, int32_t nr_all) {
     if (!v2_exact_supported(g) || nr_all <= 0) return 0;
-    const int32_t nr = v2x_ranks_per_pass(g, nr_all);
+    const int32_t nr = 1;   // one decoded sequence serves every rank of a call (v2x_pass)
     const V2xGeo x = v2x_geo(g);
     if (v2x_chain(x)) {   // K1, ANS (ns each), K2, Q2 (T2 each), survivors, chunk maps, chunk starts
         const V2xChain ch = v2x_chain_plan(x, nr);
@@ -904,16 +922,24 @@ static void v2x_global_levels(const V2xGeo &x, uint32_t nr, uint32_t *V, uint32_
         const bool last = (uint64_t)2 * w >= x.ns;
         if (!last) hipLaunchKernelGGL(k_v2x_gmerge<0>, gridt, dim3(kGNT), 0, s, x, w, V, O, Vd, Od, SP, fin);
         else if (fin_mode == 1) hipLaunchKernelGGL(k_v2x_gmerge<1>, gridt, dim3(kGNT), 0, s, x, w, V, O, Vd, Od, SP, fin);
-        else hipLaunchKernelGGL(k_v2x_gmerge<2>, gridt, dim3(kGNT), 0, s, x, w, V, O, Vd, Od, SP, fin);
+        else hipLaunchKernelGGL(k_v2x_gmerge<2>, dim3(gridt.x, (uint32_t)v2x_cdiv(fin.nout, kFanRanks)), dim3(kGNT), 0, s,
+                                x, w, V, O, Vd, Od, SP, fin);
         uint32_t *t = V; V = Vd; Vd = t;
         t = O; O = Od; Od = t;
     }
 }
 
-// one pass over nr ranks (nr * ns < 2^30)
+// The draws of every pool2 window and of the tail come from streams seeded by the epoch and the
+// window alone (seed(e + 2) for segment 0, seed(e + (s - 1) 10000), seed(e + buffers 10000) per
+// tail step, V2:107-109,147) and the pool sizes are the same for every rank (ns = ceil(N / R)),
+// so the decoded stream of virtual indices is the same for all of them; a rank's ids are that
+// stream through its (old, new) start (V2:135-148).  One pass decodes it once and its last stage
+// writes the ids of all nr ranks of the call.
 static hipError_t v2x_pass(const Geometry &g, const V2xGeo &x, const RankDesc *ranks, int32_t rank_lo,
-                           int32_t nr, int32_t nr_plan, int64_t pos_lo, int64_t count, int64_t epoch,
+                           int32_t nout, int64_t pos_lo, int64_t count, int64_t epoch,
                            int64_t *out, uint32_t *ws, hipStream_t s, const MapArgs &ma) {
+    const int32_t nr = 1, nr_plan = 1;   // decoded sequences
+    const uint32_t ngrp = (uint32_t)v2x_cdiv(nout, kFanRanks);   // output block rows
     const size_t nsr = (size_t)nr * x.ns, tr = (size_t)nr * x.T2;
     // merge-levels layout: K1 | V | O | Vd | Od | K2 | Q2 | splits | tables
     // chain layout:        K1 | V (answers) | K2 | Q2 | survivors | chunk maps | chunk starts
@@ -966,8 +992,8 @@ static hipError_t v2x_pass(const Geometry &g, const V2xGeo &x, const RankDesc *r
         const size_t lds = 2 * (size_t)x.P * sizeof(uint32_t);
         hipLaunchKernelGGL(k_v2x_compose, dim3(nru * ch.nch), dim3(kChainNT), lds, s, x, ch);
         hipLaunchKernelGGL(k_v2x_link, dim3(nru), dim3(kChainNT), lds, s, x, ch);
-        hipLaunchKernelGGL(k_v2x_emit, dim3(nru * ch.nch), dim3(kChainNT), lds, s, g, x, ch, ranks, rank_lo, ANS,
-                           (const uint32_t *)Q2, pos_lo, count, out, ma);
+        hipLaunchKernelGGL(k_v2x_emit, dim3(ngrp * ch.nch), dim3(kChainNT), lds, s, g, x, ch, ranks, rank_lo, nout,
+                           ANS, (const uint32_t *)Q2, pos_lo, count, out, ma);
         return hipGetLastError();
     }
     uint32_t *SP = Q2 + tr;                    // merge-path splits: 2 words per tile
@@ -989,7 +1015,7 @@ static hipError_t v2x_pass(const Geometry &g, const V2xGeo &x, const RankDesc *r
         tile(b0, nb, x, per_rank, K1, K2, V, O, Q2, (uint32_t *)nullptr, kTileLds);
     });
     V2xFin f{};
-    f.g = g; f.ranks = ranks; f.rank_lo = rank_lo; f.Q2 = Q2;
+    f.g = g; f.ranks = ranks; f.rank_lo = rank_lo; f.nout = nout; f.Q2 = Q2;
     f.pos_lo = pos_lo; f.count = count; f.out = out; f.ma = ma;
     v2x_global_levels(x, nru, V, O, Vd, Od, SP, 2, f, s);
     return hipGetLastError();
@@ -1008,16 +1034,8 @@ hipError_t launch_v2_exact(const Geometry &g, const RankDesc *ranks, int32_t ran
                                    hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     }();
     if (attr != hipSuccess) return attr;
-    const int32_t per = v2x_ranks_per_pass(g, nr);
-    for (int32_t r0 = 0; r0 < nr; r0 += per) {
-        const int32_t n = nr - r0 < per ? nr - r0 : per;
-        MapArgs ma = mapped ? *mapped : MapArgs{};
-        if (ma.fpos) { ma.fpos += (int64_t)r0 * count; ma.off += (int64_t)r0 * count; }
-        const hipError_t e = v2x_pass(g, x, ranks, rank_lo + r0, n, per, pos_lo, count, epoch,
-                                      out ? out + (int64_t)r0 * count : nullptr, ws, s, ma);
-        if (e != hipSuccess) return e;
-    }
-    return hipSuccess;
+    const MapArgs ma = mapped ? *mapped : MapArgs{};
+    return v2x_pass(g, x, ranks, rank_lo, nr, pos_lo, count, epoch, out, ws, s, ma);
 }
 
 }  // namespace pss

@@ -256,7 +256,9 @@ def test_v2_displacement_bounds():
 
 
 def test_exchange_emit_path_is_the_default():
-    # MI355X passes the start-up lane-order check: the one-exchange-per-step kernel runs
+    # MI355X passes the start-up lane-order check -- the synthetic exchange patterns AND the
+    # replay cross-check (k_v2_emit_x == the order-free probe replay k_v2_emit on two real
+    # geometries, pss_v2.hip xchg_replay_crosscheck): the one-exchange-per-step kernel runs
     eng = _engine(np.full(10, 1000), 10000, 2, 256, 2)
     assert eng.emit_path() == "xchg"
 
