@@ -659,14 +659,14 @@ __global__ __launch_bounds__(kGNT) void k_v2x_gmerge(V2xGeo x, uint32_t w, const
 // tile j is A_j[q] below B_j = alive_at(t0_j), else the tile's own insertion P + t0_j + q - B_j,
 // and A_{j+1}[r] is frame position S_j[r] of tile j.  Three kernels replace the global merge
 // levels: per chunk of tiles the composite survivor map relative to the chunk's start
-// (compose), the chunks' A in rank order (link, one workgroup per rank), then every tile again
-// from its chunk's A, emitting the ids of its steps (emit).
+// (compose), the chunks' A by a parallel prefix over those maps (link levels), then every tile
+// again from its chunk's A, emitting the ids of its steps (emit).
 constexpr uint32_t kAbs = 0x80000000u;   // composite entry: an absolute insertion number
 constexpr int kChainNT = 1024;
 
 struct V2xChain {
     uint32_t nch, tpc;     // chunks per rank, tiles per chunk
-    uint32_t *SV, *CC, *AA;
+    uint32_t *SV, *CC, *AA, *PP;   // PP: the prefix levels' spare buffer (nch maps)
 };
 
 __global__ __launch_bounds__(kChainNT) void k_v2x_compose(V2xGeo x, V2xChain ch) {
@@ -694,27 +694,39 @@ __global__ __launch_bounds__(kChainNT) void k_v2x_compose(V2xGeo x, V2xChain ch)
     for (uint32_t r = threadIdx.x; r < Bend; r += kChainNT) cc[r] = G[r];
 }
 
-__global__ __launch_bounds__(kChainNT) void k_v2x_link(V2xGeo x, V2xChain ch) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-    uint32_t *A = smem, *An = smem + x.P;
-    const uint32_t rl = blockIdx.x;
-    for (uint32_t r = threadIdx.x; r < x.P; r += kChainNT) A[r] = r;   // alive_at(0) = P
-    __syncthreads();
-    for (uint32_t c = 0; c < ch.nch; c++) {
-        const uint32_t j0 = c * ch.tpc, j1 = j0 + ch.tpc < x.tiles1 ? j0 + ch.tpc : x.tiles1;
-        const uint32_t Ba = alive_at(x.P, x.T, j0 * (uint32_t)kTile);
-        const uint32_t te = j1 * (uint32_t)kTile < x.ns ? j1 * (uint32_t)kTile : x.ns;
-        const uint32_t Bm = alive_at(x.P, x.T, te);
-        uint32_t *aa = ch.AA + ((size_t)rl * ch.nch + c) * x.P;
-        const uint32_t *cc = ch.CC + ((size_t)rl * ch.nch + c) * x.P;
-        for (uint32_t r = threadIdx.x; r < Ba; r += kChainNT) aa[r] = A[r];
-        for (uint32_t r = threadIdx.x; r < Bm; r += kChainNT) {
-            const uint32_t v = cc[r];
-            An[r] = (v & kAbs) ? (v & ~kAbs) : A[v];
-        }
-        __syncthreads();
-        uint32_t *t = A; A = An; An = t;
+// The chunks' A as a parallel prefix instead of k_v2x_link's serial walk (one decoded sequence
+// per call since round 5: the walk over ~500 chunks on one workgroup took 0.82 ms at C2).
+// P_c maps the alive set at the END of chunk c to the alive set at the start of chunk
+// c - 2^k + 1 (entries: a frame index, or kAbs | an absolute insertion number); a level doubles
+// the span: P'_c[r] = P_c[r] if absolute, else P_{c-2^k}[P_c[r]] (c >= 2^k).  After
+// ceil(log2 nch) levels P_c reaches chunk 0's start, whose alive set is the identity (A_0[r] = r),
+// so A at chunk c + 1's start is P_c with the flag cleared (k_v2x_link_fin).
+__global__ __launch_bounds__(kChainNT) void k_v2x_link_lvl(V2xGeo x, V2xChain ch, uint32_t span,
+                                                            const uint32_t *__restrict__ src,
+                                                            uint32_t *__restrict__ dst) {
+    const uint32_t c = blockIdx.x;
+    const uint32_t j1 = (c + 1) * ch.tpc < x.tiles1 ? (c + 1) * ch.tpc : x.tiles1;
+    const uint32_t te = j1 * (uint32_t)kTile < x.ns ? j1 * (uint32_t)kTile : x.ns;
+    const uint32_t Bm = alive_at(x.P, x.T, te);
+    const uint32_t *pc = src + (size_t)c * x.P;
+    uint32_t *dc = dst + (size_t)c * x.P;
+    if (c < span) {
+        for (uint32_t r = threadIdx.x; r < Bm; r += kChainNT) dc[r] = pc[r];
+        return;
     }
+    const uint32_t *pp = src + (size_t)(c - span) * x.P;
+    for (uint32_t r = threadIdx.x; r < Bm; r += kChainNT) {
+        const uint32_t v = pc[r];
+        dc[r] = (v & kAbs) ? v : pp[v];
+    }
+}
+
+__global__ __launch_bounds__(kChainNT) void k_v2x_link_fin(V2xGeo x, V2xChain ch, const uint32_t *__restrict__ pref) {
+    const uint32_t c = blockIdx.x;   // A at chunk c's start
+    const uint32_t Ba = alive_at(x.P, x.T, c * ch.tpc * (uint32_t)kTile);
+    uint32_t *aa = ch.AA + (size_t)c * x.P;
+    const uint32_t *pc = pref + (size_t)(c ? c - 1 : 0) * x.P;
+    for (uint32_t r = threadIdx.x; r < Ba; r += kChainNT) aa[r] = c ? (pc[r] & ~kAbs) : r;
 }
 
 // Software-pipelined over the chunk's tiles: a thread's answers and survivor entries of tile
@@ -904,7 +916,7 @@ size_t v2_exact_ws_bytes(const Geometry &g, int32_t nr_all) {
     if (v2x_chain(x)) {   // K1, ANS (ns each), K2, Q2 (T2 each), survivors, chunk maps, chunk starts
         const V2xChain ch = v2x_chain_plan(x, nr);
         return (size_t)nr * ((size_t)2 * x.ns + (size_t)2 * x.T2 + (size_t)x.tiles1 * x.P +
-                             (size_t)2 * ch.nch * x.P) * sizeof(uint32_t);
+                             (size_t)3 * ch.nch * x.P) * sizeof(uint32_t);
     }
     // K1, V, O, Vd, Od (ns each) + K2, Q2 (T2 each), per local rank; tile splits.  Windows
     // beyond kTile are decoded in V, O, Vd, Od (S * B <= ns per rank).
@@ -985,13 +997,22 @@ static hipError_t v2x_pass(const Geometry &g, const V2xGeo &x, const RankDesc *r
         ch.SV = Q2 + tr;
         ch.CC = ch.SV + (size_t)nr * x.tiles1 * x.P;
         ch.AA = ch.CC + (size_t)nr * ch.nch * x.P;
+        ch.PP = ch.AA + (size_t)nr * ch.nch * x.P;
         const uint32_t per_rank = x.tiles1 + x.S;
         v2x_launch_blocks((uint64_t)per_rank * nru, [&](uint64_t b0, uint32_t nb) {
             tile(b0, nb, x, per_rank, K1, K2, ANS, (uint32_t *)nullptr, Q2, ch.SV, kTileLds0);
         });
         const size_t lds = 2 * (size_t)x.P * sizeof(uint32_t);
         hipLaunchKernelGGL(k_v2x_compose, dim3(nru * ch.nch), dim3(kChainNT), lds, s, x, ch);
-        hipLaunchKernelGGL(k_v2x_link, dim3(nru), dim3(kChainNT), lds, s, x, ch);
+        {   // the chunks' A: log2(nch) prefix levels between CC and the spare buffer PP
+            uint32_t *src = ch.CC, *dst = ch.PP;
+            for (uint32_t span = 1; span < ch.nch; span <<= 1) {
+                hipLaunchKernelGGL(k_v2x_link_lvl, dim3(ch.nch), dim3(kChainNT), 0, s, x, ch, span,
+                                   (const uint32_t *)src, dst);
+                uint32_t *t = src; src = dst; dst = t;
+            }
+            hipLaunchKernelGGL(k_v2x_link_fin, dim3(ch.nch), dim3(kChainNT), 0, s, x, ch, (const uint32_t *)src);
+        }
         hipLaunchKernelGGL(k_v2x_emit, dim3(ngrp * ch.nch), dim3(kChainNT), lds, s, g, x, ch, ranks, rank_lo, nout,
                            ANS, (const uint32_t *)Q2, pos_lo, count, out, ma);
         return hipGetLastError();
