@@ -544,30 +544,65 @@ struct V2xFin {
     Geometry g;
     const RankDesc *ranks;
     int32_t rank_lo;
-    int32_t nout;                 // FIN 2: ranks of the call (groups of kFanRanks per grid row y)
+    int32_t nout;                 // ranks of the call
+    uint32_t *VV;                 // FIN 2: the virtual index of every step of the sequence
     uint32_t *Q2;                 // FIN 1: written ([seq][B]); FIN 2: read ([rank][T2])
     int64_t pos_lo, count;
     int64_t *out;
     MapArgs ma;
 };
-// the decoded sequence (rl) is every rank's: ranks [r_a, r_b) of the call get its ids
-__device__ __forceinline__ void v2x_put(const V2xFin &f, const V2xGeo &x, uint32_t rl, int32_t r_a, int32_t r_b,
-                                        uint32_t q, uint32_t t) {
-    if ((int64_t)t < f.pos_lo || (int64_t)t >= f.pos_lo + f.count) return;
-    bool old_side;
-    int64_t v;
+// FIN 2: the decoded sequence's virtual index at step t -- q < P the initial pool1 position, else
+// the element's window base + its pool2 rank (window 0 is the old start's second window,
+// V2:135-138) -- into VV[t] (u32: v < ns < 2^31).  The merge order is by position, so these are
+// scattered 4-byte stores into one sequence-sized array (MALL-resident at C5's 50 MB); the ids of
+// every rank of the call then come from k_v2x_fanout in step order, coalesced.
+__device__ __forceinline__ void v2x_put(const V2xFin &f, const V2xGeo &x, uint32_t rl, uint32_t q, uint32_t t) {
+    uint32_t v;
     if (q < x.P) {
         v = q;
-        old_side = true;
     } else {
         const uint32_t uu = q - x.P, sw = uu / x.B;
-        v = (int64_t)(sw + 1) * x.B + f.Q2[(size_t)rl * x.T2 + uu];
-        old_side = sw == 0;
+        v = (sw + 1u) * x.B + f.Q2[(size_t)rl * x.T2 + uu];
     }
-    for (int32_t r = r_a; r < r_b; r++) {
-        const RankDesc rd = f.ranks[f.rank_lo + r];
-        put_id_or_pair(f.out, f.ma, (int64_t)r * f.count + ((int64_t)t - f.pos_lo),
-                       wrap_id((old_side ? rd.old_start : rd.new_start) + v, f.g.N));
+    f.VV[t] = v;
+}
+
+// ids of nout ranks from the virtual-index stream: v < min(2B, ns) came from the old start, the
+// rest from the new one (V2:135-148), wrapped at N (V2:113-114); one position per thread, its
+// ranks in turn (each rank's row written coalesced)
+// One-shot: 4 consecutive positions per thread (a 16-byte VV load, two 16-byte stores per rank
+// when the rank rows are 16-byte aligned -- the store shape of torch's fill_).
+__global__ __launch_bounds__(256) void k_v2x_fanout(Geometry g, const RankDesc *__restrict__ ranks, int32_t rank_lo,
+                                                    int32_t nout, const uint32_t *__restrict__ VV, int64_t pos_lo,
+                                                    int64_t count, int64_t *__restrict__ out, MapArgs ma) {
+    const int64_t twoB = 2 * g.B < g.ns ? 2 * g.B : g.ns;
+    const int64_t pos_hi = pos_lo + count < g.ns ? pos_lo + count : g.ns;
+    const int64_t t0 = pos_lo + ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+    if (t0 >= pos_hi) return;
+    const bool vec = !ma.fpos && t0 + 4 <= pos_hi && (t0 & 3) == 0 && ((count | pos_lo) & 1) == 0 &&
+                     (((uintptr_t)out) & 15u) == 0;
+    if (vec) {
+        const uint4 w = *(const uint4 *)(VV + t0);
+        const int64_t v[4] = {w.x, w.y, w.z, w.w};
+        for (int32_t r = 0; r < nout; r++) {
+            const RankDesc rd = ranks[rank_lo + r];
+            int64_t id[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) id[k] = wrap_id((v[k] < twoB ? rd.old_start : rd.new_start) + v[k], g.N);
+            longlong2 *o = (longlong2 *)(out + (int64_t)r * count + (t0 - pos_lo));
+            o[0] = make_longlong2(id[0], id[1]);
+            o[1] = make_longlong2(id[2], id[3]);
+        }
+        return;
+    }
+    for (int64_t t = t0; t < t0 + 4 && t < pos_hi; t++) {
+        const int64_t v = VV[t];
+        const bool old_side = v < twoB;
+        for (int32_t r = 0; r < nout; r++) {
+            const RankDesc rd = ranks[rank_lo + r];
+            put_id_or_pair(out, ma, (int64_t)r * count + (t - pos_lo),
+                           wrap_id((old_side ? rd.old_start : rd.new_start) + v, g.N));
+        }
     }
 }
 
@@ -584,12 +619,10 @@ __global__ __launch_bounds__(kGNT) void k_v2x_gmerge(V2xGeo x, uint32_t w, const
     uint32_t *vd = Vd + base, *od = Od + base;
     const uint32_t on = x.ns - o0 < kGTile ? x.ns - o0 : kGTile;
     const uint32_t a = (o0 / (2 * w)) * (2 * w), m = a + w;
-    const int32_t r_a = (int32_t)blockIdx.y * kFanRanks;
-    const int32_t r_b = r_a + kFanRanks < fin.nout ? r_a + kFanRanks : fin.nout;
     auto emit = [&](uint32_t p, uint32_t val, uint32_t st) {   // output p (of the tile) = (val, st)
         if constexpr (FIN == 0) { vd[o0 + p] = val; od[o0 + p] = st; }
         else if constexpr (FIN == 1) fin.Q2[(size_t)rl * x.ns + st] = val;
-        else v2x_put(fin, x, rl, r_a, r_b, val, st);
+        else v2x_put(fin, x, rl, val, st);
     };
     if (m >= x.ns) {                           // lone left block: already merged
         for (uint32_t u = threadIdx.x; u < on; u += kGNT) emit(u, v[o0 + u], o[o0 + u]);
@@ -836,6 +869,9 @@ __global__ __launch_bounds__(kChainNT) void k_v2x_emit(Geometry g, V2xGeo x, V2x
 }
 
 static int64_t v2x_cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+static int64_t pos_hi_of(const Geometry &g, int64_t pos_lo, int64_t count) {
+    return pos_lo + count < g.ns ? pos_lo + count : g.ns;
+}
 
 static V2xGeo v2x_geo(const Geometry &g) {
     V2xGeo x{};
@@ -934,8 +970,7 @@ static void v2x_global_levels(const V2xGeo &x, uint32_t nr, uint32_t *V, uint32_
         const bool last = (uint64_t)2 * w >= x.ns;
         if (!last) hipLaunchKernelGGL(k_v2x_gmerge<0>, gridt, dim3(kGNT), 0, s, x, w, V, O, Vd, Od, SP, fin);
         else if (fin_mode == 1) hipLaunchKernelGGL(k_v2x_gmerge<1>, gridt, dim3(kGNT), 0, s, x, w, V, O, Vd, Od, SP, fin);
-        else hipLaunchKernelGGL(k_v2x_gmerge<2>, dim3(gridt.x, (uint32_t)v2x_cdiv(fin.nout, kFanRanks)), dim3(kGNT), 0, s,
-                                x, w, V, O, Vd, Od, SP, fin);
+        else hipLaunchKernelGGL(k_v2x_gmerge<2>, gridt, dim3(kGNT), 0, s, x, w, V, O, Vd, Od, SP, fin);
         uint32_t *t = V; V = Vd; Vd = t;
         t = O; O = Od; Od = t;
     }
@@ -1038,7 +1073,17 @@ static hipError_t v2x_pass(const Geometry &g, const V2xGeo &x, const RankDesc *r
     V2xFin f{};
     f.g = g; f.ranks = ranks; f.rank_lo = rank_lo; f.nout = nout; f.Q2 = Q2;
     f.pos_lo = pos_lo; f.count = count; f.out = out; f.ma = ma;
+    // the last level's virtual indices go to a spare list buffer: O and Od alternate as the
+    // levels' step lists, V / Vd as their positions; the last level reads one pair and writes
+    // neither, and K1 (the draws, consumed by the pool1 tiles) is free by then
+    f.VV = K1;
     v2x_global_levels(x, nru, V, O, Vd, Od, SP, 2, f, s);
+    {
+        const int64_t n = pos_hi_of(g, pos_lo, count) - (pos_lo & ~(int64_t)3);
+        const uint32_t blocks = (uint32_t)v2x_cdiv(n, 1024);   // (n < 2^31: v2_exact_supported)
+        hipLaunchKernelGGL(k_v2x_fanout, dim3(blocks), dim3(256), 0, s, g, ranks, rank_lo, nout,
+                           (const uint32_t *)K1, pos_lo, count, out, ma);
+    }
     return hipGetLastError();
 }
 

@@ -15,6 +15,7 @@
 #   ab:<lib>:<w>       3 interleaved runs of bench workload w: in-tree library vs <lib> (PSS_LIB)
 #   abx:<lib>:<cfg>    the same for a tools/bench_configs.py config (c2x, c5x, c2v1x, ...)
 #   env:<K=V>:<w>      3 interleaved runs of bench workload w: as is vs with K=V
+#   envx:<K=V>:<cfg>   the same for a tools/bench_configs.py config
 cd "$GRAFT_REPO_ROOT"; O=gpurun_out/$1; shift; mkdir -p $O; export TMPDIR=/tmp
 BN="--no-cpu-baseline --no-latency --no-exact"
 run() {   # run <limit s> <log> <cmd...>
@@ -45,6 +46,10 @@ for s in "$@"; do
          for i in 1 2 3; do
            run 300 abx_${t}_cur_${b}_$i.json python tools/bench_configs.py $b
            run 300 abx_${t}_alt_${b}_$i.json env PSS_LIB=$a python tools/bench_configs.py $b
+         done ;;
+    envx) for i in 1 2 3; do
+           run 300 envx_cur_${b}_$i.json python tools/bench_configs.py $b
+           run 300 envx_alt_${b}_$i.json env "$a" python tools/bench_configs.py $b
          done ;;
     env) for i in 1 2 3; do
            run 240 env_cur_${b}_$i.json python bench.py --steps 100 --workload $b $BN
