@@ -209,7 +209,10 @@ PSS_HD uint32_t slot_draw(uint32_t t, uint32_t s0, uint32_t s1, uint32_t P1) {
 // one step in G), so the residence law of the reference's single pool is kept.
 // ------------------------------------------------------------------------------------------
 constexpr uint32_t kLdsSlotMax = 16384;   // largest V2 pool replayed as one LDS slot table
-constexpr uint32_t kGroupSlots = 4096;    // slots per group (at most)
+#ifndef PSS_GROUP_SLOTS
+#define PSS_GROUP_SLOTS 4096
+#endif
+constexpr uint32_t kGroupSlots = PSS_GROUP_SLOTS;    // slots per group (at most)
 constexpr uint32_t kBurst = 16;           // consecutive steps of one group
 
 struct Groups {

@@ -746,6 +746,106 @@ __device__ void mt_draws_wg(MtWgShared &sh, int cur, uint32_t nd, Bound bound, E
     }
 }
 
+// ---- seeding many streams ahead of their draws ----------------------------------------------
+// The wave-per-stream draw kernels used to seed in the wave itself: ~12K scalar instructions,
+// and a CU's waves take turns on its scalar unit, so with several streams per CU the seeding
+// was a large share of the launch.  k_mt_seed_streams instead runs init_by_array for
+// kMtSeedLanes streams per wave, one per lane on vector registers, the loop-1 words of each in
+// LDS for loop 2; the draw kernels then load the finished 624 words (mt_load).  Stream i's seed
+// is epoch + zero_add for idx = first + i == 0, else epoch + (idx + off) * 10000 (V1:102,165-171:
+// first = w_lo, off = 0, zero_add = 0; V2:107-109,147: first = 0, off = -1, zero_add = 2).
+constexpr int kMtSeedLanes = 16;
+constexpr int kMtSeedPitch = kMtSeedLanes + 1;   // LDS words per state word (conflict-free)
+
+struct MtSeedSpec {
+    int64_t epoch, first, off, zero_add;
+    uint32_t n;   // streams
+};
+
+__device__ __forceinline__ int64_t mt_seed_of(const MtSeedSpec &sp, uint32_t i) {
+    const int64_t idx = sp.first + (int64_t)i;
+    return idx == 0 ? sp.epoch + sp.zero_add : sp.epoch + (idx + sp.off) * 10000;
+}
+
+constexpr int kMtSeedLdsWords = kMtN * kMtSeedPitch;
+
+// streams [blk * kMtSeedLanes, ...) by one wave; t: kMtSeedLdsWords of LDS
+__device__ __forceinline__ void mt_seed_streams_block(const MtSeedSpec &sp, uint32_t *__restrict__ st,
+                                                      uint32_t *t, uint32_t blk) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t s0 = blk * (uint32_t)kMtSeedLanes;
+    if (lane < kMtSeedLanes) {
+        const uint32_t si = s0 + (uint32_t)lane;
+        const int64_t a = mt_seed_of(sp, si < sp.n ? si : s0);
+        const uint64_t m = a < 0 ? (uint64_t)(-(a + 1)) + 1u : (uint64_t)a;
+        const uint32_t key0 = (uint32_t)m, key1 = (uint32_t)(m >> 32);
+        const uint32_t add_even = key0, add_odd = key1 ? key1 + 1u : key0;
+        // loop 1: k = 0..622 at i = k + 1 (step k adds key[k % klen] + k % klen), then the wrap
+        // (mt[0] = mt[623]) and k = 623 at i = 1; init_genrand(19650218)'s words g alongside
+        uint32_t g = 19650218u, prev = g;
+#pragma unroll 2
+        for (int i = 1; i < kMtN; i++) {
+            g = 1812433253u * (g ^ (g >> 30)) + (uint32_t)i;
+            prev = (g ^ ((prev ^ (prev >> 30)) * 1664525u)) + (((i - 1) & 1) ? add_odd : add_even);
+            t[i * kMtSeedPitch + lane] = prev;
+        }
+        const uint32_t v1 = (t[kMtSeedPitch + lane] ^ ((prev ^ (prev >> 30)) * 1664525u)) + add_odd;
+        // loop 2: i = 2..623, the wrap, i = 1.  The loop-1 words come from LDS one block of 8
+        // ahead of the chain (a read waited on at its use would put LDS latency on every step).
+        prev = v1;
+        constexpr int kAhead = 8;
+        static_assert((kMtN - 2) % kAhead == 6, "the last block is short");
+        uint32_t cur[kAhead], nxt[kAhead];
+#pragma unroll
+        for (int k = 0; k < kAhead; k++) cur[k] = t[(2 + k) * kMtSeedPitch + lane];
+        for (int i0 = 2; i0 < kMtN; i0 += kAhead) {
+#pragma unroll
+            for (int k = 0; k < kAhead; k++) {
+                const int i = i0 + kAhead + k;
+                nxt[k] = i < kMtN ? t[i * kMtSeedPitch + lane] : 0u;
+            }
+#pragma unroll
+            for (int k = 0; k < kAhead; k++) {
+                const int i = i0 + k;
+                if (i < kMtN) {
+                    prev = (cur[k] ^ ((prev ^ (prev >> 30)) * 1566083941u)) - (uint32_t)i;
+                    t[i * kMtSeedPitch + lane] = prev;
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < kAhead; k++) cur[k] = nxt[k];
+        }
+        t[kMtSeedPitch + lane] = (v1 ^ ((prev ^ (prev >> 30)) * 1566083941u)) - 1u;
+        t[lane] = 0x80000000u;
+    }
+    wave_lds_order();
+    // each stream's 624 words: coalesced rows
+    for (int l = 0; l < kMtSeedLanes; l++) {
+        if (s0 + (uint32_t)l >= sp.n) break;
+        uint32_t *dst = st + (size_t)(s0 + (uint32_t)l) * kMtN;
+        for (int i = lane; i < kMtN; i += 64) dst[i] = t[i * kMtSeedPitch + l];
+    }
+}
+
+__host__ __device__ __forceinline__ uint32_t mt_seed_blocks(uint32_t n) { return (n + kMtSeedLanes - 1) / kMtSeedLanes; }
+
+__global__ __launch_bounds__(64) void k_mt_seed_streams(MtSeedSpec sp, uint32_t *__restrict__ st) {
+    __shared__ uint32_t t[kMtSeedLdsWords];
+    mt_seed_streams_block(sp, st, t, blockIdx.x);
+}
+
+__host__ __forceinline__ void launch_mt_seed_streams(const MtSeedSpec &sp, uint32_t *st, hipStream_t s) {
+    if (sp.n)
+        hipLaunchKernelGGL(k_mt_seed_streams, dim3(mt_seed_blocks(sp.n)), dim3(64), 0, s, sp, st);
+}
+
+// a stream's state seeded by k_mt_seed_streams, into the wave's LDS
+__device__ __forceinline__ void mt_load(uint32_t *mt, const uint32_t *__restrict__ st) {
+    const int lane = threadIdx.x & 63;
+    for (int i = lane; i < kMtN; i += 64) mt[i] = st[i];
+    wave_lds_order();
+}
+
 // The first _randbelow(n) draw of a freshly seeded stream, ONE SEED PER LANE (V2's tail steps
 // reseed before every draw, V2:107-112, and use only its first word or few).  Seeding is
 // init_by_array over the 1-2 key words (klen), two serial chains of 624 + 623 steps; draw word

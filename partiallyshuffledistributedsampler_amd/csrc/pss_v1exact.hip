@@ -38,21 +38,24 @@ constexpr int32_t kV1FanRanks = 8;   // ranks whose ids one workgroup writes
 
 // Phases 1-2 alone, one wave per window (2.5 KB of LDS, so a CU holds 32 of them): the draws
 // j_i of every window go to HBM (u16, B per window) for k_v1_exact's resolution.  Grid: nw.
+// The windows' MT states come seeded by k_mt_seed_streams (ST: [window slot][624]).
 __global__ __launch_bounds__(64) void k_v1x_draws(Geometry g, int64_t w_lo, int64_t nw, int64_t epoch,
-                                                  uint16_t *__restrict__ J) {
+                                                  const uint32_t *__restrict__ ST, uint16_t *__restrict__ J) {
     __shared__ uint32_t mt[kMtN];
     const int64_t w = w_lo + (int64_t)(blockIdx.x % nw);
     const int64_t wb = w * g.B;
     const int n = (int)(g.ns - wb < g.B ? g.ns - wb : g.B);
     if (n <= 1) return;
     uint16_t *jw = J + (size_t)blockIdx.x * (size_t)(g.B < g.ns ? g.B : g.ns);
-    mt_seed_int(mt, w == 0 ? epoch : epoch + w * 10000);
+    mt_load(mt, ST + (size_t)blockIdx.x * kMtN);
     mt_draws(mt, (uint32_t)(n - 1), [&](uint32_t d) { return (uint32_t)n - d; },
              [&](uint32_t d, uint32_t r) { jw[n - 1 - (int)d] = (uint16_t)r; });
 }
 
 // One workgroup per (rank group, window) of [w_lo, w_lo + nw): the window's permutation, then
-// the ids of ranks [group * kV1FanRanks, ...) of the call (nout ranks from rank_lo).
+// the ids of ranks [group * kV1FanRanks, ...) of the call (nout ranks from rank_lo).  (Writing
+// the window offsets once for a one-shot fan-out grid instead, as the exact V2 does, measured
+// slower at C2: 0.42 -> 0.48 ms -- the resolution, not the stores, sets this kernel's time.)
 __global__ __launch_bounds__(kExactNT) void k_v1_exact(Geometry g, const RankDesc *__restrict__ ranks,
                                                        int32_t rank_lo, int32_t nout, int64_t w_lo, int64_t nw,
                                                        int64_t pos_lo, int64_t count, int64_t epoch,
@@ -504,13 +507,19 @@ size_t v1_exact_lds_bytes(int64_t n) {
 
 bool v1_exact_supported(const Geometry &g) { return g.B < ((int64_t)1 << 31); }
 
+// the windows' seeded MT states follow the draws (16-byte aligned)
+static size_t v1x_st_offset(int64_t jobs, int64_t W) {
+    return ((size_t)jobs * (size_t)W * sizeof(uint16_t) + 15u) & ~(size_t)15u;
+}
+
 size_t v1_exact_ws_bytes(const Geometry &g, int32_t nr, int64_t pos_lo, int64_t count) {
     const int64_t pos_hi = pos_lo + count < g.ns ? pos_lo + count : g.ns;
     if (nr <= 0 || pos_hi <= pos_lo || !v1_exact_supported(g)) return 0;
     const int64_t nw = (pos_hi - 1) / g.B - pos_lo / g.B + 1;
     const int64_t jobs = nw;   // a window's draws and resolution serve every rank of the call
     const int64_t W = g.B < g.ns ? g.B : g.ns;   // the longest window
-    if (W <= kV1ExactMaxB) return (size_t)jobs * (size_t)W * sizeof(uint16_t);
+    if (W <= kV1ExactMaxB)   // the draws (u16), then the windows' seeded MT states
+        return v1x_st_offset(jobs, W) + (size_t)jobs * kMtN * sizeof(uint32_t);
     const int64_t pj = jobs < v1x_jobs_per_pass(W) ? jobs : v1x_jobs_per_pass(W);
     return (size_t)pj * v1x_job_words(W) * sizeof(uint32_t);
 }
@@ -593,10 +602,17 @@ hipError_t launch_v1_exact(const Geometry &g, const RankDesc *ranks, int32_t ran
         (const void *)k_v1_exact, hipFuncAttributeMaxDynamicSharedMemorySize,
         (int)v1_exact_lds_bytes(kV1ExactMaxB));
     if (attr != hipSuccess) return attr;
-    const uint32_t ngrp = (uint32_t)((nr + kV1FanRanks - 1) / kV1FanRanks);
     // with a workspace, the serial MT phases run one wave per window (many windows in flight)
-    // ahead of the resolution; without one, each workgroup's first wave does them in place
-    if (ws) hipLaunchKernelGGL(k_v1x_draws, dim3((uint32_t)nw), dim3(64), 0, s, g, w_lo, nw, epoch, (uint16_t *)ws);
+    // ahead of the resolution, the windows' states seeded before them (k_mt_seed_streams, 16
+    // streams a wave on vector registers); without one, each workgroup's first wave does them
+    // in place
+    const uint32_t ngrp = (uint32_t)((nr + kV1FanRanks - 1) / kV1FanRanks);
+    if (ws) {
+        uint32_t *ST = (uint32_t *)((char *)ws + v1x_st_offset(nw, g.B < g.ns ? g.B : g.ns));
+        launch_mt_seed_streams(MtSeedSpec{epoch, w_lo, 0, 0, (uint32_t)nw}, ST, s);
+        hipLaunchKernelGGL(k_v1x_draws, dim3((uint32_t)nw), dim3(64), 0, s, g, w_lo, nw, epoch,
+                           (const uint32_t *)ST, (uint16_t *)ws);
+    }
     hipLaunchKernelGGL(k_v1_exact, dim3((uint32_t)(ngrp * nw)), dim3(kExactNT), lds, s, g, ranks, rank_lo, nr,
                        w_lo, nw, pos_lo, count, epoch, (const uint16_t *)ws, out, ma);
     return hipGetLastError();

@@ -63,26 +63,6 @@ __device__ __forceinline__ uint32_t alive_at(uint32_t B0, uint32_t insu, uint32_
 }
 }  // namespace
 
-// ---- draws: one wave per pool2 window's MT stream -----------------------------------------------
-__global__ __launch_bounds__(64) void k_v2x_draws(V2xGeo x, int64_t epoch, uint32_t jobs, uint64_t blk0,
-                                                  uint32_t *__restrict__ K1, uint32_t *__restrict__ K2) {
-    __shared__ uint32_t mt[kMtN];
-    const uint64_t b = blk0 + blockIdx.x;
-    const uint32_t rl = (uint32_t)(b / jobs), job = (uint32_t)(b % jobs);
-    uint32_t *k1 = K1 + (size_t)rl * x.ns;
-    uint32_t *k2 = K2 + (size_t)rl * x.T2;
-    if (job < x.S) {          // pool2 window s: k1, k2 alternating from its own stream
-        const uint32_t s = job;
-        const uint32_t W = x.T - s * x.B < x.B ? x.T - s * x.B : x.B, t0 = s * x.B;
-        mt_seed_int(mt, s == 0 ? epoch + 2 : epoch + (int64_t)(s - 1) * 10000);
-        mt_draws_pair(mt, W, x.P, [&](bool second, uint32_t i, uint32_t r) {
-            if (second) k2[t0 + i] = r;
-            else k1[t0 + i] = r;
-        });
-        for (uint32_t u = W + threadIdx.x; u < x.B; u += 64) k2[t0 + u] = 0;   // padding steps
-    }
-}
-
 // seed of tail step j (pool2 stays empty: every step reseeds first, V2:107-109)
 __device__ __forceinline__ int64_t v2x_tail_seed(const V2xGeo &x, int64_t epoch, uint32_t j) {
     return x.S >= 1 ? epoch + (int64_t)(x.S - 1 + j) * 10000
@@ -115,6 +95,38 @@ __device__ __forceinline__ void v2x_tail_block(const V2xGeo &x, int64_t epoch, u
         const uint32_t nl = x.P - jl, t = x.T + jl;
         mt_draws(mt, 1u, [&](uint32_t) { return nl; }, [&](uint32_t, uint32_t rr) { k1[t] = rr; });
         wave_lds_order();
+    }
+}
+
+// ---- seeding: the windows' MT states (k_mt_seed_streams' blocks), the tail draws alongside ----
+// Both are latency-bound chains on few waves (C2: 191 seeding waves, 64 tail waves), so they share
+// one launch ahead of the window draws.
+__global__ __launch_bounds__(64) void k_v2x_seed(MtSeedSpec sp, uint32_t *__restrict__ ST, V2xGeo x, int64_t epoch,
+                                                 uint32_t *__restrict__ K1) {
+    __shared__ uint32_t t[kMtSeedLdsWords];
+    const uint32_t nsb = mt_seed_blocks(sp.n);
+    if (blockIdx.x < nsb) mt_seed_streams_block(sp, ST, t, blockIdx.x);
+    else v2x_tail_block(x, epoch, 0u, (blockIdx.x - nsb) * 64u, K1, t);
+}
+
+// ---- draws: one wave per pool2 window's MT stream -----------------------------------------------
+// The windows' MT states come seeded by k_v2x_seed (ST: [window][624]).
+__global__ __launch_bounds__(64) void k_v2x_draws(V2xGeo x, uint32_t jobs, uint64_t blk0, const uint32_t *__restrict__ ST,
+                                                  uint32_t *__restrict__ K1, uint32_t *__restrict__ K2) {
+    __shared__ uint32_t mt[kMtN];
+    const uint64_t b = blk0 + blockIdx.x;
+    const uint32_t rl = (uint32_t)(b / jobs), job = (uint32_t)(b % jobs);
+    uint32_t *k1 = K1 + (size_t)rl * x.ns;
+    uint32_t *k2 = K2 + (size_t)rl * x.T2;
+    if (job < x.S) {          // pool2 window s: k1, k2 alternating from its own stream
+        const uint32_t s = job;
+        const uint32_t W = x.T - s * x.B < x.B ? x.T - s * x.B : x.B, t0 = s * x.B;
+        mt_load(mt, ST + (size_t)s * kMtN);
+        mt_draws_pair(mt, W, x.P, [&](bool second, uint32_t i, uint32_t r) {
+            if (second) k2[t0 + i] = r;
+            else k1[t0 + i] = r;
+        });
+        for (uint32_t u = W + threadIdx.x; u < x.B; u += 64) k2[t0 + u] = 0;   // padding steps
     }
 }
 
@@ -567,20 +579,22 @@ __device__ __forceinline__ void v2x_put(const V2xFin &f, const V2xGeo &x, uint32
     f.VV[t] = v;
 }
 
-// ids of nout ranks from the virtual-index stream: v < min(2B, ns) came from the old start, the
-// rest from the new one (V2:135-148), wrapped at N (V2:113-114); one position per thread, its
-// ranks in turn (each rank's row written coalesced)
+// ids of nout ranks from the virtual-index stream VV (position t at VV[t - vv_lo]): v < old_lim
+// came from the old start, the rest from the new one (V2:135-148: old_lim = min(2B, ns); V1:
+// 0, every id from the new start), wrapped at N (V2:113-114); each rank's row written coalesced.
 // One-shot: 4 consecutive positions per thread (a 16-byte VV load, two 16-byte stores per rank
 // when the rank rows are 16-byte aligned -- the store shape of torch's fill_).
 __global__ __launch_bounds__(256) void k_v2x_fanout(Geometry g, const RankDesc *__restrict__ ranks, int32_t rank_lo,
-                                                    int32_t nout, const uint32_t *__restrict__ VV, int64_t pos_lo,
-                                                    int64_t count, int64_t *__restrict__ out, MapArgs ma) {
-    const int64_t twoB = 2 * g.B < g.ns ? 2 * g.B : g.ns;
+                                                    int32_t nout, const uint32_t *__restrict__ VV, int64_t vv_lo,
+                                                    int64_t old_lim, int64_t pos_lo, int64_t count,
+                                                    int64_t *__restrict__ out, MapArgs ma) {
+    const int64_t twoB = old_lim;
     const int64_t pos_hi = pos_lo + count < g.ns ? pos_lo + count : g.ns;
     const int64_t t0 = pos_lo + ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
     if (t0 >= pos_hi) return;
+    VV -= vv_lo;
     const bool vec = !ma.fpos && t0 + 4 <= pos_hi && (t0 & 3) == 0 && ((count | pos_lo) & 1) == 0 &&
-                     (((uintptr_t)out) & 15u) == 0;
+                     (((uintptr_t)out) & 15u) == 0 && (vv_lo & 3) == 0;
     if (vec) {
         const uint4 w = *(const uint4 *)(VV + t0);
         const int64_t v[4] = {w.x, w.y, w.z, w.w};
@@ -770,12 +784,16 @@ constexpr int kChainPer = kTile / kChainNT;
 static_assert(kChainPer * kChainNT == kTile, "a tile's steps and survivors: kChainPer per thread");
 
 // The decoded sequence is every rank's (the draws depend on the epoch and the window only,
-// V2:108,147): block (chunk c, group) writes the ids of ranks [group * kFanRanks, ...) of the call.
+// V2:108,147): block (chunk c, group) writes the ids of ranks [group * kFanRanks, ...) of the call
+// -- or, with VV, the virtual indices alone (4 bytes a step), which k_v2x_fanout turns into every
+// rank's ids as a one-shot grid (more than one rank: this kernel's ~500 long-running workgroups
+// store at about half the rate of a one-shot grid).
 __global__ __launch_bounds__(kChainNT) void k_v2x_emit(Geometry g, V2xGeo x, V2xChain ch,
                                                        const RankDesc *__restrict__ ranks, int32_t rank_lo,
                                                        int32_t nout, const uint32_t *__restrict__ ANS,
                                                        const uint32_t *__restrict__ Q2, int64_t pos_lo,
-                                                       int64_t count, int64_t *__restrict__ out, MapArgs ma) {
+                                                       int64_t count, int64_t *__restrict__ out, MapArgs ma,
+                                                       uint32_t *__restrict__ VV) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     uint32_t *A = smem, *An = smem + x.P;
     const uint32_t rl = 0, c = blockIdx.x % ch.nch;
@@ -852,6 +870,10 @@ __global__ __launch_bounds__(kChainNT) void k_v2x_emit(Geometry g, V2xGeo x, V2x
                 v = (int64_t)(sw + 1) * x.B + g2[k];
                 old_side = sw == 0;
             }
+            if (VV) {
+                VV[t] = (uint32_t)v;
+                continue;
+            }
             for (int32_t r = r_a; r < r_b; r++) {   // (wave-uniform rank: scalar descriptor loads)
                 const RankDesc rd = ranks[rank_lo + r];
                 put_id_or_pair(out, ma, (int64_t)r * count + (t - pos_lo),
@@ -871,6 +893,23 @@ __global__ __launch_bounds__(kChainNT) void k_v2x_emit(Geometry g, V2xGeo x, V2x
 static int64_t v2x_cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 static int64_t pos_hi_of(const Geometry &g, int64_t pos_lo, int64_t count) {
     return pos_lo + count < g.ns ? pos_lo + count : g.ns;
+}
+
+void launch_id_fanout(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, int32_t nout,
+                      const uint32_t *VV, int64_t vv_lo, int64_t old_lim, int64_t pos_lo, int64_t count,
+                      int64_t *out, const MapArgs &ma, hipStream_t s) {
+    const int64_t n = pos_hi_of(g, pos_lo, count) - pos_lo;
+    const uint32_t blocks = (uint32_t)v2x_cdiv(n, 1024);   // (n < 2^31: one exact call's positions)
+    if (blocks)
+        hipLaunchKernelGGL(k_v2x_fanout, dim3(blocks), dim3(256), 0, s, g, ranks, rank_lo, nout, VV, vv_lo,
+                           old_lim, pos_lo, count, out, ma);
+}
+
+static void v2x_launch_fanout(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, int32_t nout,
+                              const uint32_t *VV, int64_t pos_lo, int64_t count, int64_t *out,
+                              const MapArgs &ma, hipStream_t s) {
+    const int64_t twoB = 2 * g.B < g.ns ? 2 * g.B : g.ns;
+    launch_id_fanout(g, ranks, rank_lo, nout, VV, 0, twoB, pos_lo, count, out, ma, s);
 }
 
 static V2xGeo v2x_geo(const Geometry &g) {
@@ -945,18 +984,23 @@ static V2xChain v2x_chain_plan(const V2xGeo &x, int32_t nr) {
     return ch;
 }
 
-size_t v2_exact_ws_bytes(const Geometry &g, int32_t nr_all) {
-    if (!v2_exact_supported(g) || nr_all <= 0) return 0;
+// workspace words before the windows' seeded MT states (S x 624, the one-wave draw form)
+static size_t v2x_base_words(const V2xGeo &x) {
     const int32_t nr = 1;   // one decoded sequence serves every rank of a call (v2x_pass)
-    const V2xGeo x = v2x_geo(g);
     if (v2x_chain(x)) {   // K1, ANS (ns each), K2, Q2 (T2 each), survivors, chunk maps, chunk starts
         const V2xChain ch = v2x_chain_plan(x, nr);
         return (size_t)nr * ((size_t)2 * x.ns + (size_t)2 * x.T2 + (size_t)x.tiles1 * x.P +
-                             (size_t)3 * ch.nch * x.P) * sizeof(uint32_t);
+                             (size_t)3 * ch.nch * x.P);
     }
     // K1, V, O, Vd, Od (ns each) + K2, Q2 (T2 each), per local rank; tile splits.  Windows
     // beyond kTile are decoded in V, O, Vd, Od (S * B <= ns per rank).
-    return ((size_t)nr * ((size_t)5 * x.ns + (size_t)2 * x.T2) + v2x_split_words(x, nr)) * sizeof(uint32_t);
+    return (size_t)nr * ((size_t)5 * x.ns + (size_t)2 * x.T2) + v2x_split_words(x, nr);
+}
+
+size_t v2_exact_ws_bytes(const Geometry &g, int32_t nr_all) {
+    if (!v2_exact_supported(g) || nr_all <= 0) return 0;
+    const V2xGeo x = v2x_geo(g);
+    return (v2x_base_words(x) + (size_t)x.S * kMtN) * sizeof(uint32_t);
 }
 
 // global merge levels w = kTile, 2 kTile, ... of nr sequences of x.ns > kTile steps (V, O sorted
@@ -1000,14 +1044,18 @@ static hipError_t v2x_pass(const Geometry &g, const V2xGeo &x, const RankDesc *r
         // few long windows (the streams alone do not fill the chip): a workgroup per stream, the
         // tail draws riding along on the idle CUs
         const bool wg = v2x_draws_wg((uint64_t)x.S * (uint64_t)nr, x.B);
+        uint32_t *ST = ws + v2x_base_words(x);
         const uint64_t wblocks = (uint64_t)x.S * (uint64_t)nr;
         const uint64_t tblocks = wg ? ((uint64_t)tail_blocks * (uint64_t)nr + kMtWgWaves - 1) / kMtWgWaves : 0u;
+        if (!wg)   // (nr = 1: one decoded sequence; S < 2^31 / B windows, tail_blocks <= 2^24)
+            hipLaunchKernelGGL(k_v2x_seed, dim3(mt_seed_blocks(x.S) + tail_blocks), dim3(64), 0, s,
+                               MtSeedSpec{epoch, 0, -1, 2, x.S}, ST, x, epoch, K1);
         v2x_launch_blocks(wblocks + tblocks, [&](uint64_t b0, uint32_t nb) {
             if (wg) hipLaunchKernelGGL(k_v2x_draws_wg, dim3(nb), dim3(kMtWgThreads), 0, s, x, epoch, x.S, b0,
                                        (uint32_t)nr, tail_blocks, K1, K2);
-            else hipLaunchKernelGGL(k_v2x_draws, dim3(nb), dim3(64), 0, s, x, epoch, x.S, b0, K1, K2);
+            else hipLaunchKernelGGL(k_v2x_draws, dim3(nb), dim3(64), 0, s, x, x.S, b0, (const uint32_t *)ST, K1, K2);
         });
-        tail_done = wg;
+        tail_done = true;
     }
     if (!tail_done)
         v2x_launch_blocks((uint64_t)tail_blocks * (uint64_t)nr, [&](uint64_t b0, uint32_t nb) {
@@ -1048,8 +1096,11 @@ static hipError_t v2x_pass(const Geometry &g, const V2xGeo &x, const RankDesc *r
             }
             hipLaunchKernelGGL(k_v2x_link_fin, dim3(ch.nch), dim3(kChainNT), 0, s, x, ch, (const uint32_t *)src);
         }
-        hipLaunchKernelGGL(k_v2x_emit, dim3(ngrp * ch.nch), dim3(kChainNT), lds, s, g, x, ch, ranks, rank_lo, nout,
-                           ANS, (const uint32_t *)Q2, pos_lo, count, out, ma);
+        // K1 (the draws) is free once the tiles ran: the virtual indices for the fan-out
+        const bool fan = nout > 1;
+        hipLaunchKernelGGL(k_v2x_emit, dim3((fan ? 1u : ngrp) * ch.nch), dim3(kChainNT), lds, s, g, x, ch, ranks,
+                           rank_lo, nout, ANS, (const uint32_t *)Q2, pos_lo, count, out, ma, fan ? K1 : nullptr);
+        if (fan) v2x_launch_fanout(g, ranks, rank_lo, nout, K1, pos_lo, count, out, ma, s);
         return hipGetLastError();
     }
     uint32_t *SP = Q2 + tr;                    // merge-path splits: 2 words per tile
@@ -1078,12 +1129,7 @@ static hipError_t v2x_pass(const Geometry &g, const V2xGeo &x, const RankDesc *r
     // neither, and K1 (the draws, consumed by the pool1 tiles) is free by then
     f.VV = K1;
     v2x_global_levels(x, nru, V, O, Vd, Od, SP, 2, f, s);
-    {
-        const int64_t n = pos_hi_of(g, pos_lo, count) - (pos_lo & ~(int64_t)3);
-        const uint32_t blocks = (uint32_t)v2x_cdiv(n, 1024);   // (n < 2^31: v2_exact_supported)
-        hipLaunchKernelGGL(k_v2x_fanout, dim3(blocks), dim3(256), 0, s, g, ranks, rank_lo, nout,
-                           (const uint32_t *)K1, pos_lo, count, out, ma);
-    }
+    v2x_launch_fanout(g, ranks, rank_lo, nout, K1, pos_lo, count, out, ma, s);
     return hipGetLastError();
 }
 

@@ -17,8 +17,9 @@
 
 constexpr uint64_t kIds = 100000000ull;
 constexpr int kWaves = 2048;
+constexpr int kMaxWaves = 8192;
 
-struct Stats { unsigned long long xcc_bytes[8]; unsigned long long end[kWaves]; unsigned long long t0; unsigned int xcc[kWaves]; };
+struct Stats { unsigned long long xcc_bytes[8]; unsigned long long end[kMaxWaves]; unsigned long long t0; unsigned int xcc[kMaxWaves]; };
 
 __device__ __forceinline__ uint32_t xcc_id() { return __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (15 << 11)) & 7u; }
 
@@ -150,6 +151,72 @@ __global__ __launch_bounds__(64) void persist_x(int64_t *o, uint64_t n, int64_t 
     record(st, c1 - c0);
 }
 
+// own runs with 16-byte stores: lane l writes ids 2l, 2l + 1 of each 128-id half chunk (each
+// store instruction 1 KB contiguous, the shape of oneshot4)
+__global__ __launch_bounds__(64) void persist_r16(int64_t *o, uint64_t n, int64_t salt, Stats *st) {
+    extern __shared__ uint32_t pad[];
+    if (n == 0) pad[threadIdx.x] = 0;
+    const uint64_t chunks = n / 256, per = chunks / gridDim.x;
+    for (uint64_t c = blockIdx.x * per; c < blockIdx.x * per + per; c++) {
+        int64_t *p = o + c * 256;
+#pragma unroll
+        for (int j = 0; j < 2; j++) {
+            const uint64_t i = 128 * j + 2 * threadIdx.x;
+            longlong2 a;
+            a.x = (int64_t)(c * 256 + i) + salt; a.y = (int64_t)(c * 256 + i + 1) + salt;
+            *(longlong2 *)(p + i) = a;
+        }
+    }
+    record(st, per);
+}
+
+// own runs with 16-byte stores after a lane exchange: the values come out as the replay makes
+// them (lane l holds ids l + 64 j, j < 4) and two ds_bpermute-style shuffles per pair of
+// registers move them to lane order 2l, 2l + 1
+__global__ __launch_bounds__(64) void persist_r16x(int64_t *o, uint64_t n, int64_t salt, Stats *st) {
+    extern __shared__ uint32_t pad[];
+    if (n == 0) pad[threadIdx.x] = 0;
+    const uint64_t chunks = n / 256, per = chunks / gridDim.x;
+    const int l = threadIdx.x;
+    for (uint64_t c = blockIdx.x * per; c < blockIdx.x * per + per; c++) {
+        int64_t *p = o + c * 256;
+        int64_t v[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) v[j] = (int64_t)(c * 256 + 64 * j + l) + salt;
+#pragma unroll
+        for (int h = 0; h < 2; h++) {   // ids [128 h, 128 h + 128): registers 2h, 2h + 1
+            const int s0 = (2 * l) & 63, s1 = (2 * l + 1) & 63;
+            const bool hi = l >= 32;
+            const int64_t a0 = __shfl(v[2 * h], s0), b0 = __shfl(v[2 * h + 1], s0);
+            const int64_t a1 = __shfl(v[2 * h], s1), b1 = __shfl(v[2 * h + 1], s1);
+            longlong2 a;
+            a.x = hi ? b0 : a0; a.y = hi ? b1 : a1;
+            *(longlong2 *)(p + 128 * h + 2 * l) = a;
+        }
+    }
+    record(st, per);
+}
+
+// the same bytes per wave, chunk-interleaved over groups of IL waves: wave w = IL a + b writes
+// chunks base_a + c IL + b, so the waves of a group write adjacent 2 KB chunks at any moment
+// (IL = gridDim: the whole grid sweeps the output together, like a one-shot grid)
+template <int IL>
+__global__ __launch_bounds__(64) void persist_il(int64_t *o, uint64_t n, int64_t salt, Stats *st) {
+    extern __shared__ uint32_t pad[];
+    if (n == 0) pad[threadIdx.x] = 0;
+    const uint64_t chunks = n / 256, per = chunks / gridDim.x;
+    const uint64_t il = IL ? IL : gridDim.x;
+    const uint64_t a = blockIdx.x / il, b = blockIdx.x % il;
+    const uint64_t base = a * il * per;
+    for (uint64_t c = 0; c < per; c++) {
+        const uint64_t ch = base + c * il + b;
+        int64_t *p = o + ch * 256;
+#pragma unroll
+        for (int j = 0; j < 4; j++) p[64 * j + threadIdx.x] = (int64_t)(ch * 256 + 64 * j + threadIdx.x) + salt;
+    }
+    record(st, per);
+}
+
 __global__ void stamp_t0(Stats *st) { if (threadIdx.x == 0) st->t0 = __builtin_amdgcn_s_memrealtime(); }
 
 template <class F>
@@ -177,7 +244,7 @@ void timeit(const char *name, Stats *st, unsigned long long *ctr, F launch) {
            (double)kIds * 8 / (sum / 10 * 1e-3) / 1e12);
     if (h.t0) {
         std::vector<double> e, ex[8];
-        for (int i = 0; i < kWaves; i++) if (h.end[i]) {
+        for (int i = 0; i < kMaxWaves; i++) if (h.end[i]) {
             e.push_back((h.end[i] - h.t0) / 100.0);
             ex[h.xcc[i] & 7].push_back((h.end[i] - h.t0) / 100.0);
         }
@@ -207,12 +274,25 @@ int main() {
     for (auto fn : {(const void *)persist_r, (const void *)queue<8>, (const void *)queue<32>, (const void *)queue<128>,
                     (const void *)guided, (const void *)persist_bar<4, 8>, (const void *)persist_bar<8, 8>,
                     (const void *)persist_bar<8, 1>, (const void *)persist_bar<8, 0>, (const void *)persist_x<14>,
-                    (const void *)persist_x<13>, (const void *)persist_x<12>})
+                    (const void *)persist_x<13>, (const void *)persist_x<12>, (const void *)persist_r16,
+                    (const void *)persist_r16x, (const void *)persist_il<0>, (const void *)persist_il<8>,
+                    (const void *)persist_il<64>, (const void *)persist_il<256>})
         (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     const size_t lds = 18220;   // 8 one-wave blocks per CU, as the replay
     for (int rep = 0; rep < 2; rep++) {
         timeit("oneshot4", st, ctr, [&](int s) { hipLaunchKernelGGL(oneshot4, dim3((uint32_t)((n / 4 + 255) / 256)), dim3(256), 0, 0, o, n, (int64_t)s); });
         timeit("persist_r", st, ctr, [&](int s) { hipLaunchKernelGGL(persist_r, dim3(kWaves), dim3(64), lds, 0, o, n, (int64_t)s, st); });
+        timeit("il_all", st, ctr, [&](int s) { hipLaunchKernelGGL(persist_il<0>, dim3(kWaves), dim3(64), lds, 0, o, n, (int64_t)s, st); });
+        timeit("il_8", st, ctr, [&](int s) { hipLaunchKernelGGL(persist_il<8>, dim3(kWaves), dim3(64), lds, 0, o, n, (int64_t)s, st); });
+        timeit("il_64", st, ctr, [&](int s) { hipLaunchKernelGGL(persist_il<64>, dim3(kWaves), dim3(64), lds, 0, o, n, (int64_t)s, st); });
+        timeit("il_256", st, ctr, [&](int s) { hipLaunchKernelGGL(persist_il<256>, dim3(kWaves), dim3(64), lds, 0, o, n, (int64_t)s, st); });
+        if (rep == 0) continue;
+        timeit("persist_r16", st, ctr, [&](int s) { hipLaunchKernelGGL(persist_r16, dim3(kWaves), dim3(64), lds, 0, o, n, (int64_t)s, st); });
+        timeit("persist_r16x", st, ctr, [&](int s) { hipLaunchKernelGGL(persist_r16x, dim3(kWaves), dim3(64), lds, 0, o, n, (int64_t)s, st); });
+        timeit("persist_4096", st, ctr, [&](int s) { hipLaunchKernelGGL(persist_r, dim3(4096), dim3(64), lds, 0, o, n, (int64_t)s, st); });
+        timeit("persist_8192", st, ctr, [&](int s) { hipLaunchKernelGGL(persist_r, dim3(8192), dim3(64), lds, 0, o, n, (int64_t)s, st); });
+        timeit("r16_8192", st, ctr, [&](int s) { hipLaunchKernelGGL(persist_r16, dim3(8192), dim3(64), lds, 0, o, n, (int64_t)s, st); });
+        if (rep == 0) continue;
         timeit("queue_256K", st, ctr, [&](int s) { hipLaunchKernelGGL(queue<128>, dim3(kWaves), dim3(64), lds, 0, o, n, (int64_t)s, st, ctr); });
         timeit("xsplit_14", st, ctr, [&](int s) { hipLaunchKernelGGL(persist_x<14>, dim3(kWaves), dim3(64), lds, 0, o, n, (int64_t)s, st); });
         timeit("xsplit_13", st, ctr, [&](int s) { hipLaunchKernelGGL(persist_x<13>, dim3(kWaves), dim3(64), lds, 0, o, n, (int64_t)s, st); });
