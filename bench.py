@@ -453,7 +453,7 @@ def main():
                     help="time the steps without the per-launch HIP events (roofline omitted)")
     ap.add_argument("--pipeline", type=int, default=1,
                     help="epochs in flight: 2 alternates two streams and output buffers")
-    ap.add_argument("--timing-every", type=int, default=4,
+    ap.add_argument("--timing-every", type=int, default=16,
                     help="HIP-event timing of the generation kernel on every n-th timed step")
     args = ap.parse_args()
 
@@ -516,8 +516,8 @@ def main():
     if distributed:
         dist.barrier()
     # live timing of the dominant kernel: two HIP events around the generation kernel on its
-    # stream, on every 4th step of the timed region (events around every launch cost ~4 % of
-    # the step, two per step ~3 %)
+    # stream, on every 16th step of the timed region (C2, same box: every 4th step 557-559 G
+    # idx/s, every 16th 564-565, none 567; profiles/r05/bench_overheads.txt)
     eng.profile(not args.no_kernel_timing, generation_only=True, every=args.timing_every)
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
