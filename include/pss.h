@@ -181,8 +181,10 @@ int pss_emit_path(pss_sampler *h, int32_t *path);
  *       Device workspace: V1 windows beyond 16000 entries take ~18 B per entry of the windows
  *       one pass resolves (J, S, H, PART as u32 and PARTP as u16: <= 2.3 GB up to 2^27-entry
  *       windows, one window per pass beyond: ~19 GB at shuffle_buffer = 2^30, ~39 GB near
- *       2^31); V2 ~28 B per position of the ranks of a pass.  A
- *       workspace the device cannot hold makes pss_generate return PSS_EHIP.
+ *       2^31), windows up to 16000 entries 2 B per position and 2.5 KB per window (its
+ *       seeded MT state); V2 ~28 B per position of num_samples and 2.5 KB per pool2 window --
+ *       one decode serves every rank of a call, whatever their number.  A workspace the
+ *       device cannot hold makes pss_generate return PSS_EHIP.
  * Replaces nothing in the reference: its order IS the exact one. */
 #define PSS_ORDER_COUNTER 0
 #define PSS_ORDER_EXACT 1
