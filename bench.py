@@ -378,37 +378,53 @@ def handoff_figures(device, reps=5):
 
 def exact_order_figures(device):
     """order="exact" (the reference's own CPython-MT19937 draws, bit-identical id streams) at
-    the bench shapes: C2 (V2 and V1, B = 4096) and C5's pool (B = 2^20), all 8 logical ranks,
-    one warm-up epoch then timed epochs; ms per epoch (init_iter + generate, synchronised), G
-    idx/s, and the exact pipeline's span on the stream (HIP events around the launch)."""
+    the bench shapes: C2 (V2 and V1, B = 4096) and C5's pool (B = 2^20), all 8 logical ranks.
+    cold: an epoch that does not follow the previous call's, drawn in its own call; steady:
+    consecutive epochs after two warm-up epochs, the draws of the coming epochs made ahead on side streams (the
+    exact lookahead); ms per epoch (init_iter + generate, synchronised), G idx/s, and the
+    pipeline's span on the caller's stream (HIP events around the launch)."""
     res = {}
-    for name, cfg, ver, reps in (("c2_v2", "c2", 2, 3), ("c2_v1", "c2", 1, 3), ("c5_v2", "c5", 2, 2),
-                                 ("c5_v1", "c5", 1, 2)):
+    for name, cfg, ver, reps in (("c2_v2", "c2", 2, 12), ("c2_v1", "c2", 1, 12), ("c5_v2", "c5", 2, 12),
+                                 ("c5_v1", "c5", 1, 12)):
         lengths, N, R, B, _ = W.shape(cfg)
         eng = IndexEngine(lengths, N, R, B, ver, seed=0, device=device, order="exact")
         ns = eng.num_samples
         out = torch.empty((R, ns), dtype=torch.int64, device=device)
-        eng.init_iter(0)
+        eng.init_iter(0)                 # workspaces
         eng.generate(0, R, out=out)
+        torch.cuda.synchronize(device)
+        t0 = time.perf_counter()
+        eng.init_iter(5)                 # not epoch 0 + 1: its own draws, none made ahead
+        eng.generate(0, R, out=out)
+        torch.cuda.synchronize(device)
+        cold = (time.perf_counter() - t0) * 1e3
+        for e in (6, 7):                 # 6 queues the draws of 7, 8, ...
+            eng.init_iter(e)
+            eng.generate(0, R, out=out)
         torch.cuda.synchronize(device)
         eng.profile(True)
         t0 = time.perf_counter()
         for e in range(reps):
-            eng.init_iter(1 + e)
+            eng.init_iter(8 + e)
             eng.generate(0, R, out=out)
-        torch.cuda.synchronize(device)
+        # the caller's stream: the draws made ahead for the epochs after these belong to them
+        torch.cuda.current_stream(device).synchronize()
         ms = (time.perf_counter() - t0) / reps * 1e3
+        torch.cuda.synchronize(device)
         prof = eng.profile_read()
         eng.check()
         eng.close()
         kname = "v2_emit" if ver == 2 else "v1_window"
         k_ms, k_n = prof.get(kname, (0.0, 0))
         res[name] = {"ms_per_epoch": ms, "G_idx_per_s": R * ns / ms / 1e6,
+                     "cold_ms_per_epoch": cold,
                      "pipeline_ms_per_epoch": k_ms / max(1, k_n), "ids_per_epoch": R * ns,
                      "shuffle_buffer": B}
         del out
     res["config"] = ("order='exact' (CPython MT19937 draws: the reference's id streams bit for bit); "
-                     "c2: 10K files x 10K, R=8, B=4096; c5: the same files, B=2^20; all 8 ranks per epoch")
+                     "c2: 10K files x 10K, R=8, B=4096; c5: the same files, B=2^20; all 8 ranks per epoch; "
+                     "ms_per_epoch: consecutive epochs (draws made ahead), cold: an epoch that does not "
+                     "follow the previous call's (its own draws)")
     return res
 
 

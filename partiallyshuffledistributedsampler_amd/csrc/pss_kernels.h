@@ -118,7 +118,13 @@ size_t v1_exact_ws_bytes(const Geometry &g, int32_t nr, int64_t pos_lo, int64_t 
 // place of the ids (out unused), through the global bucketed map -- same values as pss_map
 hipError_t launch_v1_exact(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, int32_t nr,
                            int64_t pos_lo, int64_t count, int64_t epoch, int64_t *out, void *ws,
-                           hipStream_t s, const MapArgs *mapped = nullptr);
+                           hipStream_t s, const MapArgs *mapped = nullptr, uint32_t *slot = nullptr);
+// a draw slot of a call's windows (0 bytes: none -- windows through HBM in several passes) and
+// the epochs the runtime draws ahead for it (as the V2 slots below)
+size_t v1_exact_slot_bytes(const Geometry &g, int64_t pos_lo, int64_t count);
+int v1_exact_lookahead_depth(const Geometry &g, int64_t pos_lo, int64_t count);
+hipError_t launch_v1_exact_draws(const Geometry &g, int64_t pos_lo, int64_t count, int64_t epoch,
+                                 uint32_t *slot, hipStream_t s);
 
 // ids of nout ranks from one decoded stream of virtual indices (exact order: every rank of a call
 // shares it): position t's v = VV[t - vv_lo]; id = wrap(v < old_lim ? old_start + v : new_start + v)
@@ -130,9 +136,15 @@ void launch_id_fanout(const Geometry &g, const RankDesc *ranks, int32_t rank_lo,
 // V2 in the reference's exact order (pss_v2exact.hip): shuffle_buffer < 2^30, ns < 2^31
 bool v2_exact_supported(const Geometry &g);
 size_t v2_exact_ws_bytes(const Geometry &g, int32_t nr);
+// a draw slot: one epoch's MT draws (they depend on the epoch and (ns, B) only); the runtime
+// fills slots of coming epochs ahead of their calls and passes one as `slot` (else the call
+// draws into its workspace's own slot)
+size_t v2_exact_slot_bytes(const Geometry &g);
+int v2_exact_lookahead_depth(const Geometry &g);   // epochs drawn ahead (0: none)
+hipError_t launch_v2_exact_draws(const Geometry &g, int64_t epoch, uint32_t *slot, hipStream_t s);
 hipError_t launch_v2_exact(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, int32_t nr,
                            int64_t pos_lo, int64_t count, int64_t epoch, int64_t *out, uint32_t *ws,
-                           hipStream_t s, const MapArgs *mapped = nullptr);
+                           hipStream_t s, const MapArgs *mapped = nullptr, uint32_t *slot = nullptr);
 
 // V2 replay kernel: EMIT_XCHG = one LDS exchange per step (needs the lane-ordered exchange the
 // start-up check confirms), EMIT_PROBE = collision probe + per-clash fix-up (any hardware)

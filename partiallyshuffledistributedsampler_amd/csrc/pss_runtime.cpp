@@ -265,6 +265,29 @@ struct pss_sampler {
     // waits for the last such call when that one ran on another stream (SharedUse).  The V2
     // counter-order replays of whole streams with their ranks as kernel arguments use none of it
     // (their VAL ring orders itself with events), so consecutive epochs on two streams overlap.
+    // Exact-order draw lookahead: the reference's draws depend on the epoch and the windows alone
+    // (V1:165-171; V2:107-109,147), so once pss_generate ran in exact order for consecutive
+    // epochs of one call shape, the MT draws of the next epochs are made ahead into draw slots,
+    // each on its own low-priority side stream (a few long windows keep ~11 CUs busy for
+    // milliseconds: several epochs' draws run side by side).  The call of a prepared epoch only
+    // decodes (V2) / resolves (V1).  PSS_EXACT_LOOKAHEAD=0 turns it off.
+    static constexpr int kXSlots = 9;
+    DevBuf<uint32_t> xslot[kXSlots];
+    hipStream_t xside[kXSlots] = {};
+    hipEvent_t xev_done[kXSlots] = {};   // per slot: its last draws
+    hipEvent_t xev_read[kXSlots] = {};   // per slot: the last decode that read it
+    struct XKey {                        // what a slot's draws depend on besides the epoch
+        int32_t version;
+        int64_t ns, B, pos_lo, pos_hi;   // (V2: the whole stream, positions 0, 0)
+        bool operator==(const XKey &o) const {
+            return version == o.version && ns == o.ns && B == o.B && pos_lo == o.pos_lo && pos_hi == o.pos_hi;
+        }
+    };
+    struct XPend { bool valid; XKey key; int64_t epoch; };
+    XPend xpend[kXSlots] = {};           // the epoch a slot holds (or is being filled with)
+    bool xlast_valid = false;            // key and epoch of the previous exact call
+    XKey xlast_key{};
+    int64_t xlast_epoch = 0;
     hipEvent_t ev_shared = nullptr;
     hipStream_t last_shared = nullptr;
     bool shared_used = false;
@@ -499,6 +522,12 @@ int pss_destroy(pss_sampler *h) {
         for (hipEvent_t e : h->ev_done) if (e) (void)hipEventDestroy(e);
         if (h->ev_shared) (void)hipEventDestroy(h->ev_shared);
         h->d_val2.release(); h->d_buf2.release(); h->d_val3.release(); h->d_buf3.release();
+        for (int k = 0; k < pss_sampler::kXSlots; k++) {
+            if (h->xside[k]) { (void)hipStreamSynchronize(h->xside[k]); (void)hipStreamDestroy(h->xside[k]); }
+            if (h->xev_done[k]) (void)hipEventDestroy(h->xev_done[k]);
+            if (h->xev_read[k]) (void)hipEventDestroy(h->xev_read[k]);
+            h->xslot[k].release();
+        }
     }
     delete h;
     return PSS_OK;
@@ -699,6 +728,89 @@ int generate_v2_lookahead(pss_sampler *h, const pss::Geometry &g, int32_t rank_l
     return PSS_OK;
 }
 
+bool exact_lookahead_on() {
+    static const bool on = [] {
+        const char *e = getenv("PSS_EXACT_LOOKAHEAD");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
+// Exact order: this epoch's decode (V2) / resolution (V1) from the draw slot a previous call
+// prepared (else drawing first); then, if the previous call was epoch - 1 of this shape, the
+// draws of the coming epochs into free slots on their side streams.
+int generate_exact(pss_sampler *h, const pss::Geometry &g, int32_t rank_lo, int32_t nr, int64_t pos_lo,
+                   int64_t count, int64_t *out_dev, hipStream_t s, const pss::Marker &mk) {
+    constexpr int NX = pss_sampler::kXSlots;
+    auto words = [](size_t bytes) { return (bytes + sizeof(uint32_t) - 1) / sizeof(uint32_t); };
+    const int64_t e = h->epoch;
+    const bool v1 = h->version == 1;
+    const pss_sampler::XKey key{h->version, g.ns, g.B, v1 ? pos_lo : 0,
+                                v1 ? (pos_lo + count < g.ns ? pos_lo + count : g.ns) : 0};
+    int use = -1;
+    for (int k = 0; k < NX; k++) {
+        const auto &p = h->xpend[k];
+        if (p.valid && p.key == key && p.epoch == e) use = k;
+    }
+    if (use >= 0) {
+        PSS_HIP(hipStreamWaitEvent(s, h->xev_done[use], 0));
+        h->xpend[use].valid = false;
+    }
+    uint32_t *slot = use >= 0 ? h->xslot[use].p : nullptr;
+    mk(v1 ? pss::K_V1 : pss::K_V2_EMIT, s);
+    if (v1)
+        PSS_HIP(pss::launch_v1_exact(g, h->d_ranks.p, rank_lo, nr, pos_lo, count, e, out_dev, h->d_sort.p, s,
+                                     nullptr, slot));
+    else
+        PSS_HIP(pss::launch_v2_exact(g, h->d_ranks.p, rank_lo, nr, pos_lo, count, e, out_dev, h->d_sort.p, s,
+                                     nullptr, slot));
+    mk(-1, s);
+    if (use >= 0) PSS_HIP(hipEventRecord(h->xev_read[use], s));
+    // (a later call of the same epoch -- another rank range -- draws for itself: a slot is used
+    // once (V2's decode takes K1 as scratch, V1's scan its bucket counts); the coming epochs'
+    // slots stay)
+    const bool same_key = h->xlast_valid && h->xlast_key == key;
+    if (same_key && h->xlast_epoch == e) return PSS_OK;
+    const bool sequential = same_key && h->xlast_epoch == e - 1;
+    h->xlast_valid = true;
+    h->xlast_key = key;
+    h->xlast_epoch = e;
+    const int depth = !exact_lookahead_on() ? 0
+                      : v1 ? pss::v1_exact_lookahead_depth(g, pos_lo, count) : pss::v2_exact_lookahead_depth(g);
+    for (auto &p : h->xpend)   // keep only slots of the coming epochs of this shape
+        if (p.valid && !(sequential && p.key == key && p.epoch > e && p.epoch <= e + depth))
+            p.valid = false;
+    if (!sequential || depth <= 0) return PSS_OK;
+    const size_t sw = words(v1 ? pss::v1_exact_slot_bytes(g, pos_lo, count) : pss::v2_exact_slot_bytes(g));
+    for (int d = 1; d <= depth && d < NX; d++) {
+        bool queued = false;
+        for (const auto &p : h->xpend) queued |= p.valid && p.epoch == e + d;
+        if (queued) continue;
+        int k = -1;
+        for (int j = 0; j < NX && k < 0; j++) if (!h->xpend[j].valid && j != use) k = j;
+        if (k < 0) break;
+        if (!h->xside[k]) {
+            int least = 0, greatest = 0;
+            PSS_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
+            (void)greatest;
+            PSS_HIP(hipStreamCreateWithPriority(&h->xside[k], hipStreamNonBlocking, least));
+            PSS_HIP(hipEventCreateWithFlags(&h->xev_done[k], PSS_LA_EVENT_FLAGS));
+            PSS_HIP(hipEventCreateWithFlags(&h->xev_read[k], PSS_LA_EVENT_FLAGS));
+        }
+        if (h->xslot[k].n < sw) {   // grows once: after its last draws and its last reader
+            PSS_HIP(hipStreamSynchronize(h->xside[k]));
+            PSS_HIP(hipEventSynchronize(h->xev_read[k]));
+            PSS_HIP(h->xslot[k].ensure(sw));
+        }
+        PSS_HIP(hipStreamWaitEvent(h->xside[k], h->xev_read[k], 0));   // the decode that read it
+        if (v1) PSS_HIP(pss::launch_v1_exact_draws(g, pos_lo, count, e + d, h->xslot[k].p, h->xside[k]));
+        else PSS_HIP(pss::launch_v2_exact_draws(g, e + d, h->xslot[k].p, h->xside[k]));
+        PSS_HIP(hipEventRecord(h->xev_done[k], h->xside[k]));
+        h->xpend[k] = {true, key, e + d};
+    }
+    return PSS_OK;
+}
+
 // pss_generate's device path; ma != nullptr (V2 counter order, v2_mapped_fused shapes): the
 // replay writes (file, offset) into ma's arrays instead of ids into out_dev
 int generate_impl(pss_sampler *h, int32_t rank_lo, int32_t rank_hi, int64_t pos_lo, int64_t count,
@@ -757,10 +869,7 @@ int generate_impl(pss_sampler *h, int32_t rank_lo, int32_t rank_hi, int64_t pos_
     auto words = [](size_t bytes) { return (bytes + sizeof(uint32_t) - 1) / sizeof(uint32_t); };
     if (h->version == 1 && h->order_mode == PSS_ORDER_EXACT && g.shuffle) {
         PSS_HIP(h->d_sort.ensure(words(pss::v1_exact_ws_bytes(g, nr, pos_lo, count))));
-        mk(pss::K_V1, s);
-        PSS_HIP(pss::launch_v1_exact(g, h->d_ranks.p, rank_lo, nr, pos_lo, count, h->epoch, out_dev,
-                                     h->d_sort.p, s));
-        mk(-1, s);
+        return generate_exact(h, g, rank_lo, nr, pos_lo, count, out_dev, s, mk);
     } else if (h->version == 1) {
         const size_t sb = pss::v1_workspace_bytes(g, nr, pos_lo, count);
         if (sb) PSS_HIP(h->d_sort.ensure(words(sb)));
@@ -768,10 +877,7 @@ int generate_impl(pss_sampler *h, int32_t rank_lo, int32_t rank_hi, int64_t pos_
                                nullptr, rap));
     } else if (h->order_mode == PSS_ORDER_EXACT) {
         PSS_HIP(h->d_sort.ensure(words(pss::v2_exact_ws_bytes(g, nr))));
-        mk(pss::K_V2_EMIT, s);
-        PSS_HIP(pss::launch_v2_exact(g, h->d_ranks.p, rank_lo, nr, pos_lo, count, h->epoch, out_dev,
-                                     h->d_sort.p, s));
-        mk(-1, s);
+        return generate_exact(h, g, rank_lo, nr, pos_lo, count, out_dev, s, mk);
     } else if (lookahead_on() && pss::v2_stage_split(g, nr, h->emit_path)) {
         return generate_v2_lookahead(h, g, rank_lo, nr, pos_lo, count, out_dev, s, mk, ma, rap);
     } else {

@@ -512,6 +512,72 @@ static size_t v1x_st_offset(int64_t jobs, int64_t W) {
     return ((size_t)jobs * (size_t)W * sizeof(uint16_t) + 15u) & ~(size_t)15u;
 }
 
+static hipError_t v1x_big_draws(const Geometry &g, const V1xBig &b, int64_t epoch, hipStream_t s);
+
+// the LDS path's draws: J (u16, W per window) then the windows' seeded MT states
+static void v1x_small_draws(const Geometry &g, int64_t w_lo, int64_t nw, int64_t epoch, uint32_t *dst,
+                            hipStream_t s) {
+    uint32_t *ST = (uint32_t *)((char *)dst + v1x_st_offset(nw, g.B < g.ns ? g.B : g.ns));
+    launch_mt_seed_streams(MtSeedSpec{epoch, w_lo, 0, 0, (uint32_t)nw}, ST, s);
+    hipLaunchKernelGGL(k_v1x_draws, dim3((uint32_t)nw), dim3(64), 0, s, g, w_lo, nw, epoch,
+                       (const uint32_t *)ST, (uint16_t *)dst);
+}
+
+// A draw slot: the MT draws of a call's windows -- they depend on the epoch and the windows
+// alone (V1:165-171) -- made ahead of the call by the runtime (exact lookahead).  LDS windows:
+// J and the seeded states; windows through HBM: J and the bucket counts, when one pass covers
+// the call (else no slot: 0).
+struct V1xSlot { bool ok, big; int64_t w_lo, nw, W; size_t bytes; };
+static V1xSlot v1x_slot(const Geometry &g, int64_t pos_lo, int64_t count) {
+    V1xSlot t{};
+    const int64_t pos_hi = pos_lo + count < g.ns ? pos_lo + count : g.ns;
+    if (pos_hi <= pos_lo || !v1_exact_supported(g) || !g.shuffle) return t;
+    t.w_lo = pos_lo / g.B;
+    t.nw = (pos_hi - 1) / g.B - t.w_lo + 1;
+    t.W = g.B < g.ns ? g.B : g.ns;
+    if (t.W <= kV1ExactMaxB) {
+        t.ok = true;
+        t.bytes = v1x_st_offset(t.nw, t.W) + (size_t)t.nw * kMtN * sizeof(uint32_t);
+    } else if (t.nw <= v1x_jobs_per_pass(t.W)) {
+        t.ok = t.big = true;
+        t.bytes = ((size_t)t.nw * (size_t)t.W + (size_t)t.nw * v1x_nbk(t.W)) * sizeof(uint32_t);
+    }
+    return t;
+}
+
+size_t v1_exact_slot_bytes(const Geometry &g, int64_t pos_lo, int64_t count) {
+    const V1xSlot t = v1x_slot(g, pos_lo, count);
+    return t.ok ? t.bytes : 0;
+}
+
+// epochs drawn ahead: windows through HBM on a workgroup each (few, long: C5's 12 keep 12 CUs
+// busy for ~3 ms) 8 (C5 V1 exact 3.75 -> 1.12 ms per epoch); one-wave draws of many windows fill
+// the chip, and drawn ahead beside the resolution they slowed C2 from 0.40 to 0.80 ms: none.
+// At most 4 GiB of slots; none without a slot.
+int v1_exact_lookahead_depth(const Geometry &g, int64_t pos_lo, int64_t count) {
+    const V1xSlot t = v1x_slot(g, pos_lo, count);
+    if (!t.ok) return 0;
+    const int want = t.big && t.nw < 1024 ? 8 : 0;
+    const size_t cap = ((size_t)4 << 30) / (t.bytes ? t.bytes : 1);
+    return cap < (size_t)want ? (int)cap : want;
+}
+
+hipError_t launch_v1_exact_draws(const Geometry &g, int64_t pos_lo, int64_t count, int64_t epoch,
+                                 uint32_t *slot, hipStream_t s) {
+    const V1xSlot t = v1x_slot(g, pos_lo, count);
+    if (!t.ok || !slot) return hipErrorInvalidValue;
+    if (!t.big) {
+        v1x_small_draws(g, t.w_lo, t.nw, epoch, slot, s);
+        return hipGetLastError();
+    }
+    V1xBig b{};
+    b.w_lo = t.w_lo; b.nw = t.nw; b.j0 = 0; b.B = (uint32_t)t.W; b.nbk = v1x_nbk(t.W);
+    b.nj = (uint32_t)t.nw;
+    b.J = slot;
+    b.BCNT = slot + (size_t)b.nj * b.B;
+    return v1x_big_draws(g, b, epoch, s);
+}
+
 size_t v1_exact_ws_bytes(const Geometry &g, int32_t nr, int64_t pos_lo, int64_t count) {
     const int64_t pos_hi = pos_lo + count < g.ns ? pos_lo + count : g.ns;
     if (nr <= 0 || pos_hi <= pos_lo || !v1_exact_supported(g)) return 0;
@@ -524,9 +590,25 @@ size_t v1_exact_ws_bytes(const Geometry &g, int32_t nr, int64_t pos_lo, int64_t 
     return (size_t)pj * v1x_job_words(W) * sizeof(uint32_t);
 }
 
+// the draw stage of one pass (J and its bucket counts BCNT)
+static hipError_t v1x_big_draws(const Geometry &g, const V1xBig &b, int64_t epoch, hipStream_t s) {
+    hipError_t e = hipMemsetAsync(b.BCNT, 0, sizeof(uint32_t) * (size_t)b.nj * b.nbk, s);
+    if (e != hipSuccess) return e;
+    // few windows: a workgroup per window's MT stream (PSS_V1X_DRAWS_WG=0 / 1 forces a form)
+    static const int wg_env = [] {
+        const char *e = getenv("PSS_V1X_DRAWS_WG");
+        return e ? atoi(e) : -1;
+    }();
+    const bool wg = wg_env == 0 || wg_env == 1 ? wg_env == 1 : b.nj < 1024;
+    if (wg) hipLaunchKernelGGL(k_v1x_draws32_wg, dim3(b.nj), dim3(kMtWgThreads), 0, s, g, b, epoch);
+    else hipLaunchKernelGGL(k_v1x_draws32, dim3(b.nj), dim3(64), 0, s, g, b, epoch);
+    return hipGetLastError();
+}
+
+// slot: the single pass's J and BCNT drawn ahead (v1_exact_slot_bytes), or null
 static hipError_t launch_v1_exact_big(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, int32_t nr,
                                       int64_t pos_lo, int64_t count, int64_t epoch, int64_t *out,
-                                      uint32_t *ws, hipStream_t s, const MapArgs &ma) {
+                                      uint32_t *ws, uint32_t *slot, hipStream_t s, const MapArgs &ma) {
     const int64_t pos_hi = pos_lo + count < g.ns ? pos_lo + count : g.ns;
     const int64_t w_lo = pos_lo / g.B, w_hi = (pos_hi - 1) / g.B;
     const int64_t nw = w_hi - w_lo + 1;
@@ -558,16 +640,14 @@ static hipError_t launch_v1_exact_big(const Geometry &g, const RankDesc *ranks, 
         b.PART = b.H + (size_t)b.nj * B;
         b.BCNT = b.PART + (size_t)b.nj * B;
         b.PARTP = (uint16_t *)(b.BCNT + (size_t)b.nj * nbk);
-        hipError_t e = hipMemsetAsync(b.BCNT, 0, sizeof(uint32_t) * (size_t)b.nj * nbk, s);
-        if (e != hipSuccess) return e;
-        // few windows: a workgroup per window's MT stream (PSS_V1X_DRAWS_WG=0 / 1 forces a form)
-        static const int wg_env = [] {
-            const char *e = getenv("PSS_V1X_DRAWS_WG");
-            return e ? atoi(e) : -1;
-        }();
-        const bool wg = wg_env == 0 || wg_env == 1 ? wg_env == 1 : b.nj < 1024;
-        if (wg) hipLaunchKernelGGL(k_v1x_draws32_wg, dim3(b.nj), dim3(kMtWgThreads), 0, s, g, b, epoch);
-        else hipLaunchKernelGGL(k_v1x_draws32, dim3(b.nj), dim3(64), 0, s, g, b, epoch);
+        hipError_t e;
+        if (slot && jobs <= per) {   // drawn ahead (one pass)
+            b.J = slot;
+            b.BCNT = slot + (size_t)b.nj * B;
+        } else {
+            e = v1x_big_draws(g, b, epoch, s);
+            if (e != hipSuccess) return e;
+        }
         hipLaunchKernelGGL(k_v1x_bscan, dim3(b.nj), dim3(kV1xScanNT), 0, s, g, b);
         V1xBig bp = b;
         const dim3 gp = grid(bp, (B + kV1pChunk - 1) / kV1pChunk);
@@ -586,14 +666,14 @@ static hipError_t launch_v1_exact_big(const Geometry &g, const RankDesc *ranks, 
 
 hipError_t launch_v1_exact(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, int32_t nr,
                            int64_t pos_lo, int64_t count, int64_t epoch, int64_t *out, void *ws,
-                           hipStream_t s, const MapArgs *mapped) {
+                           hipStream_t s, const MapArgs *mapped, uint32_t *slot) {
     const MapArgs ma = mapped ? *mapped : MapArgs{};
     const int64_t pos_hi = pos_lo + count < g.ns ? pos_lo + count : g.ns;
     if (nr <= 0 || pos_hi <= pos_lo) return hipSuccess;
     if (!v1_exact_supported(g)) return hipErrorInvalidValue;
     if ((g.B < g.ns ? g.B : g.ns) > kV1ExactMaxB) {
         if (!ws) return hipErrorInvalidValue;
-        return launch_v1_exact_big(g, ranks, rank_lo, nr, pos_lo, count, epoch, out, (uint32_t *)ws, s, ma);
+        return launch_v1_exact_big(g, ranks, rank_lo, nr, pos_lo, count, epoch, out, (uint32_t *)ws, slot, s, ma);
     }
     const int64_t w_lo = pos_lo / g.B, w_hi = (pos_hi - 1) / g.B;
     const int64_t nw = w_hi - w_lo + 1;
@@ -607,14 +687,10 @@ hipError_t launch_v1_exact(const Geometry &g, const RankDesc *ranks, int32_t ran
     // streams a wave on vector registers); without one, each workgroup's first wave does them
     // in place
     const uint32_t ngrp = (uint32_t)((nr + kV1FanRanks - 1) / kV1FanRanks);
-    if (ws) {
-        uint32_t *ST = (uint32_t *)((char *)ws + v1x_st_offset(nw, g.B < g.ns ? g.B : g.ns));
-        launch_mt_seed_streams(MtSeedSpec{epoch, w_lo, 0, 0, (uint32_t)nw}, ST, s);
-        hipLaunchKernelGGL(k_v1x_draws, dim3((uint32_t)nw), dim3(64), 0, s, g, w_lo, nw, epoch,
-                           (const uint32_t *)ST, (uint16_t *)ws);
-    }
+    // (slot: the draws made ahead -- the slot holds what the workspace's first part would)
+    if (ws && !slot) v1x_small_draws(g, w_lo, nw, epoch, (uint32_t *)ws, s);
     hipLaunchKernelGGL(k_v1_exact, dim3((uint32_t)(ngrp * nw)), dim3(kExactNT), lds, s, g, ranks, rank_lo, nr,
-                       w_lo, nw, pos_lo, count, epoch, (const uint16_t *)ws, out, ma);
+                       w_lo, nw, pos_lo, count, epoch, (const uint16_t *)(slot ? (void *)slot : ws), out, ma);
     return hipGetLastError();
 }
 

@@ -984,23 +984,77 @@ static V2xChain v2x_chain_plan(const V2xGeo &x, int32_t nr) {
     return ch;
 }
 
-// workspace words before the windows' seeded MT states (S x 624, the one-wave draw form)
-static size_t v2x_base_words(const V2xGeo &x) {
+// The workspace of a call: the decode's arrays, then a draw slot -- the epoch's draws K1 (ns
+// words), K2 (T2 words) and the windows' seeded MT states ST (S x 624, the one-wave draw form).
+// A slot depends on the epoch and (ns, B) only, so the runtime can fill slots of coming epochs
+// ahead of their calls (pss_runtime.cpp, exact lookahead) and hand one to launch_v2_exact.
+static size_t v2x_rest_words(const V2xGeo &x) {
     const int32_t nr = 1;   // one decoded sequence serves every rank of a call (v2x_pass)
-    if (v2x_chain(x)) {   // K1, ANS (ns each), K2, Q2 (T2 each), survivors, chunk maps, chunk starts
+    if (v2x_chain(x)) {   // ANS (ns), Q2 (T2), survivors, chunk maps, chunk starts
         const V2xChain ch = v2x_chain_plan(x, nr);
-        return (size_t)nr * ((size_t)2 * x.ns + (size_t)2 * x.T2 + (size_t)x.tiles1 * x.P +
-                             (size_t)3 * ch.nch * x.P);
+        return (size_t)x.ns + (size_t)x.T2 + (size_t)x.tiles1 * x.P + (size_t)3 * ch.nch * x.P;
     }
-    // K1, V, O, Vd, Od (ns each) + K2, Q2 (T2 each), per local rank; tile splits.  Windows
-    // beyond kTile are decoded in V, O, Vd, Od (S * B <= ns per rank).
-    return (size_t)nr * ((size_t)5 * x.ns + (size_t)2 * x.T2) + v2x_split_words(x, nr);
+    // V, O, Vd, Od (ns each), Q2 (T2), tile splits.  Windows beyond kTile are decoded in V, O,
+    // Vd, Od (S * B <= ns).
+    return (size_t)4 * x.ns + (size_t)x.T2 + v2x_split_words(x, nr);
 }
+static size_t v2x_slot_words(const V2xGeo &x) { return (size_t)x.ns + (size_t)x.T2 + (size_t)x.S * kMtN; }
 
 size_t v2_exact_ws_bytes(const Geometry &g, int32_t nr_all) {
     if (!v2_exact_supported(g) || nr_all <= 0) return 0;
     const V2xGeo x = v2x_geo(g);
-    return (v2x_base_words(x) + (size_t)x.S * kMtN) * sizeof(uint32_t);
+    return (v2x_rest_words(x) + v2x_slot_words(x)) * sizeof(uint32_t);
+}
+
+size_t v2_exact_slot_bytes(const Geometry &g) {
+    if (!v2_exact_supported(g)) return 0;
+    return v2x_slot_words(v2x_geo(g)) * sizeof(uint32_t);
+}
+
+// the draws of one epoch into a slot: the pool2 windows' k1 / k2 (seeded ahead, then one wave or
+// one workgroup per window) and the tail's first draws
+static void v2x_draws(const V2xGeo &x, int64_t epoch, uint32_t *slot, hipStream_t s) {
+    const uint32_t nr = 1;
+    uint32_t *K1 = slot, *K2 = slot + x.ns, *ST = K2 + x.T2;
+    const uint32_t tail_blocks = (x.P + 63u) / 64u;
+    if (x.S) {
+        // few long windows (the streams alone do not fill the chip): a workgroup per stream, the
+        // tail draws riding along on the idle CUs
+        const bool wg = v2x_draws_wg((uint64_t)x.S * (uint64_t)nr, x.B);
+        const uint64_t wblocks = (uint64_t)x.S * (uint64_t)nr;
+        const uint64_t tblocks = wg ? ((uint64_t)tail_blocks * (uint64_t)nr + kMtWgWaves - 1) / kMtWgWaves : 0u;
+        if (!wg)   // (nr = 1: one decoded sequence; S < 2^31 / B windows, tail_blocks <= 2^24)
+            hipLaunchKernelGGL(k_v2x_seed, dim3(mt_seed_blocks(x.S) + tail_blocks), dim3(64), 0, s,
+                               MtSeedSpec{epoch, 0, -1, 2, x.S}, ST, x, epoch, K1);
+        v2x_launch_blocks(wblocks + tblocks, [&](uint64_t b0, uint32_t nb) {
+            if (wg) hipLaunchKernelGGL(k_v2x_draws_wg, dim3(nb), dim3(kMtWgThreads), 0, s, x, epoch, x.S, b0,
+                                       nr, tail_blocks, K1, K2);
+            else hipLaunchKernelGGL(k_v2x_draws, dim3(nb), dim3(64), 0, s, x, x.S, b0, (const uint32_t *)ST, K1, K2);
+        });
+    } else {
+        v2x_launch_blocks((uint64_t)tail_blocks * (uint64_t)nr, [&](uint64_t b0, uint32_t nb) {
+            hipLaunchKernelGGL(k_v2x_tail_draws, dim3(nb), dim3(64), 0, s, x, epoch, tail_blocks, b0, K1);
+        });
+    }
+}
+
+// epochs drawn ahead: the few long windows of the workgroup form keep ~S CUs busy for
+// milliseconds, so several epochs' draws run side by side (8: C5 V2 exact 10.9 -> 3.4 ms per
+// epoch); the one-wave form already fills the chip, and drawn ahead beside the decode it slowed
+// C2 from 0.83 to 1.19 ms (profiles/r05/ab_exact_tile.txt §7): none.  At most 4 GiB of slots.
+int v2_exact_lookahead_depth(const Geometry &g) {
+    if (!v2_exact_supported(g)) return 0;
+    const V2xGeo x = v2x_geo(g);
+    const int want = x.S && v2x_draws_wg((uint64_t)x.S, x.B) ? 8 : 0;
+    const size_t sb = v2x_slot_words(x) * sizeof(uint32_t);
+    const size_t cap = ((size_t)4 << 30) / (sb ? sb : 1);
+    return cap < (size_t)want ? (int)cap : want;
+}
+
+hipError_t launch_v2_exact_draws(const Geometry &g, int64_t epoch, uint32_t *slot, hipStream_t s) {
+    if (!v2_exact_supported(g) || !slot) return hipErrorInvalidValue;
+    v2x_draws(v2x_geo(g), epoch, slot, s);
+    return hipGetLastError();
 }
 
 // global merge levels w = kTile, 2 kTile, ... of nr sequences of x.ns > kTile steps (V, O sorted
@@ -1025,42 +1079,25 @@ static void v2x_global_levels(const V2xGeo &x, uint32_t nr, uint32_t *V, uint32_
 // tail step, V2:107-109,147) and the pool sizes are the same for every rank (ns = ceil(N / R)),
 // so the decoded stream of virtual indices is the same for all of them; a rank's ids are that
 // stream through its (old, new) start (V2:135-148).  One pass decodes it once and its last stage
-// writes the ids of all nr ranks of the call.
+// writes the ids of all nr ranks of the call.  slot: the epoch's draws (v2x_draws), already made
+// when the call brings one, else made here into the workspace's own slot.
 static hipError_t v2x_pass(const Geometry &g, const V2xGeo &x, const RankDesc *ranks, int32_t rank_lo,
                            int32_t nout, int64_t pos_lo, int64_t count, int64_t epoch,
-                           int64_t *out, uint32_t *ws, hipStream_t s, const MapArgs &ma) {
+                           int64_t *out, uint32_t *ws, uint32_t *slot, hipStream_t s, const MapArgs &ma) {
     const int32_t nr = 1, nr_plan = 1;   // decoded sequences
     const uint32_t ngrp = (uint32_t)v2x_cdiv(nout, kFanRanks);   // output block rows
     const size_t nsr = (size_t)nr * x.ns, tr = (size_t)nr * x.T2;
-    // merge-levels layout: K1 | V | O | Vd | Od | K2 | Q2 | splits | tables
-    // chain layout:        K1 | V (answers) | K2 | Q2 | survivors | chunk maps | chunk starts
+    // merge-levels layout: V | O | Vd | Od | Q2 | splits, then the slot K1 | K2 | ST
+    // chain layout:        V (answers) | Q2 | survivors | chunk maps | chunk starts, then the slot
     const bool chain = v2x_chain(x);
-    uint32_t *K1 = ws, *V = K1 + nsr;
-    uint32_t *O = chain ? nullptr : V + nsr, *Vd = chain ? nullptr : O + nsr, *Od = chain ? nullptr : Vd + nsr;
-    uint32_t *K2 = chain ? V + nsr : Od + nsr, *Q2 = K2 + tr;
-    const uint32_t tail_blocks = (x.P + 63u) / 64u;
-    bool tail_done = false;
-    if (x.S) {
-        // few long windows (the streams alone do not fill the chip): a workgroup per stream, the
-        // tail draws riding along on the idle CUs
-        const bool wg = v2x_draws_wg((uint64_t)x.S * (uint64_t)nr, x.B);
-        uint32_t *ST = ws + v2x_base_words(x);
-        const uint64_t wblocks = (uint64_t)x.S * (uint64_t)nr;
-        const uint64_t tblocks = wg ? ((uint64_t)tail_blocks * (uint64_t)nr + kMtWgWaves - 1) / kMtWgWaves : 0u;
-        if (!wg)   // (nr = 1: one decoded sequence; S < 2^31 / B windows, tail_blocks <= 2^24)
-            hipLaunchKernelGGL(k_v2x_seed, dim3(mt_seed_blocks(x.S) + tail_blocks), dim3(64), 0, s,
-                               MtSeedSpec{epoch, 0, -1, 2, x.S}, ST, x, epoch, K1);
-        v2x_launch_blocks(wblocks + tblocks, [&](uint64_t b0, uint32_t nb) {
-            if (wg) hipLaunchKernelGGL(k_v2x_draws_wg, dim3(nb), dim3(kMtWgThreads), 0, s, x, epoch, x.S, b0,
-                                       (uint32_t)nr, tail_blocks, K1, K2);
-            else hipLaunchKernelGGL(k_v2x_draws, dim3(nb), dim3(64), 0, s, x, x.S, b0, (const uint32_t *)ST, K1, K2);
-        });
-        tail_done = true;
+    if (!slot) {
+        slot = ws + v2x_rest_words(x);
+        v2x_draws(x, epoch, slot, s);
     }
-    if (!tail_done)
-        v2x_launch_blocks((uint64_t)tail_blocks * (uint64_t)nr, [&](uint64_t b0, uint32_t nb) {
-            hipLaunchKernelGGL(k_v2x_tail_draws, dim3(nb), dim3(64), 0, s, x, epoch, tail_blocks, b0, K1);
-        });
+    uint32_t *K1 = slot, *K2 = slot + x.ns;
+    uint32_t *V = ws;
+    uint32_t *O = chain ? nullptr : V + nsr, *Vd = chain ? nullptr : O + nsr, *Od = chain ? nullptr : Vd + nsr;
+    uint32_t *Q2 = chain ? V + nsr : Od + nsr;
     const uint32_t nru = (uint32_t)nr;
     const bool narrow = v2x_narrow(x.P, x.B);
     // one decode-tile launch of nb blocks from block b0 (the entry width; kTileOut merge outputs
@@ -1135,7 +1172,7 @@ static hipError_t v2x_pass(const Geometry &g, const V2xGeo &x, const RankDesc *r
 
 hipError_t launch_v2_exact(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, int32_t nr,
                            int64_t pos_lo, int64_t count, int64_t epoch, int64_t *out, uint32_t *ws,
-                           hipStream_t s, const MapArgs *mapped) {
+                           hipStream_t s, const MapArgs *mapped, uint32_t *slot) {
     const int64_t pos_hi = pos_lo + count < g.ns ? pos_lo + count : g.ns;
     if (nr <= 0 || pos_hi <= pos_lo) return hipSuccess;
     if (!v2_exact_supported(g) || !ws) return hipErrorInvalidValue;
@@ -1147,7 +1184,7 @@ hipError_t launch_v2_exact(const Geometry &g, const RankDesc *ranks, int32_t ran
     }();
     if (attr != hipSuccess) return attr;
     const MapArgs ma = mapped ? *mapped : MapArgs{};
-    return v2x_pass(g, x, ranks, rank_lo, nr, pos_lo, count, epoch, out, ws, s, ma);
+    return v2x_pass(g, x, ranks, rank_lo, nr, pos_lo, count, epoch, out, ws, slot, s, ma);
 }
 
 }  // namespace pss

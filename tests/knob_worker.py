@@ -7,7 +7,8 @@ when every check passes and prints the first mismatch otherwise.
 Checks:
   exact     order="exact" against the reference-captured fixtures (tests/golden/big) and the
             exact oracle: V1 windows through HBM (2^17 and 2^20 entries) and V2 pools beyond one
-            decode tile (2^16) -- the paths PSS_V1X_DRAWS_WG / PSS_V2X_DRAWS_WG switch between
+            decode tile (2^16) over consecutive epochs -- the paths PSS_V1X_DRAWS_WG /
+            PSS_V2X_DRAWS_WG switch between, and the draw lookahead PSS_EXACT_LOOKAHEAD turns off
   counter   the counter order (V2 small pools with the lookahead ring over consecutive epochs,
             grouped pools, V1) against the oracle twin -- the path PSS_V2_LOOKAHEAD switches
   cpu       CPU mode, exact and counter order, against the oracle (PSS_CPU_THREADS)
@@ -63,7 +64,7 @@ def check_exact(device):
         lens, N, R = _two_rank_shape(B)
         eng = IndexEngine(lens, N, R, B, version, device=device, order="exact")
         ns = eng.num_samples
-        for epoch in (3, 4):
+        for epoch in (3, 4, 5, 6):   # consecutive: from epoch 5 on the draws were made ahead
             eng.init_iter(epoch)
             old, new = eng.rank_starts()
             out = _gen(eng, 0, R)

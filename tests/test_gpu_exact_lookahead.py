@@ -1,0 +1,76 @@
+"""Exact-order draw lookahead (pss_runtime.cpp generate_exact): once an engine generated
+consecutive epochs of one call shape, the MT draws of the coming epochs are made ahead on side
+streams into draw slots, and the call of a prepared epoch only decodes (V2) / resolves (V1).  The
+reference's draws depend on the epoch and the window alone (V1:165-171, V2:107-109,147), so a
+prepared epoch must give the same stream as one drawn in its own call: checked here against an
+engine that visits the same epochs out of order (never sequential, so it never draws ahead) and
+against the exact oracle.
+"""
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from partiallyshuffledistributedsampler_amd.engine import IndexEngine
+
+pytestmark = pytest.mark.gpu
+
+EPOCHS = list(range(11))
+
+
+def _shape(B, R=3, mult=3.5, pad=2):
+    ns = int(mult * B)
+    N, F = ns * R - pad, 90
+    lens = np.full(F, N // F, dtype=np.int64)
+    lens[-1] += N - lens.sum()
+    return lens, N, R
+
+
+def _check_epochs(B, version, order, calls_per_epoch=1):
+    """Every epoch of `order` (rank starts from the engine's own epoch history, which depends on
+    the order the epochs are visited in, V2:142-152) against the exact oracle."""
+    lens, N, R = _shape(B)
+    eng = IndexEngine(lens, N, R, B, version, device=0, order="exact")
+    ns = eng.num_samples
+    for e in order:
+        eng.init_iter(e)
+        if calls_per_epoch == 1:
+            got = eng.generate(0, R).cpu().numpy()
+        else:   # one call per rank, the last rank in two position ranges
+            rows = [eng.generate(r, r + 1).cpu().numpy()[0] for r in range(R - 1)]
+            h = ns // 3
+            rows.append(np.concatenate([eng.generate(R - 1, R, pos_lo=0, count=h).cpu().numpy()[0],
+                                        eng.generate(R - 1, R, pos_lo=h).cpu().numpy()[0]]))
+            got = np.stack(rows)
+        eng.check()
+        old, new = eng.rank_starts()
+        for r in range(R):
+            ref = (O.v1_exact_stream(e, int(new[r]), ns, B, N) if version == 1 else
+                   O.v2_exact_stream_rs(e, int(old[r]), int(new[r]), ns, B, N))
+            assert np.array_equal(got[r], ref), ("epoch", e, "rank", r, "B", B, "version", version)
+    eng.close()
+
+
+# V2: B = 4096 chain mode, one wave per pool2 window, and 5000, merge levels (no lookahead for
+# the one-wave draws: they check the slot-less path beside it); 2^16 pools beyond one decode
+# tile, few long windows (the workgroup draws, eight epochs ahead)
+@pytest.mark.parametrize("B", [4096, 5000, 1 << 16])
+def test_v2_consecutive_epochs_with_draws_made_ahead(B):
+    _check_epochs(B, 2, EPOCHS)
+
+
+# V1: B = 4096 windows resolved in LDS (no lookahead); 2^17 windows through HBM (workgroup
+# draws, 8 ahead)
+@pytest.mark.parametrize("B", [4096, 1 << 17])
+def test_v1_consecutive_epochs_with_draws_made_ahead(B):
+    _check_epochs(B, 1, EPOCHS)
+
+
+def test_epoch_jumps_drop_the_prepared_draws():
+    # 0, 1 (queues 2, 3), 5 (not 1 + 1: its own draws, the slots of 2, 3 dropped), 6, 7, 3, 4
+    _check_epochs(1 << 16, 2, [0, 1, 5, 6, 7, 3, 4])
+    _check_epochs(1 << 17, 1, [0, 1, 5, 6, 7, 3, 4])
+
+
+@pytest.mark.parametrize("version,B", [(1, 1 << 17), (2, 1 << 16)])
+def test_several_calls_per_epoch_keep_the_lookahead_correct(version, B):
+    _check_epochs(B, version, EPOCHS[:6], calls_per_epoch=3)

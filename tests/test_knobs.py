@@ -9,6 +9,8 @@ tests/knob_worker.py in a child interpreter with the variable set before any GPU
                                        slot in blockIdx.y) instead of the XCD-major flat grids
   PSS_V2_LOOKAHEAD=0                   no epoch lookahead: the V2 last-occurrence passes run in
                                        line on the caller's stream
+  PSS_EXACT_LOOKAHEAD=0                no exact-order draw lookahead: every exact V2 call makes its
+                                       own MT draws
   PSS_CPU_THREADS=1 / 3                host threads of the CPU mode
 
 `test_every_knob_is_covered` fails when a source gains a getenv that is not listed here.
@@ -27,6 +29,7 @@ GPU_CASES = [
     ("exact", {"PSS_V1X_DRAWS_WG": "0", "PSS_V2X_DRAWS_WG": "0"}),
     ("exact", {"PSS_V1X_DRAWS_WG": "1", "PSS_V2X_DRAWS_WG": "1"}),
     ("exact", {"PSS_V1X_GRID2D": "1"}),
+    ("exact", {"PSS_EXACT_LOOKAHEAD": "0"}),
     ("counter", {"PSS_V2_LOOKAHEAD": "0"}),
 ]
 CPU_CASES = [("cpu", {"PSS_CPU_THREADS": "1"}), ("cpu", {"PSS_CPU_THREADS": "3"})]

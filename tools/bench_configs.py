@@ -14,7 +14,9 @@ survey names, each as the share one of 8 GPUs would generate:
   c5     V2, C2 files, B=2^20 (HBM slot-table path), 100 epochs       (reports per-epoch mean)
   c5x    c5 with order="exact"
   c5v1x  V1 on c5's shape (B=2^20 windows, HBM-staged resolution) with order="exact"
-Prints one JSON line per config: ids per step, ms per step, G idx/s, per-kernel ms.
+Prints one JSON line per config: ids per step, ms per step, G idx/s, per-kernel ms.  Steps are
+consecutive epochs after 2 warm-up epochs: the exact configs run with their draws made ahead
+(the exact lookahead, PSS_EXACT_LOOKAHEAD=0 to compare).
 """
 import json
 import os
@@ -43,8 +45,11 @@ def run(name, lengths, R, r_hi, B, ver, steps, warmup=2, order="counter"):
     for i in range(steps):
         eng.init_iter(warmup + i)
         eng.generate(0, r_hi, out=out)
-    torch.cuda.synchronize()
+    # the caller's stream: the draws of the epochs after the timed ones, made ahead on side
+    # streams (exact order), belong to those epochs
+    torch.cuda.current_stream().synchronize()
     dt = (time.perf_counter() - t0) / steps
+    torch.cuda.synchronize()
     prof = eng.profile_read()
     eng.close()
     ids = r_hi * ns
@@ -63,9 +68,9 @@ def main():
         elif w == "c1x":   # C1 in the reference's exact order (CPython MT per window)
             run(w, np.full(64, 10_000, dtype=np.int64), 2, 2, 4096, 1, 50, order="exact")
         elif w == "c2x":   # C2 in the reference's exact order (CPython MT, rank-deletion decode)
-            run(w, c2, 8, 8, 4096, 2, 3, warmup=1, order="exact")
+            run(w, c2, 8, 8, 4096, 2, 12, order="exact")
         elif w == "c2v1x":
-            run(w, c2, 8, 8, 4096, 1, 5, order="exact")
+            run(w, c2, 8, 8, 4096, 1, 12, order="exact")
         elif w == "c2":
             run(w, c2, 8, 8, 4096, 2, 20)
         elif w == "c2v1":
@@ -78,9 +83,9 @@ def main():
         elif w == "c5":
             run(w, c2, 8, 8, 1 << 20, 2, 100)
         elif w == "c5x":
-            run(w, c2, 8, 8, 1 << 20, 2, 2, warmup=1, order="exact")
+            run(w, c2, 8, 8, 1 << 20, 2, 12, order="exact")
         elif w == "c5v1x":
-            run(w, c2, 8, 8, 1 << 20, 1, 3, warmup=1, order="exact")
+            run(w, c2, 8, 8, 1 << 20, 1, 12, order="exact")
 
 
 if __name__ == "__main__":
