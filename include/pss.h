@@ -184,7 +184,11 @@ int pss_emit_path(pss_sampler *h, int32_t *path);
  *       2^31), windows up to 16000 entries 2 B per position and 2.5 KB per window (its
  *       seeded MT state); V2 ~28 B per position of num_samples and 2.5 KB per pool2 window --
  *       one decode serves every rank of a call, whatever their number.  A workspace the
- *       device cannot hold makes pss_generate return PSS_EHIP.
+ *       device cannot hold makes pss_generate return PSS_EHIP.  After calls for consecutive
+ *       epochs of one shape, the MT draws of the next 8 epochs are made ahead on the handle's
+ *       own low-priority streams where they are few long streams (shuffle_buffer beyond 4096
+ *       with few windows: up to 4 GiB of draw slots; PSS_EXACT_LOOKAHEAD=0 turns it off);
+ *       pss_destroy waits for them.
  * Replaces nothing in the reference: its order IS the exact one. */
 #define PSS_ORDER_COUNTER 0
 #define PSS_ORDER_EXACT 1
