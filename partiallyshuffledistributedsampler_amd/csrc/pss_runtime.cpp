@@ -924,6 +924,17 @@ int pss_set_order_mode(pss_sampler *h, int32_t mode) {
         if (h->version == 2 && !pss::v2_exact_supported(h->geometry()))
             return fail(PSS_ENOTSUP, "V2 exact order needs num_samples < 2^31 and shuffle_buffer < 2^30");
     }
+    if (mode != h->order_mode && mode == PSS_ORDER_COUNTER && !h->cpu && h->dev_init) {
+        // leaving the exact order: the draws made ahead and their slots go
+        DeviceGuard dg(h->device);
+        for (int k = 0; k < pss_sampler::kXSlots; k++) {
+            if (h->xside[k]) PSS_HIP(hipStreamSynchronize(h->xside[k]));
+            if (h->xev_read[k]) PSS_HIP(hipEventSynchronize(h->xev_read[k]));
+            h->xpend[k].valid = false;
+            h->xslot[k].release();
+        }
+        h->xlast_valid = false;
+    }
     h->order_mode = mode;
     return PSS_OK;
 }

@@ -74,3 +74,31 @@ def test_epoch_jumps_drop_the_prepared_draws():
 @pytest.mark.parametrize("version,B", [(1, 1 << 17), (2, 1 << 16)])
 def test_several_calls_per_epoch_keep_the_lookahead_correct(version, B):
     _check_epochs(B, version, EPOCHS[:6], calls_per_epoch=3)
+
+
+def test_leaving_the_exact_order_drops_the_slots_and_coming_back_restarts():
+    B = 1 << 16
+    lens, N, R = _shape(B)
+    eng = IndexEngine(lens, N, R, B, 2, device=0, order="exact")
+    ns = eng.num_samples
+
+    def check(e):
+        eng.init_iter(e)
+        got = eng.generate(0, R).cpu().numpy()
+        eng.check()
+        old, new = eng.rank_starts()
+        for r in range(R):
+            ref = O.v2_exact_stream_rs(e, int(old[r]), int(new[r]), ns, B, N)
+            assert np.array_equal(got[r], ref), ("epoch", e, "rank", r)
+
+    for e in (0, 1, 2):          # 2 from a slot, 3.. queued
+        check(e)
+    eng.set_order_mode("counter")
+    eng.init_iter(3)
+    c = eng.generate(0, R).cpu().numpy()
+    eng.check()
+    assert c.shape == (R, ns) and c.min() >= 0 and c.max() < N
+    eng.set_order_mode("exact")
+    for e in (4, 5, 6):          # 4: own draws (the slots went), 5 queued by 4 ... 6 from a slot
+        check(e)
+    eng.close()
