@@ -976,7 +976,10 @@ static bool v2x_chain(const V2xGeo &x) { return x.P <= (uint32_t)kTile; }
 // chunks of tiles per rank: about two 1024-thread workgroups per CU over the pass's ranks
 static V2xChain v2x_chain_plan(const V2xGeo &x, int32_t nr) {
     V2xChain ch{};
-    uint32_t want = (uint32_t)((512 + nr - 1) / (nr > 0 ? nr : 1));
+#ifndef PSS_CHAIN_CHUNKS
+#define PSS_CHAIN_CHUNKS 512
+#endif
+    uint32_t want = (uint32_t)((PSS_CHAIN_CHUNKS + nr - 1) / (nr > 0 ? nr : 1));
     if (want < 1) want = 1;
     if (want > x.tiles1) want = x.tiles1;
     ch.tpc = (x.tiles1 + want - 1) / want;
@@ -1134,7 +1137,10 @@ static hipError_t v2x_pass(const Geometry &g, const V2xGeo &x, const RankDesc *r
             hipLaunchKernelGGL(k_v2x_link_fin, dim3(ch.nch), dim3(kChainNT), 0, s, x, ch, (const uint32_t *)src);
         }
         // K1 (the draws) is free once the tiles ran: the virtual indices for the fan-out
-        const bool fan = nout > 1;
+#ifndef PSS_CHAIN_FAN
+#define PSS_CHAIN_FAN 1
+#endif
+        const bool fan = PSS_CHAIN_FAN && nout > 1;
         hipLaunchKernelGGL(k_v2x_emit, dim3((fan ? 1u : ngrp) * ch.nch), dim3(kChainNT), lds, s, g, x, ch, ranks,
                            rank_lo, nout, ANS, (const uint32_t *)Q2, pos_lo, count, out, ma, fan ? K1 : nullptr);
         if (fan) v2x_launch_fanout(g, ranks, rank_lo, nout, K1, pos_lo, count, out, ma, s);
