@@ -217,6 +217,28 @@ __global__ __launch_bounds__(64) void persist_il(int64_t *o, uint64_t n, int64_t
     record(st, per);
 }
 
+// own runs, each wave starting inside its run at a wave-dependent chunk and wrapping (ROT: chunk
+// (w * 37) mod per), or its run shifted by (w mod 16) chunks of 2 KB (SKEW: neighbouring runs
+// overlap by up to 30 KB, timing only): are equal-phase runs conflicting in the HBM channels?
+template <int MODE>
+__global__ __launch_bounds__(64) void persist_phase(int64_t *o, uint64_t n, int64_t salt, Stats *st) {
+    extern __shared__ uint32_t pad[];
+    if (n == 0) pad[threadIdx.x] = 0;
+    const uint64_t chunks = n / 256, per = chunks / gridDim.x - 16;
+    const uint64_t w = blockIdx.x;
+    const uint64_t base = w * (per + 16) + (MODE == 1 ? (w % 16) : 0);
+    const uint64_t rot = MODE == 0 ? (w * 37) % per : 0;
+    for (uint64_t c = 0; c < per; c++) {
+        uint64_t cc = c + rot;
+        if (cc >= per) cc -= per;
+        const uint64_t ch = base + cc;
+        int64_t *p = o + ch * 256;
+#pragma unroll
+        for (int j = 0; j < 4; j++) p[64 * j + threadIdx.x] = (int64_t)(ch * 256 + 64 * j + threadIdx.x) + salt;
+    }
+    record(st, per);
+}
+
 __global__ void stamp_t0(Stats *st) { if (threadIdx.x == 0) st->t0 = __builtin_amdgcn_s_memrealtime(); }
 
 template <class F>
@@ -276,12 +298,17 @@ int main() {
                     (const void *)persist_bar<8, 1>, (const void *)persist_bar<8, 0>, (const void *)persist_x<14>,
                     (const void *)persist_x<13>, (const void *)persist_x<12>, (const void *)persist_r16,
                     (const void *)persist_r16x, (const void *)persist_il<0>, (const void *)persist_il<8>,
-                    (const void *)persist_il<64>, (const void *)persist_il<256>})
+                    (const void *)persist_il<64>, (const void *)persist_il<256>, (const void *)persist_phase<0>,
+                    (const void *)persist_phase<1>, (const void *)persist_phase<2>})
         (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     const size_t lds = 18220;   // 8 one-wave blocks per CU, as the replay
     for (int rep = 0; rep < 2; rep++) {
         timeit("oneshot4", st, ctr, [&](int s) { hipLaunchKernelGGL(oneshot4, dim3((uint32_t)((n / 4 + 255) / 256)), dim3(256), 0, 0, o, n, (int64_t)s); });
         timeit("persist_r", st, ctr, [&](int s) { hipLaunchKernelGGL(persist_r, dim3(kWaves), dim3(64), lds, 0, o, n, (int64_t)s, st); });
+        timeit("phase_none", st, ctr, [&](int s) { hipLaunchKernelGGL(persist_phase<2>, dim3(kWaves), dim3(64), lds, 0, o, n, (int64_t)s, st); });
+        timeit("phase_rot", st, ctr, [&](int s) { hipLaunchKernelGGL(persist_phase<0>, dim3(kWaves), dim3(64), lds, 0, o, n, (int64_t)s, st); });
+        timeit("phase_skew", st, ctr, [&](int s) { hipLaunchKernelGGL(persist_phase<1>, dim3(kWaves), dim3(64), lds, 0, o, n, (int64_t)s, st); });
+        if (rep == 0) continue;
         timeit("il_all", st, ctr, [&](int s) { hipLaunchKernelGGL(persist_il<0>, dim3(kWaves), dim3(64), lds, 0, o, n, (int64_t)s, st); });
         timeit("il_8", st, ctr, [&](int s) { hipLaunchKernelGGL(persist_il<8>, dim3(kWaves), dim3(64), lds, 0, o, n, (int64_t)s, st); });
         timeit("il_64", st, ctr, [&](int s) { hipLaunchKernelGGL(persist_il<64>, dim3(kWaves), dim3(64), lds, 0, o, n, (int64_t)s, st); });
