@@ -126,13 +126,6 @@ int v1_exact_lookahead_depth(const Geometry &g, int64_t pos_lo, int64_t count);
 hipError_t launch_v1_exact_draws(const Geometry &g, int64_t pos_lo, int64_t count, int64_t epoch,
                                  uint32_t *slot, hipStream_t s);
 
-// ids of nout ranks from one decoded stream of virtual indices (exact order: every rank of a call
-// shares it): position t's v = VV[t - vv_lo]; id = wrap(v < old_lim ? old_start + v : new_start + v)
-// (pss_v2exact.hip k_v2x_fanout).  One-shot grid of 4 positions per thread.
-void launch_id_fanout(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, int32_t nout,
-                      const uint32_t *VV, int64_t vv_lo, int64_t old_lim, int64_t pos_lo, int64_t count,
-                      int64_t *out, const MapArgs &ma, hipStream_t s);
-
 // V2 in the reference's exact order (pss_v2exact.hip): shuffle_buffer < 2^30, ns < 2^31
 bool v2_exact_supported(const Geometry &g);
 size_t v2_exact_ws_bytes(const Geometry &g, int32_t nr);

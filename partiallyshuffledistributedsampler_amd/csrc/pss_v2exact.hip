@@ -579,22 +579,20 @@ __device__ __forceinline__ void v2x_put(const V2xFin &f, const V2xGeo &x, uint32
     f.VV[t] = v;
 }
 
-// ids of nout ranks from the virtual-index stream VV (position t at VV[t - vv_lo]): v < old_lim
-// came from the old start, the rest from the new one (V2:135-148: old_lim = min(2B, ns); V1:
-// 0, every id from the new start), wrapped at N (V2:113-114); each rank's row written coalesced.
+// ids of nout ranks from the virtual-index stream VV (position t at VV[t]): v < min(2B, ns) came
+// from the old start, the rest from the new one (V2:135-148), wrapped at N (V2:113-114); each
+// rank's row written coalesced.
 // One-shot: 4 consecutive positions per thread (a 16-byte VV load, two 16-byte stores per rank
 // when the rank rows are 16-byte aligned -- the store shape of torch's fill_).
 __global__ __launch_bounds__(256) void k_v2x_fanout(Geometry g, const RankDesc *__restrict__ ranks, int32_t rank_lo,
-                                                    int32_t nout, const uint32_t *__restrict__ VV, int64_t vv_lo,
-                                                    int64_t old_lim, int64_t pos_lo, int64_t count,
-                                                    int64_t *__restrict__ out, MapArgs ma) {
-    const int64_t twoB = old_lim;
+                                                    int32_t nout, const uint32_t *__restrict__ VV, int64_t pos_lo,
+                                                    int64_t count, int64_t *__restrict__ out, MapArgs ma) {
+    const int64_t twoB = 2 * g.B < g.ns ? 2 * g.B : g.ns;
     const int64_t pos_hi = pos_lo + count < g.ns ? pos_lo + count : g.ns;
     const int64_t t0 = pos_lo + ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
     if (t0 >= pos_hi) return;
-    VV -= vv_lo;
     const bool vec = !ma.fpos && t0 + 4 <= pos_hi && (t0 & 3) == 0 && ((count | pos_lo) & 1) == 0 &&
-                     (((uintptr_t)out) & 15u) == 0 && (vv_lo & 3) == 0;
+                     (((uintptr_t)out) & 15u) == 0;
     if (vec) {
         const uint4 w = *(const uint4 *)(VV + t0);
         const int64_t v[4] = {w.x, w.y, w.z, w.w};
@@ -895,21 +893,14 @@ static int64_t pos_hi_of(const Geometry &g, int64_t pos_lo, int64_t count) {
     return pos_lo + count < g.ns ? pos_lo + count : g.ns;
 }
 
-void launch_id_fanout(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, int32_t nout,
-                      const uint32_t *VV, int64_t vv_lo, int64_t old_lim, int64_t pos_lo, int64_t count,
-                      int64_t *out, const MapArgs &ma, hipStream_t s) {
-    const int64_t n = pos_hi_of(g, pos_lo, count) - pos_lo;
-    const uint32_t blocks = (uint32_t)v2x_cdiv(n, 1024);   // (n < 2^31: one exact call's positions)
-    if (blocks)
-        hipLaunchKernelGGL(k_v2x_fanout, dim3(blocks), dim3(256), 0, s, g, ranks, rank_lo, nout, VV, vv_lo,
-                           old_lim, pos_lo, count, out, ma);
-}
-
 static void v2x_launch_fanout(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, int32_t nout,
                               const uint32_t *VV, int64_t pos_lo, int64_t count, int64_t *out,
                               const MapArgs &ma, hipStream_t s) {
-    const int64_t twoB = 2 * g.B < g.ns ? 2 * g.B : g.ns;
-    launch_id_fanout(g, ranks, rank_lo, nout, VV, 0, twoB, pos_lo, count, out, ma, s);
+    const int64_t n = pos_hi_of(g, pos_lo, count) - pos_lo;
+    const uint32_t blocks = (uint32_t)v2x_cdiv(n, 1024);   // (n < 2^31: v2_exact_supported)
+    if (blocks)
+        hipLaunchKernelGGL(k_v2x_fanout, dim3(blocks), dim3(256), 0, s, g, ranks, rank_lo, nout, VV, pos_lo, count,
+                           out, ma);
 }
 
 static V2xGeo v2x_geo(const Geometry &g) {
