@@ -228,7 +228,7 @@ __device__ __forceinline__ uint32_t wave_role_scan(uint32_t x) {
 
 // One 64-word block of a pool2 window's stream, exactly (the wave's lanes = the block's words):
 // the role scan settles it in one pass where every k2 verdict is fixed over the block's possible
-// k2 indices [i2, i2 + 32], else the lanes' k2 indices are guessed and re-derived to the fixed
+// k2 indices (lane l: [i2, i2 + ceil(l / 2)]), else the lanes' k2 indices are guessed and re-derived to the fixed
 // point.  Emits the block's draws and advances (st, i1, i2).
 template <class Emit>
 __device__ __forceinline__ void pair_block(uint32_t word, bool valid, uint32_t W, uint32_t P, uint32_t kb1,
@@ -252,10 +252,12 @@ __device__ __forceinline__ void pair_block(uint32_t word, bool valid, uint32_t W
         const uint64_t m2 = __ballot(valid && role == 1u && a2);
         j = i2 + (uint32_t)__popcll(m2 & below);
     };
-    // a block holds at most 32 k2 draws, so each lane's k2 index lies in [i2, i2 + 32]: where
-    // every lane's k2 verdict is the same over that whole range (all but ~1 % of lanes), one
-    // scan settles the block; otherwise iterate guess -> true index
-    const uint32_t nhi = i2 < W ? W - i2 : 1u, nlo = i2 + 32u < W ? W - (i2 + 32u) : 1u;
+    // an accepted k2 is followed by a k1 offer, so the lanes below l hold at most ceil(l / 2)
+    // accepted k2 draws and lane l's k2 index lies in [i2, i2 + ceil(l / 2)]: where every lane's
+    // k2 verdict is the same over its range (all but ~0.5 % of lanes), one scan settles the block;
+    // otherwise iterate guess -> true index
+    const uint32_t jl = i2 + ((uint32_t)lane + 1u) / 2u;
+    const uint32_t nhi = i2 < W ? W - i2 : 1u, nlo = jl < W ? W - jl : 1u;
     const uint32_t kbh = 32u - (uint32_t)__builtin_clz(nhi);
     const uint32_t rh = word >> (32u - kbh);
     const bool sure = kbh == 32u - (uint32_t)__builtin_clz(nlo) && (rh < nlo || rh >= nhi);
@@ -466,7 +468,7 @@ __device__ void mt_draws_pair_wg(MtWgShared &sh, int cur, uint32_t W, uint32_t P
                 const bool a1 = valid && (word >> (32u - kb1)) < P;
                 uint32_t jlo, jhi;   // the k2 index at the block's start (at most 1 per 2 words)
                 mt_window(i2_0, rate, var, (uint32_t)q0, (uint32_t)q0 / 2u + 1u, jlo, jhi);
-                const uint32_t jtop = jhi + 32u;
+                const uint32_t jtop = jhi + ((uint32_t)lane + 1u) / 2u;   // (pair_block's per-lane range)
                 const uint32_t nhi = jlo < W ? W - jlo : 1u, nlo = jtop < W ? W - jtop : 1u;
                 const uint32_t kbh = 32u - (uint32_t)__builtin_clz(nhi);
                 const uint32_t rh = word >> (32u - kbh);
@@ -632,7 +634,7 @@ __device__ void mt_draws_pair_wg(MtWgShared &sh, int cur, uint32_t W, uint32_t P
 
 // mt_draws on a workgroup per stream (V1 windows beyond LDS: ~12 windows per rank at C5), for a
 // non-increasing bound(d), in the rounds of mt_draws_pair_wg: a block whose every verdict is
-// fixed over the bounds of its window's draw indices ([lo, hi + 64]) makes exactly
+// fixed over the bounds of its window's draw indices (lane l: [lo, hi + l]) makes exactly
 // popc(accepted) draws wherever in the window it starts.
 template <class Bound, class Emit>
 __device__ void mt_draws_wg(MtWgShared &sh, int cur, uint32_t nd, Bound bound, Emit emit) {
@@ -666,7 +668,7 @@ __device__ void mt_draws_wg(MtWgShared &sh, int cur, uint32_t nd, Bound bound, E
                 const uint32_t word = valid ? tc[q0 + lane] : 0u;
                 uint32_t dlo, dhi;
                 mt_window(d0, rate, var, (uint32_t)q0, (uint32_t)q0, dlo, dhi);
-                const uint32_t dtop = dhi + 64u;
+                const uint32_t dtop = dhi + (uint32_t)lane;   // lane l: at most l draws below it
                 const uint32_t nhi = bound(dlo < nd ? dlo : nd - 1u), nlo = bound(dtop < nd ? dtop : nd - 1u);
                 const uint32_t kbh = 32u - (uint32_t)__builtin_clz(nhi);
                 const uint32_t r = word >> (32u - kbh);
