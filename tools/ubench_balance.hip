@@ -239,6 +239,30 @@ __global__ __launch_bounds__(64) void persist_phase(int64_t *o, uint64_t n, int6
     record(st, per);
 }
 
+// own runs with non-temporal stores (global_store ... nt): does the L2's write allocation of
+// 2048 concurrent runs cost the persistent streams their rate?
+__global__ __launch_bounds__(64) void persist_nt(int64_t *o, uint64_t n, int64_t salt, Stats *st) {
+    extern __shared__ uint32_t pad[];
+    if (n == 0) pad[threadIdx.x] = 0;
+    const uint64_t chunks = n / 256, per = chunks / gridDim.x;
+    for (uint64_t c = blockIdx.x * per; c < blockIdx.x * per + per; c++) {
+        int64_t *p = o + c * 256;
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+            __builtin_nontemporal_store((int64_t)(c * 256 + 64 * j + threadIdx.x) + salt, p + 64 * j + threadIdx.x);
+    }
+    record(st, per);
+}
+
+// one-shot with non-temporal stores
+__global__ __launch_bounds__(256) void oneshot_nt(int64_t *o, uint64_t n, int64_t salt) {
+    const uint64_t i = ((uint64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+    if (i + 3 < n) {
+#pragma unroll
+        for (int k = 0; k < 4; k++) __builtin_nontemporal_store((int64_t)(i + k) + salt, o + i + k);
+    }
+}
+
 __global__ void stamp_t0(Stats *st) { if (threadIdx.x == 0) st->t0 = __builtin_amdgcn_s_memrealtime(); }
 
 template <class F>
@@ -299,12 +323,14 @@ int main() {
                     (const void *)persist_x<13>, (const void *)persist_x<12>, (const void *)persist_r16,
                     (const void *)persist_r16x, (const void *)persist_il<0>, (const void *)persist_il<8>,
                     (const void *)persist_il<64>, (const void *)persist_il<256>, (const void *)persist_phase<0>,
-                    (const void *)persist_phase<1>, (const void *)persist_phase<2>})
+                    (const void *)persist_phase<1>, (const void *)persist_phase<2>, (const void *)persist_nt})
         (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     const size_t lds = 18220;   // 8 one-wave blocks per CU, as the replay
     for (int rep = 0; rep < 2; rep++) {
         timeit("oneshot4", st, ctr, [&](int s) { hipLaunchKernelGGL(oneshot4, dim3((uint32_t)((n / 4 + 255) / 256)), dim3(256), 0, 0, o, n, (int64_t)s); });
         timeit("persist_r", st, ctr, [&](int s) { hipLaunchKernelGGL(persist_r, dim3(kWaves), dim3(64), lds, 0, o, n, (int64_t)s, st); });
+        timeit("persist_nt", st, ctr, [&](int s) { hipLaunchKernelGGL(persist_nt, dim3(kWaves), dim3(64), lds, 0, o, n, (int64_t)s, st); });
+        timeit("oneshot_nt", st, ctr, [&](int s) { hipLaunchKernelGGL(oneshot_nt, dim3((uint32_t)((n / 4 + 255) / 256)), dim3(256), 0, 0, o, n, (int64_t)s); });
         timeit("phase_none", st, ctr, [&](int s) { hipLaunchKernelGGL(persist_phase<2>, dim3(kWaves), dim3(64), lds, 0, o, n, (int64_t)s, st); });
         timeit("phase_rot", st, ctr, [&](int s) { hipLaunchKernelGGL(persist_phase<0>, dim3(kWaves), dim3(64), lds, 0, o, n, (int64_t)s, st); });
         timeit("phase_skew", st, ctr, [&](int s) { hipLaunchKernelGGL(persist_phase<1>, dim3(kWaves), dim3(64), lds, 0, o, n, (int64_t)s, st); });
