@@ -117,10 +117,20 @@ __global__ __launch_bounds__(kExactNT) void k_v1_exact(Geometry g, const RankDes
         nxt[k] = (uint16_t)(pk < 0 ? k : pk);
     }
     __syncthreads();
-    for (int round = 0; (1 << round) < n; round++) {   // pointer jumping to the chain roots
-        for (int k = tid; k < n; k += kExactNT) nxt[k] = nxt[nxt[k]];
-        __syncthreads();
+    // the chain roots: each thread climbs from its k (the chains are short -- they climb
+    // geometrically, ~1-2 steps -- where log2(n) rounds of pointer jumping with a barrier each took
+    // 54 of this kernel's ~180 us at C2) and writes the root in place.  Threads race on nxt, but
+    // every value written is an ancestor of its entry and a root is never changed, so a climb that
+    // reads an already compressed entry only gets there sooner.
+    {
+        volatile uint16_t *vn = nxt;
+        for (int k = tid; k < n; k += kExactNT) {
+            int r = vn[k];
+            for (int q = vn[r]; q != r; q = vn[r]) r = q;
+            vn[k] = (uint16_t)r;
+        }
     }
+    __syncthreads();
     // ---- output: x[i] for the positions of this window inside [pos_lo, pos_lo + count) ----
     int64_t p0 = 0, p1 = n;
     if (wb < pos_lo) p0 = pos_lo - wb;
