@@ -135,23 +135,37 @@ __global__ __launch_bounds__(kExactNT) void k_v1_exact(Geometry g, const RankDes
     int64_t p0 = 0, p1 = n;
     if (wb < pos_lo) p0 = pos_lo - wb;
     if (wb + n > pos_lo + count) p1 = pos_lo + count - wb;
-    for (int64_t p = p0 + tid; p < p1; p += kExactNT) {
-        const int i = (int)p;
-        int x;
-        if (n <= 1) {
-            x = 0;
-        } else if (i == 0) {
+    auto x_of = [&](int i) -> int {
+        if (n <= 1) return 0;
+        if (i == 0) {
             const int k = succ(0, 0);
-            x = k < 0 ? 0 : nxt[k];
-        } else {
-            const int pj = jv[i];
-            if (pj == i) {
-                x = nxt[i];
-            } else {
-                const int k = succ(pj, i);
-                x = k < 0 ? pj : nxt[k];
+            return k < 0 ? 0 : nxt[k];
+        }
+        const int pj = jv[i];
+        if (pj == i) return nxt[i];
+        const int k = succ(pj, i);
+        return k < 0 ? pj : nxt[k];
+    };
+    // two consecutive positions per thread, one 16-byte store per rank where the rows allow it
+    // (an even first element and a 16-byte aligned output), else one id at a time
+    const int64_t e0 = -pos_lo + wb + p0;   // element of position p0 in rank row 0
+    const bool pairs = !ma.fpos && ((count | e0) & 1) == 0 && (((uintptr_t)out) & 15u) == 0;
+    if (pairs) {
+        for (int64_t p = p0 + 2 * tid; p < p1; p += 2 * kExactNT) {
+            const int x0 = x_of((int)p);
+            const bool two = p + 1 < p1;
+            const int x1 = two ? x_of((int)p + 1) : 0;
+            for (int32_t r = r_a; r < r_b; r++) {   // (wave-uniform rank: scalar descriptor loads)
+                const int64_t ns0 = ranks[rank_lo + r].new_start + wb;
+                int64_t *o = out + (int64_t)r * count - pos_lo + wb + p;
+                if (two) *(longlong2 *)o = make_longlong2(wrap_id(ns0 + x0, g.N), wrap_id(ns0 + x1, g.N));
+                else o[0] = wrap_id(ns0 + x0, g.N);
             }
         }
+        return;
+    }
+    for (int64_t p = p0 + tid; p < p1; p += kExactNT) {
+        const int x = x_of((int)p);
         for (int32_t r = r_a; r < r_b; r++)   // (wave-uniform rank: scalar descriptor loads)
             put_id_or_pair(out, ma, (int64_t)r * count - pos_lo + wb + p, wrap_id(ranks[rank_lo + r].new_start + wb + x, g.N));
     }
