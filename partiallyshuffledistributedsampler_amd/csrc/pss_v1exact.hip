@@ -510,6 +510,56 @@ __global__ __launch_bounds__(256) void k_v1x_out(Geometry g, V1xBig b, const Ran
         put_id_or_pair(out, ma, (int64_t)r * count + (p - pos_lo), wrap_id(ranks[rank_lo + r].new_start + wb + x, g.N));
 }
 
+// The same for two consecutive positions per thread: both climbs in flight together and one
+// 16-byte store per rank (ids only; the launcher checks the rows' alignment)
+__global__ __launch_bounds__(256) void k_v1x_out2(Geometry g, V1xBig b, const RankDesc *__restrict__ ranks,
+                                                  int32_t rank_lo, int32_t nout, int64_t pos_lo, int64_t count,
+                                                  int64_t *__restrict__ out) {
+    uint32_t slot, xblk;
+    if (!v1x_block(b, slot, xblk)) return;
+    const uint64_t job = b.j0 + slot;
+    const int64_t w = b.w_lo + (int64_t)(job % (uint64_t)b.nw);
+    const int n = v1x_len(g, w);
+    const int64_t wb = w * g.B;
+    const int i0 = (int)(xblk * 512u + 2u * threadIdx.x);
+    const int64_t p = wb + i0;
+    const int64_t pos_hi = pos_lo + count;
+    if (i0 >= n || p + 1 < pos_lo || p >= pos_hi) return;
+    const uint32_t *J = b.J + (size_t)slot * b.B;
+    const uint32_t *S = b.S + (size_t)slot * b.B, *H = b.H + (size_t)slot * b.B;
+    const bool has1 = i0 + 1 < n;
+    uint32_t x[2] = {0u, 0u};
+    if (n > 1) {
+        uint32_t k[2], j[2];
+        k[0] = S[i0]; j[0] = J[i0];
+        k[1] = has1 ? S[i0 + 1] : kV1bNone; j[1] = has1 ? J[i0 + 1] : 0u;
+        bool run[2];
+#pragma unroll
+        for (int c = 0; c < 2; c++) {
+            run[c] = k[c] != kV1bNone;
+            x[c] = run[c] ? k[c] : (i0 + c == 0 ? 0u : j[c]);
+        }
+        while (run[0] || run[1]) {   // both chains' next links in flight together
+            uint32_t h[2];
+#pragma unroll
+            for (int c = 0; c < 2; c++) h[c] = run[c] ? H[x[c]] : kV1bNone;
+#pragma unroll
+            for (int c = 0; c < 2; c++) {
+                if (h[c] == kV1bNone) run[c] = false;
+                else x[c] = h[c];
+            }
+        }
+    }
+    const bool in0 = p >= pos_lo && p < pos_hi, in1 = has1 && p + 1 >= pos_lo && p + 1 < pos_hi;
+    for (int32_t r = 0; r < nout; r++) {   // (wave-uniform rank: scalar descriptor loads)
+        const int64_t ns0 = ranks[rank_lo + r].new_start + wb;
+        int64_t *o = out + (int64_t)r * count + (p - pos_lo);
+        if (in0 && in1) *(longlong2 *)o = make_longlong2(wrap_id(ns0 + x[0], g.N), wrap_id(ns0 + x[1], g.N));
+        else if (in0) o[0] = wrap_id(ns0 + x[0], g.N);
+        else if (in1) o[1] = wrap_id(ns0 + x[1], g.N);
+    }
+}
+
 namespace {
 // entries per pass of the HBM path (~18 B each: a pass's workspace is <= 2.3 GB while windows
 // have at most 2^27 entries; a longer window is one job of ~18 B per entry, up to ~39 GB near
@@ -679,9 +729,17 @@ static hipError_t launch_v1_exact_big(const Geometry &g, const RankDesc *ranks, 
         V1xBig bs = b;
         const dim3 gs = grid(bs, nbk);
         hipLaunchKernelGGL(k_v1x_solve, gs, dim3(kV1sNT), 0, s, g, bs);
+        // ids: two positions per thread and 16-byte stores when every rank row's pairs are
+        // aligned (count, pos_lo and the window length even, a 16-byte aligned output)
         V1xBig bo = b;
-        const dim3 go = grid(bo, (B + 255) / 256);
-        hipLaunchKernelGGL(k_v1x_out, go, dim3(256), 0, s, g, bo, ranks, rank_lo, nr, pos_lo, count, out, ma);
+        const bool pairs = !ma.fpos && ((count | pos_lo | g.B) & 1) == 0 && (((uintptr_t)out) & 15u) == 0;
+        if (pairs) {
+            const dim3 go = grid(bo, (B + 511) / 512);
+            hipLaunchKernelGGL(k_v1x_out2, go, dim3(256), 0, s, g, bo, ranks, rank_lo, nr, pos_lo, count, out);
+        } else {
+            const dim3 go = grid(bo, (B + 255) / 256);
+            hipLaunchKernelGGL(k_v1x_out, go, dim3(256), 0, s, g, bo, ranks, rank_lo, nr, pos_lo, count, out, ma);
+        }
         e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
