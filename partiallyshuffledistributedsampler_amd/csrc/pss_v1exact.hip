@@ -21,8 +21,8 @@
 //      A_i(p) = value at position p just before the swap of step i,
 //        x[i] = A_i(j_i);  A_i(p) = R(k) for the smallest k > i with j_k = p, else p;
 //        R(k) = A_k(k)   = R(parent(k)), parent(k) = smallest k' > k with j_k' = k, else k.
-//      Bucket the steps by j (count, scan, scatter), take parents from the buckets, pointer-
-//      jump to the roots, and read each x[i] off its bucket.  tests/test_gpu_parity.py checks
+//      Bucket the steps by j (count, scan, scatter), take parents from the buckets, climb to
+//      the roots (in place, one pass), and read each x[i] off its bucket.  tests/test_gpu_parity.py checks
 //      the streams against oracle/pss_oracle.c's exact V1 (CPython restatement, pinned by the
 //      reference's golden streams).
 #include <cstdlib>
