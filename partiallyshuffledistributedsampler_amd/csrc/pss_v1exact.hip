@@ -69,12 +69,16 @@ __global__ __launch_bounds__(kExactNT) void k_v1_exact(Geometry g, const RankDes
     const int64_t wb = w * g.B;
     const int n = (int)(g.ns - wb < g.B ? g.ns - wb : g.B);
     const int tid = threadIdx.x, wid = tid >> 6;
-    uint32_t *mt = smem;                                   // [624]
-    uint32_t *cnt = smem + kMtN;                           // [n + 1] bucket counts -> ends
-    uint16_t *jv = (uint16_t *)(cnt + n + 1);              // [n] j_i
+    // LDS (v1_exact_lds_bytes): [624] MT state only when this block draws itself, then 10 B per
+    // entry -- 40 KB at n = 4096, four workgroups per CU
+    uint32_t *mt = smem;                                   // [624] (no J)
+    uint32_t *cnt = J ? smem : smem + kMtN;                // [n] bucket counts -> ends
+    uint16_t *jv = (uint16_t *)(cnt + n);                  // [n] j_i
     uint16_t *lst = jv + n;                                // [n] steps bucketed by j
     uint16_t *nxt = lst + n;                               // [n] parent -> root
-    __shared__ uint32_t tot[kExactNT / 64];
+    // the block scan's wave totals in nxt, unused until after the scan (n >= 8; tiny windows:
+    // the 16 bytes after the arrays)
+    uint32_t *tot = n >= 8 ? (uint32_t *)nxt : (uint32_t *)(((uintptr_t)(nxt + n) + 3u) & ~(uintptr_t)3u);
 
     if (J) {                 // draws already made by k_v1x_draws
         const uint16_t *jw = J + (size_t)wslot * (size_t)(g.B < g.ns ? g.B : g.ns);
@@ -87,7 +91,7 @@ __global__ __launch_bounds__(kExactNT) void k_v1_exact(Geometry g, const RankDes
                  [&](uint32_t d, uint32_t r) { jv[n - 1 - (int)d] = (uint16_t)r; });
     }
     // ---- 3. resolve the swap sequence (all threads) ----
-    for (int p = tid; p <= n; p += kExactNT) cnt[p] = 0;
+    for (int p = tid; p < n; p += kExactNT) cnt[p] = 0;
     __syncthreads();
     for (int k = 1 + tid; k < n; k += kExactNT) atomicAdd(&cnt[jv[k]], 1u);
     __syncthreads();
@@ -575,8 +579,9 @@ uint32_t v1x_nbk(int64_t W) { return (uint32_t)((W + kV1bBW - 1) / kV1bBW); }
 size_t v1x_job_words(int64_t W) { return (size_t)4 * W + (size_t)(W + 1) / 2 + v1x_nbk(W); }
 }  // namespace
 
-size_t v1_exact_lds_bytes(int64_t n) {
-    return (size_t)(kMtN + n + 1) * sizeof(uint32_t) + (size_t)3 * n * sizeof(uint16_t) + 16;
+size_t v1_exact_lds_bytes(int64_t n, bool with_mt) {
+    return (with_mt ? (size_t)kMtN * sizeof(uint32_t) : 0u) + (size_t)n * sizeof(uint32_t) +
+           (size_t)3 * n * sizeof(uint16_t) + (n < 8 ? 20u : 0u);
 }
 
 bool v1_exact_supported(const Geometry &g) { return g.B < ((int64_t)1 << 31); }
@@ -759,10 +764,10 @@ hipError_t launch_v1_exact(const Geometry &g, const RankDesc *ranks, int32_t ran
     }
     const int64_t w_lo = pos_lo / g.B, w_hi = (pos_hi - 1) / g.B;
     const int64_t nw = w_hi - w_lo + 1;
-    const size_t lds = v1_exact_lds_bytes(g.B < g.ns ? g.B : g.ns);
+    const size_t lds = v1_exact_lds_bytes(g.B < g.ns ? g.B : g.ns, ws == nullptr);
     static const hipError_t attr = hipFuncSetAttribute(
         (const void *)k_v1_exact, hipFuncAttributeMaxDynamicSharedMemorySize,
-        (int)v1_exact_lds_bytes(kV1ExactMaxB));
+        (int)v1_exact_lds_bytes(kV1ExactMaxB, true));
     if (attr != hipSuccess) return attr;
     // with a workspace, the serial MT phases run one wave per window (many windows in flight)
     // ahead of the resolution, the windows' states seeded before them (k_mt_seed_streams, 16
