@@ -420,6 +420,53 @@ struct SegMap {
     }
 };
 
+// ---- packed-pair slots of the exchange replay (MapArgs::pack, pss_generate_mapped) -----------
+// The slot table carries the pair (file << pob) | offset instead of the id.  It is computed where
+// a value is inserted -- the inserted values of pool2 window w are the ids a + y, y < B, of one
+// id interval, which crosses at most two file boundaries when files are not much shorter than
+// the window: y -> y + Q_k on segment k, three SGPR constants and two compares -- so emitting a
+// value is a shift and a mask.  Values without a pair (windows that wrap at N, reach past the
+// scanned total T, or cross three or more file boundaries; slot-table values older than
+// kPairBack windows at a tile's start) carry kPairEsc | virtual index and take the global
+// bucketed map when emitted.  Results equal pss_map's.
+constexpr uint32_t kPairEsc = 0x80000000u;
+constexpr uint32_t kPairBack = 8;       // windows before the tile's first with constants
+constexpr uint32_t kPairWords = 5;      // per window: Q0, Q1, Q2, s1, s2 (Q0 = kNone: no pairs)
+
+// constants of pool2 window w (virtual values [w B, w B + len)) of rank rd into c[kPairWords]
+__device__ __forceinline__ void pair_window_consts(const MapArgs &ma, const RankDesc &rd, const Geometry &g,
+                                                   uint32_t B, uint32_t twoB, uint32_t w, uint32_t *c) {
+    c[0] = kNone; c[1] = 0u; c[2] = 0u; c[3] = kNone; c[4] = kNone;
+    const int64_t v0 = (int64_t)w * B;
+    if (v0 >= g.ns) return;
+    const int64_t len = g.ns - v0 < (int64_t)B ? g.ns - v0 : (int64_t)B;
+    if (v0 < (int64_t)twoB && v0 + len > (int64_t)twoB) return;   // (2B and ns are window ends)
+    int64_t a = (v0 < (int64_t)twoB ? rd.old_start : rd.new_start) + v0;
+    if (a >= g.N) a -= g.N;
+    if (a + len > g.N || a + len > ma.T) return;                 // wraps, or reflected ids
+    int32_t f;
+    int64_t o;
+    map_one_bucketed_t(ma.prefix, ma.F, ma.T, ma.BT, ma.kb, ma.nb, a, f, o);
+    if (f < 0) return;
+    uint32_t Q[3] = {((uint32_t)f << ma.pob) + (uint32_t)o, 0u, 0u}, s[2] = {kNone, kNone};
+    for (int k = 0; k < 3; k++) {
+        const int64_t end = ma.prefix[f + 1] - a;   // the next file boundary (prefix[F] = T)
+        if (end >= len) break;
+        if (k == 2) return;                         // a third boundary: no pairs
+        int64_t ob;
+        map_one_bucketed_t(ma.prefix, ma.F, ma.T, ma.BT, ma.kb, ma.nb, a + end, f, ob);   // skips empty files
+        s[k] = (uint32_t)end;
+        Q[k + 1] = ((uint32_t)f << ma.pob) - (uint32_t)end;
+    }
+    c[0] = Q[0]; c[1] = Q[1]; c[2] = Q[2]; c[3] = s[0]; c[4] = s[1];
+}
+
+// the pair of value y of a window with constants (Q0, Q1, Q2, s1, s2)
+__device__ __forceinline__ uint32_t pair_of_y(uint32_t y, uint32_t Q0, uint32_t Q1, uint32_t Q2, uint32_t s1,
+                                              uint32_t s2) {
+    return y + (y < s1 ? Q0 : (y < s2 ? Q1 : Q2));
+}
+
 // The id interval staged for virtual values [v_lo, v_hi) of one rank: ids are base + v (base =
 // old start below twoB, new start above) wrapped modulo N, so the values may map to two or three
 // id intervals; the one holding the value v_pref (the tile's own first window) is staged.

@@ -95,7 +95,29 @@ struct MapArgs {
     int32_t kb;
     int64_t nb;
     int32_t *fpos, *off;
+    // host-known shortcuts of the map (map_shortcuts, pss_runtime.cpp; all zero = none):
+    int64_t T;          // scanned total prefix[F] = sum of the dataset files' lengths
+    // pack: every (file position, offset) pair fits 31 bits as (file << pob) | offset (the
+    // exchange replay then carries pairs in its slot table)
+    uint32_t pack, pob;
+    // uni: every file holds uL samples and T < 2^32: file = id / uL by the round-up magic
+    // (um, ul) of udiv_magic, offset = id - file * uL, for ids < T
+    uint32_t uni, uL, um, ul;
 };
+
+// u32 division by an invariant d >= 1 (Granlund-Montgomery round-up form): l = ceil(log2 d),
+// m = floor(2^32 (2^l - d) / d) + 1; q = (t + ((n - t) >> 1)) >> (l - 1), t = mulhi(m, n);
+// d = 1: l = 0, m = 0 and q = n (udiv_apply's l == 0 case)
+inline void udiv_magic(uint32_t d, uint32_t &m, uint32_t &l) {
+    l = 0;
+    while (l < 32 && ((uint64_t)1 << l) < d) l++;
+    m = d <= 1 ? 0u : (uint32_t)((((uint64_t)1 << 32) * (((uint64_t)1 << l) - d)) / d + 1);
+}
+__host__ __device__ inline uint32_t udiv_apply(uint32_t n, uint32_t m, uint32_t l) {
+    if (l == 0) return n;
+    const uint32_t t = (uint32_t)(((uint64_t)m * n) >> 32);   // v_mul_hi_u32 on the device
+    return (t + ((n - t) >> 1)) >> (l - 1);
+}
 
 // V1: ids of positions [pos_lo, pos_lo+count) of ranks [rank_lo, rank_lo+nr) -> out[r][count];
 // each window ordered by its keyed Feistel bijection (key table of the windows in key_ws).

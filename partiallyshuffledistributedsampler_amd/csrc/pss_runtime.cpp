@@ -221,6 +221,7 @@ struct pss_sampler {
     DevBuf<int32_t> d_bucket;     // bucket index of the prefix (pss_map.h), kb / nb below
     int32_t kb = 0;
     int64_t nb = 0, max_len = 0;
+    pss::MapArgs map_sc{};        // host-known map shortcuts (map_shortcuts): T, pack, uni
     hipEvent_t ids_free = nullptr;   // last reader of d_ids
     DevBuf<int32_t> d_order, d_err;
     DevBuf<pss::RankDesc> d_ranks;
@@ -446,6 +447,49 @@ struct CpuTimer {   // pss_profile in CPU mode: wall milliseconds per kernel kin
     }
 };
 
+// The map's host-known shortcuts (MapArgs: T, pack / pob, uni / uL / um / ul), fixed by the
+// files' lengths at create -- the file order changes per epoch, the lengths and their total do not:
+//   pack -- every pair (file position, offset) fits 31 bits as (file << pob) | offset, and every
+//           virtual index fits 31 bits (an escaped slot value is kPairEsc | v): the exchange
+//           replay carries pairs in its slot table (pss_device.h pair_window_consts)
+//   uni  -- every file holds the same L > 0 samples and T < 2^32: the file position of id < T is
+//           id / L (one multiply-high by a magic), offset id - file * L (prefix[f] = f * L in any
+//           file order)
+void map_shortcuts(pss_sampler *h, int64_t scanned) {
+    pss::MapArgs &m = h->map_sc;
+    m = pss::MapArgs{};
+    m.T = scanned;
+    const int64_t F = h->F;
+    if (F <= 0 || h->max_len <= 0) return;
+    uint32_t pob = 0;
+    while (pob < 31 && (((int64_t)1 << pob) < h->max_len)) pob++;   // offsets < max_len <= 2^pob
+    if (((F - 1) << pob) + (((int64_t)1 << pob) - 1) < ((int64_t)1 << 31) && h->ns < ((int64_t)1 << 31)) {
+        m.pack = 1;
+        m.pob = pob;
+    }
+    const int64_t L = h->files_len[0];
+    bool uni = L > 0 && scanned < ((int64_t)1 << 32);
+    for (int64_t i = 1; i < F && uni; i++) uni = h->files_len[i] == L;
+    if (uni) {
+        m.uni = 1;
+        m.uL = (uint32_t)L;
+        pss::udiv_magic((uint32_t)L, m.um, m.ul);
+    }
+}
+
+// the map arguments of the current epoch's device tables and the caller's outputs
+pss::MapArgs map_args(const pss_sampler *h, int32_t *fpos, int32_t *off) {
+    pss::MapArgs m = h->map_sc;
+    m.prefix = h->d_prefix.p;
+    m.F = h->F;
+    m.BT = h->d_bucket.p;
+    m.kb = h->kb;
+    m.nb = h->nb;
+    m.fpos = fpos;
+    m.off = off;
+    return m;
+}
+
 }  // namespace
 
 extern "C" {
@@ -489,6 +533,7 @@ int pss_create(const int64_t *files_len, int64_t num_files, int64_t total_size,
     h->cpu = device == PSS_DEVICE_CPU;
     h->ns = (int64_t)std::ceil((double)total_size / (double)num_replicas);  // V1:42 (float ceil)
     if (h->ns >= (int64_t)UINT32_MAX) { delete h; return fail(PSS_ENOTSUP, "num_samples >= 2^32 per rank"); }
+    map_shortcuts(h, scanned);
     h->order.resize(num_files);
     for (int64_t i = 0; i < num_files; i++) h->order[i] = (int32_t)i;
     h->blocks.resize(num_replicas);
@@ -1055,13 +1100,13 @@ int pss_generate_mapped(pss_sampler *h, int32_t rank_lo, int32_t rank_hi, int64_
         // order of both modes)
         const size_t sb = pss::v1_workspace_bytes(g, nr, pos_lo, count);
         if (sb) PSS_HIP(h->d_sort.ensure(words(sb)));
-        pss::MapArgs ma{h->d_prefix.p, h->F, h->d_bucket.p, h->kb, h->nb, file_pos_dev, offset_dev};
+        const pss::MapArgs ma = map_args(h, file_pos_dev, offset_dev);
         PSS_HIP(pss::launch_v1(g, h->d_ranks.p, rank_lo, nr, pos_lo, count, nullptr, h->d_sort.p, s, mk, &ma));
         return PSS_OK;
     }
     if (exact) {
         // fused: the exact pipelines' output kernels map each id where they would write it
-        pss::MapArgs ma{h->d_prefix.p, h->F, h->d_bucket.p, h->kb, h->nb, file_pos_dev, offset_dev};
+        const pss::MapArgs ma = map_args(h, file_pos_dev, offset_dev);
         if (h->version == 1) {
             PSS_HIP(h->d_sort.ensure(words(pss::v1_exact_ws_bytes(g, nr, pos_lo, count))));
             mk(pss::K_V1, s);
@@ -1078,7 +1123,7 @@ int pss_generate_mapped(pss_sampler *h, int32_t rank_lo, int32_t rank_hi, int64_
     }
     if (h->version == 2 && h->order_mode == PSS_ORDER_COUNTER && pss::v2_mapped_fused(g, h->emit_path)) {
         // fused: the replay maps each id as it emits it (LDS segment map per tile)
-        pss::MapArgs ma{h->d_prefix.p, h->F, h->d_bucket.p, h->kb, h->nb, file_pos_dev, offset_dev};
+        const pss::MapArgs ma = map_args(h, file_pos_dev, offset_dev);
         return generate_impl(h, rank_lo, rank_hi, pos_lo, count, nullptr, stream, &ma);
     }
     // the V2 collision-probe path: ids into the handle's scratch, then the bucket map

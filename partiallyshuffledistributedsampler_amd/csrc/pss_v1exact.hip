@@ -579,9 +579,13 @@ uint32_t v1x_nbk(int64_t W) { return (uint32_t)((W + kV1bBW - 1) / kV1bBW); }
 size_t v1x_job_words(int64_t W) { return (size_t)4 * W + (size_t)(W + 1) / 2 + v1x_nbk(W); }
 }  // namespace
 
+// n = the longest window of the launch.  The 20 bytes after the arrays hold the block scan's
+// wave totals of a window shorter than 8 entries (k_v1_exact places them after its own arrays,
+// which a short last window ends early) -- always reserved, whatever the longest window (ADVICE
+// r05: B = 8 with a 7-entry last window wrote past a 10 * W allocation).
 size_t v1_exact_lds_bytes(int64_t n, bool with_mt) {
     return (with_mt ? (size_t)kMtN * sizeof(uint32_t) : 0u) + (size_t)n * sizeof(uint32_t) +
-           (size_t)3 * n * sizeof(uint16_t) + (n < 8 ? 20u : 0u);
+           (size_t)3 * n * sizeof(uint16_t) + 20u;
 }
 
 bool v1_exact_supported(const Geometry &g) { return g.B < ((int64_t)1 << 31); }

@@ -433,8 +433,9 @@ __global__ __launch_bounds__(64) void k_v2_emit(Geometry g, V2Plan pl,
 // each step is ONE exchange -- no probe, no ballot, no per-clash fix-up -- and the four
 // exchanges of a super-batch issue back to back behind a single wait.
 // MAPPED: (int32 file position, int32 offset) into ma.fpos / ma.off instead of int64 ids into
-// out, through the wave's LDS segment map (SegMap, pss_device.h)
-template <bool NARROW, bool POW2, bool MAPPED>
+// out -- PAIR: the slot table carries packed pairs (MapArgs::pack, pair_window_consts), emitting
+// is a shift and a mask; else through the wave's LDS segment map (SegMap, pss_device.h)
+template <bool NARROW, bool POW2, bool MAPPED, bool PAIR = false>
 __global__ __launch_bounds__(64) void k_v2_emit_x(Geometry g, V2Plan pl,
                                                   const RankDesc *__restrict__ ranks,
                                                   int32_t rank_lo, int64_t g_lo, int64_t ng,
@@ -442,6 +443,7 @@ __global__ __launch_bounds__(64) void k_v2_emit_x(Geometry g, V2Plan pl,
                                                   int64_t pos_lo, int64_t count, int do_tail,
                                                   int64_t *__restrict__ out, MapArgs ma, RankArgs ra,
                                                   int use_ra) {
+    static_assert(MAPPED || !PAIR, "pair slots are a form of the mapped replay");
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     PSS_TWO_WAVES_PER_SIMD();
 #ifdef PSS_STAMPS
@@ -468,20 +470,47 @@ __global__ __launch_bounds__(64) void k_v2_emit_x(Geometry g, V2Plan pl,
     const uint32_t twoB = pl.twoB;
     const uint32_t old32 = (uint32_t)rd.old_start, new32 = (uint32_t)rd.new_start;
     const uint32_t N32 = (uint32_t)g.N;
-    // NARROW: the slot table holds final ids (converted on insertion, emitted as they come out
-    // of the exchange); otherwise virtual indices, converted on emission
-    auto to_slot = [&](uint32_t v) -> uint32_t {
-        if constexpr (NARROW) return (uint32_t)emit_id<true>(v, twoB, old32, new32, N32, rd, g);
-        else return v;
-    };
-    auto from_slot = [&](uint32_t x) -> int64_t {
-        if constexpr (NARROW) return (int64_t)x;
-        else return emit_id<false>(x, twoB, old32, new32, N32, rd, g);
-    };
     const uint32_t tlo = tile * pl.L32;
     const uint32_t thi = pl.T32 - tlo < pl.L32 ? pl.T32 : tlo + pl.L32;
     const uint32_t w_lo = 1 + tlo / B;
     const int nwin = (int)(1 + (thi - 1) / B - w_lo + 1);
+    // PAIR: the pair constants of the tile's windows and the kPairBack before them (after the
+    // round keys), one lane per window
+    uint32_t *pw = rk + kRoundKeyWords * nwin_max;
+    const uint32_t wc_lo = w_lo > kPairBack ? w_lo - kPairBack : 0u;
+    const uint32_t nwc = w_lo + (uint32_t)nwin - wc_lo;
+    const uint32_t pob = ma.pob, omask = (1u << pob) - 1u;
+    if constexpr (PAIR) {
+        for (uint32_t i = lane; i < nwc; i += 64) pair_window_consts(ma, rd, g, B, twoB, wc_lo + i, pw + kPairWords * i);
+        __syncthreads();
+    }
+    const float invB = 1.0f / (float)B;
+    // PAIR, one lane: the pair of virtual value v from its window's constants, else an escape
+    auto pair_lookup = [&](uint32_t v) -> uint32_t {
+        uint32_t w = (uint32_t)((float)v * invB);     // v / B to within one (v < 2^31), corrected
+        int32_t y = (int32_t)(v - w * B);
+        if (y < 0) { w--; y += (int32_t)B; }
+        if (y >= (int32_t)B) { w++; y -= (int32_t)B; }
+        const uint32_t i = w - wc_lo;
+        if (i < nwc) {
+            const uint32_t *c = pw + kPairWords * i;
+            const uint32_t Q0 = c[0];
+            if (Q0 != kNone) return pair_of_y((uint32_t)y, Q0, c[1], c[2], c[3], c[4]);
+        }
+        return kPairEsc | v;
+    };
+    // NARROW: the slot table holds final ids (converted on insertion, emitted as they come out
+    // of the exchange); PAIR: (file, offset) pairs (or escaped virtual indices); otherwise
+    // virtual indices, converted on emission
+    auto to_slot = [&](uint32_t v) -> uint32_t {
+        if constexpr (PAIR) return pair_lookup(v);
+        else if constexpr (NARROW) return (uint32_t)emit_id<true>(v, twoB, old32, new32, N32, rd, g);
+        else return v;
+    };
+    auto from_slot = [&](uint32_t x) -> int64_t {
+        if constexpr (NARROW && !PAIR) return (int64_t)x;
+        else return emit_id<false>(x, twoB, old32, new32, N32, rd, g);
+    };
     const SlotKey sk = slot_key(g, rank);
     {   // slot table at the tile's start: 16-byte loads, up to 16 per lane in flight (the whole
         // 16 KB table of P1 = 4096 in one round trip); slots the previous tile never drew walk
@@ -532,7 +561,7 @@ __global__ __launch_bounds__(64) void k_v2_emit_x(Geometry g, V2Plan pl,
     int64_t *o = out + (int64_t)rl * count + ((int64_t)tlo - pos_lo);
     const int64_t ebase = (int64_t)rl * count + ((int64_t)tlo - pos_lo);   // element index of tl = 0
     SegMap sm;
-    if constexpr (MAPPED) {
+    if constexpr (MAPPED && !PAIR) {
         // ids of the tile's windows and the kSegBackWin before them
         const uint32_t vl = w_lo > kSegBackWin ? (w_lo - kSegBackWin) * B : 0u;
         const int64_t vh64 = (int64_t)(w_lo + (uint32_t)nwin) * B;
@@ -543,9 +572,34 @@ __global__ __launch_bounds__(64) void k_v2_emit_x(Geometry g, V2Plan pl,
     }
     auto put_m = [&](int64_t e, int64_t id) {
         int32_t f, of;
+#ifdef PSS_DIAG_MAP_NONE   // (timing-only build: the stores of the mapped form without the map)
+        f = (int32_t)id; of = (int32_t)(id >> 3);
+#else
         sm.map(id, f, of);
+#endif
         ma.fpos[e] = f;
         ma.off[e] = of;
+    };
+    // emit slot value x at element e: MAPPED + PAIR the pair itself (an escaped value through the
+    // global bucketed map), MAPPED its id through the segment map, else the id
+    auto emit_m = [&](int64_t e, uint32_t x) {
+        if constexpr (PAIR) {
+            int32_t f, of;
+            if (x & kPairEsc) {
+                int64_t o;
+                map_one_bucketed_t(ma.prefix, ma.F, ma.T, ma.BT, ma.kb, ma.nb, from_slot(x & ~kPairEsc), f, o);
+                of = (int32_t)o;
+            } else {
+                f = (int32_t)(x >> pob);
+                of = (int32_t)(x & omask);
+            }
+            ma.fpos[e] = f;
+            ma.off[e] = of;
+        } else if constexpr (MAPPED) {
+            put_m(e, from_slot(x));
+        } else {
+            out[e] = from_slot(x);
+        }
     };
     const uint32_t hB = pl.hB;
     const bool walk_full = pl.walk_full;                     // full windows need cycle walking
@@ -573,7 +627,7 @@ __global__ __launch_bounds__(64) void k_v2_emit_x(Geometry g, V2Plan pl,
         // and tlo % 256 == 0 put every super-batch inside one window.
         const uint32_t avail = (w_last - 1 - w_lo) * B - p0;     // steps before window w_last-1
         uint32_t left = (avail < nvalid ? avail : nvalid) >> 8;  // super-batches
-        if constexpr (NARROW && POW2) {
+        if constexpr ((NARROW || PAIR) && POW2) {
             // Keyed-carry form of the packed Feistel (feistel4_pk16's values): with
             // A_i = R_i ^ K_i, A_{i+1} = A_{i-1} ^ F(A_i) ^ (K_{i-1} ^ K_{i+1}), one 3-input xor
             // per round; the output is L = A_5 ^ K_5, R = A_4 ^ F(A_5) ^ K_4.  p0 is a multiple
@@ -617,10 +671,24 @@ __global__ __launch_bounds__(64) void k_v2_emit_x(Geometry g, V2Plan pl,
                 const uint32_t A00 = Ri0 ^ kw[0], A01 = Ri1 ^ kw[0];
                 const uint32_t C0 = Li0 ^ F(A00) ^ kw[1], C1 = Li1 ^ F(A01) ^ kw[1];
                 // ids of the window's values wB + y: one add when the window maps contiguously
+                // (PAIR: the window's pair constants in SGPRs, y -> y + Q_k on segment k)
                 const uint32_t wB = w0 * B;
-                const uint32_t id_first = to_slot(wB), id_last = to_slot(wB + B - 1);
-                const bool contiguous = __builtin_amdgcn_readfirstlane(
-                    id_last - id_first == B - 1 && ((wB < twoB) == (wB + B - 1 < twoB)));
+                uint32_t id_first = 0, PQ0 = 0, PQ1 = 0, PQ2 = 0, Ps1 = 0, Ps2 = 0;
+                bool contiguous;
+                if constexpr (PAIR) {
+                    const uint32_t *c = pw + kPairWords * (w0 - wc_lo);
+                    PQ0 = __builtin_amdgcn_readfirstlane(c[0]);
+                    PQ1 = __builtin_amdgcn_readfirstlane(c[1]);
+                    PQ2 = __builtin_amdgcn_readfirstlane(c[2]);
+                    Ps1 = __builtin_amdgcn_readfirstlane(c[3]);
+                    Ps2 = __builtin_amdgcn_readfirstlane(c[4]);
+                    contiguous = PQ0 != kNone;
+                } else {
+                    id_first = to_slot(wB);
+                    const uint32_t id_last = to_slot(wB + B - 1);
+                    contiguous = __builtin_amdgcn_readfirstlane(
+                        id_last - id_first == B - 1 && ((wB < twoB) == (wB + B - 1 < twoB)));
+                }
                 pace.step(tl0);
                 // one 256-step super-batch at (tlx, px): its 4 slots and 4 inserted values
                 auto batch = [&](auto contig, uint32_t tlx, uint32_t px, uint32_t (&k)[4], uint32_t (&ins)[4]) {
@@ -643,12 +711,18 @@ __global__ __launch_bounds__(64) void k_v2_emit_x(Geometry g, V2Plan pl,
                     const uint32_t Y0 = S0 ^ (A40 ^ F50 ^ KY), Y1 = S1 ^ (A41 ^ F51 ^ KY);
                     const uint32_t y[4] = {Y0 & 0xFFFFu, Y0 >> 16, Y1 & 0xFFFFu, Y1 >> 16};
 #pragma unroll
-                    for (int j = 0; j < 4; j++) ins[j] = decltype(contig)::value ? id_first + y[j] : to_slot(wB + y[j]);
+                    for (int j = 0; j < 4; j++) {
+                        if constexpr (PAIR)
+                            ins[j] = decltype(contig)::value ? pair_of_y(y[j], PQ0, PQ1, PQ2, Ps1, Ps2)
+                                                             : kPairEsc | (wB + y[j]);
+                        else
+                            ins[j] = decltype(contig)::value ? id_first + y[j] : to_slot(wB + y[j]);
+                    }
                 };
                 auto emit4 = [&](uint32_t tlx, const uint32_t (&v)[4]) {
                     if constexpr (MAPPED) {
 #pragma unroll
-                        for (int j = 0; j < 4; j++) put_m(ebase + tlx + 64u * j + lane, (int64_t)v[j]);
+                        for (int j = 0; j < 4; j++) emit_m(ebase + tlx + 64u * j + lane, v[j]);
                     } else {
                         int64_t *ob = o + tlx;
 #pragma unroll
@@ -681,6 +755,11 @@ __global__ __launch_bounds__(64) void k_v2_emit_x(Geometry g, V2Plan pl,
                 for (int i = 0; i < kFeistelRounds; i++)
                     kw[i] = (__builtin_amdgcn_readfirstlane(rk[kRoundKeyWords * (w0 - wl) + i]) & 0xFFFFu) * 0x10001u;
                 const uint32_t wB = w0 * B;
+                uint32_t PQ[5] = {kNone, 0u, 0u, kNone, kNone};   // PAIR: the window's constants
+                if constexpr (PAIR) {
+#pragma unroll
+                    for (int i = 0; i < 5; i++) PQ[i] = __builtin_amdgcn_readfirstlane(pw[kPairWords * (w0 - wc_lo) + i]);
+                }
                 pace.step(tl0);
                 for (uint32_t i = 0; i < n; i++) {
                     uint32_t k[4], ins[4], v[4];
@@ -688,11 +767,18 @@ __global__ __launch_bounds__(64) void k_v2_emit_x(Geometry g, V2Plan pl,
                     const uint32_t x[4] = {p0 + lane, p0 + 64u + lane, p0 + 128u + lane, p0 + 192u + lane};
                     feistel4_pk16(x, hB, kw, ins);
 #pragma unroll
-                    for (int j = 0; j < 4; j++) v[j] = atomicExch(&buf[k[j]], to_slot(wB + ins[j]));
+                    for (int j = 0; j < 4; j++) {
+                        uint32_t sv;
+                        if constexpr (PAIR)
+                            sv = PQ[0] != kNone ? pair_of_y(ins[j], PQ[0], PQ[1], PQ[2], PQ[3], PQ[4]) : kPairEsc | (wB + ins[j]);
+                        else
+                            sv = to_slot(wB + ins[j]);
+                        v[j] = atomicExch(&buf[k[j]], sv);
+                    }
                     // wave-uniform base: the stores take (lane * 8 + 512 j) as offset
                     if constexpr (MAPPED) {
 #pragma unroll
-                        for (int j = 0; j < 4; j++) put_m(ebase + tl0 + 64u * j + lane, from_slot(v[j]));
+                        for (int j = 0; j < 4; j++) emit_m(ebase + tl0 + 64u * j + lane, v[j]);
                     } else {
                         int64_t *ob = o + tl0;
 #pragma unroll
@@ -720,7 +806,7 @@ __global__ __launch_bounds__(64) void k_v2_emit_x(Geometry g, V2Plan pl,
                                                     rk + kRoundKeyWords * (w - wl));
                 const uint32_t vv = atomicExch(&buf[kk], to_slot(in));
                 if (tl >= e_lo && tl < e_hi) {
-                    if constexpr (MAPPED) put_m(ebase + tl, from_slot(vv));
+                    if constexpr (MAPPED) emit_m(ebase + tl, vv);
                     else o[tl] = from_slot(vv);
                 }
             }
@@ -764,7 +850,7 @@ __global__ __launch_bounds__(64) void k_v2_emit_x(Geometry g, V2Plan pl,
                 for (int u = 0; u < 4; u++) v[u] = buf[y[u]];
 #pragma unroll
                 for (int u = 0; u < 4; u++) {
-                    if constexpr (MAPPED) put_m(etail + j0 + 64u * u + lane, from_slot(v[u]));
+                    if constexpr (MAPPED) emit_m(etail + j0 + 64u * u + lane, v[u]);
                     else ot[j0 + 64u * u + lane] = from_slot(v[u]);
                 }
             }
@@ -772,7 +858,7 @@ __global__ __launch_bounds__(64) void k_v2_emit_x(Geometry g, V2Plan pl,
             for (uint32_t j = lane; j < P1; j += 64) {
                 const int64_t pos = pl.T + j;
                 if (pos < pos_lo || pos >= pos_hi) continue;
-                if constexpr (MAPPED) put_m(etail + j, from_slot(buf[feistel(j, P1, hT, tk)]));
+                if constexpr (MAPPED) emit_m(etail + j, buf[feistel(j, P1, hT, tk)]);
                 else ot[j] = from_slot(buf[feistel(j, P1, hT, tk)]);
             }
         }
@@ -1041,8 +1127,12 @@ hipError_t launch_v2(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, 
             const dim3 grid((uint32_t)(nr * ng));
             if (emit_path == EMIT_XCHG) {
                 mk(K_V2_EMIT, s);
+                // mapped: pair slots (MapArgs::pack) with their window constants, else the
+                // segment map, after the keys
+                const bool pair = mapped && mapped->pack;
                 const size_t need = lds_keys + (size_t)((pl.P1 + 3) & ~3) * 4 +
-                                    (mapped ? (size_t)kSegLdsWords * 4 : 0);
+                                    (pair ? (size_t)kPairWords * (size_t)(nwin_max + kPairBack) * 4
+                                          : mapped ? (size_t)kSegLdsWords * 4 : 0);
                 const size_t lds = need > (size_t)pl.emit_lds ? need : (size_t)pl.emit_lds;
                 tail_fused = need_tail && last_emit == pl.G - 1;
                 const int dt = tail_fused ? 1 : 0;
@@ -1051,7 +1141,9 @@ hipError_t launch_v2(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, 
                 RankArgs ra;
                 const int use_ra = rank_args ? 1 : 0;
                 if (rank_args) ra = *rank_args;
-#define PSS_EX(N, P2) do { if (mapped) hipLaunchKernelGGL((k_v2_emit_x<N, P2, true>), grid, dim3(64), lds, s, g, pl, ranks, rank_lo, \
+#define PSS_EX(N, P2) do { if (pair) hipLaunchKernelGGL((k_v2_emit_x<N, P2, true, true>), grid, dim3(64), lds, s, g, pl, ranks, rank_lo, \
+                                         g_lo, ng, (const uint32_t *)VAL, pos_lo, count, dt, out, ma, ra, use_ra); \
+                           else if (mapped) hipLaunchKernelGGL((k_v2_emit_x<N, P2, true>), grid, dim3(64), lds, s, g, pl, ranks, rank_lo, \
                                          g_lo, ng, (const uint32_t *)VAL, pos_lo, count, dt, out, ma, ra, use_ra); \
                            else hipLaunchKernelGGL((k_v2_emit_x<N, P2, false>), grid, dim3(64), lds, s, g, pl, ranks, rank_lo, \
                                          g_lo, ng, (const uint32_t *)VAL, pos_lo, count, dt, out, ma, ra, use_ra); } while (0)
@@ -1208,6 +1300,10 @@ hipError_t init_kernel_attributes_v2() {
     PSS_ATTR((k_v2_emit_x<true, false, true>));
     PSS_ATTR((k_v2_emit_x<false, true, true>));
     PSS_ATTR((k_v2_emit_x<false, false, true>));
+    PSS_ATTR((k_v2_emit_x<true, true, true, true>));
+    PSS_ATTR((k_v2_emit_x<true, false, true, true>));
+    PSS_ATTR((k_v2_emit_x<false, true, true, true>));
+    PSS_ATTR((k_v2_emit_x<false, false, true, true>));
     PSS_ATTR((k_v2_emit<true, false>));
     PSS_ATTR((k_v2_emit<false, false>));
     PSS_ATTR((k_v2_emit<true, true>));

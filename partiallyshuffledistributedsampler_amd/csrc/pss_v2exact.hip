@@ -591,8 +591,10 @@ __global__ __launch_bounds__(256) void k_v2x_fanout(Geometry g, const RankDesc *
     const int64_t pos_hi = pos_lo + count < g.ns ? pos_lo + count : g.ns;
     const int64_t t0 = pos_lo + ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
     if (t0 >= pos_hi) return;
-    const bool vec = !ma.fpos && t0 + 4 <= pos_hi && (t0 & 3) == 0 && ((count | pos_lo) & 1) == 0 &&
-                     (((uintptr_t)out) & 15u) == 0;
+    // (the 16-byte VV load needs VV + t0 itself 16-byte aligned, not only t0 % 4 == 0: VV follows
+    // the workspace's other arrays)
+    const bool vec = !ma.fpos && t0 + 4 <= pos_hi && (((uintptr_t)(VV + t0)) & 15u) == 0 &&
+                     ((count | pos_lo) & 1) == 0 && (((uintptr_t)out) & 15u) == 0;
     if (vec) {
         const uint4 w = *(const uint4 *)(VV + t0);
         const int64_t v[4] = {w.x, w.y, w.z, w.w};
@@ -982,15 +984,20 @@ static V2xChain v2x_chain_plan(const V2xGeo &x, int32_t nr) {
 // words), K2 (T2 words) and the windows' seeded MT states ST (S x 624, the one-wave draw form).
 // A slot depends on the epoch and (ns, B) only, so the runtime can fill slots of coming epochs
 // ahead of their calls (pss_runtime.cpp, exact lookahead) and hand one to launch_v2_exact.
+// (rounded up to 4 words: the slot that follows in the workspace -- whose K1 doubles as VV, read
+// by 16-byte loads in k_v2x_fanout -- starts 16-byte aligned)
 static size_t v2x_rest_words(const V2xGeo &x) {
     const int32_t nr = 1;   // one decoded sequence serves every rank of a call (v2x_pass)
+    size_t w;
     if (v2x_chain(x)) {   // ANS (ns), Q2 (T2), survivors, chunk maps, chunk starts
         const V2xChain ch = v2x_chain_plan(x, nr);
-        return (size_t)x.ns + (size_t)x.T2 + (size_t)x.tiles1 * x.P + (size_t)3 * ch.nch * x.P;
+        w = (size_t)x.ns + (size_t)x.T2 + (size_t)x.tiles1 * x.P + (size_t)3 * ch.nch * x.P;
+    } else {
+        // V, O, Vd, Od (ns each), Q2 (T2), tile splits.  Windows beyond kTile are decoded in V, O,
+        // Vd, Od (S * B <= ns).
+        w = (size_t)4 * x.ns + (size_t)x.T2 + v2x_split_words(x, nr);
     }
-    // V, O, Vd, Od (ns each), Q2 (T2), tile splits.  Windows beyond kTile are decoded in V, O,
-    // Vd, Od (S * B <= ns).
-    return (size_t)4 * x.ns + (size_t)x.T2 + v2x_split_words(x, nr);
+    return (w + 3u) & ~(size_t)3u;
 }
 static size_t v2x_slot_words(const V2xGeo &x) { return (size_t)x.ns + (size_t)x.T2 + (size_t)x.S * kMtN; }
 

@@ -522,7 +522,11 @@ __global__ __launch_bounds__(64) void k_g_emit(Geometry g, GPlan pl, const RankD
                         if constexpr (MAPPED) {
                             int32_t f;
                             int64_t of;
+#ifdef PSS_DIAG_MAP_NONE   // (timing-only build: the stores of the mapped form without the map)
+                            of = ids.from_slot(v[j]); f = (int32_t)of; of >>= 3;
+#else
                             map_one_bucketed(ma.prefix, ma.F, ma.BT, ma.kb, ma.nb, ids.from_slot(v[j]), f, of);
+#endif
                             __builtin_amdgcn_raw_buffer_store_b32((uint32_t)f, orsrc, (int)voff, (int)(4u * (uint32_t)j * G64), 0);
                             __builtin_amdgcn_raw_buffer_store_b32((uint32_t)of, frsrc, (int)voff, (int)(4u * (uint32_t)j * G64), 0);
                         } else {

@@ -136,16 +136,25 @@ class IndexEngine:
                   _stream_ptr(stream, d))
         return fpos, off
 
-    def generate_mapped(self, rank_lo, rank_hi, pos_lo=0, count=None, stream=None):
+    def generate_mapped(self, rank_lo, rank_hi, pos_lo=0, count=None, stream=None, out=None):
         """(file_pos, offset) int32 tensors [ranks, count] of positions [pos_lo, pos_lo+count):
-        the fused hand-off (pss_generate_mapped) -- 8 bytes per id, no int64 id pass."""
+        the fused hand-off (pss_generate_mapped) -- 8 bytes per id, no int64 id pass.
+        out: an optional (file_pos, offset) pair of contiguous int32 tensors to write into."""
         d = self._dev()
         if count is None:
             count = self.num_samples - pos_lo
         count = max(0, int(count))
         nr = rank_hi - rank_lo
-        fpos = torch.empty((nr, count), dtype=torch.int32, device=d)
-        off = torch.empty((nr, count), dtype=torch.int32, device=d)
+        if out is None:
+            fpos = torch.empty((nr, count), dtype=torch.int32, device=d)
+            off = torch.empty((nr, count), dtype=torch.int32, device=d)
+        else:
+            fpos, off = out
+            for t in (fpos, off):
+                if not (t.is_contiguous() and t.dtype == torch.int32 and t.numel() >= nr * count
+                        and t.device == d):
+                    raise ValueError("generate_mapped: out tensors must be contiguous int32 "
+                                     "[ranks, count] on the engine's device")
         _lib.call("pss_generate_mapped", self._h, int(rank_lo), int(rank_hi), int(pos_lo), count,
                   ctypes.c_void_p(fpos.data_ptr()), ctypes.c_void_p(off.data_ptr()),
                   _stream_ptr(stream, d))
