@@ -312,16 +312,30 @@ constexpr uint32_t kSegBuckets = 256, kSegBackWin = 40;
 constexpr uint32_t kSegLdsWords = 3 * kSegBuckets;
 constexpr uint32_t kSegMulti = 0xFFFFu;    // bucket with >= 2 boundaries: global path
 
+// id -> (file position, int32 offset): when every file holds uL samples (MapArgs::uni) and
+// id < T, the file is id / uL -- one multiply-high by the host's magic, no table read -- else the
+// global bucketed map; the same values pss_map gives either way
+__device__ __forceinline__ void map_id_fast(const MapArgs &ma, int64_t id, int32_t &f, int32_t &off) {
+    if (ma.uni && (uint64_t)id < (uint64_t)ma.T) {
+        const uint32_t q = udiv_apply((uint32_t)id, ma.um, ma.ul);
+        f = (int32_t)q;
+        off = (int32_t)((uint32_t)id - q * ma.uL);
+    } else {
+        int64_t o;
+        map_one_bucketed_t(ma.prefix, ma.F, ma.T, ma.BT, ma.kb, ma.nb, id, f, o);
+        off = (int32_t)o;
+    }
+}
+
 // exact orders (pss_v1exact.hip, pss_v2exact.hip): the id into out[e], or -- ma.fpos set, the
-// fused hand-off of pss_generate_mapped -- its (file position, offset) pair through the global
-// bucketed map, the same values pss_map gives
+// fused hand-off of pss_generate_mapped -- its (file position, offset) pair, the same values
+// pss_map gives
 __device__ __forceinline__ void put_id_or_pair(int64_t *out, const MapArgs &ma, int64_t e, int64_t id) {
     if (ma.fpos) {
-        int32_t f;
-        int64_t o;
-        map_one_bucketed(ma.prefix, ma.F, ma.BT, ma.kb, ma.nb, id, f, o);
+        int32_t f, o;
+        map_id_fast(ma, id, f, o);
         ma.fpos[e] = f;
-        ma.off[e] = (int32_t)o;
+        ma.off[e] = o;
     } else {
         out[e] = id;
     }
@@ -330,9 +344,8 @@ __device__ __forceinline__ void put_id_or_pair(int64_t *out, const MapArgs &ma, 
 // the global map for the rare ids the LDS buckets miss
 __device__ __forceinline__ void seg_global_map(const MapArgs &ma, int64_t T, int64_t id,
                                                int32_t &f, int32_t &off) {
-    int64_t o;
-    map_one_bucketed_t(ma.prefix, ma.F, T, ma.BT, ma.kb, ma.nb, id, f, o);
-    off = (int32_t)o;
+    (void)T;   // (ma.T, the same total)
+    map_id_fast(ma, id, f, off);
 }
 
 struct SegMap {
@@ -433,6 +446,31 @@ constexpr uint32_t kPairEsc = 0x80000000u;
 constexpr uint32_t kPairBack = 8;       // windows before the tile's first with constants
 constexpr uint32_t kPairWords = 5;      // per window: Q0, Q1, Q2, s1, s2 (Q0 = kNone: no pairs)
 
+// The map of one contiguous id interval [a, a + len) (a window's ids) as at most three segments:
+// y < s1 -> (f0, d0 + y), s1 <= y < s2 -> (f1, y - s1), y >= s2 -> (f2, y - s2) -- s = kNone
+// where a segment is absent.  False when the interval reaches past the scanned total T (reflected
+// ids) or crosses three or more file boundaries.  Empty files are skipped as the map skips them.
+__device__ __forceinline__ bool window_map_segments(const MapArgs &ma, int64_t a, int64_t len, int32_t f[3],
+                                                    uint32_t &d0, uint32_t s[2]) {
+    s[0] = kNone; s[1] = kNone;
+    if (a < 0 || a + len > ma.T) return false;
+    int64_t o;
+    map_one_bucketed_t(ma.prefix, ma.F, ma.T, ma.BT, ma.kb, ma.nb, a, f[0], o);
+    if (f[0] < 0) return false;
+    d0 = (uint32_t)o;
+    f[1] = f[2] = f[0];
+    for (int k = 0; k < 3; k++) {
+        const int64_t end = ma.prefix[f[k] + 1] - a;   // the next file boundary (prefix[F] = T)
+        if (end >= len) return true;
+        if (k == 2) return false;                      // a third boundary
+        int64_t ob;
+        map_one_bucketed_t(ma.prefix, ma.F, ma.T, ma.BT, ma.kb, ma.nb, a + end, f[k + 1], ob);
+        if (k == 0) f[2] = f[1];
+        s[k] = (uint32_t)end;
+    }
+    return true;
+}
+
 // constants of pool2 window w (virtual values [w B, w B + len)) of rank rd into c[kPairWords]
 __device__ __forceinline__ void pair_window_consts(const MapArgs &ma, const RankDesc &rd, const Geometry &g,
                                                    uint32_t B, uint32_t twoB, uint32_t w, uint32_t *c) {
@@ -443,22 +481,15 @@ __device__ __forceinline__ void pair_window_consts(const MapArgs &ma, const Rank
     if (v0 < (int64_t)twoB && v0 + len > (int64_t)twoB) return;   // (2B and ns are window ends)
     int64_t a = (v0 < (int64_t)twoB ? rd.old_start : rd.new_start) + v0;
     if (a >= g.N) a -= g.N;
-    if (a + len > g.N || a + len > ma.T) return;                 // wraps, or reflected ids
-    int32_t f;
-    int64_t o;
-    map_one_bucketed_t(ma.prefix, ma.F, ma.T, ma.BT, ma.kb, ma.nb, a, f, o);
-    if (f < 0) return;
-    uint32_t Q[3] = {((uint32_t)f << ma.pob) + (uint32_t)o, 0u, 0u}, s[2] = {kNone, kNone};
-    for (int k = 0; k < 3; k++) {
-        const int64_t end = ma.prefix[f + 1] - a;   // the next file boundary (prefix[F] = T)
-        if (end >= len) break;
-        if (k == 2) return;                         // a third boundary: no pairs
-        int64_t ob;
-        map_one_bucketed_t(ma.prefix, ma.F, ma.T, ma.BT, ma.kb, ma.nb, a + end, f, ob);   // skips empty files
-        s[k] = (uint32_t)end;
-        Q[k + 1] = ((uint32_t)f << ma.pob) - (uint32_t)end;
-    }
-    c[0] = Q[0]; c[1] = Q[1]; c[2] = Q[2]; c[3] = s[0]; c[4] = s[1];
+    if (a + len > g.N) return;                                    // wraps inside the window
+    int32_t f[3];
+    uint32_t d0, s[2];
+    if (!window_map_segments(ma, a, len, f, d0, s)) return;
+    c[0] = ((uint32_t)f[0] << ma.pob) + d0;
+    c[1] = ((uint32_t)f[1] << ma.pob) - s[0];
+    c[2] = ((uint32_t)f[2] << ma.pob) - s[1];
+    c[3] = s[0];
+    c[4] = s[1];
 }
 
 // the pair of value y of a window with constants (Q0, Q1, Q2, s1, s2)

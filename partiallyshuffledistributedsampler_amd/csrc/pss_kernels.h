@@ -58,6 +58,8 @@ V2Plan v2_plan(const Geometry &g, int32_t nr);
 constexpr int32_t kArgRanks = 128;
 constexpr int32_t kArgRanksMax = 1024;
 hipError_t launch_put_ranks(const RankDesc *host, int32_t R, RankDesc *dst, hipStream_t s);
+// bytes (a multiple of 4) from pinned host memory (hipHostMalloc) to device memory by a kernel
+hipError_t launch_upload(const void *host_pinned, void *dst, size_t bytes, hipStream_t s);
 // up to kArgRanks rank descriptors by value (kernel arguments): [0, nr) = ranks rank_lo..
 struct RankArgs { RankDesc r[kArgRanks]; };
 

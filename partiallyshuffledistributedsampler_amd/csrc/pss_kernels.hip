@@ -222,8 +222,14 @@ __global__ void k_debug_wave_scan(const uint64_t *in, uint64_t *out, int64_t n) 
 // compute + coalesced-store stream (the sort-based kernel it replaces spent its time in Philox
 // sort keys and LDS bucket passes).
 // ------------------------------------------------------------------------------------------
+// mc != nullptr (the mapped one-shot kernel): also each (rank, window)'s map segments
+// (window_map_segments) as kV1MapWords words -- f0, f1, f2, d0, -s1, -s2, s1, s2; f0 = -1: the
+// window has none (it wraps at N, reaches past the scanned total or crosses three boundaries)
+constexpr int kV1MapWords = 8;
 __global__ __launch_bounds__(256) void k_v1_keys(Geometry g, int32_t rank_lo, int64_t w_lo,
-                                                 int64_t nw, uint32_t *__restrict__ kt) {
+                                                 int64_t nw, uint32_t *__restrict__ kt,
+                                                 uint32_t *__restrict__ mc, MapArgs ma,
+                                                 const RankDesc *__restrict__ ranks, RankArgs ra, int use_ra) {
     const int32_t rl = (int32_t)blockIdx.y;
     const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (j >= nw) return;
@@ -232,6 +238,21 @@ __global__ __launch_bounds__(256) void k_v1_keys(Geometry g, int32_t rank_lo, in
     uint32_t *b = kt + ((int64_t)rl * nw + j) * kRoundKeyWords;
 #pragma unroll
     for (int i = 0; i < kRoundKeyWords; i++) b[i] = k[i];
+    if (!mc) return;
+    uint32_t c[kV1MapWords] = {kNone, 0u, 0u, 0u, 0u, 0u, kNone, kNone};
+    const int64_t wB = (w_lo + j) * g.B;
+    const int64_t len = g.ns - wB < g.B ? g.ns - wB : g.B;
+    int64_t a = (use_ra ? ra.r[rl].new_start : ranks[rank_lo + rl].new_start) + wB;
+    if (a >= g.N) a -= g.N;
+    int32_t f[3];
+    uint32_t d0, sg[2];
+    if (a + len <= g.N && window_map_segments(ma, a, len, f, d0, sg)) {
+        c[0] = (uint32_t)f[0]; c[1] = (uint32_t)f[1]; c[2] = (uint32_t)f[2];
+        c[3] = d0; c[4] = 0u - sg[0]; c[5] = 0u - sg[1]; c[6] = sg[0]; c[7] = sg[1];
+    }
+    uint32_t *m = mc + ((int64_t)rl * nw + j) * kV1MapWords;
+#pragma unroll
+    for (int i = 0; i < kV1MapWords; i++) m[i] = c[i];
 }
 
 struct V1Plan {
@@ -265,11 +286,10 @@ __global__ __launch_bounds__(64) void k_v1_feistel(Geometry g, V1Plan vp, const 
     int32_t *ooff = ma.off + (int64_t)rl * count - pos_lo;
     auto put = [&](int64_t p, int64_t id) __attribute__((always_inline)) {
         if constexpr (MAPPED) {
-            int32_t f;
-            int64_t of;
-            map_one_bucketed(ma.prefix, ma.F, ma.BT, ma.kb, ma.nb, id, f, of);
+            int32_t f, of;
+            map_id_fast(ma, id, f, of);
             ofp[p] = f;
-            ooff[p] = (int32_t)of;
+            ooff[p] = of;
         } else {
             o[p] = id;
         }
@@ -363,12 +383,11 @@ __global__ __launch_bounds__(64) void k_v1_feistel(Geometry g, V1Plan vp, const 
                         const int64_t p = p0 + 128 * h + l2;
                         const int64_t ia = wrap(y[2 * h]), ib = wrap(y[2 * h + 1]);
                         if constexpr (MAPPED) {
-                            int32_t fa, fb;
-                            int64_t oa, ob;
-                            map_one_bucketed(ma.prefix, ma.F, ma.BT, ma.kb, ma.nb, ia, fa, oa);
-                            map_one_bucketed(ma.prefix, ma.F, ma.BT, ma.kb, ma.nb, ib, fb, ob);
+                            int32_t fa, fb, oa, ob;
+                            map_id_fast(ma, ia, fa, oa);
+                            map_id_fast(ma, ib, fb, ob);
                             *(int2 *)(ofp + p) = make_int2(fa, fb);
-                            *(int2 *)(ooff + p) = make_int2((int32_t)oa, (int32_t)ob);
+                            *(int2 *)(ooff + p) = make_int2(oa, ob);
                         } else {
                             longlong2 v;
                             v.x = ia;
@@ -418,23 +437,46 @@ struct V1OsPlan {
     uint32_t B, hB, fast_ok, b_pow2;
 };
 
-template <bool PACKED, bool NARROW>
+// MAPPED (pss_generate_mapped): (int32 file position, int32 offset) into ma.fpos / ma.off --
+// on fast workgroups from the window's map segments (mc, k_v1_keys: two compares and selects
+// per position, 16-byte stores of 4 file positions and 4 offsets), elsewhere through the global
+// bucketed map
+template <bool PACKED, bool NARROW, bool MAPPED = false>
 __global__ __launch_bounds__(256) void k_v1_os(Geometry g, V1OsPlan vp, const RankDesc *__restrict__ ranks,
                                                int32_t rank_lo, const uint32_t *__restrict__ kt,
                                                int64_t pos_lo, int64_t count, int64_t *__restrict__ out,
-                                               RankArgs ra, int use_ra) {
+                                               RankArgs ra, int use_ra, MapArgs ma,
+                                               const uint32_t *__restrict__ mc) {
     const uint32_t rl = blockIdx.x / vp.bpr;
     const int64_t p0 = (vp.blk_lo + (int64_t)(blockIdx.x - rl * vp.bpr)) * kV1OsSpan;
     const int64_t pos_hi = pos_lo + count < g.ns ? pos_lo + count : g.ns;
     // (use_ra: the rank's descriptor from the kernel arguments, no upload kernel ahead)
     const int64_t start = use_ra ? ra.r[rl].new_start : ranks[rank_lo + (int32_t)rl].new_start;
     int64_t *o = out + (int64_t)rl * count - pos_lo;
+    int32_t *ofp = ma.fpos + (int64_t)rl * count - pos_lo;
+    int32_t *ooff = ma.off + (int64_t)rl * count - pos_lo;
     const uint32_t *ktr = kt + (int64_t)rl * vp.nw * kRoundKeyWords;
     const int64_t B = vp.B;
     const int64_t w = vp.b_pow2 ? (p0 >> vp.b_log) : p0 / B;
     const int64_t wB = w * B;
+    uint32_t mcw[kV1MapWords];   // MAPPED: the window's map segments (wave-uniform)
+    bool aligned;
+    if constexpr (MAPPED) {
+        static_assert(!MAPPED || kV1OsPer % 4 == 0, "mapped stores: 4 positions per 16-byte store");
+        const bool inw = vp.fast_ok && w >= vp.w_lo && w < vp.w_lo + vp.nw;
+        const uint32_t *m = mc + ((int64_t)rl * vp.nw + (inw ? w - vp.w_lo : 0)) * kV1MapWords;
+#pragma unroll
+        for (int i = 0; i < kV1MapWords; i++) mcw[i] = kNone;
+        if (inw) {
+#pragma unroll
+            for (int i = 0; i < kV1MapWords; i++) mcw[i] = __builtin_amdgcn_readfirstlane(m[i]);
+        }
+        aligned = mcw[0] != kNone && ((((uintptr_t)(ofp + p0)) | ((uintptr_t)(ooff + p0))) & 15u) == 0;
+    } else {
+        aligned = (((uintptr_t)(o + p0)) & 15u) == 0;
+    }
     const bool fast = vp.fast_ok && wB + B <= g.ns && p0 + kV1OsSpan <= wB + B && p0 >= pos_lo &&
-                      p0 + kV1OsSpan <= pos_hi && (((uintptr_t)(o + p0)) & 15u) == 0;
+                      p0 + kV1OsSpan <= pos_hi && aligned;
     const uint32_t l4 = (uint32_t)kV1OsPer * threadIdx.x;
     if (fast) {
         uint32_t kp[kFeistelRounds];
@@ -469,6 +511,23 @@ __global__ __launch_bounds__(256) void k_v1_os(Geometry g, V1OsPlan vp, const Ra
         } else {
 #pragma unroll
             for (int j = 0; j < kV1OsPer; j++) y[j] = feistel_once(x[j], vp.hB, kp);
+        }
+        if constexpr (MAPPED) {
+            // y -> (f_k, y + d_k) on segment k of the window's ids (window_map_segments)
+            uint32_t fv[kV1OsPer], ov[kV1OsPer];
+#pragma unroll
+            for (int j = 0; j < kV1OsPer; j++) {
+                const bool a1 = y[j] >= mcw[6], a2 = y[j] >= mcw[7];
+                fv[j] = a2 ? mcw[2] : (a1 ? mcw[1] : mcw[0]);
+                ov[j] = y[j] + (a2 ? mcw[5] : (a1 ? mcw[4] : mcw[3]));
+            }
+            const int64_t e = p0 + it * kV1OsPos + l4;
+#pragma unroll
+            for (int j = 0; j < kV1OsPer; j += 4) {
+                *(uint4 *)(ofp + e + j) = make_uint4(fv[j], fv[j + 1], fv[j + 2], fv[j + 3]);
+                *(uint4 *)(ooff + e + j) = make_uint4(ov[j], ov[j + 1], ov[j + 2], ov[j + 3]);
+            }
+            continue;
         }
         int64_t id[kV1OsPer];
 #pragma unroll
@@ -508,7 +567,14 @@ __global__ __launch_bounds__(256) void k_v1_os(Geometry g, V1OsPlan vp, const Ra
 #endif
             y = wp * B + feistel((uint32_t)(p - wp * B), (uint32_t)len, feistel_half_bits((uint32_t)len), kk);
         }
-        o[p] = wrap_id(start + y, g.N);
+        if constexpr (MAPPED) {
+            int32_t f, of;
+            map_id_fast(ma, wrap_id(start + y, g.N), f, of);
+            ofp[p] = f;
+            ooff[p] = of;
+        } else {
+            o[p] = wrap_id(start + y, g.N);
+        }
     }
 }
 
@@ -519,6 +585,36 @@ static inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
 __global__ __launch_bounds__(kArgRanks) void k_put_ranks(RankArgs a, int32_t n, RankDesc *dst) {
     if ((int32_t)threadIdx.x < n) dst[threadIdx.x] = a.r[threadIdx.x];
+}
+
+// Host -> device upload by a kernel reading pinned host memory (mapped into the device's address
+// space), in place of hipMemcpyAsync: on the epoch path the runtime's async copy of the 40 KB file
+// order once blocked the calling thread for 7-8 ms (the 8th upload of a process, every run; the
+// other uploads 2 us, HIP API trace in profiles/r06/).  16-byte loads when both ends allow.
+__global__ __launch_bounds__(256) void k_upload(const uint32_t *__restrict__ src, uint32_t *__restrict__ dst,
+                                                int64_t nwords) {
+    const int64_t stride = (int64_t)gridDim.x * 256;
+    int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if ((((uintptr_t)src | (uintptr_t)dst) & 15u) == 0) {
+        const int64_t n4 = nwords / 4;
+        for (int64_t q = i; q < n4; q += stride) ((uint4 *)dst)[q] = ((const uint4 *)src)[q];
+        for (int64_t k = n4 * 4 + i; k < nwords; k += stride) dst[k] = src[k];
+    } else {
+        for (int64_t k = i; k < nwords; k += stride) dst[k] = src[k];
+    }
+}
+
+hipError_t launch_upload(const void *host_pinned, void *dst, size_t bytes, hipStream_t s) {
+    if (bytes == 0) return hipSuccess;
+    if (bytes % 4) return hipErrorInvalidValue;
+    void *src = nullptr;
+    hipError_t e = hipHostGetDevicePointer(&src, const_cast<void *>(host_pinned), 0);
+    if (e != hipSuccess) return e;
+    const int64_t nwords = (int64_t)(bytes / 4);
+    const int64_t blocks = (nwords / 4 + 255) / 256;
+    hipLaunchKernelGGL(k_upload, dim3((uint32_t)(blocks < 1 ? 1 : (blocks > 1024 ? 1024 : blocks))), dim3(256), 0, s,
+                       (const uint32_t *)src, (uint32_t *)dst, nwords);
+    return hipGetLastError();
 }
 
 hipError_t launch_put_ranks(const RankDesc *host, int32_t R, RankDesc *dst, hipStream_t s) {
@@ -639,7 +735,8 @@ static bool v1_window_range(const Geometry &g, int64_t pos_lo, int64_t count, in
 size_t v1_workspace_bytes(const Geometry &g, int32_t nr, int64_t pos_lo, int64_t count) {
     int64_t w_lo, nw;
     if (!g.shuffle || nr <= 0 || !v1_window_range(g, pos_lo, count, w_lo, nw)) return 0;
-    return (size_t)nr * (size_t)nw * kRoundKeyWords * sizeof(uint32_t);
+    // the round keys, then (a mapped launch) the windows' map segments
+    return (size_t)nr * (size_t)nw * (kRoundKeyWords + kV1MapWords) * sizeof(uint32_t);
 }
 
 hipError_t launch_v1(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, int32_t nr,
@@ -650,14 +747,19 @@ hipError_t launch_v1(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, 
     if (rank_args && nr > kArgRanks) return hipErrorInvalidValue;
     const int64_t pos_hi = pos_lo + count < g.ns ? pos_lo + count : g.ns;
     mk(K_V1, s);
+    const MapArgs ma = mapped ? *mapped : MapArgs{};
+    RankArgs ra;
+    if (rank_args) ra = *rank_args;
+    const int use_ra = rank_args ? 1 : 0;
+    uint32_t *mc = mapped && key_ws ? key_ws + (size_t)nr * (size_t)nw * kRoundKeyWords : nullptr;
 #ifdef PSS_V1OS_INKEYS
     if (g.shuffle && (mapped || (uint64_t)((pos_hi - 1) / kV1OsSpan - pos_lo / kV1OsSpan + 1) * (uint64_t)nr >= ((uint64_t)1 << 31)))
 #else
     if (g.shuffle)
 #endif
         hipLaunchKernelGGL(k_v1_keys, dim3((uint32_t)cdiv(nw, 256), (uint32_t)nr), dim3(256), 0, s,
-                           g, rank_lo, w_lo, nw, key_ws);
-    if (!mapped) {
+                           g, rank_lo, w_lo, nw, key_ws, mc, ma, ranks, ra, use_ra);
+    {
         V1OsPlan op{};
         op.blk_lo = pos_lo / kV1OsSpan;
         const int64_t bpr = (pos_hi - 1) / kV1OsSpan - op.blk_lo + 1;
@@ -673,11 +775,12 @@ hipError_t launch_v1(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, 
         const uint64_t blocks = (uint64_t)bpr * (uint64_t)nr;
         if (blocks < ((uint64_t)1 << 31)) {
             const dim3 grid((uint32_t)blocks);
-            RankArgs ra;
-            if (rank_args) ra = *rank_args;
-            const int use_ra = rank_args ? 1 : 0;
-#define PSS_V1OS(PK, NA) hipLaunchKernelGGL((k_v1_os<PK, NA>), grid, dim3(256), 0, s, g, op, ranks, rank_lo, \
-                                            (const uint32_t *)key_ws, pos_lo, count, out, ra, use_ra)
+#define PSS_V1OS(PK, NA) do { if (mapped) hipLaunchKernelGGL((k_v1_os<PK, NA, true>), grid, dim3(256), 0, s, g, op, ranks, \
+                                                             rank_lo, (const uint32_t *)key_ws, pos_lo, count, out, ra, \
+                                                             use_ra, ma, (const uint32_t *)mc); \
+                              else hipLaunchKernelGGL((k_v1_os<PK, NA>), grid, dim3(256), 0, s, g, op, ranks, rank_lo, \
+                                                      (const uint32_t *)key_ws, pos_lo, count, out, ra, use_ra, ma, \
+                                                      (const uint32_t *)nullptr); } while (0)
             const bool pk = feistel_packed_ok(op.hB);
             if (pk && narrow) PSS_V1OS(true, true);
             else if (pk) PSS_V1OS(true, false);
@@ -720,7 +823,6 @@ hipError_t launch_v1(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, 
     if (per < 1) per = 1;
     vp.per_wave = per;
     const int64_t waves = (int64_t)nr * cdiv(vp.nsb, per);
-    const MapArgs ma = mapped ? *mapped : MapArgs{};
     const size_t v1_lds = (size_t)(160 * 1024 / wpc_run - 64);   // caps the resident waves per CU
 #define PSS_V1(PK, MP) hipLaunchKernelGGL((k_v1_feistel<PK, MP>), dim3((uint32_t)waves), dim3(64), v1_lds, s, g, vp, \
                                           ranks, rank_lo, (const uint32_t *)key_ws, pos_lo, count, out, ma)

@@ -215,19 +215,33 @@ struct pss_sampler {
     // device state
     bool dev_init = false;
     bool dirty = true;            // rank descriptors of the epoch not on the device yet
-    bool order_dirty = true;      // file order not uploaded (only map / partition need it)
-    bool prefix_dirty = true;     // prefix scan owed (run lazily by map / partition)
-    DevBuf<int64_t> d_lens, d_prefix, d_ids;   // d_ids: scratch ids of pss_generate_mapped
-    DevBuf<int32_t> d_bucket;     // bucket index of the prefix (pss_map.h), kb / nb below
+    bool prefix_dirty = true;     // CPU mode: the host prefix is owed (cpu_prefix)
+    DevBuf<int64_t> d_lens, d_ids;   // d_ids: scratch ids of pss_generate_mapped
+    // The epoch's device tables -- the file order, its exclusive prefix (+ the scan's scratch) and
+    // the prefix's bucket index (pss_map.h; kb / nb below) -- in two sets, built on first use after
+    // an init_iter on the handle's table stream: epoch e's upload, scan and bucket index run beside
+    // epoch e - 1's kernels on the caller's stream, which only waits for the set to be ready (they
+    // had run in line, ~35 us per epoch before a mapped replay at C2).  A set is rebuilt after its
+    // last reader (`freed`); its pinned staging is reused after the upload that read it (`staged`).
+    struct TabSet {
+        DevBuf<int32_t> order, bucket;
+        DevBuf<int64_t> prefix;
+        int32_t *stage = nullptr;
+        hipEvent_t ready = nullptr, freed = nullptr, staged = nullptr;
+        bool built = false, read = false;
+    };
+    TabSet tab[2];
+    int tab_cur = 0;
+    bool tab_dirty = true;        // this epoch's tables not built yet
+    hipStream_t tstream = nullptr;
     int32_t kb = 0;
     int64_t nb = 0, max_len = 0;
     pss::MapArgs map_sc{};        // host-known map shortcuts (map_shortcuts): T, pack, uni
     hipEvent_t ids_free = nullptr;   // last reader of d_ids
-    DevBuf<int32_t> d_order, d_err;
+    DevBuf<int32_t> d_err;
     DevBuf<pss::RankDesc> d_ranks;
     DevBuf<uint32_t> d_val, d_buf, d_sort;
-    int32_t *h_stage_order = nullptr;      // pinned staging of the epoch upload
-    pss::RankDesc *h_stage_ranks = nullptr;
+    pss::RankDesc *h_stage_ranks = nullptr;   // pinned staging of the rank table (R > kArgRanksMax)
     hipEvent_t upload_done = nullptr;
     bool upload_pending = false;
     // optional per-kernel timing (pss_profile): events recorded around every launch
@@ -340,14 +354,20 @@ int ensure_device(pss_sampler *h) {
     if (h->dev_init) return PSS_OK;
     PSS_HIP(pss::init_kernel_attributes());
     PSS_HIP(h->d_lens.ensure((size_t)h->F));
-    PSS_HIP(h->d_order.ensure((size_t)h->F));
-    PSS_HIP(h->d_prefix.ensure((size_t)h->F + 1 + pss::scan_scratch_words(h->F)));
     PSS_HIP(h->d_ranks.ensure((size_t)h->R));
     PSS_HIP(h->d_err.ensure(1));
-    PSS_HIP(h->d_bucket.ensure((size_t)h->nb));
+    for (auto &t : h->tab) {
+        PSS_HIP(t.order.ensure((size_t)h->F));
+        PSS_HIP(t.prefix.ensure((size_t)h->F + 1 + pss::scan_scratch_words(h->F)));
+        PSS_HIP(t.bucket.ensure((size_t)h->nb));
+        PSS_HIP(hipHostMalloc((void **)&t.stage, sizeof(int32_t) * (h->F ? h->F : 1)));
+        PSS_HIP(hipEventCreateWithFlags(&t.ready, hipEventDisableTiming));
+        PSS_HIP(hipEventCreateWithFlags(&t.freed, hipEventDisableTiming));
+        PSS_HIP(hipEventCreateWithFlags(&t.staged, hipEventDisableTiming));
+    }
+    PSS_HIP(hipStreamCreateWithFlags(&h->tstream, hipStreamNonBlocking));
     PSS_HIP(hipMemset(h->d_err.p, 0, sizeof(int32_t)));
     if (h->F) PSS_HIP(hipMemcpy(h->d_lens.p, h->files_len.data(), sizeof(int64_t) * h->F, hipMemcpyHostToDevice));
-    PSS_HIP(hipHostMalloc((void **)&h->h_stage_order, sizeof(int32_t) * (h->F ? h->F : 1)));
     PSS_HIP(hipHostMalloc((void **)&h->h_stage_ranks, sizeof(pss::RankDesc) * h->R));
     PSS_HIP(hipEventCreateWithFlags(&h->upload_done, hipEventDisableTiming));
     h->dev_init = true;
@@ -366,7 +386,7 @@ int prepare(pss_sampler *h, hipStream_t s) {
     } else {
         if (h->upload_pending) PSS_HIP(hipEventSynchronize(h->upload_done));
         std::memcpy(h->h_stage_ranks, h->ranks.data(), sizeof(pss::RankDesc) * h->R);
-        PSS_HIP(hipMemcpyAsync(h->d_ranks.p, h->h_stage_ranks, sizeof(pss::RankDesc) * h->R, hipMemcpyHostToDevice, s));
+        PSS_HIP(pss::launch_upload(h->h_stage_ranks, h->d_ranks.p, sizeof(pss::RankDesc) * h->R, s));
         PSS_HIP(hipEventRecord(h->upload_done, s));
         h->upload_pending = true;
     }
@@ -374,32 +394,41 @@ int prepare(pss_sampler *h, hipStream_t s) {
     return PSS_OK;
 }
 
-// the shuffled file order, uploaded on first use after an init_iter
-int prepare_order(pss_sampler *h, hipStream_t s) {
-    int rc = prepare(h, s);
-    if (rc || !h->order_dirty) return rc;
-    if (h->upload_pending) PSS_HIP(hipEventSynchronize(h->upload_done));
-    std::memcpy(h->h_stage_order, h->order.data(), sizeof(int32_t) * h->F);
-    if (h->F) PSS_HIP(hipMemcpyAsync(h->d_order.p, h->h_stage_order, sizeof(int32_t) * h->F, hipMemcpyHostToDevice, s));
-    PSS_HIP(hipEventRecord(h->upload_done, s));
-    h->upload_pending = true;
-    h->order_dirty = false;
-    h->prefix_dirty = true;
+// The epoch's tables (TabSet: the shuffled file order, its prefix and bucket index), needed by
+// the map, the fused hand-off, the gather and the partition only: built on first use after an
+// init_iter into the other set, on the table stream, after that set's last reader; then `s`
+// waits for them.  A call that reads them records tables_read on its stream afterwards.
+int prepare_tables(pss_sampler *h, hipStream_t s) {
+    if (!h->iterated) return fail(PSS_ESTATE, "pss_init_iter must be called before device work");
+    int rc = ensure_device(h);
+    if (rc) return rc;
+    if (h->tab_dirty) {
+        const int k = h->tab_cur ^ 1;
+        pss_sampler::TabSet &t = h->tab[k];
+        if (t.built) PSS_HIP(hipEventSynchronize(t.staged));   // the upload that read `stage`
+        std::memcpy(t.stage, h->order.data(), sizeof(int32_t) * h->F);
+        if (t.read) PSS_HIP(hipStreamWaitEvent(h->tstream, t.freed, 0));
+        if (h->F) PSS_HIP(pss::launch_upload(t.stage, t.order.p, sizeof(int32_t) * h->F, h->tstream));
+        PSS_HIP(hipEventRecord(t.staged, h->tstream));
+        const pss::Marker mk = marker_of(h);
+        mk(pss::K_SCAN, h->tstream);
+        PSS_HIP(pss::launch_scan_prefix(h->d_lens.p, t.order.p, h->F, t.prefix.p,
+                                        (uint64_t *)(t.prefix.p + h->F + 1), h->tstream));
+        PSS_HIP(pss::launch_bucket_index(t.prefix.p, h->F, h->kb, h->nb, t.bucket.p, h->tstream));
+        mk(-1, h->tstream);
+        PSS_HIP(hipEventRecord(t.ready, h->tstream));
+        t.built = true;
+        h->tab_cur = k;
+        h->tab_dirty = false;
+    }
+    PSS_HIP(hipStreamWaitEvent(s, h->tab[h->tab_cur].ready, 0));
     return PSS_OK;
 }
 
-// the exclusive prefix over the epoch's file order is needed only by the id -> (file, offset)
-// map and the partition, so it is scanned on first use after an init_iter
-int prepare_prefix(pss_sampler *h, hipStream_t s) {
-    int rc = prepare_order(h, s);
-    if (rc || !h->prefix_dirty) return rc;
-    const pss::Marker mk = marker_of(h);
-    mk(pss::K_SCAN, s);
-    PSS_HIP(pss::launch_scan_prefix(h->d_lens.p, h->d_order.p, h->F, h->d_prefix.p,
-                                    (uint64_t *)(h->d_prefix.p + h->F + 1), s));
-    PSS_HIP(pss::launch_bucket_index(h->d_prefix.p, h->F, h->kb, h->nb, h->d_bucket.p, s));
-    mk(-1, s);
-    h->prefix_dirty = false;
+int tables_read(pss_sampler *h, hipStream_t s) {
+    pss_sampler::TabSet &t = h->tab[h->tab_cur];
+    PSS_HIP(hipEventRecord(t.freed, s));
+    t.read = true;
     return PSS_OK;
 }
 
@@ -480,9 +509,9 @@ void map_shortcuts(pss_sampler *h, int64_t scanned) {
 // the map arguments of the current epoch's device tables and the caller's outputs
 pss::MapArgs map_args(const pss_sampler *h, int32_t *fpos, int32_t *off) {
     pss::MapArgs m = h->map_sc;
-    m.prefix = h->d_prefix.p;
+    m.prefix = h->tab[h->tab_cur].prefix.p;
     m.F = h->F;
-    m.BT = h->d_bucket.p;
+    m.BT = h->tab[h->tab_cur].bucket.p;
     m.kb = h->kb;
     m.nb = h->nb;
     m.fpos = fpos;
@@ -553,11 +582,18 @@ int pss_destroy(pss_sampler *h) {
         DeviceGuard dg(h->device);
         if (h->upload_pending) (void)hipEventSynchronize(h->upload_done);
         if (h->side) (void)hipStreamSynchronize(h->side);   // a lookahead still writing VAL
-        h->d_lens.release(); h->d_prefix.release(); h->d_order.release(); h->d_err.release();
+        if (h->tstream) (void)hipStreamSynchronize(h->tstream);
+        (void)hipDeviceSynchronize();   // readers of the tables on the callers' streams
+        h->d_lens.release(); h->d_err.release();
         h->d_ranks.release(); h->d_val.release(); h->d_buf.release(); h->d_sort.release();
-        h->d_bucket.release(); h->d_ids.release();
+        h->d_ids.release();
+        for (auto &t : h->tab) {
+            t.order.release(); t.prefix.release(); t.bucket.release();
+            if (t.stage) (void)hipHostFree(t.stage);
+            for (hipEvent_t e : {t.ready, t.freed, t.staged}) if (e) (void)hipEventDestroy(e);
+        }
+        if (h->tstream) (void)hipStreamDestroy(h->tstream);
         if (h->ids_free) (void)hipEventDestroy(h->ids_free);
-        if (h->h_stage_order) (void)hipHostFree(h->h_stage_order);
         if (h->h_stage_ranks) (void)hipHostFree(h->h_stage_ranks);
         if (h->upload_done) (void)hipEventDestroy(h->upload_done);
         for (hipEvent_t e : h->ev_pool) (void)hipEventDestroy(e);
@@ -616,7 +652,7 @@ int pss_init_iter(pss_sampler *h, int64_t epoch) {
     h->epoch = epoch;
     h->iterated = true;
     h->dirty = true;
-    h->order_dirty = true;
+    h->tab_dirty = true;
     h->prefix_dirty = true;
     return PSS_OK;
 }
@@ -647,7 +683,8 @@ int pss_prepare(pss_sampler *h, void *stream) {
     if (h->cpu) return cpu_prefix(h);
     DeviceGuard dg(h->device);
     SharedUse su(h, (hipStream_t)stream);
-    return prepare_prefix(h, (hipStream_t)stream);
+    const int rc = prepare(h, (hipStream_t)stream);
+    return rc ? rc : prepare_tables(h, (hipStream_t)stream);
 }
 
 namespace {
@@ -1053,12 +1090,17 @@ int pss_map(pss_sampler *h, const int64_t *ids_dev, int64_t n, int32_t *file_pos
     DeviceGuard dg(h->device);
     hipStream_t s = (hipStream_t)stream;
     SharedUse su(h, s);
-    int rc = prepare_prefix(h, s);
+    int rc = prepare_tables(h, s);
     if (rc) return rc;
-    PSS_HIP(pss::launch_map(h->d_prefix.p, h->F, h->d_bucket.p, h->kb, h->nb, ids_dev, n, file_pos_dev,
+    const pss_sampler::TabSet &t = h->tab[h->tab_cur];
+    PSS_HIP(pss::launch_map(t.prefix.p, h->F, t.bucket.p, h->kb, h->nb, ids_dev, n, file_pos_dev,
                             offset_dev, nullptr, s));
-    return PSS_OK;
+    return tables_read(h, s);
 }
+
+// pss_generate_mapped's device work after the epoch's tables are ready on s
+static int generate_mapped_dev(pss_sampler *h, int32_t rank_lo, int32_t rank_hi, int64_t pos_lo,
+                               int64_t count, int32_t *file_pos_dev, int32_t *offset_dev, hipStream_t s);
 
 int pss_generate_mapped(pss_sampler *h, int32_t rank_lo, int32_t rank_hi, int64_t pos_lo,
                         int64_t count, int32_t *file_pos_dev, int32_t *offset_dev, void *stream) {
@@ -1089,23 +1131,42 @@ int pss_generate_mapped(pss_sampler *h, int32_t rank_lo, int32_t rank_hi, int64_
     DeviceGuard dg(h->device);
     hipStream_t s = (hipStream_t)stream;
     SharedUse su(h, s);
-    int rc = prepare_prefix(h, s);
+    int rc = prepare_tables(h, s);
     if (rc) return rc;
+    rc = generate_mapped_dev(h, rank_lo, rank_hi, pos_lo, count, file_pos_dev, offset_dev, s);
+    return rc ? rc : tables_read(h, s);
+}
+
+static int generate_mapped_dev(pss_sampler *h, int32_t rank_lo, int32_t rank_hi, int64_t pos_lo,
+                               int64_t count, int32_t *file_pos_dev, int32_t *offset_dev, hipStream_t s) {
+    const int32_t nr = rank_hi - rank_lo;
+    const size_t n = (size_t)nr * (size_t)count;
+    void *stream = (void *)s;
+    int rc = PSS_OK;
     const pss::Geometry g = h->geometry();
     const pss::Marker mk = marker_of(h);
     auto words = [](size_t bytes) { return (bytes + sizeof(uint32_t) - 1) / sizeof(uint32_t); };
     const bool exact = h->order_mode == PSS_ORDER_EXACT && (h->version == 2 || g.shuffle);
     if (h->version == 1 && !exact) {
         // fused: the V1 kernel maps each id as it computes it (shuffle = false is the identity
-        // order of both modes)
+        // order of both modes); up to kArgRanks ranks' descriptors by value (no upload kernel)
         const size_t sb = pss::v1_workspace_bytes(g, nr, pos_lo, count);
         if (sb) PSS_HIP(h->d_sort.ensure(words(sb)));
         const pss::MapArgs ma = map_args(h, file_pos_dev, offset_dev);
-        PSS_HIP(pss::launch_v1(g, h->d_ranks.p, rank_lo, nr, pos_lo, count, nullptr, h->d_sort.p, s, mk, &ma));
+        pss::RankArgs ra;
+        const bool by_value = nr <= pss::kArgRanks;
+        if (by_value) {
+            for (int32_t i = 0; i < nr; i++) ra.r[i] = h->ranks[rank_lo + i];
+        } else if ((rc = prepare(h, s)) != PSS_OK) {
+            return rc;
+        }
+        PSS_HIP(pss::launch_v1(g, h->d_ranks.p, rank_lo, nr, pos_lo, count, nullptr, h->d_sort.p, s, mk, &ma,
+                               by_value ? &ra : nullptr));
         return PSS_OK;
     }
     if (exact) {
         // fused: the exact pipelines' output kernels map each id where they would write it
+        if ((rc = prepare(h, s)) != PSS_OK) return rc;
         const pss::MapArgs ma = map_args(h, file_pos_dev, offset_dev);
         if (h->version == 1) {
             PSS_HIP(h->d_sort.ensure(words(pss::v1_exact_ws_bytes(g, nr, pos_lo, count))));
@@ -1137,9 +1198,10 @@ int pss_generate_mapped(pss_sampler *h, int32_t rank_lo, int32_t rank_hi, int64_
     if (rc) return rc;
     const int64_t valid = std::min(count, h->ns - pos_lo);
     mk(pss::K_MAP, s);
+    const pss_sampler::TabSet &t = h->tab[h->tab_cur];
     for (int32_t r = 0; r < nr; r++) {
         const size_t o = (size_t)r * count;
-        PSS_HIP(pss::launch_map(h->d_prefix.p, h->F, h->d_bucket.p, h->kb, h->nb, h->d_ids.p + o, valid,
+        PSS_HIP(pss::launch_map(t.prefix.p, h->F, t.bucket.p, h->kb, h->nb, h->d_ids.p + o, valid,
                                 file_pos_dev + o, nullptr, offset_dev + o, s));
     }
     mk(-1, s);
@@ -1167,11 +1229,11 @@ int pss_gather(pss_sampler *h, const void *data_dev, int64_t row_bytes, const in
     DeviceGuard dg(h->device);
     hipStream_t s = (hipStream_t)stream;
     SharedUse su(h, s);
-    const int rc = prepare_order(h, s);
+    const int rc = prepare_tables(h, s);
     if (rc) return rc;
-    PSS_HIP(pss::launch_gather(data_dev, row_bytes, base_rows_dev, h->d_order.p, file_pos_dev, offset_dev, n,
-                               out_dev, s));
-    return PSS_OK;
+    PSS_HIP(pss::launch_gather(data_dev, row_bytes, base_rows_dev, h->tab[h->tab_cur].order.p, file_pos_dev,
+                               offset_dev, n, out_dev, s));
+    return tables_read(h, s);
 }
 
 int pss_partition(pss_sampler *h, int32_t rank_lo, int32_t rank_hi, int64_t *seg_off_dev,
@@ -1193,12 +1255,13 @@ int pss_partition(pss_sampler *h, int32_t rank_lo, int32_t rank_hi, int64_t *seg
     DeviceGuard dg(h->device);
     hipStream_t s = (hipStream_t)stream;
     SharedUse su(h, s);
-    int rc = prepare_prefix(h, s);
+    int rc = prepare(h, s);
+    if (rc == PSS_OK) rc = prepare_tables(h, s);
     if (rc) return rc;
     PSS_HIP(pss::launch_partition(h->geometry(), h->d_ranks.p, rank_lo, rank_hi - rank_lo,
-                                  h->d_prefix.p, h->F, seg_off_dev, seg_file_dev, seg_lo_dev,
+                                  h->tab[h->tab_cur].prefix.p, h->F, seg_off_dev, seg_file_dev, seg_lo_dev,
                                   seg_hi_dev, seg_cap, h->d_err.p, s));
-    return PSS_OK;
+    return tables_read(h, s);
 }
 
 int pss_digest(const int64_t *ids_dev, int64_t n, uint64_t *acc_dev, void *stream) {

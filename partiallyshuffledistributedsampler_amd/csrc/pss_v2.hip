@@ -519,14 +519,20 @@ __global__ __launch_bounds__(64) void k_v2_emit_x(Geometry g, V2Plan pl,
         const uint32_t *prev = VALr + ((int64_t)tile - 1) * pl.P1;   // tile 0: never read
         if (tile == 0) {
             for (uint32_t s = lane; s < P1; s += 64) buf[s] = to_slot(s);
-        } else if ((P1 & 1023u) == 0) {
+        } else if ((P1 & 255u) == 0) {
+            // rounds of up to 16 x 64 quads; P1 % 256 == 0 makes every 64-quad row whole (the
+            // rows past P1 / 4 -- P1 not a multiple of 4096 -- are skipped: they would read the
+            // next tile's table and write past this one's in LDS)
             const uint4 *p4 = (const uint4 *)prev;
-            for (uint32_t q0 = 0; q0 < P1 / 4; q0 += 1024) {
+            const uint32_t nq = P1 / 4;
+            for (uint32_t q0 = 0; q0 < nq; q0 += 1024) {
                 uint4 v[16];
 #pragma unroll
-                for (int u = 0; u < 16; u++) v[u] = p4[q0 + 64u * u + lane];   // q < P1/4: P1 % 1024 == 0
+                for (int u = 0; u < 16; u++)
+                    if (q0 + 64u * u < nq) v[u] = p4[q0 + 64u * u + lane];
 #pragma unroll
                 for (int u = 0; u < 16; u++) {
+                    if (q0 + 64u * u >= nq) continue;
                     const uint32_t q = q0 + 64u * u + lane;
                     uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
 #pragma unroll
@@ -586,9 +592,7 @@ __global__ __launch_bounds__(64) void k_v2_emit_x(Geometry g, V2Plan pl,
         if constexpr (PAIR) {
             int32_t f, of;
             if (x & kPairEsc) {
-                int64_t o;
-                map_one_bucketed_t(ma.prefix, ma.F, ma.T, ma.BT, ma.kb, ma.nb, from_slot(x & ~kPairEsc), f, o);
-                of = (int32_t)o;
+                map_id_fast(ma, from_slot(x & ~kPairEsc), f, of);
             } else {
                 f = (int32_t)(x >> pob);
                 of = (int32_t)(x & omask);
@@ -710,17 +714,38 @@ __global__ __launch_bounds__(64) void k_v2_emit_x(Geometry g, V2Plan pl,
                     const uint32_t S1 = __builtin_bit_cast(uint32_t, __builtin_bit_cast(pss_u16x2, A51) << HS);
                     const uint32_t Y0 = S0 ^ (A40 ^ F50 ^ KY), Y1 = S1 ^ (A41 ^ F51 ^ KY);
                     const uint32_t y[4] = {Y0 & 0xFFFFu, Y0 >> 16, Y1 & 0xFFFFu, Y1 >> 16};
+                    // contig: 0 = the window's values through to_slot (PAIR: escaped), else one
+                    // add -- PAIR: on 1, 2 or 3 file segments (the window's boundaries)
+                    constexpr int M = decltype(contig)::value;
 #pragma unroll
                     for (int j = 0; j < 4; j++) {
-                        if constexpr (PAIR)
-                            ins[j] = decltype(contig)::value ? pair_of_y(y[j], PQ0, PQ1, PQ2, Ps1, Ps2)
-                                                             : kPairEsc | (wB + y[j]);
-                        else
-                            ins[j] = decltype(contig)::value ? id_first + y[j] : to_slot(wB + y[j]);
+                        if constexpr (PAIR) {
+                            if constexpr (M == 0) ins[j] = kPairEsc | (wB + y[j]);
+                            else if constexpr (M == 1) ins[j] = y[j] + PQ0;
+                            else if constexpr (M == 2) ins[j] = y[j] + (y[j] < Ps1 ? PQ0 : PQ1);
+                            else ins[j] = pair_of_y(y[j], PQ0, PQ1, PQ2, Ps1, Ps2);
+                        } else {
+                            ins[j] = M ? id_first + y[j] : to_slot(wB + y[j]);
+                        }
                     }
                 };
                 auto emit4 = [&](uint32_t tlx, const uint32_t (&v)[4]) {
-                    if constexpr (MAPPED) {
+                    if constexpr (PAIR) {
+                        // branch-free unless some lane holds an escaped value (one wave-uniform
+                        // test per super-batch, not an exec-masked branch per value)
+                        const uint32_t any = (v[0] | v[1] | v[2] | v[3]) & kPairEsc;
+                        if (__builtin_amdgcn_ballot_w64(any != 0u) == 0u) {
+#pragma unroll
+                            for (int j = 0; j < 4; j++) {
+                                const int64_t e = ebase + tlx + 64u * j + lane;
+                                ma.fpos[e] = (int32_t)(v[j] >> pob);
+                                ma.off[e] = (int32_t)(v[j] & omask);
+                            }
+                        } else {
+#pragma unroll
+                            for (int j = 0; j < 4; j++) emit_m(ebase + tlx + 64u * j + lane, v[j]);
+                        }
+                    } else if constexpr (MAPPED) {
 #pragma unroll
                         for (int j = 0; j < 4; j++) emit_m(ebase + tlx + 64u * j + lane, v[j]);
                     } else {
@@ -741,8 +766,15 @@ __global__ __launch_bounds__(64) void k_v2_emit_x(Geometry g, V2Plan pl,
                         p0 += 256;
                     }
                 };
-                if (contiguous) run(std::true_type{});
-                else run(std::false_type{});
+                if constexpr (PAIR) {
+                    if (!contiguous) run(std::integral_constant<int, 0>{});
+                    else if (Ps1 == kNone) run(std::integral_constant<int, 1>{});
+                    else if (Ps2 == kNone) run(std::integral_constant<int, 2>{});
+                    else run(std::integral_constant<int, 3>{});
+                } else {
+                    if (contiguous) run(std::integral_constant<int, 1>{});
+                    else run(std::integral_constant<int, 0>{});
+                }
                 left -= n;
                 if (p0 == B) { p0 = 0; w0++; }
             }
@@ -954,12 +986,11 @@ __global__ __launch_bounds__(256) void k_v2_tail_f(Geometry g, V2Plan pl,
         const uint32_t s = feistel(j, P1, hT, tk);
         const int64_t id = v2_id(slot_value_after(VALr, pl.P1, pl.G - 1, s), rd, g);
         if (ma.fpos) {      // mapped output: the global bucketed map (P1 ids per rank)
-            int32_t f;
-            int64_t of;
-            map_one_bucketed(ma.prefix, ma.F, ma.BT, ma.kb, ma.nb, id, f, of);
+            int32_t f, of;
+            map_id_fast(ma, id, f, of);
             const int64_t e = (int64_t)rl * count - pos_lo + pos;
             ma.fpos[e] = f;
-            ma.off[e] = (int32_t)of;
+            ma.off[e] = of;
         } else {
             o[pos] = id;
         }

@@ -372,11 +372,10 @@ __global__ __launch_bounds__(64) void k_g_emit(Geometry g, GPlan pl, const RankD
     int32_t *ofp = ma.fpos + (int64_t)rl * count - pos_lo, *ooff = ma.off + (int64_t)rl * count - pos_lo;
     auto put = [&](int64_t pos, int64_t id) {   // one id, outside the runs' buffer stores
         if constexpr (MAPPED) {
-            int32_t f;
-            int64_t of;
-            map_one_bucketed(ma.prefix, ma.F, ma.BT, ma.kb, ma.nb, id, f, of);
+            int32_t f, of;
+            map_id_fast(ma, id, f, of);
             ofp[pos] = f;
-            ooff[pos] = (int32_t)of;
+            ooff[pos] = of;
         } else {
             o[pos] = id;
         }
@@ -520,12 +519,11 @@ __global__ __launch_bounds__(64) void k_g_emit(Geometry g, GPlan pl, const RankD
 #pragma unroll
                     for (int j = 0; j < 4; j++) {
                         if constexpr (MAPPED) {
-                            int32_t f;
-                            int64_t of;
+                            int32_t f, of;
 #ifdef PSS_DIAG_MAP_NONE   // (timing-only build: the stores of the mapped form without the map)
-                            of = ids.from_slot(v[j]); f = (int32_t)of; of >>= 3;
+                            of = (int32_t)ids.from_slot(v[j]); f = of; of >>= 3;
 #else
-                            map_one_bucketed(ma.prefix, ma.F, ma.BT, ma.kb, ma.nb, ids.from_slot(v[j]), f, of);
+                            map_id_fast(ma, ids.from_slot(v[j]), f, of);
 #endif
                             __builtin_amdgcn_raw_buffer_store_b32((uint32_t)f, orsrc, (int)voff, (int)(4u * (uint32_t)j * G64), 0);
                             __builtin_amdgcn_raw_buffer_store_b32((uint32_t)of, frsrc, (int)voff, (int)(4u * (uint32_t)j * G64), 0);

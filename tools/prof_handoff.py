@@ -1,6 +1,6 @@
 """Profiling driver of the fused hand-off pss_generate_mapped (all 8 logical ranks, 100M
-positions -> int32 (file, offset)): for each of C2 V2, C2 V1 and C5 V2, two warm-up epochs (the
-V2 lookahead primed), then `--epochs` consecutive epochs into preallocated outputs; prints one
+positions -> int32 (file, offset)): for each of C2 V2, C2 V1 and C5 V2, four warm-up epochs (the
+V2 lookahead primed, its buffers grown), then `--epochs` consecutive epochs into preallocated outputs; prints one
 JSON line of ms per epoch (host clock around the synchronised loop) and, with --events, the
 generation kernels' HIP-event spans.  Run under rocprofv3 --kernel-trace --stats to see the
 mapped kernels' durations.
@@ -19,6 +19,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import workloads as W  # noqa: E402
 from partiallyshuffledistributedsampler_amd.engine import IndexEngine  # noqa: E402
 
+WARM = 4   # warm-up epochs: the V2 lookahead's VAL ring grows over the first sequential calls
 CFGS = {"c2v2": ("c2", 2), "c2v1": ("c2", 1), "c5v2": ("c5", 2)}
 
 
@@ -29,7 +30,7 @@ def run(name, epochs, events):
     ns = eng.num_samples
     fpos = torch.empty((R, ns), dtype=torch.int32, device="cuda")
     off = torch.empty((R, ns), dtype=torch.int32, device="cuda")
-    for e in range(2):
+    for e in range(WARM):
         eng.init_iter(e)
         eng.generate_mapped(0, R, out=(fpos, off))
     torch.cuda.synchronize()
@@ -37,7 +38,7 @@ def run(name, epochs, events):
         eng.profile(True)
     t0 = time.perf_counter()
     for e in range(epochs):
-        eng.init_iter(2 + e)
+        eng.init_iter(WARM + e)
         eng.generate_mapped(0, R, out=(fpos, off))
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t0) / epochs * 1e3
