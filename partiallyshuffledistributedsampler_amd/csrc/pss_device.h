@@ -459,6 +459,25 @@ __device__ __forceinline__ bool window_map_segments(const MapArgs &ma, int64_t a
     if (f[0] < 0) return false;
     d0 = (uint32_t)o;
     f[1] = f[2] = f[0];
+    {   // the usual case in one round trip: the next three prefix entries, non-empty files
+        const int64_t f0 = f[0];
+        const int64_t p1 = ma.prefix[f0 + 1];
+        const int64_t p2 = f0 + 2 <= ma.F ? ma.prefix[f0 + 2] : p1;
+        const int64_t p3 = f0 + 3 <= ma.F ? ma.prefix[f0 + 3] : p2;
+        if (p1 - a >= len) return true;                       // one file
+        if (p2 > p1) {                                        // file f0 + 1 not empty
+            s[0] = (uint32_t)(p1 - a);
+            f[1] = f[2] = (int32_t)(f0 + 1);
+            if (p2 - a >= len) return true;                   // two files
+            if (p3 > p2) {
+                s[1] = (uint32_t)(p2 - a);
+                f[2] = (int32_t)(f0 + 2);
+                return p3 - a >= len;                         // three files, else a third boundary
+            }
+        }
+        s[0] = kNone; s[1] = kNone;                           // empty files: the general walk
+        f[1] = f[2] = f[0];
+    }
     for (int k = 0; k < 3; k++) {
         const int64_t end = ma.prefix[f[k] + 1] - a;   // the next file boundary (prefix[F] = T)
         if (end >= len) return true;

@@ -217,19 +217,23 @@ struct pss_sampler {
     bool dirty = true;            // rank descriptors of the epoch not on the device yet
     bool prefix_dirty = true;     // CPU mode: the host prefix is owed (cpu_prefix)
     DevBuf<int64_t> d_lens, d_ids;   // d_ids: scratch ids of pss_generate_mapped
-    // The epoch's device tables -- the file order, its exclusive prefix (+ the scan's scratch) and
-    // the prefix's bucket index (pss_map.h; kb / nb below) -- in two sets, built on first use after
-    // an init_iter on the handle's table stream: epoch e's upload, scan and bucket index run beside
-    // epoch e - 1's kernels on the caller's stream, which only waits for the set to be ready (they
-    // had run in line, ~35 us per epoch before a mapped replay at C2).  A set is rebuilt after its
-    // last reader (`freed`); its pinned staging is reused after the upload that read it (`staged`).
+    // The epoch's device tables -- the file order, its exclusive prefix and the prefix's bucket
+    // index (pss_map.h; kb / nb below) -- in two sets.  A set is computed on the host on first use
+    // after an init_iter (tables_host: O(F + nb), the host runs ahead of the GPU) into pinned
+    // staging and uploaded as one blob by a short copy kernel on the handle's table stream, beside
+    // epoch e - 1's kernels; the caller's stream only waits for it.  (Round 6: the device scan in
+    // line cost ~30 us per epoch before a mapped replay at C2; the same three scan kernels on the
+    // side stream delayed the replay's one round of waves by ~22 us, a one-workgroup scan by ~40.)
+    // A set is rewritten after its last reader (`freed`); its staging after its upload (`staged`).
     struct TabSet {
-        DevBuf<int32_t> order, bucket;
-        DevBuf<int64_t> prefix;
-        int32_t *stage = nullptr;
+        DevBuf<uint32_t> blob;        // order | prefix | bucket index, 16-byte aligned parts
+        int32_t *order = nullptr, *bucket = nullptr;
+        int64_t *prefix = nullptr;
+        uint32_t *stage = nullptr;    // pinned, the same layout
         hipEvent_t ready = nullptr, freed = nullptr, staged = nullptr;
         bool built = false, read = false;
     };
+    size_t tab_prefix_off = 0, tab_bucket_off = 0, tab_bytes = 0;   // blob layout (bytes)
     TabSet tab[2];
     int tab_cur = 0;
     bool tab_dirty = true;        // this epoch's tables not built yet
@@ -356,11 +360,17 @@ int ensure_device(pss_sampler *h) {
     PSS_HIP(h->d_lens.ensure((size_t)h->F));
     PSS_HIP(h->d_ranks.ensure((size_t)h->R));
     PSS_HIP(h->d_err.ensure(1));
+    auto a16 = [](size_t b) { return (b + 15) & ~(size_t)15; };
+    h->tab_prefix_off = a16(sizeof(int32_t) * (size_t)h->F);
+    h->tab_bucket_off = a16(h->tab_prefix_off + sizeof(int64_t) * ((size_t)h->F + 1));
+    h->tab_bytes = a16(h->tab_bucket_off + sizeof(int32_t) * (size_t)h->nb);
     for (auto &t : h->tab) {
-        PSS_HIP(t.order.ensure((size_t)h->F));
-        PSS_HIP(t.prefix.ensure((size_t)h->F + 1 + pss::scan_scratch_words(h->F)));
-        PSS_HIP(t.bucket.ensure((size_t)h->nb));
-        PSS_HIP(hipHostMalloc((void **)&t.stage, sizeof(int32_t) * (h->F ? h->F : 1)));
+        PSS_HIP(t.blob.ensure(h->tab_bytes / sizeof(uint32_t)));
+        char *b = (char *)t.blob.p;
+        t.order = (int32_t *)b;
+        t.prefix = (int64_t *)(b + h->tab_prefix_off);
+        t.bucket = (int32_t *)(b + h->tab_bucket_off);
+        PSS_HIP(hipHostMalloc((void **)&t.stage, h->tab_bytes));
         PSS_HIP(hipEventCreateWithFlags(&t.ready, hipEventDisableTiming));
         PSS_HIP(hipEventCreateWithFlags(&t.freed, hipEventDisableTiming));
         PSS_HIP(hipEventCreateWithFlags(&t.staged, hipEventDisableTiming));
@@ -394,6 +404,25 @@ int prepare(pss_sampler *h, hipStream_t s) {
     return PSS_OK;
 }
 
+// The epoch's tables on the host (the device layout of a TabSet): the shuffled file order, its
+// exclusive prefix over files_len (the reference's past_files_samples, V1:126,182-190; prefix[F] =
+// the scanned total) and the bucket index BT[b] = file_of(prefix, F, b << kb) -- the largest f
+// with prefix[f] <= b << kb: the non-empty file holding that id, F - 1 past the total (pss_map.h).
+void tables_host(const pss_sampler *h, int32_t *order, int64_t *prefix, int32_t *BT) {
+    const int64_t F = h->F;
+    std::memcpy(order, h->order.data(), sizeof(int32_t) * (size_t)F);
+    int64_t run = 0, b = 0;
+    for (int64_t f = 0; f < F; f++) {
+        prefix[f] = run;
+        const int64_t v = h->files_len[(size_t)order[f]];
+        run += v;
+        if (v > 0)
+            for (; b < h->nb && (b << h->kb) < run; b++) BT[b] = (int32_t)f;
+    }
+    prefix[F] = run;
+    for (; b < h->nb; b++) BT[b] = (int32_t)(F > 0 ? F - 1 : 0);
+}
+
 // The epoch's tables (TabSet: the shuffled file order, its prefix and bucket index), needed by
 // the map, the fused hand-off, the gather and the partition only: built on first use after an
 // init_iter into the other set, on the table stream, after that set's last reader; then `s`
@@ -402,20 +431,26 @@ int prepare_tables(pss_sampler *h, hipStream_t s) {
     if (!h->iterated) return fail(PSS_ESTATE, "pss_init_iter must be called before device work");
     int rc = ensure_device(h);
     if (rc) return rc;
+#ifdef PSS_DIAG_TABLES_INLINE   // (timing-only build: the tables built in line on the caller's stream)
+    h->tstream = s;
+#endif
     if (h->tab_dirty) {
         const int k = h->tab_cur ^ 1;
         pss_sampler::TabSet &t = h->tab[k];
         if (t.built) PSS_HIP(hipEventSynchronize(t.staged));   // the upload that read `stage`
-        std::memcpy(t.stage, h->order.data(), sizeof(int32_t) * h->F);
+        char *st = (char *)t.stage;
+        tables_host(h, (int32_t *)st, (int64_t *)(st + h->tab_prefix_off), (int32_t *)(st + h->tab_bucket_off));
         if (t.read) PSS_HIP(hipStreamWaitEvent(h->tstream, t.freed, 0));
-        if (h->F) PSS_HIP(pss::launch_upload(t.stage, t.order.p, sizeof(int32_t) * h->F, h->tstream));
-        PSS_HIP(hipEventRecord(t.staged, h->tstream));
+        // Behind the last queued V2 lookahead pass too: that pass starts as the previous replay
+        // ends, i.e. as this epoch's predecessor replay is launched, and the upload would otherwise
+        // start right then and hold CU slots the one round of replay waves is waiting for (C2
+        // mapped: replay 222 against 200 us).  After the pass it runs inside the replay instead.
+        if (h->side && h->last_valid) PSS_HIP(hipStreamWaitEvent(h->tstream, h->ev_side, 0));
         const pss::Marker mk = marker_of(h);
         mk(pss::K_SCAN, h->tstream);
-        PSS_HIP(pss::launch_scan_prefix(h->d_lens.p, t.order.p, h->F, t.prefix.p,
-                                        (uint64_t *)(t.prefix.p + h->F + 1), h->tstream));
-        PSS_HIP(pss::launch_bucket_index(t.prefix.p, h->F, h->kb, h->nb, t.bucket.p, h->tstream));
+        PSS_HIP(pss::launch_upload(t.stage, t.blob.p, h->tab_bytes, h->tstream));
         mk(-1, h->tstream);
+        PSS_HIP(hipEventRecord(t.staged, h->tstream));
         PSS_HIP(hipEventRecord(t.ready, h->tstream));
         t.built = true;
         h->tab_cur = k;
@@ -509,9 +544,9 @@ void map_shortcuts(pss_sampler *h, int64_t scanned) {
 // the map arguments of the current epoch's device tables and the caller's outputs
 pss::MapArgs map_args(const pss_sampler *h, int32_t *fpos, int32_t *off) {
     pss::MapArgs m = h->map_sc;
-    m.prefix = h->tab[h->tab_cur].prefix.p;
+    m.prefix = h->tab[h->tab_cur].prefix;
     m.F = h->F;
-    m.BT = h->tab[h->tab_cur].bucket.p;
+    m.BT = h->tab[h->tab_cur].bucket;
     m.kb = h->kb;
     m.nb = h->nb;
     m.fpos = fpos;
@@ -588,7 +623,7 @@ int pss_destroy(pss_sampler *h) {
         h->d_ranks.release(); h->d_val.release(); h->d_buf.release(); h->d_sort.release();
         h->d_ids.release();
         for (auto &t : h->tab) {
-            t.order.release(); t.prefix.release(); t.bucket.release();
+            t.blob.release();
             if (t.stage) (void)hipHostFree(t.stage);
             for (hipEvent_t e : {t.ready, t.freed, t.staged}) if (e) (void)hipEventDestroy(e);
         }
@@ -1093,7 +1128,7 @@ int pss_map(pss_sampler *h, const int64_t *ids_dev, int64_t n, int32_t *file_pos
     int rc = prepare_tables(h, s);
     if (rc) return rc;
     const pss_sampler::TabSet &t = h->tab[h->tab_cur];
-    PSS_HIP(pss::launch_map(t.prefix.p, h->F, t.bucket.p, h->kb, h->nb, ids_dev, n, file_pos_dev,
+    PSS_HIP(pss::launch_map(t.prefix, h->F, t.bucket, h->kb, h->nb, ids_dev, n, file_pos_dev,
                             offset_dev, nullptr, s));
     return tables_read(h, s);
 }
@@ -1201,7 +1236,7 @@ static int generate_mapped_dev(pss_sampler *h, int32_t rank_lo, int32_t rank_hi,
     const pss_sampler::TabSet &t = h->tab[h->tab_cur];
     for (int32_t r = 0; r < nr; r++) {
         const size_t o = (size_t)r * count;
-        PSS_HIP(pss::launch_map(t.prefix.p, h->F, t.bucket.p, h->kb, h->nb, h->d_ids.p + o, valid,
+        PSS_HIP(pss::launch_map(t.prefix, h->F, t.bucket, h->kb, h->nb, h->d_ids.p + o, valid,
                                 file_pos_dev + o, nullptr, offset_dev + o, s));
     }
     mk(-1, s);
@@ -1231,7 +1266,7 @@ int pss_gather(pss_sampler *h, const void *data_dev, int64_t row_bytes, const in
     SharedUse su(h, s);
     const int rc = prepare_tables(h, s);
     if (rc) return rc;
-    PSS_HIP(pss::launch_gather(data_dev, row_bytes, base_rows_dev, h->tab[h->tab_cur].order.p, file_pos_dev,
+    PSS_HIP(pss::launch_gather(data_dev, row_bytes, base_rows_dev, h->tab[h->tab_cur].order, file_pos_dev,
                                offset_dev, n, out_dev, s));
     return tables_read(h, s);
 }
@@ -1259,7 +1294,7 @@ int pss_partition(pss_sampler *h, int32_t rank_lo, int32_t rank_hi, int64_t *seg
     if (rc == PSS_OK) rc = prepare_tables(h, s);
     if (rc) return rc;
     PSS_HIP(pss::launch_partition(h->geometry(), h->d_ranks.p, rank_lo, rank_hi - rank_lo,
-                                  h->tab[h->tab_cur].prefix.p, h->F, seg_off_dev, seg_file_dev, seg_lo_dev,
+                                  h->tab[h->tab_cur].prefix, h->F, seg_off_dev, seg_file_dev, seg_lo_dev,
                                   seg_hi_dev, seg_cap, h->d_err.p, s));
     return tables_read(h, s);
 }

@@ -480,10 +480,13 @@ __global__ __launch_bounds__(64) void k_v2_emit_x(Geometry g, V2Plan pl,
     const uint32_t wc_lo = w_lo > kPairBack ? w_lo - kPairBack : 0u;
     const uint32_t nwc = w_lo + (uint32_t)nwin - wc_lo;
     const uint32_t pob = ma.pob, omask = (1u << pob) - 1u;
-    if constexpr (PAIR) {
-        for (uint32_t i = lane; i < nwc; i += 64) pair_window_consts(ma, rd, g, B, twoB, wc_lo + i, pw + kPairWords * i);
-        __syncthreads();
-    }
+    // (computed while the slot table's loads are in flight: both are chains of global loads)
+    auto pair_consts = [&]() {
+        if constexpr (PAIR) {
+            for (uint32_t i = lane; i < nwc; i += 64) pair_window_consts(ma, rd, g, B, twoB, wc_lo + i, pw + kPairWords * i);
+            __syncthreads();
+        }
+    };
     const float invB = 1.0f / (float)B;
     // PAIR, one lane: the pair of virtual value v from its window's constants, else an escape
     auto pair_lookup = [&](uint32_t v) -> uint32_t {
@@ -518,6 +521,7 @@ __global__ __launch_bounds__(64) void k_v2_emit_x(Geometry g, V2Plan pl,
         const uint32_t *VALr = VAL + (int64_t)rl * pl.G * pl.P1;
         const uint32_t *prev = VALr + ((int64_t)tile - 1) * pl.P1;   // tile 0: never read
         if (tile == 0) {
+            pair_consts();
             for (uint32_t s = lane; s < P1; s += 64) buf[s] = to_slot(s);
         } else if ((P1 & 255u) == 0) {
             // rounds of up to 16 x 64 quads; P1 % 256 == 0 makes every 64-quad row whole (the
@@ -530,6 +534,7 @@ __global__ __launch_bounds__(64) void k_v2_emit_x(Geometry g, V2Plan pl,
 #pragma unroll
                 for (int u = 0; u < 16; u++)
                     if (q0 + 64u * u < nq) v[u] = p4[q0 + 64u * u + lane];
+                if (q0 == 0) pair_consts();
 #pragma unroll
                 for (int u = 0; u < 16; u++) {
                     if (q0 + 64u * u >= nq) continue;
@@ -542,6 +547,7 @@ __global__ __launch_bounds__(64) void k_v2_emit_x(Geometry g, V2Plan pl,
                 }
             }
         } else {
+            pair_consts();
             for (uint32_t s0 = lane; s0 < P1; s0 += 256) {
                 uint32_t v[4];
 #pragma unroll
