@@ -52,20 +52,30 @@ WORKLOADS = {
 
 
 def _pmc_traffic(workload, symbols):
-    """HBM bytes per launch of the first kernel symbol found for this workload in
+    """(HBM bytes per launch, source) of the first kernel symbol found for this workload in
     profiles/pmc_traffic.json (written by tools/pmc_summary.py from separate rocprofv3 --pmc
-    FETCH_SIZE / WRITE_SIZE passes over this same bench at N=1), or None."""
+    FETCH_SIZE / WRITE_SIZE passes over this same bench at N=1 -- not measured in this run), or
+    (None, None)."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(p) as f:
             d = json.load(f)
     except (OSError, ValueError):
-        return None
+        return None, None
     for sym in symbols:
-        v = d.get(workload, {}).get(sym, {}).get("hbm_bytes_per_launch")
+        e = d.get(workload, {}).get(sym, {})
+        v = e.get("hbm_bytes_per_launch")
         if v is not None:
-            return v
-    return None
+            src = {"file": "profiles/pmc_traffic.json", "workload": workload, "symbol": sym,
+                   "measured": "separate rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE) of this bench, "
+                               "not this run"}
+            for k in ("round", "source", "build", "passes"):
+                if k in e:
+                    src[k] = e[k]
+            if "_meta" in d:
+                src["meta"] = d["_meta"]
+            return v, src
+    return None, None
 
 
 # ---- CPU baseline --------------------------------------------------------------------------------
@@ -135,7 +145,7 @@ def cpu_baseline():
     on = _reference_processes("c2", 2, nproc, 64, 1024, True)
     off = _reference_processes("c2", 2, nproc, 64, 1024, False)
     out = {"value": on["idx_per_s"] / 1e9, "unit": "G idx/s", "cores": nproc,
-           "kind": "port",
+           "kind": "python_restatement",
            "port_of": "the reference's Python __next__ loop restated line for line in Python "
                       "(oracle/pyref.py, pinned to the reference's recorded streams), run by the "
                       "CPython interpreter -- not a compiled port",
@@ -244,9 +254,11 @@ def _reader_for(fl, width):
 def latency_dropin(device, reps=5):
     """set_epoch(e); next(iter(sampler)) at 1B samples / 100K files / R = 1024 (C3) through the
     drop-in DistributedSamplerViaLocallyShuffleV2 class with an in-memory reader: host
-    init_iter + epoch upload + generation of the rank's epoch + prefix scan + id -> (file,
-    offset) map + pinned D2H + the first batch's grouping and file read.  Also the 128 logical
-    ranks one of 8 GPUs owns (ranks=(0, 128)), and the engine-level figure."""
+    init_iter + the epoch's tables + the rank's epoch as (file, offset) pairs (the fused
+    hand-off) + pinned D2H + the first batch's grouping and file read.  Also the 128 logical
+    ranks one of 8 GPUs owns (ranks=(0, 128)), order="exact" (the reference's own draws: the
+    bit-identical stream; warm = consecutive epochs, cold = an epoch that does not follow the
+    previous one, its MT draws made in the call), and the engine-level figure."""
     from partiallyshuffledistributedsampler_amd.DistributedSamplerViaLocallyShuffleV2 import \
         DistributedSamplerViaLocallyShuffle as V2
     lengths, N, R, B, _ = W.shape("c3")
@@ -255,7 +267,8 @@ def latency_dropin(device, reps=5):
     reader = _reader_for(fl, int(lengths.max()))
     res = {}
     for key, kw in (("set_epoch_to_first_batch_ms", {}),
-                    ("set_epoch_to_first_batch_128_ranks_ms", {"ranks": (0, 128)})):
+                    ("set_epoch_to_first_batch_128_ranks_ms", {"ranks": (0, 128)}),
+                    ("exact_set_epoch_to_first_batch_ms", {"order": "exact"})):
         s = V2(_DS(files), reader, num_replicas=R, rank=0, shuffle_buffer=B, total_size=1,
                batch_size=1024, files_len=fl, device=device, **kw)
         times = []
@@ -269,10 +282,11 @@ def latency_dropin(device, reps=5):
             if e:
                 times.append((t1 - t0) * 1e3)
         res[key] = float(np.median(times))
-        if not kw:
+        if not kw or kw.get("order") == "exact":
             # cold: a resume at an epoch the host prefetcher has not prepared (it computes the
             # coming epochs' file permutations, V2:143-144, on worker threads): the O(F) CPython-MT
-            # shuffle of 100K files runs inside set_epoch -> first batch
+            # shuffle of 100K files runs inside set_epoch -> first batch (exact order: also the
+            # epoch's MT draws, none made ahead)
             cold = []
             for e in (57, 113, 171, 229, 287):
                 torch.cuda.synchronize(device)
@@ -281,7 +295,7 @@ def latency_dropin(device, reps=5):
                 b = next(iter(s))
                 cold.append((time.perf_counter() - t0) * 1e3)
                 assert sum(len(d["x"]) for d in b[0]) == 1024
-            res["cold_set_epoch_to_first_batch_ms"] = float(np.median(cold))
+            res["cold_" + key] = float(np.median(cold))
             res["cold_epochs"] = "57, 113, 171, 229, 287 after 0..%d (prefetcher misses), median" % reps
     # engine only: init_iter + generate + map + D2H of the first batch
     eng = IndexEngine(lengths, N, R, B, 2, seed=0, device=device)
@@ -311,10 +325,10 @@ def latency_dropin(device, reps=5):
     return res
 
 
-def sampler_data_path(device, reps=3):
+def sampler_data_path(device, reps=5):
     """The drop-in's per-epoch device path at C2 for one rank (12.5M ids): set_epoch + iter ->
-    generation + prefix scan + id -> (file, offset) map + pinned D2H of every (file, offset)
-    pair; ms until all of it is on the host."""
+    the epoch's tables + the fused hand-off (the rank's (int32 file, int32 offset) pairs in one
+    pass) + pinned D2H of every pair; ms until all of it is on the host."""
     from partiallyshuffledistributedsampler_amd.DistributedSamplerViaLocallyShuffleV2 import \
         DistributedSamplerViaLocallyShuffle as V2
     lengths, N, R, B, _ = W.shape("c2")
@@ -334,31 +348,44 @@ def sampler_data_path(device, reps=3):
             times.append((t1 - t0) * 1e3)
     ms = float(np.median(times))
     return {"epoch_ms": ms, "ids": s.num_samples, "G_idx_per_s": s.num_samples / ms / 1e6,
-            "host_bytes": s.num_samples * 12,
-            "config": "C2, one rank (12.5M ids): generate + map + pinned D2H of (int32 file, "
-                      "int64 offset) per id"}
+            "host_bytes": s.num_samples * 8,
+            "host_GBps": s.num_samples * 8 / (ms * 1e-3) / 1e9,
+            "config": "C2, one rank (12.5M ids): fused hand-off (pss_generate_mapped) + pinned D2H "
+                      "of (int32 file, int32 offset) per id"}
 
 
-def handoff_figures(device, reps=5):
+def handoff_figures(device, reps=20, warm=4):
     """The fused hand-off (all 8 logical ranks, 100M positions): pss_generate_mapped -> (int32
     file, int32 offset) per position in HBM, mapped inside the generation kernels -- V1 and V2 at
-    C2, V2 at C5 (the grouped replay); and the standalone map of 100M int64 ids."""
-    lengths, N, R, B, _ = W.shape("c2")
+    C2, V2 at C5 (the grouped replay), and C4's Zipf file sizes (the pairs do not fit 31 bits
+    there: the segment map) at C2's size; consecutive epochs after `warm` warm-up epochs (the V2
+    lookahead primed and its buffers grown) into preallocated outputs; and the standalone map of
+    100M int64 ids.  frac_of_8TBps: 8 B per position against the HBM spec."""
     out = {}
-    for ver, cfg in ((1, "c2"), (2, "c2"), (2, "c5")):
+    for key, ver, cfg in (("v1_mapped", 1, "c2"), ("v2_mapped", 2, "c2"), ("c5_v2_mapped", 2, "c5"),
+                          ("zipf_v2_mapped", 2, "c4")):
         lengths, N, R, B, _ = W.shape(cfg)
+        if cfg == "c4":                 # C4's file sizes, C2's sample count and ranks
+            lengths = lengths[np.cumsum(lengths) <= 100_000_000]
+            N, R = int(lengths.sum()), 8
         eng = IndexEngine(lengths, N, R, B, ver, seed=0, device=device)
-        eng.init_iter(0)
-        eng.generate_mapped(0, R)
+        ns = eng.num_samples
+        fp = torch.empty((R, ns), dtype=torch.int32, device=device)
+        of = torch.empty_like(fp)
+        for e in range(warm):
+            eng.init_iter(e)
+            eng.generate_mapped(0, R, out=(fp, of))
         torch.cuda.synchronize(device)
         t0 = time.perf_counter()
         for e in range(reps):
-            eng.init_iter(1 + e)
-            eng.generate_mapped(0, R)
+            eng.init_iter(warm + e)
+            eng.generate_mapped(0, R, out=(fp, of))
         torch.cuda.synchronize(device)
         ms = (time.perf_counter() - t0) / reps * 1e3
-        key = "v%d_mapped" % ver if cfg == "c2" else "c5_v2_mapped"
-        out[key] = {"ms_per_epoch": ms, "G_pos_per_s": R * eng.num_samples / ms / 1e6}
+        out[key] = {"ms_per_epoch": ms, "G_pos_per_s": R * ns / ms / 1e6,
+                    "frac_of_8TBps": R * ns * 8 / (ms * 1e-3) / (HBM_PEAK_GBS * 1e9),
+                    "files": len(lengths), "positions": R * ns}
+        del fp, of
         if ver == 2 and cfg == "c2":
             ids = eng.generate(0, R)
             fp, off = eng.map(ids.view(-1))
@@ -371,8 +398,9 @@ def handoff_figures(device, reps=5):
             out["map_100M_ids_ms"] = ms
             del ids, fp, off
         eng.close()
-    out["config"] = ("C2 (V1, V2) and C5 (V2, B = 2^20: the grouped replay), 8 logical ranks x 12.5M "
-                     "positions -> (int32 file_pos, int32 offset)")
+    out["config"] = ("C2 (V1, V2), C5 (V2, B = 2^20: the grouped replay) and C4's Zipf sizes cut to "
+                     "~100M samples (V2), 8 logical ranks, ~12.5M positions each -> (int32 file_pos, "
+                     "int32 offset); %d epochs after %d warm-up epochs" % (reps, warm))
     return out
 
 
@@ -385,7 +413,7 @@ def exact_order_figures(device):
     pipeline's span on the caller's stream (HIP events around the launch)."""
     res = {}
     for name, cfg, ver, reps in (("c2_v2", "c2", 2, 12), ("c2_v1", "c2", 1, 12), ("c5_v2", "c5", 2, 12),
-                                 ("c5_v1", "c5", 1, 12)):
+                                 ("c5_v1", "c5", 1, 12), ("c3_v2", "c3", 2, 6)):
         lengths, N, R, B, _ = W.shape(cfg)
         eng = IndexEngine(lengths, N, R, B, ver, seed=0, device=device, order="exact")
         ns = eng.num_samples
@@ -423,6 +451,7 @@ def exact_order_figures(device):
         del out
     res["config"] = ("order='exact' (CPython MT19937 draws: the reference's id streams bit for bit); "
                      "c2: 10K files x 10K, R=8, B=4096; c5: the same files, B=2^20; all 8 ranks per epoch; "
+                     "c3: 100K files x 10K, R=1024, B=4096, all 1024 ranks (1B ids) per epoch; "
                      "ms_per_epoch: consecutive epochs (draws made ahead), cold: an epoch that does not "
                      "follow the previous call's (its own draws)")
     return res
@@ -469,8 +498,9 @@ def main():
                     help="time the steps without the per-launch HIP events (roofline omitted)")
     ap.add_argument("--pipeline", type=int, default=1,
                     help="epochs in flight: 2 alternates two streams and output buffers")
-    ap.add_argument("--timing-every", type=int, default=16,
-                    help="HIP-event timing of the generation kernel on every n-th timed step")
+    ap.add_argument("--timing-every", type=int, default=0,
+                    help="HIP-event timing of the generation kernel on every n-th timed step "
+                         "(default: min(16, steps // 8), i.e. at least 8 timed launches)")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -534,7 +564,8 @@ def main():
     # live timing of the dominant kernel: two HIP events around the generation kernel on its
     # stream, on every 16th step of the timed region (C2, same box: every 4th step 557-559 G
     # idx/s, every 16th 564-565, none 567; profiles/r05/bench_overheads.txt)
-    eng.profile(not args.no_kernel_timing, generation_only=True, every=args.timing_every)
+    every = args.timing_every if args.timing_every > 0 else max(1, min(16, args.steps // 8))
+    eng.profile(not args.no_kernel_timing, generation_only=True, every=every)
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for i in range(args.steps):
@@ -593,7 +624,7 @@ def main():
         syms = ["k_v1_os"]           # the one-shot V1 kernel (k_v1_feistel serves the mapped form)
     achieved = units * BYTES_PER_ID / (per_launch_ms * 1e-3) / 1e9 if per_launch_ms > 0 else 0.0
     out_bytes = out.numel() * out.element_size()
-    traffic = _pmc_traffic(args.workload, syms) if world == 1 else None
+    traffic, traffic_src = _pmc_traffic(args.workload, syms) if world == 1 else (None, None)
     desc = W.CONFIGS[cfg_name][0] + (" (V1 variant)" if args.workload == "c2v1" else "")
     line = {
         "metric": METRIC,
@@ -620,7 +651,7 @@ def main():
                    "epochs_in_flight": npipe},
         "roofline": {"bound": "hbm", "kernel": kname, "symbols": syms, "achieved": achieved,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                     "traffic": traffic, "launch_ms": per_launch_ms,
+                     "traffic": traffic, "traffic_source": traffic_src, "launch_ms": per_launch_ms,
                      "algorithmic_bytes_per_launch": units * BYTES_PER_ID,
                      "write_floor": None if not fill_ms else {
                          "GBps": out_bytes / (fill_ms * 1e-3) / 1e9, "ms": fill_ms,
@@ -629,6 +660,7 @@ def main():
                                 "kernel), HIP events, mean of 20 on this box"}},
         "kernels_ms_per_launch": {k: v[0] / max(1, v[1]) for k, v in prof.items()},
         "timed_launches": k_n,
+        "timing_every": every,
         "coverage_ok": coverage,
         "collective": (dist.get_backend() if distributed else None),
         "process_group_world_size": pg_world,

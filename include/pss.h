@@ -185,15 +185,37 @@ int pss_emit_path(pss_sampler *h, int32_t *path);
  *       seeded MT state); V2 ~28 B per position of num_samples and 2.5 KB per pool2 window --
  *       one decode serves every rank of a call, whatever their number.  A workspace the
  *       device cannot hold makes pss_generate return PSS_EHIP.  After calls for consecutive
- *       epochs of one shape, the MT draws of the next 8 epochs are made ahead on the handle's
- *       own low-priority streams where they are few long streams (shuffle_buffer beyond 4096
- *       with few windows: up to 4 GiB of draw slots; PSS_EXACT_LOOKAHEAD=0 turns it off);
- *       pss_destroy waits for them.
+ *       epochs of one shape, the MT draws of the next epochs (up to 8) are made ahead on the
+ *       handle's own low-priority streams where they are few long streams (shuffle_buffer
+ *       beyond 4096 with few windows), within pss_set_lookahead's bounds (1 GiB of draw slots
+ *       by default); pss_destroy waits for them.
  * Replaces nothing in the reference: its order IS the exact one. */
 #define PSS_ORDER_COUNTER 0
 #define PSS_ORDER_EXACT 1
 int pss_set_order_mode(pss_sampler *h, int32_t mode);
 int pss_order_mode(const pss_sampler *h, int32_t *mode);
+
+/* Bounds of the work a handle does ahead of its calls, and the device memory it holds for it
+ * (extension; results never depend on them):
+ *   exact_depth     -- exact order: epochs whose MT draws are made ahead (-1: by geometry, the
+ *                      default -- up to 8 where a call's draws are few long serial streams, 0
+ *                      where they fill the chip; 0: none; at most 8);
+ *   exact_max_bytes -- the bytes ALL the exact draw slots together may hold, the one a call is
+ *                      reading included (default 1 GiB; 0: none); the depth shrinks to fit;
+ *   v2_depth        -- V2 counter order (pools up to 16384): epochs whose last-occurrence pass
+ *                      is queued ahead on a low-priority stream (-1: 2, the default; 0: the pass
+ *                      runs in line; 1 or 2), each in its own VAL buffer (v2 VAL ring).
+ * Slot memory beyond the bounds is released by later calls once idle (no host wait).  The
+ * lookaheads are best effort: an error while preparing one (e.g. hipMalloc of a slot) turns
+ * the exact lookahead off for the handle and the call still returns PSS_OK; a later
+ * pss_set_lookahead turns it back on.  PSS_EXACT_LOOKAHEAD=0 / PSS_V2_LOOKAHEAD=0 still force
+ * them off process-wide. */
+int pss_set_lookahead(pss_sampler *h, int32_t exact_depth, int64_t exact_max_bytes, int32_t v2_depth);
+/* Device bytes the handle holds now: tables, workspaces, VAL ring, draw slots. */
+int pss_workspace_bytes(const pss_sampler *h, int64_t *bytes);
+/* Counters since create: stats[0] exact draw slots made ahead, [1] exact calls that used one,
+ * [2] V2 passes queued ahead, [3] V2 replays that used one. */
+int pss_lookahead_stats(const pss_sampler *h, int64_t *stats /* [4] */);
 
 /* Self-test of the wave64 DPP scan primitive: out_dev[2i] = 64-bit inclusive wave scan,
  * out_dev[2i+1] = 32-bit one (low words), for n inputs. */

@@ -52,6 +52,9 @@ SIGNATURES = {
     "pss_map_prefix_host": ([_vp, _i64, _vp, _i64, _vp, _vp], ctypes.c_int),
     "pss_generate_mapped": ([_vp, _i32, _i32, _i64, _i64, _vp, _vp, _vp], ctypes.c_int),
     "pss_gather": ([_vp, _vp, _i64, _vp, _vp, _vp, _i64, _vp, _vp], ctypes.c_int),
+    "pss_set_lookahead": ([_vp, _i32, _i64, _i32], ctypes.c_int),
+    "pss_workspace_bytes": ([_vp, _c_i64p], ctypes.c_int),
+    "pss_lookahead_stats": ([_vp, _c_i64p], ctypes.c_int),
 }
 
 _lib = None

@@ -304,9 +304,19 @@ struct pss_sampler {
     };
     struct XPend { bool valid; XKey key; int64_t epoch; };
     XPend xpend[kXSlots] = {};           // the epoch a slot holds (or is being filled with)
-    bool xlast_valid = false;            // key and epoch of the previous exact call
-    XKey xlast_key{};
-    int64_t xlast_epoch = 0;
+    // the last epoch called for each of a few recent call shapes (several rank or position
+    // ranges per epoch each keep their own lookahead)
+    struct XHist { bool valid; XKey key; int64_t epoch; uint64_t stamp; };
+    static constexpr int kXHist = 4;
+    XHist xhist[kXHist] = {};
+    uint64_t xstamp = 0;
+    // lookahead bounds (pss_set_lookahead): exact depth (-1: by geometry), the bytes all the draw
+    // slots together may hold, V2 counter-order passes queued ahead (-1: 2); x_failed: an error
+    // while preparing a slot turned the exact lookahead off for this handle (best effort)
+    int32_t x_depth = -1, v2_depth = -1;
+    int64_t x_cap = (int64_t)1 << 30;
+    bool x_failed = false;
+    int64_t st_x_made = 0, st_x_used = 0, st_v2_queued = 0, st_v2_used = 0;   // pss_lookahead_stats
     hipEvent_t ev_shared = nullptr;
     hipStream_t last_shared = nullptr;
     bool shared_used = false;
@@ -774,7 +784,7 @@ int generate_v2_lookahead(pss_sampler *h, const pss::Geometry &g, int32_t rank_l
     }
     // epochs queued ahead: 2 keeps the wait for a pass off the replay's critical path (one
     // epoch ahead: the replay waits 33 us per step, 491 against 526 G idx/s, round 2)
-    constexpr int depth = 2;
+    const int depth = h->v2_depth < 0 ? 2 : h->v2_depth;   // (pss_set_lookahead; 0 never gets here)
     const pss_sampler::Shape shape{g.N, g.ns, g.B, pos_lo, count, g.R, rank_lo, nr, h->emit_path};
     auto held = [&](int b) {
         for (const auto &p : h->pend) if (p.valid && p.buf == b) return true;
@@ -788,6 +798,7 @@ int generate_v2_lookahead(pss_sampler *h, const pss::Geometry &g, int32_t rank_l
         }
     if (buf >= 0 && small(buf)) buf = -1;   // (cannot happen: queued passes had their size)
     if (buf >= 0) {
+        h->st_v2_used++;
 #if !defined(PSS_DIAG_NO_STREAM_EVENTS) && !defined(PSS_DIAG_NO_STREAM_WAIT)
         // (diagnostics: the replay stream's gaps without its wait and/or record; racy)
         PSS_HIP(hipStreamWaitEvent(s, h->ev_done[buf], 0));
@@ -841,6 +852,7 @@ int generate_v2_lookahead(pss_sampler *h, const pss::Geometry &g, int32_t rank_l
         PSS_HIP(hipEventRecord(h->ev_side, h->side));
         for (auto &p : h->pend)
             if (!p.valid) { p = {true, shape, k0[d], k1[d], nb}; break; }
+        h->st_v2_queued++;
     }
     return PSS_OK;
 }
@@ -872,6 +884,7 @@ int generate_exact(pss_sampler *h, const pss::Geometry &g, int32_t rank_lo, int3
     if (use >= 0) {
         PSS_HIP(hipStreamWaitEvent(s, h->xev_done[use], 0));
         h->xpend[use].valid = false;
+        h->st_x_used++;
     }
     uint32_t *slot = use >= 0 ? h->xslot[use].p : nullptr;
     mk(v1 ? pss::K_V1 : pss::K_V2_EMIT, s);
@@ -883,47 +896,84 @@ int generate_exact(pss_sampler *h, const pss::Geometry &g, int32_t rank_lo, int3
                                      nullptr, slot));
     mk(-1, s);
     if (use >= 0) PSS_HIP(hipEventRecord(h->xev_read[use], s));
-    // (a later call of the same epoch -- another rank range -- draws for itself: a slot is used
-    // once (V2's decode takes K1 as scratch, V1's scan its bucket counts); the coming epochs'
-    // slots stay)
-    const bool same_key = h->xlast_valid && h->xlast_key == key;
-    if (same_key && h->xlast_epoch == e) return PSS_OK;
-    const bool sequential = same_key && h->xlast_epoch == e - 1;
-    h->xlast_valid = true;
-    h->xlast_key = key;
-    h->xlast_epoch = e;
-    const int depth = !exact_lookahead_on() ? 0
-                      : v1 ? pss::v1_exact_lookahead_depth(g, pos_lo, count) : pss::v2_exact_lookahead_depth(g);
-    for (auto &p : h->xpend)   // keep only slots of the coming epochs of this shape
-        if (p.valid && !(sequential && p.key == key && p.epoch > e && p.epoch <= e + depth))
-            p.valid = false;
+    // The lookahead below is best effort: this call's result is already enqueued, and nothing
+    // that fails while preparing the coming epochs' slots fails the call -- the slot
+    // is dropped, the exact lookahead turned off for the handle, PSS_OK returned.
+    // (a later call of the same epoch and shape -- another rank range -- draws for itself: a slot
+    // is used once, V2's decode takes K1 as scratch, V1's scan its bucket counts)
+    int hx = -1;
+    for (int i = 0; i < pss_sampler::kXHist; i++)
+        if (h->xhist[i].valid && h->xhist[i].key == key) hx = i;
+    if (hx >= 0 && h->xhist[hx].epoch == e) return PSS_OK;
+    const bool sequential = hx >= 0 && h->xhist[hx].epoch == e - 1;
+    if (hx < 0) {   // the least recently called shape's entry
+        hx = 0;
+        for (int i = 1; i < pss_sampler::kXHist; i++)
+            if (!h->xhist[i].valid || (h->xhist[hx].valid && h->xhist[i].stamp < h->xhist[hx].stamp)) hx = i;
+    }
+    h->xhist[hx] = {true, key, e, ++h->xstamp};
+    const size_t sbytes = v1 ? pss::v1_exact_slot_bytes(g, pos_lo, count) : pss::v2_exact_slot_bytes(g);
+    const size_t sw = words(sbytes);
+    int depth = (!exact_lookahead_on() || h->x_failed) ? 0
+                : v1 ? pss::v1_exact_lookahead_depth(g, pos_lo, count) : pss::v2_exact_lookahead_depth(g);
+    if (h->x_depth >= 0 && h->x_depth < depth) depth = h->x_depth;
+    // the byte cap counts every slot that holds memory, the one this call's decode reads included
+    const int64_t cap_slots = sbytes ? std::min<int64_t>(NX, h->x_cap / (int64_t)(sw * sizeof(uint32_t))) : 0;
+    if (depth > cap_slots - 1) depth = (int)std::max<int64_t>(0, cap_slots - 1);
+    for (auto &p : h->xpend) {   // keep the slots of the coming epochs of the shapes called lately
+        if (!p.valid) continue;
+        bool keep = false;
+        for (const auto &x : h->xhist)
+            keep |= x.valid && x.key == p.key && p.epoch > x.epoch && p.epoch <= x.epoch + depth;
+        if (!keep) p.valid = false;
+    }
+    // memory of idle slots beyond what the bounds allow goes back (no host wait: slots still
+    // being drawn or read are released by a later call)
+    for (int k = 0; k < NX; k++) {
+        if (!h->xslot[k].p || h->xpend[k].valid || k == use || (k < cap_slots && depth > 0)) continue;
+        if (hipStreamQuery(h->xside[k]) == hipSuccess && hipEventQuery(h->xev_read[k]) == hipSuccess)
+            h->xslot[k].release();
+    }
+    (void)hipGetLastError();   // (a query's hipErrorNotReady)
     if (!sequential || depth <= 0) return PSS_OK;
-    const size_t sw = words(v1 ? pss::v1_exact_slot_bytes(g, pos_lo, count) : pss::v2_exact_slot_bytes(g));
-    for (int d = 1; d <= depth && d < NX; d++) {
-        bool queued = false;
-        for (const auto &p : h->xpend) queued |= p.valid && p.epoch == e + d;
-        if (queued) continue;
-        int k = -1;
-        for (int j = 0; j < NX && k < 0; j++) if (!h->xpend[j].valid && j != use) k = j;
-        if (k < 0) break;
+    auto prepare_slot = [&](int k, int64_t ep) -> hipError_t {
+        hipError_t r;
         if (!h->xside[k]) {
             int least = 0, greatest = 0;
-            PSS_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
-            (void)greatest;
-            PSS_HIP(hipStreamCreateWithPriority(&h->xside[k], hipStreamNonBlocking, least));
-            PSS_HIP(hipEventCreateWithFlags(&h->xev_done[k], PSS_LA_EVENT_FLAGS));
-            PSS_HIP(hipEventCreateWithFlags(&h->xev_read[k], PSS_LA_EVENT_FLAGS));
+            if ((r = hipDeviceGetStreamPriorityRange(&least, &greatest)) != hipSuccess) return r;
+            if ((r = hipStreamCreateWithPriority(&h->xside[k], hipStreamNonBlocking, least)) != hipSuccess) return r;
+            if ((r = hipEventCreateWithFlags(&h->xev_done[k], PSS_LA_EVENT_FLAGS)) != hipSuccess) return r;
+            if ((r = hipEventCreateWithFlags(&h->xev_read[k], PSS_LA_EVENT_FLAGS)) != hipSuccess) return r;
         }
         if (h->xslot[k].n < sw) {   // grows once: after its last draws and its last reader
-            PSS_HIP(hipStreamSynchronize(h->xside[k]));
-            PSS_HIP(hipEventSynchronize(h->xev_read[k]));
-            PSS_HIP(h->xslot[k].ensure(sw));
+            if ((r = hipStreamSynchronize(h->xside[k])) != hipSuccess) return r;
+            if ((r = hipEventSynchronize(h->xev_read[k])) != hipSuccess) return r;
+            if ((r = h->xslot[k].ensure(sw)) != hipSuccess) return r;
         }
-        PSS_HIP(hipStreamWaitEvent(h->xside[k], h->xev_read[k], 0));   // the decode that read it
-        if (v1) PSS_HIP(pss::launch_v1_exact_draws(g, pos_lo, count, e + d, h->xslot[k].p, h->xside[k]));
-        else PSS_HIP(pss::launch_v2_exact_draws(g, e + d, h->xslot[k].p, h->xside[k]));
-        PSS_HIP(hipEventRecord(h->xev_done[k], h->xside[k]));
+        if ((r = hipStreamWaitEvent(h->xside[k], h->xev_read[k], 0)) != hipSuccess) return r;   // its last decode
+        r = v1 ? pss::launch_v1_exact_draws(g, pos_lo, count, ep, h->xslot[k].p, h->xside[k])
+               : pss::launch_v2_exact_draws(g, ep, h->xslot[k].p, h->xside[k]);
+        if (r != hipSuccess) return r;
+        return hipEventRecord(h->xev_done[k], h->xside[k]);
+    };
+    for (int d = 1; d <= depth && d < NX; d++) {
+        bool queued = false;
+        for (const auto &p : h->xpend) queued |= p.valid && p.key == key && p.epoch == e + d;
+        if (queued) continue;
+        int k = -1;
+        for (int j = 0; j < cap_slots && k < 0; j++) if (!h->xpend[j].valid && j != use) k = j;
+        if (k < 0) break;
+        if (prepare_slot(k, e + d) != hipSuccess) {
+            (void)hipGetLastError();
+            h->xpend[k].valid = false;
+            if (h->xside[k]) (void)hipStreamSynchronize(h->xside[k]);
+            h->xslot[k].release();
+            (void)hipGetLastError();
+            h->x_failed = true;
+            return PSS_OK;
+        }
         h->xpend[k] = {true, key, e + d};
+        h->st_x_made++;
     }
     return PSS_OK;
 }
@@ -970,7 +1020,7 @@ int generate_impl(pss_sampler *h, int32_t rank_lo, int32_t rank_hi, int64_t pos_
                           (h->version == 2 ? pss::v2_ranks_by_value(g, nr, h->emit_path) : nr <= pss::kArgRanks);
     // whole V2 streams, ranks by value, the lookahead ring: no shared device state (pss_sampler)
     const bool own_state = h->version == 2 && by_value && !ma && pos_lo == 0 && count >= h->ns && lookahead_on() &&
-                           pss::v2_stage_split(g, nr, h->emit_path);
+                           h->v2_depth != 0 && pss::v2_stage_split(g, nr, h->emit_path);
     std::unique_ptr<SharedUse> su;
     if (!own_state) su.reset(new SharedUse(h, s));
     pss::RankArgs ra;
@@ -995,7 +1045,7 @@ int generate_impl(pss_sampler *h, int32_t rank_lo, int32_t rank_hi, int64_t pos_
     } else if (h->order_mode == PSS_ORDER_EXACT) {
         PSS_HIP(h->d_sort.ensure(words(pss::v2_exact_ws_bytes(g, nr))));
         return generate_exact(h, g, rank_lo, nr, pos_lo, count, out_dev, s, mk);
-    } else if (lookahead_on() && pss::v2_stage_split(g, nr, h->emit_path)) {
+    } else if (lookahead_on() && h->v2_depth != 0 && pss::v2_stage_split(g, nr, h->emit_path)) {
         return generate_v2_lookahead(h, g, rank_lo, nr, pos_lo, count, out_dev, s, mk, ma, rap);
     } else {
         for (auto &p : h->pend) p.valid = false;
@@ -1050,7 +1100,7 @@ int pss_set_order_mode(pss_sampler *h, int32_t mode) {
             h->xpend[k].valid = false;
             h->xslot[k].release();
         }
-        h->xlast_valid = false;
+        for (auto &x : h->xhist) x.valid = false;
     }
     h->order_mode = mode;
     return PSS_OK;
@@ -1308,6 +1358,46 @@ int pss_digest(const int64_t *ids_dev, int64_t n, uint64_t *acc_dev, void *strea
 int pss_digest_range(int64_t lo, int64_t hi, uint64_t *acc_dev, void *stream) {
     if (!acc_dev) return fail(PSS_EINVAL, "acc_dev is NULL");
     PSS_HIP(pss::launch_digest_range(lo, hi, acc_dev, (hipStream_t)stream));
+    return PSS_OK;
+}
+
+int pss_set_lookahead(pss_sampler *h, int32_t exact_depth, int64_t exact_max_bytes, int32_t v2_depth) {
+    if (!h) return fail(PSS_EINVAL, "NULL handle");
+    if (exact_depth < -1 || exact_depth > pss_sampler::kXSlots - 1) return fail(PSS_EINVAL, "exact_depth must be -1 .. 8");
+    if (exact_max_bytes < 0) return fail(PSS_EINVAL, "exact_max_bytes must be >= 0");
+    if (v2_depth < -1 || v2_depth > 2) return fail(PSS_EINVAL, "v2_depth must be -1 .. 2");
+    if (v2_depth != h->v2_depth) {
+        // queued passes were sized and keyed for the previous depth: drop them (their buffers
+        // stay, ordered by their events)
+        for (auto &p : h->pend) p.valid = false;
+        h->last_valid = false;
+    }
+    h->x_depth = exact_depth;
+    h->x_cap = exact_max_bytes;
+    h->v2_depth = v2_depth;
+    h->x_failed = false;
+    return PSS_OK;
+}
+
+int pss_lookahead_stats(const pss_sampler *h, int64_t *stats) {
+    if (!h || !stats) return fail(PSS_EINVAL, "NULL argument");
+    stats[0] = h->st_x_made;
+    stats[1] = h->st_x_used;
+    stats[2] = h->st_v2_queued;
+    stats[3] = h->st_v2_used;
+    return PSS_OK;
+}
+
+int pss_workspace_bytes(const pss_sampler *h, int64_t *bytes) {
+    if (!h || !bytes) return fail(PSS_EINVAL, "NULL argument");
+    int64_t b = 0;
+    auto add = [&](const auto &d) { b += (int64_t)(d.n * sizeof(*d.p)); };
+    add(h->d_lens); add(h->d_ids); add(h->d_ranks); add(h->d_err);
+    add(h->d_val); add(h->d_buf); add(h->d_sort);
+    add(h->d_val2); add(h->d_buf2); add(h->d_val3); add(h->d_buf3);
+    for (const auto &t : h->tab) add(t.blob);
+    for (const auto &x : h->xslot) add(x);
+    *bytes = b;
     return PSS_OK;
 }
 

@@ -228,6 +228,24 @@ class IndexEngine:
         _lib.call("pss_order_mode", self._h, ctypes.byref(v))
         return {0: "counter", 1: "exact"}[v.value]
 
+    def set_lookahead(self, exact_depth=-1, exact_max_bytes=1 << 30, v2_depth=-1):
+        """Bounds of the work done ahead of the calls (pss_set_lookahead): exact-order epochs
+        drawn ahead (-1: by geometry), the bytes all exact draw slots may hold, V2 passes queued
+        ahead (-1: 2, 0: in line).  Results never depend on them."""
+        _lib.call("pss_set_lookahead", self._h, int(exact_depth), int(exact_max_bytes), int(v2_depth))
+
+    def workspace_bytes(self):
+        """Device bytes the handle holds (tables, workspaces, VAL ring, draw slots)."""
+        v = ctypes.c_int64()
+        _lib.call("pss_workspace_bytes", self._h, ctypes.byref(v))
+        return v.value
+
+    def lookahead_stats(self):
+        """{exact_made, exact_used, v2_queued, v2_used} since create."""
+        a = (ctypes.c_int64 * 4)()
+        _lib.call("pss_lookahead_stats", self._h, a)
+        return dict(zip(("exact_made", "exact_used", "v2_queued", "v2_used"), list(a)))
+
     KERNEL_KINDS = ("scan", "v1_window", "v2_lastocc", "v2_emit", "v2_tail", "map",
                     "partition", "digest")
 

@@ -16,8 +16,9 @@ Differences from the reference, all deliberate:
     leaves the current window unshuffled, V1:139; V2's replays every draw, V2:121-122).
   * no per-batch gc.collect() (V1:258, V2:253); eviction collects only with gc_on_evict.
 Extensions (keyword-only): seed, device ("cpu" or a GPU), order, ranks=(lo, hi) -- the block of
-logical ranks this process generates in one launch (one process per GPU owning R / G ranks),
-copy_chunk, gc_on_evict.
+logical ranks this process owns (one process per GPU owning R / G ranks; block_indices()),
+copy_chunk, gc_on_evict, lookahead=(exact_depth, exact_max_bytes, v2_depth) -- bounds of the
+device work and memory the engine spends ahead of the calls (pss_set_lookahead).
 """
 import math
 from collections.abc import Sequence
@@ -82,7 +83,7 @@ class _PartialShuffleSampler(Sampler):
     def __init__(self, dataset, reader, num_replicas=None, rank=None, shuffle=True,
                  shuffle_buffer=None, total_size=None, batch_size=1, file_buffer=10,
                  debug=False, files_len=None, *, seed=0, device=None, copy_chunk=1 << 18,
-                 gc_on_evict=False, order="counter", ranks=None):
+                 gc_on_evict=False, order="counter", ranks=None, lookahead=None):
         if num_replicas is None:                                    # V1:19-26
             if not dist.is_available():
                 raise RuntimeError("Requires distributed package to be available")
@@ -128,12 +129,16 @@ class _PartialShuffleSampler(Sampler):
             raise ValueError("ranks=(lo, hi) must hold rank and lie in [0, num_replicas)")
         self.ranks = (lo, hi)
         self.copy_chunk = int(copy_chunk)
+        # (exact_depth, exact_max_bytes, v2_depth) for pss_set_lookahead; None: the defaults
+        self.lookahead = None if lookahead is None else tuple(lookahead)
         self._engine = None
         self._cache = FileCache(reader, file_buffer, debug, rank, gc_on_evict)
         self._pos = 0
         self._end = 0
-        self._block = None     # [hi - lo, ns] ids of the rank block (device or host tensor)
-        self._dev = None       # (ids, file_pos, offset) of this rank's epoch (None in lazy mode)
+        self._block = None     # [hi - lo, ns] ids of the rank block, generated on first request
+        self._ids = None       # [ns] ids of this rank's epoch, generated on first request
+        self._dev = None       # (file_pos, offset) of this rank's epoch (None in lazy mode)
+        self._iterated = False
         self._host = None      # host copies of (file_pos, offset) or (ids,) + per-chunk events
         self._err = None       # pinned int32: the device error word after this epoch's kernels
         self._scan = None      # lazy-length mode: the epoch's _LazyScan
@@ -141,6 +146,9 @@ class _PartialShuffleSampler(Sampler):
         # every dataset file's length known up front -> device map; else lazy probing in scan
         # order (V1:186-190) with the library's host map over the scanned prefix
         self._lazy = any(p not in self.files_len for p in self.dataset.files)
+        # the fused hand-off (pss_generate_mapped: int32 file position + int32 offset, 8 bytes per
+        # id, no id pass) unless an offset could need 64 bits; else generate + pss_map
+        self._fused = not self._lazy and all(int(self.files_len[p]) < (1 << 31) for p in self.dataset.files)
 
     # ---- engine ---------------------------------------------------------------------------
     def _lengths(self):
@@ -160,13 +168,16 @@ class _PartialShuffleSampler(Sampler):
             self._engine = IndexEngine(self._lengths(), self.ori_total_size, self.num_replicas,
                                        self.shuffle_buffer, self._VERSION, shuffle=self.shuffle,
                                        seed=self.seed, device=self.device, order=self.order)
+            if self.lookahead is not None:
+                self._engine.set_lookahead(*self.lookahead)
         return self._engine
 
     # ---- epoch ----------------------------------------------------------------------------
     def init_iter(self):
-        """One init_iter (V1:100-132 / V2:124-159): the host history, then generation of the
-        rank block's whole epoch, the id -> (file, offset) map of this rank's stream and an
-        asynchronous copy to the host."""
+        """One init_iter (V1:100-132 / V2:124-159): the host history, then this rank's whole
+        epoch as (file position, offset) pairs -- generated and mapped in one pass on the device
+        (pss_generate_mapped, 8 bytes per id) -- and an asynchronous copy of them to the host.
+        The ids themselves (device_indices, block_indices) are generated only when asked for."""
         self.dataset.reset()
         eng = self._get_engine()
         eng.init_iter(self.epoch)
@@ -183,17 +194,23 @@ class _PartialShuffleSampler(Sampler):
         cpu = eng.cpu
         dev = torch.device("cpu") if cpu else torch.device("cuda", self.device)
         stream = None if cpu else torch.cuda.current_stream(dev)
-        lo, hi = self.ranks
-        self._block = eng.generate(lo, hi, stream=stream)
-        ids = self._block[self.rank - lo]
+        self._block = None
+        self._ids = None
+        self._iterated = True
         if self._lazy:
+            # lengths probed in scan order on the host (V1:186-190): ids only
             self._dev = None
             self._scan = _LazyScan(self.files, self.files_len, self.reader)
-            payload = (ids,)
+            payload = (self._rank_ids(stream),)
+        elif self._fused:
+            fpos, off = eng.generate_mapped(self.rank, self.rank + 1, stream=stream)
+            self._dev = (fpos[0], off[0])
+            payload = self._dev
         else:
+            ids = self._rank_ids(stream)
             fpos, off = eng.map(ids, stream=stream)
-            self._dev = (ids, fpos, off)
-            payload = (fpos, off)
+            self._dev = (fpos, off)
+            payload = self._dev
         self._copy_to_host(eng, payload, stream, cpu)
         self._end = ns
         wraps = (self.ori_total_size - self.start_num) < self.num_samples     # V1:79-80
@@ -250,6 +267,10 @@ class _PartialShuffleSampler(Sampler):
         for k in ("sampler_version", "num_replicas", "rank", "shuffle_buffer", "total_size", "order",
                   "shuffle", "num_files"):
             if k not in sd:
+                if k in ("shuffle", "num_files"):
+                    # recorded since round 5 only; a state of an earlier build (the same schedule
+                    # version, checked below) resumes as before, without these two checks
+                    continue
                 raise ValueError("state_dict has no %r: it was taken by another build" % k)
             if sd[k] != mine[k]:
                 raise ValueError("state_dict was taken with %s=%r, this sampler has %r"
@@ -332,16 +353,31 @@ class _PartialShuffleSampler(Sampler):
         self.epoch = epoch
 
     # ---- extensions -----------------------------------------------------------------------
+    def _rank_ids(self, stream=None):
+        """This rank's epoch ids (generated once per epoch, on first request)."""
+        if self._ids is None:
+            if self._block is not None:
+                self._ids = self._block[self.rank - self.ranks[0]]
+            else:
+                eng = self._engine
+                if stream is None and not eng.cpu:
+                    stream = torch.cuda.current_stream(torch.device("cuda", self.device))
+                self._ids = eng.generate(self.rank, self.rank + 1, stream=stream)[0]
+        return self._ids
+
     def device_indices(self):
         """(ids, file_pos, offset) tensors of this rank's current epoch, in stream order (on
         the GPU, or host tensors in CPU mode) -- the hand-off for an on-GPU gather (positions of
-        file_pos index self.files; negative entries are reflected ids, see pss_map).  With
+        file_pos index self.files; negative entries are reflected ids, see pss_map).  file_pos
+        and offset come from the epoch's fused hand-off (int32 both; int64 offsets when a file
+        holds 2^31 samples or more); the ids are generated on the first call of the epoch.  With
         lazily probed lengths only ids exist before the scan: (ids, None, None)."""
-        if self._block is None:
+        if not self._iterated:
             raise RuntimeError("call iter(sampler) first")
+        ids = self._rank_ids()
         if self._dev is None:
-            return (self._block[self.rank - self.ranks[0]], None, None)
-        return self._dev
+            return (ids, None, None)
+        return (ids,) + tuple(self._dev)
 
     def device_batches(self, data, base_rows):
         """This rank's remaining batches of the epoch gathered on the device: yields
@@ -352,7 +388,7 @@ class _PartialShuffleSampler(Sampler):
             raise RuntimeError("device_batches needs iter(sampler) first and every file length "
                                "in files_len")
         eng = self._engine
-        _, fpos, off = self._dev
+        fpos, off = self._dev
         while self._pos < self._end:
             lo, hi = self._pos, min(self._pos + self.batch_size, self._end)
             self._pos = hi
@@ -360,9 +396,15 @@ class _PartialShuffleSampler(Sampler):
             yield eng.gather(data, base_rows, fpos[lo:hi], off[lo:hi]), fpos[lo:hi], off[lo:hi]
 
     def block_indices(self):
-        """[hi - lo, num_samples] ids of every logical rank of the block ranks=(lo, hi)."""
-        if self._block is None:
+        """[hi - lo, num_samples] ids of every logical rank of the block ranks=(lo, hi), in one
+        launch (generated on the first call of the epoch)."""
+        if not self._iterated:
             raise RuntimeError("call iter(sampler) first")
+        if self._block is None:
+            eng = self._engine
+            stream = None if eng.cpu else torch.cuda.current_stream(torch.device("cuda", self.device))
+            lo, hi = self.ranks
+            self._block = eng.generate(lo, hi, stream=stream)
         return self._block
 
     def indices(self):

@@ -25,11 +25,15 @@ def _shape(B, R=3, mult=3.5, pad=2):
     return lens, N, R
 
 
-def _check_epochs(B, version, order, calls_per_epoch=1):
+def _check_epochs(B, version, order, calls_per_epoch=1, lookahead=None):
     """Every epoch of `order` (rank starts from the engine's own epoch history, which depends on
-    the order the epochs are visited in, V2:142-152) against the exact oracle."""
+    the order the epochs are visited in, V2:142-152) against the exact oracle.  Returns the
+    engine's lookahead counters (pss_lookahead_stats) and its peak device bytes."""
     lens, N, R = _shape(B)
     eng = IndexEngine(lens, N, R, B, version, device=0, order="exact")
+    if lookahead is not None:
+        eng.set_lookahead(*lookahead)
+    peak = 0
     ns = eng.num_samples
     for e in order:
         eng.init_iter(e)
@@ -47,7 +51,10 @@ def _check_epochs(B, version, order, calls_per_epoch=1):
             ref = (O.v1_exact_stream(e, int(new[r]), ns, B, N) if version == 1 else
                    O.v2_exact_stream_rs(e, int(old[r]), int(new[r]), ns, B, N))
             assert np.array_equal(got[r], ref), ("epoch", e, "rank", r, "B", B, "version", version)
+        peak = max(peak, eng.workspace_bytes())
+    stats = eng.lookahead_stats()
     eng.close()
+    return stats, peak
 
 
 # V2: B = 4096 chain mode, one wave per pool2 window, and 5000, merge levels (no lookahead for
@@ -55,14 +62,18 @@ def _check_epochs(B, version, order, calls_per_epoch=1):
 # tile, few long windows (the workgroup draws, eight epochs ahead)
 @pytest.mark.parametrize("B", [4096, 5000, 1 << 16])
 def test_v2_consecutive_epochs_with_draws_made_ahead(B):
-    _check_epochs(B, 2, EPOCHS)
+    stats, _ = _check_epochs(B, 2, EPOCHS)
+    if B == 1 << 16:   # the prepared path really ran
+        assert stats["exact_made"] > 0 and stats["exact_used"] >= len(EPOCHS) - 3, stats
 
 
 # V1: B = 4096 windows resolved in LDS (no lookahead); 2^17 windows through HBM (workgroup
 # draws, 8 ahead)
 @pytest.mark.parametrize("B", [4096, 1 << 17])
 def test_v1_consecutive_epochs_with_draws_made_ahead(B):
-    _check_epochs(B, 1, EPOCHS)
+    stats, _ = _check_epochs(B, 1, EPOCHS)
+    if B == 1 << 17:
+        assert stats["exact_made"] > 0 and stats["exact_used"] >= len(EPOCHS) - 3, stats
 
 
 def test_epoch_jumps_drop_the_prepared_draws():
@@ -73,7 +84,37 @@ def test_epoch_jumps_drop_the_prepared_draws():
 
 @pytest.mark.parametrize("version,B", [(1, 1 << 17), (2, 1 << 16)])
 def test_several_calls_per_epoch_keep_the_lookahead_correct(version, B):
-    _check_epochs(B, version, EPOCHS[:6], calls_per_epoch=3)
+    # each call shape (rank 0, rank 1, rank 2's two position ranges) keeps its own history, so the
+    # whole-range shapes still draw ahead (one shared "last call" never did)
+    stats, _ = _check_epochs(B, version, EPOCHS[:6], calls_per_epoch=3)
+    assert stats["exact_used"] > 0, stats
+
+
+@pytest.mark.parametrize("version,B", [(1, 1 << 17), (2, 1 << 16)])
+def test_lookahead_bounds_are_honoured_and_change_nothing(version, B):
+    """pss_set_lookahead: depth 0 makes no slot; a byte cap of two slots keeps the draw slots
+    within it (the peak device bytes of the capped engine exceed the depth-0 engine's by at most
+    the cap); the default draws ahead -- and every epoch equals the exact oracle in all three."""
+    s_off, peak_off = _check_epochs(B, version, EPOCHS[:8], lookahead=(0, 1 << 30, -1))
+    assert s_off["exact_made"] == 0 and s_off["exact_used"] == 0, s_off
+    lens, N, R = _shape(B)
+    probe = IndexEngine(lens, N, R, B, version, device=0, order="exact")
+    probe.set_lookahead(1, 1 << 30, -1)
+    probe.init_iter(0)
+    probe.generate(0, R)
+    b0 = probe.workspace_bytes()
+    probe.init_iter(1)
+    probe.generate(0, R)              # queues one slot (epoch 2): its size
+    slot = probe.workspace_bytes() - b0
+    probe.close()
+    assert slot > 0
+    # a cap of 2.5 slots: at most two slots (the one a decode reads, one drawn ahead)
+    cap = int(2.5 * slot)
+    s_cap, peak_cap = _check_epochs(B, version, EPOCHS[:8], lookahead=(-1, cap, -1))
+    assert s_cap["exact_used"] > 0, s_cap
+    assert peak_cap - peak_off <= cap, (peak_cap, peak_off, cap)
+    s_def, _ = _check_epochs(B, version, EPOCHS[:8])
+    assert s_def["exact_used"] > 0, s_def
 
 
 def test_leaving_the_exact_order_drops_the_slots_and_coming_back_restarts():

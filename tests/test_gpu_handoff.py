@@ -106,3 +106,33 @@ def test_mapped_consecutive_epochs_lookahead_and_tables():
             assert torch.equal(outs[e][1].long().cpu(), o.reshape(R, -1).cpu()), (version, e)
         a.close()
         b.close()
+
+
+@pytest.mark.parametrize("v2_depth", [0, 1, 2])
+def test_v2_lookahead_depths_give_the_same_streams(v2_depth):
+    """pss_set_lookahead's V2 depth (0: the last-occurrence pass in line; 1, 2 epochs queued
+    ahead): ids and the fused hand-off over consecutive epochs equal a default engine's, and the
+    counters show the queued passes used (or none at depth 0)."""
+    rng = np.random.default_rng(9)
+    lengths = rng.integers(3000, 9000, 50)
+    N, R, B = int(lengths.sum()), 3, 4096
+    a = IndexEngine(lengths, N, R, B, 2, seed=2, device=0)
+    b = IndexEngine(lengths, N, R, B, 2, seed=2, device=0)
+    b.set_lookahead(-1, 1 << 30, v2_depth)
+    for e in range(7):
+        a.init_iter(e)
+        b.init_iter(e)
+        assert torch.equal(a.generate(0, R).cpu(), b.generate(0, R).cpu()), (v2_depth, e)
+    for e in range(7, 12):
+        a.init_iter(e)
+        b.init_iter(e)
+        fa, oa = a.generate_mapped(0, R)
+        fb, ob = b.generate_mapped(0, R)
+        assert torch.equal(fa.cpu(), fb.cpu()) and torch.equal(oa.cpu(), ob.cpu()), (v2_depth, e)
+    st = b.lookahead_stats()
+    if v2_depth == 0:
+        assert st["v2_queued"] == 0 and st["v2_used"] == 0, st
+    else:
+        assert st["v2_used"] >= 8, st
+    a.close()
+    b.close()

@@ -363,3 +363,8 @@ def test_state_dict_resume_continues_the_same_stream(device, order):
                                                         **dict(kw, shuffle=False))
             with pytest.raises(ValueError):
                 c.load_state_dict(sd)
+        # a state of a round-4 build (no 'shuffle' / 'num_files', same schedule version) resumes
+        old = {k: v for k, v in sd.items() if k not in ("shuffle", "num_files")}
+        d = mod.DistributedSamplerViaLocallyShuffle(Dataset(files), reader_for(lengths), **kw)
+        d.load_state_dict(old)
+        assert [x[2] for x in batches_of(iter(d))] == tail
