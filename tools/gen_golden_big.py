@@ -30,8 +30,13 @@ Fixtures (tests/golden/big/):
                          C2 ranks 0 and 7 (12.5M ids each, epoch 0); C3 rank 0 and the ranks
                          whose block wraps at N, epochs 0 and 1; C4 rank 0, the wrapping rank
                          and two ranks with every id above 2^31, epoch 0
+  v1_c2_r*, v1_c3_r*, v1_c4_r*   whole V1 rank streams at the same shapes (round 6, VERDICT r05
+                         item 5): C2 ranks 0 and 7 (epoch 0); C3 rank 0 and the ranks whose
+                         block wraps at N, epochs 0 and 1; C4 rank 0, the wrapping rank and a
+                         rank whose every id lies above 2^31, epoch 0 -- per-window sha256 too
 
-Usage:  python tools/gen_golden_big.py [job ... | bench_shapes]   (default: every job, 6 processes)
+Usage:  python tools/gen_golden_big.py [job ... | bench_shapes | bench_shapes_v1]
+        (default: every job, 6 processes)
 """
 import hashlib
 import importlib.util
@@ -303,6 +308,45 @@ def bench_shape_ranks(cfg):
     return sorted(ranks), epochs
 
 
+def _v1_blocks(cfg, epochs):
+    """blocks of each epoch as the reference's V1 sets them (cumulative shuffles, V1:118-121)."""
+    import workloads as W
+    lens, N, R, B, _ = W.shape(cfg)
+    s = sampler(1, lens, R, 0, B, 1)
+    out = {}
+    for e in epochs:
+        s.set_epoch(e)
+        iter(s)
+        out[e] = list(s.blocks)
+    return out, N, R, B
+
+
+def bench_shape_ranks_v1(cfg):
+    """V1 ranks recorded at a true shape: rank 0, the ranks whose block is the last one (it wraps
+    at N when N % R != 0), at C4 also a rank whose whole block lies above 2^31."""
+    if cfg == "c2":
+        return [0, 7], [0]
+    epochs = [0, 1] if cfg == "c3" else [0]
+    blocks, N, R, B = _v1_blocks(cfg, epochs)
+    ranks = {0} | {blocks[e].index(R - 1) for e in epochs}
+    if cfg == "c4":
+        ns = -(-N // R)
+        hi = [r for r in range(R) if blocks[0][r] * ns > 2 ** 31]
+        ranks |= {hi[len(hi) // 2]}
+    return sorted(ranks), epochs
+
+
+def job_bench_shape_v1(cfg, rank):
+    """Whole V1 rank streams at the true C2 / C3 / C4 shape (B = 4096): every `indices` of the
+    reference's __next__ (V1:157-172) over the init_iter history of `epochs`."""
+    import workloads as W
+    lens, N, R, B, _ = W.shape(cfg)
+    _, epochs = bench_shape_ranks_v1(cfg)
+    recs, _ = run_stream(1, lens, R, B, 1 << 16, [rank], epochs, windows=True)
+    write("v1_%s_r%d" % (cfg, rank), {"kind": "stream", "version": 1, "R": R, "B": B, "bs": 1 << 16,
+                                      "config": cfg, **lens_rec(lens), "ranks": recs})
+
+
 def job_bench_shape(cfg, rank):
     """Whole V2 rank streams at the true C2 / C3 / C4 shape (B = 4096), straight from the
     reference's get_index (V2:96-116) over the init_iter history of `epochs`."""
@@ -333,9 +377,22 @@ def bench_shape_jobs():
     return jobs
 
 
+def bench_shape_jobs_v1():
+    jobs = {}
+    for cfg in ("c2", "c3", "c4"):
+        for r in bench_shape_ranks_v1(cfg)[0]:
+            jobs["v1_%s_r%d" % (cfg, r)] = (job_bench_shape_v1, cfg, r)
+    return jobs
+
+
 def run_job(name):
     t = time.time()
-    fn, *args = JOBS[name] if name in JOBS else bench_shape_jobs()[name]
+    if name in JOBS:
+        fn, *args = JOBS[name]
+    elif name.startswith("v1_") and name[3:5] in ("c2", "c3", "c4"):
+        fn, *args = bench_shape_jobs_v1()[name]
+    else:
+        fn, *args = bench_shape_jobs()[name]
     fn(*args)
     return name, time.time() - t
 
@@ -343,6 +400,8 @@ def run_job(name):
 def main(argv):
     if argv == ["bench_shapes"]:
         argv = sorted(bench_shape_jobs())
+    elif argv == ["bench_shapes_v1"]:
+        argv = sorted(bench_shape_jobs_v1())
     todo = argv or list(JOBS) + sorted(bench_shape_jobs())
     # the longest jobs first
     order = sorted(todo, key=lambda n: ("_c2_" not in n, "c5_prefix" not in n, "b65536" not in n, n))
