@@ -233,7 +233,7 @@ struct pss_sampler {
         hipEvent_t ready = nullptr, freed = nullptr, staged = nullptr;
         bool built = false, read = false;
     };
-    size_t tab_prefix_off = 0, tab_bucket_off = 0, tab_bytes = 0;   // blob layout (bytes)
+    size_t tab_prefix_off = 0, tab_bucket_off = 0, tab_scratch_off = 0, tab_bytes = 0;   // blob layout (bytes)
     TabSet tab[2];
     int tab_cur = 0;
     bool tab_dirty = true;        // this epoch's tables not built yet
@@ -373,7 +373,8 @@ int ensure_device(pss_sampler *h) {
     auto a16 = [](size_t b) { return (b + 15) & ~(size_t)15; };
     h->tab_prefix_off = a16(sizeof(int32_t) * (size_t)h->F);
     h->tab_bucket_off = a16(h->tab_prefix_off + sizeof(int64_t) * ((size_t)h->F + 1));
-    h->tab_bytes = a16(h->tab_bucket_off + sizeof(int32_t) * (size_t)h->nb);
+    h->tab_scratch_off = a16(h->tab_bucket_off + sizeof(int32_t) * (size_t)h->nb);
+    h->tab_bytes = a16(h->tab_scratch_off + sizeof(uint64_t) * pss::scan_scratch_words(h->F));
     for (auto &t : h->tab) {
         PSS_HIP(t.blob.ensure(h->tab_bytes / sizeof(uint32_t)));
         char *b = (char *)t.blob.p;
@@ -418,6 +419,7 @@ int prepare(pss_sampler *h, hipStream_t s) {
 // exclusive prefix over files_len (the reference's past_files_samples, V1:126,182-190; prefix[F] =
 // the scanned total) and the bucket index BT[b] = file_of(prefix, F, b << kb) -- the largest f
 // with prefix[f] <= b << kb: the non-empty file holding that id, F - 1 past the total (pss_map.h).
+constexpr int64_t kHostTablesF = 16384;
 void tables_host(const pss_sampler *h, int32_t *order, int64_t *prefix, int32_t *BT) {
     const int64_t F = h->F;
     std::memcpy(order, h->order.data(), sizeof(int32_t) * (size_t)F);
@@ -449,7 +451,12 @@ int prepare_tables(pss_sampler *h, hipStream_t s) {
         pss_sampler::TabSet &t = h->tab[k];
         if (t.built) PSS_HIP(hipEventSynchronize(t.staged));   // the upload that read `stage`
         char *st = (char *)t.stage;
-        tables_host(h, (int32_t *)st, (int64_t *)(st + h->tab_prefix_off), (int32_t *)(st + h->tab_bucket_off));
+        // up to kHostTablesF files the host computes all three tables (O(F + nb), ~20 us at 10K
+        // files, off the GPU); beyond, it stages the order only and the device scans it (at C3's
+        // 100K files the host tables would sit on set_epoch -> first batch: 1.07 against 0.65 ms)
+        const bool host = h->F <= kHostTablesF;
+        if (host) tables_host(h, (int32_t *)st, (int64_t *)(st + h->tab_prefix_off), (int32_t *)(st + h->tab_bucket_off));
+        else std::memcpy(st, h->order.data(), sizeof(int32_t) * (size_t)h->F);
         if (t.read) PSS_HIP(hipStreamWaitEvent(h->tstream, t.freed, 0));
         // Behind the last queued V2 lookahead pass too: that pass starts as the previous replay
         // ends, i.e. as this epoch's predecessor replay is launched, and the upload would otherwise
@@ -458,7 +465,14 @@ int prepare_tables(pss_sampler *h, hipStream_t s) {
         if (h->side && h->last_valid) PSS_HIP(hipStreamWaitEvent(h->tstream, h->ev_side, 0));
         const pss::Marker mk = marker_of(h);
         mk(pss::K_SCAN, h->tstream);
-        PSS_HIP(pss::launch_upload(t.stage, t.blob.p, h->tab_bytes, h->tstream));
+        if (host) {
+            PSS_HIP(pss::launch_upload(t.stage, t.blob.p, h->tab_scratch_off, h->tstream));   // order | prefix | index
+        } else {
+            PSS_HIP(pss::launch_upload(t.stage, t.blob.p, sizeof(int32_t) * (size_t)h->F, h->tstream));
+            PSS_HIP(pss::launch_scan_prefix(h->d_lens.p, t.order, h->F, t.prefix,
+                                            (uint64_t *)((char *)t.blob.p + h->tab_scratch_off), h->tstream));
+            PSS_HIP(pss::launch_bucket_index(t.prefix, h->F, h->kb, h->nb, t.bucket, h->tstream));
+        }
         mk(-1, h->tstream);
         PSS_HIP(hipEventRecord(t.staged, h->tstream));
         PSS_HIP(hipEventRecord(t.ready, h->tstream));

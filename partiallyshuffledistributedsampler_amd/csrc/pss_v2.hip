@@ -523,21 +523,19 @@ __global__ __launch_bounds__(64) void k_v2_emit_x(Geometry g, V2Plan pl,
         if (tile == 0) {
             pair_consts();
             for (uint32_t s = lane; s < P1; s += 64) buf[s] = to_slot(s);
-        } else if ((P1 & 255u) == 0) {
-            // rounds of up to 16 x 64 quads; P1 % 256 == 0 makes every 64-quad row whole (the
-            // rows past P1 / 4 -- P1 not a multiple of 4096 -- are skipped: they would read the
-            // next tile's table and write past this one's in LDS)
+        } else if ((P1 & 4095u) == 0) {
+            // rounds of 16 x 64 quads, every load of a round in flight at once (P1 % 4096 == 0:
+            // whole rounds -- round 5 took this path for P1 % 1024 == 0 and, at P1 = 1024 / 2048
+            // / 3072 / 5120 ..., read the next tile's table and wrote past this one in LDS; those
+            // pools now take the loop below)
             const uint4 *p4 = (const uint4 *)prev;
-            const uint32_t nq = P1 / 4;
-            for (uint32_t q0 = 0; q0 < nq; q0 += 1024) {
+            for (uint32_t q0 = 0; q0 < P1 / 4; q0 += 1024) {
                 uint4 v[16];
 #pragma unroll
-                for (int u = 0; u < 16; u++)
-                    if (q0 + 64u * u < nq) v[u] = p4[q0 + 64u * u + lane];
+                for (int u = 0; u < 16; u++) v[u] = p4[q0 + 64u * u + lane];
                 if (q0 == 0) pair_consts();
 #pragma unroll
                 for (int u = 0; u < 16; u++) {
-                    if (q0 + 64u * u >= nq) continue;
                     const uint32_t q = q0 + 64u * u + lane;
                     uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
 #pragma unroll
