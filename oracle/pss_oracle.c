@@ -537,12 +537,13 @@ static inline int64_t v2_vid_to_id(int64_t v, int64_t old_start, int64_t new_sta
 }
 
 /* Pools beyond LDS (P1 > 16384): grouped draws.  G = ceil(P1 / 4096) groups of consecutive
- * slots, q = P1 / G each plus one for the first P1 mod G; step t belongs to burst t / 16 and
- * that burst to group (t / 16) mod G; u = the step's index inside its group's own stream.
+ * slots, q = P1 / G each plus one for the first P1 mod G; step t belongs to burst t / 32 and
+ * that burst to group (t / 32) mod G (bursts of 16 up to schedule 3); u = the step's index inside its group's own stream.
  * The step draws uniformly inside its group: power-of-two groups pair sub-steps u and u + 64
  * (u mod 128 < 64) on one hash of the lower one's step (high / low half-word), other sizes
  * hash every step. */
 #define ORC_LDS_SLOT_MAX 16384
+#define ORC_BURST 32u
 typedef struct { uint32_t G, q, r; } orc_groups;
 static orc_groups orc_groups_of(uint32_t P1) {
     orc_groups gr; gr.G = (P1 + 4095u) / 4096u; gr.q = P1 / gr.G; gr.r = P1 % gr.G; return gr;
@@ -550,13 +551,13 @@ static orc_groups orc_groups_of(uint32_t P1) {
 static uint32_t orc_gbase(orc_groups gr, uint32_t g) { return g * gr.q + (g < gr.r ? g : gr.r); }
 static uint32_t orc_gsize(orc_groups gr, uint32_t g) { return gr.q + (g < gr.r ? 1u : 0u); }
 static uint64_t orc_gstep(orc_groups gr, uint32_t g, uint64_t u) {
-    return ((u / 16u) * gr.G + g) * 16u + u % 16u;
+    return ((u / ORC_BURST) * gr.G + g) * ORC_BURST + u % ORC_BURST;
 }
 static inline uint32_t v2_slot_grouped(const uint32_t sk[4], int64_t t, uint32_t P1) {
     orc_groups gr = orc_groups_of(P1);
-    uint32_t g = (uint32_t)(((uint64_t)t / 16u) % gr.G);
+    uint32_t g = (uint32_t)(((uint64_t)t / ORC_BURST) % gr.G);
     uint32_t size = orc_gsize(gr, g);
-    uint64_t u = ((uint64_t)t / 16u / gr.G) * 16u + (uint64_t)t % 16u;
+    uint64_t u = ((uint64_t)t / ORC_BURST / gr.G) * ORC_BURST + (uint64_t)t % ORC_BURST;
     uint32_t local;
     if ((size & (size - 1u)) == 0u) {
         int b = 0; while ((1u << b) < size) b++;
@@ -571,14 +572,14 @@ static inline uint32_t v2_slot_grouped(const uint32_t sk[4], int64_t t, uint32_t
     return orc_gbase(gr, g) + local;
 }
 
-/* Grouped tail: rounds in which every group emits its next (up to) 16 elements, groups in
+/* Grouped tail: rounds in which every group emits its next (up to) ORC_BURST elements, groups in
  * order; group g's e-th element is slot orc_feistel(e, S_g, keys8(g, rank, DOM_V2_TAIL)) of
  * the group. */
 static uint32_t orc_gtail_pos(orc_groups gr, uint32_t g, uint32_t e) {
-    uint32_t full = gr.q / 16u;
-    if (e < full * 16u) return (e / 16u) * 16u * gr.G + g * 16u + e % 16u;
-    uint32_t c = gr.q % 16u;
-    return full * 16u * gr.G + g * c + (g < gr.r ? g : gr.r) + (e - full * 16u);
+    uint32_t full = gr.q / ORC_BURST;
+    if (e < full * ORC_BURST) return (e / ORC_BURST) * ORC_BURST * gr.G + g * ORC_BURST + e % ORC_BURST;
+    uint32_t c = gr.q % ORC_BURST;
+    return full * ORC_BURST * gr.G + g * c + (g < gr.r ? g : gr.r) + (e - full * ORC_BURST);
 }
 
 /* V2 under the counter schedule (slot-replacement form of V2:96-116):

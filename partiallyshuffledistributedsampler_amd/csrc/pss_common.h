@@ -202,7 +202,7 @@ PSS_HD uint32_t slot_draw(uint32_t t, uint32_t s0, uint32_t s1, uint32_t P1) {
 // ------------------------------------------------------------------------------------------
 // V2 pools beyond LDS (P1 > kLdsSlotMax): grouped slot draws.  The P1 slots
 // are split into G = ceil(P1 / 4096) groups of q or q + 1 consecutive slots (the first r = P1
-// mod G groups have q + 1); steps come in bursts of 16, burst b = t / 16 belongs to group
+// mod G groups have q + 1); steps come in bursts of 32, burst b = t / 32 belongs to group
 // b mod G and draws uniformly inside it.  Every group is then an independent slot machine of
 // <= 4096 slots fed by every G-th burst: one LDS-resident wave per (rank, group) replays it.
 // An element still leaves pool1 with probability ~1/P1 per step (1/S_g per step of its group,
@@ -213,7 +213,11 @@ constexpr uint32_t kLdsSlotMax = 16384;   // largest V2 pool replayed as one LDS
 #define PSS_GROUP_SLOTS 4096
 #endif
 constexpr uint32_t kGroupSlots = PSS_GROUP_SLOTS;    // slots per group (at most)
-constexpr uint32_t kBurst = 16;           // consecutive steps of one group
+#ifndef PSS_BURST
+#define PSS_BURST 32
+#endif
+constexpr uint32_t kBurst = PSS_BURST;    // consecutive steps of one group (16 up to schedule 3;
+                                          // other values: timing builds only)
 
 struct Groups {
     uint32_t G, q, r;   // groups; q = P1 / G, r = P1 mod G (groups g < r have q + 1 slots)
@@ -230,7 +234,7 @@ PSS_HD uint32_t group_base(const Groups &gr, uint32_t g) { return g * gr.q + (g 
 PSS_HD uint32_t group_size(const Groups &gr, uint32_t g) { return gr.q + (g < gr.r ? 1u : 0u); }
 PSS_HD uint32_t group_of_step(const Groups &gr, uint32_t t) { return (t / kBurst) % gr.G; }
 
-// global step of sub-step u of group g's stream (its bursts are b = m * G + g, m = u / 16)
+// global step of sub-step u of group g's stream (its bursts are b = m * G + g, m = u / kBurst)
 PSS_HD uint64_t group_step(const Groups &gr, uint32_t g, uint64_t u) {
     return ((u / kBurst) * gr.G + g) * kBurst + (u % kBurst);
 }
@@ -263,10 +267,10 @@ PSS_HD uint32_t slot_draw_grouped(uint32_t t, uint32_t s0, uint32_t s1, const Gr
 }
 
 // Tail of a grouped pool: the final pool is drained in rounds; in each round every group emits
-// its next (up to) 16 elements, groups in order.  Group g emits its S_g elements in the order
+// its next (up to) kBurst elements, groups in order.  Group g emits its S_g elements in the order
 // of its own Feistel bijection of [0, S_g) (keys round_keys8(g, rank, DOM_V2_TAIL)).  Position
-// (after T) of group g's e-th element: full rounds while every group still has 16 left, then
-// one last round of the q mod 16 (+1 for g < r) leftovers.
+// (after T) of group g's e-th element: full rounds while every group still has kBurst left,
+// then one last round of the q mod kBurst (+1 for g < r) leftovers.
 PSS_HD uint32_t group_tail_pos(const Groups &gr, uint32_t g, uint32_t e) {
     const uint32_t full = gr.q / kBurst;
     if (e < full * kBurst) return (e / kBurst) * kBurst * gr.G + g * kBurst + e % kBurst;

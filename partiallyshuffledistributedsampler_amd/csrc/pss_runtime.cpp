@@ -586,8 +586,9 @@ const char *pss_last_error(void) { return g_err.c_str(); }
 int pss_abi_version(void) { return 2; }
 
 // counter-order schedule: 1 round 1, 2 round 2 (grouped pools, 24-bit slot hash), 3 round 3
-// (16-bit round function at 10-bit halves, 8 fmix32 rounds at halves <= 5 bits)
-int pss_schedule_version(void) { return 3; }
+// (16-bit round function at 10-bit halves, 8 fmix32 rounds at halves <= 5 bits), 4 round 6
+// (grouped pools beyond 16384 slots: bursts of 32 steps per group instead of 16)
+int pss_schedule_version(void) { return 4; }
 
 int pss_create(const int64_t *files_len, int64_t num_files, int64_t total_size,
                int32_t num_replicas, int64_t shuffle_buffer, int32_t version, int32_t shuffle,

@@ -1,8 +1,8 @@
 // pss_v2grp.hip -- V2 pools beyond LDS (P1 > kLdsSlotMax): the grouped slot machine
 // (reference semantics V2:96-116 with pool1 = min(B, ns) > 16384).
 //
-// The P1 slots are split into G = ceil(P1 / 4096) groups; burst t / 16 of the step stream draws
-// inside group (t / 16) mod G (pss_common.h slot_draw_grouped).  Each (rank, group) is an
+// The P1 slots are split into G = ceil(P1 / 4096) groups; burst t / 32 of the step stream draws
+// inside group (t / 32) mod G (pss_common.h slot_draw_grouped).  Each (rank, group) is an
 // independent slot machine of <= 4096 slots, so one 64-lane wave replays it with its table in
 // 16 KB of LDS -- the same one-exchange-per-step replay as the small-pool kernel, with no HBM
 // slot table and no chunk bucketing.  At C5 (B = 2^20, 8 ranks) that is 2048 streams of ~45K
@@ -387,8 +387,12 @@ __global__ __launch_bounds__(64) void k_g_emit(Geometry g, GPlan pl, const RankD
     // lane l serves sub-steps u0 + 64 j + l: step t_first + c_lane + j * 64 G, where t_first is
     // the iteration's first step (wave-uniform, advanced by 256 G per iteration without
     // division, together with its pool2 window wa and offset pa)
-    const uint32_t c_lane = ((uint32_t)lane >> 4) * 16u * G + ((uint32_t)lane & 15u);
-    const uint32_t span = 240u * G + 15u;            // last step of an iteration - first step
+    // (bursts of kBurst = 32 steps: lanes 0-31 and 32-63 each serve one burst's consecutive
+    // steps, so a store instruction writes two runs of 32 positions -- 256 B of ids, 128 B of
+    // file positions -- where bursts of 16 wrote four runs of 64 / 128 B)
+    static_assert(kBurst == 16 || kBurst == 32 || kBurst == 64, "a store covers 64 / kBurst bursts");
+    const uint32_t c_lane = ((uint32_t)lane / kBurst) * kBurst * G + ((uint32_t)lane % kBurst);
+    const uint32_t span = (256u - kBurst) * G + kBurst - 1u;   // last step of an iteration - first step
     uint32_t t_first = (uint32_t)group_step(pl.gr, grp, ulo);
     uint32_t wa = 1 + t_first / B;
     uint32_t pa = t_first - (wa - 1) * B;
@@ -516,17 +520,34 @@ __global__ __launch_bounds__(64) void k_g_emit(Geometry g, GPlan pl, const RankD
                         if constexpr (ORDERED) v[j] = atomicExch(&buf[k[j]], in);
                         else v[j] = xchg_unordered(buf, mark, k[j], in, true, lane);
                     }
+                    if constexpr (MAPPED) {
+                        // the four (file, offset) pairs: the uniform-length map branch-free for
+                        // every lane, the general map only when some lane needs it (one ballot
+                        // per iteration, not an exec-masked branch per value)
+                        int32_t f[4], of[4];
+                        uint64_t idv[4];
+                        bool slow = !ma.uni;
+#pragma unroll
+                        for (int j = 0; j < 4; j++) {
+                            idv[j] = (uint64_t)ids.from_slot(v[j]);
+                            const uint32_t q = udiv_apply((uint32_t)idv[j], ma.um, ma.ul);
+                            f[j] = (int32_t)q;
+                            of[j] = (int32_t)((uint32_t)idv[j] - q * ma.uL);
+                            slow |= idv[j] >= (uint64_t)ma.T;
+                        }
+                        if (__builtin_amdgcn_ballot_w64(slow) != 0u) {
+#pragma unroll
+                            for (int j = 0; j < 4; j++) map_id_fast(ma, (int64_t)idv[j], f[j], of[j]);
+                        }
+#pragma unroll
+                        for (int j = 0; j < 4; j++) {
+                            __builtin_amdgcn_raw_buffer_store_b32((uint32_t)f[j], orsrc, (int)voff, (int)(4u * (uint32_t)j * G64), 0);
+                            __builtin_amdgcn_raw_buffer_store_b32((uint32_t)of[j], frsrc, (int)voff, (int)(4u * (uint32_t)j * G64), 0);
+                        }
+                    }
 #pragma unroll
                     for (int j = 0; j < 4; j++) {
                         if constexpr (MAPPED) {
-                            int32_t f, of;
-#ifdef PSS_DIAG_MAP_NONE   // (timing-only build: the stores of the mapped form without the map)
-                            of = (int32_t)ids.from_slot(v[j]); f = of; of >>= 3;
-#else
-                            map_id_fast(ma, ids.from_slot(v[j]), f, of);
-#endif
-                            __builtin_amdgcn_raw_buffer_store_b32((uint32_t)f, orsrc, (int)voff, (int)(4u * (uint32_t)j * G64), 0);
-                            __builtin_amdgcn_raw_buffer_store_b32((uint32_t)of, frsrc, (int)voff, (int)(4u * (uint32_t)j * G64), 0);
                         } else {
                             const uint64_t id = (uint64_t)ids.from_slot(v[j]);
                             const g_u32x2 d = {(uint32_t)id, (uint32_t)(id >> 32)};

@@ -65,13 +65,16 @@ def test_v1_window_permutation_is_uniform(B, ns):
     assert abs(d.mean()) < 0.02 * B
 
 
+BURST = 32   # steps per burst of a grouped pool (schedule 4; 16 up to schedule 3)
+
+
 def _burst_stats(streams, B, T):
-    """Per aligned run of 16 consecutive outputs among the replacement steps (a grouped pool's
-    burst: one 4096-slot group draws all 16): the spread (max - min) / B, and |diff| / B of
-    consecutive outputs inside the run."""
+    """Per aligned run of BURST consecutive outputs among the replacement steps (a grouped
+    pool's burst: one 4096-slot group draws all of them): the spread (max - min) / B, and
+    |diff| / B of consecutive outputs inside the run."""
     spread, step = [], []
     for s in streams:
-        x = np.asarray(s[:T // 16 * 16], dtype=np.float64).reshape(-1, 16)
+        x = np.asarray(s[:T // BURST * BURST], dtype=np.float64).reshape(-1, BURST)
         spread.append((x.max(1) - x.min(1)) / B)
         step.append(np.abs(np.diff(x, axis=1)).ravel() / B)
     return np.concatenate(spread), np.concatenate(step)
@@ -80,12 +83,12 @@ def _burst_stats(streams, B, T):
 @pytest.mark.parametrize("B,ns,nex,atol", [(20000, 160000, 3, 0.02), (65536, 4 * 65536, 4, 0.01),
                                            (1 << 20, 3 << 20, 2, 0.015)])
 def test_v2_grouped_pool_law_matches_reference(B, ns, nex, atol):
-    """Pools beyond LDS (P1 > 16384) draw in bursts of 16 inside G = ceil(P1 / 4096) slot
+    """Pools beyond LDS (P1 > 16384) draw in bursts of 32 inside G = ceil(P1 / 4096) slot
     groups.  Against the reference's own single-pool draws (V2:101-106, the
     exact restatement -- rank-select form for the big pools), on the grouped geometries: B =
     20000 (G = 5, groups of 4000: multiply-shift draws), 65536 (G = 16) and C5's 2^20 (G = 256,
     groups of 4096 with paired draws): displacement quantiles, spread, consecutive-output
-    statistics, and within-burst statistics (the spread of each run of 16 outputs and the gaps
+    statistics, and within-burst statistics (the spread of each run of 32 outputs and the gaps
     inside it) against the same positions of the reference's stream."""
     N = 10**12
     T = ns - B
