@@ -190,6 +190,55 @@ struct DevBuf {
     void release() { if (p) (void)hipFree(p); p = nullptr; n = 0; }
 };
 
+// Pinned host staging that k_upload reads (the per-epoch tables, a large rank table), as a ring
+// of kN buffers: the host rewrites a buffer only after the upload that read it, and with a ring
+// that upload is kN - 1 calls back.  (Round 6: with two table sets the host waited on the
+// previous set's upload event every epoch -- hipEventSynchronize returned only as the NEXT
+// upload on the table stream finished, ~110 us into the running replay -- so the host, not the
+// GPU, paced the C2 mapped loop: 31 us between replays against 10 for the id loop.)
+struct StageRing {
+    static constexpr int kN = 4;
+    void *buf[kN] = {};
+    hipEvent_t ev[kN] = {};
+    bool used[kN] = {};
+    int next = 0;
+    hipError_t init(size_t bytes) {
+        for (int i = 0; i < kN; i++) {
+            hipError_t e = hipHostMalloc(&buf[i], bytes ? bytes : 16);
+            if (e == hipSuccess) e = hipEventCreateWithFlags(&ev[i], hipEventDisableTiming);
+            if (e != hipSuccess) return e;
+        }
+        return hipSuccess;
+    }
+    hipError_t acquire(void **p, int *slot) {
+        const int i = next;
+        next = (next + 1) % kN;
+        if (used[i]) {
+            const hipError_t e = hipEventSynchronize(ev[i]);
+            if (e != hipSuccess) return e;
+        }
+        *p = buf[i];
+        *slot = i;
+        return hipSuccess;
+    }
+    hipError_t release(int slot, hipStream_t s) {   // after the upload that reads it
+        used[slot] = true;
+        return hipEventRecord(ev[slot], s);
+    }
+    void destroy() {
+        for (int i = 0; i < kN; i++) {
+            if (ev[i]) {
+                if (used[i]) (void)hipEventSynchronize(ev[i]);
+                (void)hipEventDestroy(ev[i]);
+            }
+            if (buf[i]) (void)hipHostFree(buf[i]);
+            ev[i] = nullptr;
+            buf[i] = nullptr;
+            used[i] = false;
+        }
+    }
+};
+
 }  // namespace
 
 struct pss_sampler {
@@ -224,15 +273,15 @@ struct pss_sampler {
     // epoch e - 1's kernels; the caller's stream only waits for it.  (Round 6: the device scan in
     // line cost ~30 us per epoch before a mapped replay at C2; the same three scan kernels on the
     // side stream delayed the replay's one round of waves by ~22 us, a one-workgroup scan by ~40.)
-    // A set is rewritten after its last reader (`freed`); its staging after its upload (`staged`).
+    // A set is rewritten after its last reader (`freed`); the staging comes from a ring (below).
     struct TabSet {
         DevBuf<uint32_t> blob;        // order | prefix | bucket index, 16-byte aligned parts
         int32_t *order = nullptr, *bucket = nullptr;
         int64_t *prefix = nullptr;
-        uint32_t *stage = nullptr;    // pinned, the same layout
-        hipEvent_t ready = nullptr, freed = nullptr, staged = nullptr;
+        hipEvent_t ready = nullptr, freed = nullptr;
         bool built = false, read = false;
     };
+    StageRing tab_stage;          // pinned staging of the table blobs (the blob's layout)
     size_t tab_prefix_off = 0, tab_bucket_off = 0, tab_scratch_off = 0, tab_bytes = 0;   // blob layout (bytes)
     TabSet tab[2];
     int tab_cur = 0;
@@ -245,9 +294,7 @@ struct pss_sampler {
     DevBuf<int32_t> d_err;
     DevBuf<pss::RankDesc> d_ranks;
     DevBuf<uint32_t> d_val, d_buf, d_sort;
-    pss::RankDesc *h_stage_ranks = nullptr;   // pinned staging of the rank table (R > kArgRanksMax)
-    hipEvent_t upload_done = nullptr;
-    bool upload_pending = false;
+    StageRing rank_stage;         // pinned staging of the rank table (R > kArgRanksMax)
     // optional per-kernel timing (pss_profile): events recorded around every launch
     bool profiling = false;
     int32_t profile_mode = 0;     // 1 every launch, n >= 2 every (n-1)-th generation launch
@@ -267,6 +314,7 @@ struct pss_sampler {
     DevBuf<uint32_t> d_val2, d_buf2, d_val3, d_buf3;
     hipStream_t side = nullptr;
     hipEvent_t ev_side = nullptr;       // the last pass launched on the side stream
+    hipEvent_t ev_pre = nullptr;        // the replay stream reached this call's replay (PSS_LA_PRE)
     hipEvent_t ev_read[kLaBufs] = {};   // per buffer: the last replay that read it
     hipEvent_t ev_done[kLaBufs] = {};   // per buffer: the last lookahead pass that wrote it
     struct Shape {
@@ -381,16 +429,14 @@ int ensure_device(pss_sampler *h) {
         t.order = (int32_t *)b;
         t.prefix = (int64_t *)(b + h->tab_prefix_off);
         t.bucket = (int32_t *)(b + h->tab_bucket_off);
-        PSS_HIP(hipHostMalloc((void **)&t.stage, h->tab_bytes));
         PSS_HIP(hipEventCreateWithFlags(&t.ready, hipEventDisableTiming));
         PSS_HIP(hipEventCreateWithFlags(&t.freed, hipEventDisableTiming));
-        PSS_HIP(hipEventCreateWithFlags(&t.staged, hipEventDisableTiming));
     }
+    PSS_HIP(h->tab_stage.init(h->tab_bytes));
     PSS_HIP(hipStreamCreateWithFlags(&h->tstream, hipStreamNonBlocking));
     PSS_HIP(hipMemset(h->d_err.p, 0, sizeof(int32_t)));
     if (h->F) PSS_HIP(hipMemcpy(h->d_lens.p, h->files_len.data(), sizeof(int64_t) * h->F, hipMemcpyHostToDevice));
-    PSS_HIP(hipHostMalloc((void **)&h->h_stage_ranks, sizeof(pss::RankDesc) * h->R));
-    PSS_HIP(hipEventCreateWithFlags(&h->upload_done, hipEventDisableTiming));
+    PSS_HIP(h->rank_stage.init(sizeof(pss::RankDesc) * h->R));
     h->dev_init = true;
     return PSS_OK;
 }
@@ -405,11 +451,12 @@ int prepare(pss_sampler *h, hipStream_t s) {
     if (h->R <= pss::kArgRanksMax) {
         PSS_HIP(pss::launch_put_ranks(h->ranks.data(), h->R, h->d_ranks.p, s));
     } else {
-        if (h->upload_pending) PSS_HIP(hipEventSynchronize(h->upload_done));
-        std::memcpy(h->h_stage_ranks, h->ranks.data(), sizeof(pss::RankDesc) * h->R);
-        PSS_HIP(pss::launch_upload(h->h_stage_ranks, h->d_ranks.p, sizeof(pss::RankDesc) * h->R, s));
-        PSS_HIP(hipEventRecord(h->upload_done, s));
-        h->upload_pending = true;
+        int slot = 0;
+        void *st = nullptr;
+        PSS_HIP(h->rank_stage.acquire(&st, &slot));
+        std::memcpy(st, h->ranks.data(), sizeof(pss::RankDesc) * h->R);
+        PSS_HIP(pss::launch_upload(st, h->d_ranks.p, sizeof(pss::RankDesc) * h->R, s));
+        PSS_HIP(h->rank_stage.release(slot, s));
     }
     h->dirty = false;
     return PSS_OK;
@@ -449,8 +496,10 @@ int prepare_tables(pss_sampler *h, hipStream_t s) {
     if (h->tab_dirty) {
         const int k = h->tab_cur ^ 1;
         pss_sampler::TabSet &t = h->tab[k];
-        if (t.built) PSS_HIP(hipEventSynchronize(t.staged));   // the upload that read `stage`
-        char *st = (char *)t.stage;
+        int slot = 0;
+        void *stv = nullptr;
+        PSS_HIP(h->tab_stage.acquire(&stv, &slot));
+        char *st = (char *)stv;
         // up to kHostTablesF files the host computes all three tables (O(F + nb), ~20 us at 10K
         // files, off the GPU); beyond, it stages the order only and the device scans it (at C3's
         // 100K files the host tables would sit on set_epoch -> first batch: 1.07 against 0.65 ms)
@@ -466,15 +515,15 @@ int prepare_tables(pss_sampler *h, hipStream_t s) {
         const pss::Marker mk = marker_of(h);
         mk(pss::K_SCAN, h->tstream);
         if (host) {
-            PSS_HIP(pss::launch_upload(t.stage, t.blob.p, h->tab_scratch_off, h->tstream));   // order | prefix | index
+            PSS_HIP(pss::launch_upload(st, t.blob.p, h->tab_scratch_off, h->tstream));   // order | prefix | index
         } else {
-            PSS_HIP(pss::launch_upload(t.stage, t.blob.p, sizeof(int32_t) * (size_t)h->F, h->tstream));
+            PSS_HIP(pss::launch_upload(st, t.blob.p, sizeof(int32_t) * (size_t)h->F, h->tstream));
             PSS_HIP(pss::launch_scan_prefix(h->d_lens.p, t.order, h->F, t.prefix,
                                             (uint64_t *)((char *)t.blob.p + h->tab_scratch_off), h->tstream));
             PSS_HIP(pss::launch_bucket_index(t.prefix, h->F, h->kb, h->nb, t.bucket, h->tstream));
         }
         mk(-1, h->tstream);
-        PSS_HIP(hipEventRecord(t.staged, h->tstream));
+        PSS_HIP(h->tab_stage.release(slot, h->tstream));
         PSS_HIP(hipEventRecord(t.ready, h->tstream));
         t.built = true;
         h->tab_cur = k;
@@ -640,7 +689,7 @@ int pss_destroy(pss_sampler *h) {
     if (!h) return PSS_OK;
     if (h->dev_init && !h->cpu) {
         DeviceGuard dg(h->device);
-        if (h->upload_pending) (void)hipEventSynchronize(h->upload_done);
+        h->rank_stage.destroy();
         if (h->side) (void)hipStreamSynchronize(h->side);   // a lookahead still writing VAL
         if (h->tstream) (void)hipStreamSynchronize(h->tstream);
         (void)hipDeviceSynchronize();   // readers of the tables on the callers' streams
@@ -649,16 +698,15 @@ int pss_destroy(pss_sampler *h) {
         h->d_ids.release();
         for (auto &t : h->tab) {
             t.blob.release();
-            if (t.stage) (void)hipHostFree(t.stage);
-            for (hipEvent_t e : {t.ready, t.freed, t.staged}) if (e) (void)hipEventDestroy(e);
+            for (hipEvent_t e : {t.ready, t.freed}) if (e) (void)hipEventDestroy(e);
         }
         if (h->tstream) (void)hipStreamDestroy(h->tstream);
         if (h->ids_free) (void)hipEventDestroy(h->ids_free);
-        if (h->h_stage_ranks) (void)hipHostFree(h->h_stage_ranks);
-        if (h->upload_done) (void)hipEventDestroy(h->upload_done);
+        h->tab_stage.destroy();
         for (hipEvent_t e : h->ev_pool) (void)hipEventDestroy(e);
         if (h->side) (void)hipStreamDestroy(h->side);
         if (h->ev_side) (void)hipEventDestroy(h->ev_side);
+        if (h->ev_pre) (void)hipEventDestroy(h->ev_pre);
         for (hipEvent_t e : h->ev_read) if (e) (void)hipEventDestroy(e);
         for (hipEvent_t e : h->ev_done) if (e) (void)hipEventDestroy(e);
         if (h->ev_shared) (void)hipEventDestroy(h->ev_shared);
@@ -796,6 +844,7 @@ int generate_v2_lookahead(pss_sampler *h, const pss::Geometry &g, int32_t rank_l
         for (hipEvent_t &e : h->ev_read) PSS_HIP(hipEventCreateWithFlags(&e, PSS_LA_EVENT_FLAGS));
         for (hipEvent_t &e : h->ev_done) PSS_HIP(hipEventCreateWithFlags(&e, PSS_LA_EVENT_FLAGS));
         PSS_HIP(hipEventCreateWithFlags(&h->ev_side, PSS_LA_EVENT_FLAGS));
+        PSS_HIP(hipEventCreateWithFlags(&h->ev_pre, PSS_LA_EVENT_FLAGS));
     }
     // epochs queued ahead: 2 keeps the wait for a pass off the replay's critical path (one
     // epoch ahead: the replay waits 33 us per step, 491 against 526 G idx/s, round 2)
@@ -817,6 +866,9 @@ int generate_v2_lookahead(pss_sampler *h, const pss::Geometry &g, int32_t rank_l
 #if !defined(PSS_DIAG_NO_STREAM_EVENTS) && !defined(PSS_DIAG_NO_STREAM_WAIT)
         // (diagnostics: the replay stream's gaps without its wait and/or record; racy)
         PSS_HIP(hipStreamWaitEvent(s, h->ev_done[buf], 0));
+#endif
+#ifdef PSS_LA_PRE
+        PSS_HIP(hipEventRecord(h->ev_pre, s));
 #endif
         PSS_HIP(pss::launch_v2(g, h->d_ranks.p, rank_lo, nr, pos_lo, count, out_dev, V[buf]->p,
                                bwords ? W[buf]->p : nullptr, nullptr, h->d_err.p, s, mk, h->emit_path,
@@ -860,6 +912,9 @@ int generate_v2_lookahead(pss_sampler *h, const pss::Geometry &g, int32_t rank_l
         pss::Geometry gn = g;
         gn.key0 = k0[d]; gn.key1 = k1[d];
         PSS_HIP(hipStreamWaitEvent(h->side, h->ev_read[nb], 0));   // the replay that read it
+#ifdef PSS_LA_PRE
+        if (buf >= 0) PSS_HIP(hipStreamWaitEvent(h->side, h->ev_pre, 0));
+#endif
         PSS_HIP(pss::launch_v2(gn, h->d_ranks.p, rank_lo, nr, pos_lo, count, out_dev, V[nb]->p,
                                bwords ? W[nb]->p : nullptr, nullptr, h->d_err.p, h->side, mk, h->emit_path,
                                pss::V2_STAGE_PRE));

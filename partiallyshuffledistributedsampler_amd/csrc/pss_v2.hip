@@ -739,11 +739,23 @@ __global__ __launch_bounds__(64) void k_v2_emit_x(Geometry g, V2Plan pl,
                         // test per super-batch, not an exec-masked branch per value)
                         const uint32_t any = (v[0] | v[1] | v[2] | v[3]) & kPairEsc;
                         if (__builtin_amdgcn_ballot_w64(any != 0u) == 0u) {
+#ifdef PSS_DIAG_PAIR_INTERLEAVED   // (timing-only build: one 8-byte (file, offset) store per pair into fpos)
+                            if (true) {
 #pragma unroll
-                            for (int j = 0; j < 4; j++) {
-                                const int64_t e = ebase + tlx + 64u * j + lane;
-                                ma.fpos[e] = (int32_t)(v[j] >> pob);
-                                ma.off[e] = (int32_t)(v[j] & omask);
+                                for (int j = 0; j < 4; j++) {
+                                    const int64_t e = ebase + tlx + 64u * j + lane;
+                                    ((int2 *)ma.fpos)[e] = make_int2((int)(v[j] >> pob), (int)(v[j] & omask));
+                                }
+#else
+                            if (false) {
+#endif
+                            } else {
+#pragma unroll
+                                for (int j = 0; j < 4; j++) {
+                                    const int64_t e = ebase + tlx + 64u * j + lane;
+                                    ma.fpos[e] = (int32_t)(v[j] >> pob);
+                                    ma.off[e] = (int32_t)(v[j] & omask);
+                                }
                             }
                         } else {
 #pragma unroll

@@ -572,6 +572,13 @@ __global__ __launch_bounds__(64) void k_g_emit(Geometry g, GPlan pl, const RankD
             else go(std::false_type{});
             t_first += n * G256;
             pa += n * G256;
+            // MAPPED: a run that ends on its window's end hands the next run the next window;
+            // otherwise each window begins with one iteration of the general path below (11 of
+            // C5's 175 iterations per stream).  Round 6, same box, 3 rounds each: the mapped
+            // replay 0.248 -> 0.225 ms; the id replay LOST with it (558 -> 542 G idx/s, its
+            // VALU 52.9M -> 46.9M per launch) and with a store drain in its place (541), so the
+            // id replay keeps the general iteration (profiles/r06/ab_grouped_wrap/)
+            if (MAPPED && pa >= B) { pa -= B; wa++; }
             u0 += 256u * n;
             continue;
         }

@@ -411,6 +411,11 @@ class _PartialShuffleSampler(Sampler):
         """Host numpy copy of this rank's epoch ids in stream order (debug / parity)."""
         return self.device_indices()[0].cpu().numpy()
 
+    def workspace_bytes(self):
+        """Device bytes the sampler's engine holds (pss_workspace_bytes: workspaces, the V2
+        lookahead's VAL ring, exact-order draw slots, epoch tables); 0 before the first epoch."""
+        return 0 if self._engine is None else self._engine.workspace_bytes()
+
 
 def ctypes_ptr(t):
     import ctypes

@@ -368,3 +368,25 @@ def test_state_dict_resume_continues_the_same_stream(device, order):
         d = mod.DistributedSamplerViaLocallyShuffle(Dataset(files), reader_for(lengths), **kw)
         d.load_state_dict(old)
         assert [x[2] for x in batches_of(iter(d))] == tail
+
+
+@pytest.mark.parametrize("device", DEVICES)
+def test_lookahead_bounds_and_workspace_bytes(device):
+    """lookahead=(exact_depth, exact_max_bytes, v2_depth) reaches pss_set_lookahead and changes
+    nothing in the stream; workspace_bytes() reports the engine's device bytes (0 in CPU mode
+    and before the first epoch)."""
+    fx = load(scenario_names("v2")[0])
+    s_ref = make(fx, 0, device)
+    s_cap = make(fx, 0, device, lookahead=(0, 1 << 20, 0))
+    assert s_cap.workspace_bytes() == 0
+    for e in range(3):
+        streams = []
+        for s in (s_ref, s_cap):
+            s.set_epoch(e)
+            batches_of(iter(s))
+            streams.append(s.indices())
+        assert np.array_equal(streams[0], streams[1])
+    if device == "cpu":
+        assert s_cap.workspace_bytes() == 0
+    else:
+        assert s_cap.workspace_bytes() > 0

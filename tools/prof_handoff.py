@@ -28,8 +28,10 @@ def run(name, epochs, events):
     lengths, N, R, B, _ = W.shape(cfg)
     eng = IndexEngine(lengths, N, R, B, ver, seed=0, device=0)
     ns = eng.num_samples
-    fpos = torch.empty((R, ns), dtype=torch.int32, device="cuda")
-    off = torch.empty((R, ns), dtype=torch.int32, device="cuda")
+    # one allocation, the offsets right after the file positions (a PSS_DIAG_PAIR_INTERLEAVED
+    # build writes its interleaved (file, offset) pairs over both)
+    both = torch.empty((2, R, ns), dtype=torch.int32, device="cuda")
+    fpos, off = both[0], both[1]
     for e in range(WARM):
         eng.init_iter(e)
         eng.generate_mapped(0, R, out=(fpos, off))
