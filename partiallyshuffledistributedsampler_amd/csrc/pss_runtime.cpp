@@ -314,7 +314,7 @@ struct pss_sampler {
     DevBuf<uint32_t> d_val2, d_buf2, d_val3, d_buf3;
     hipStream_t side = nullptr;
     hipEvent_t ev_side = nullptr;       // the last pass launched on the side stream
-    hipEvent_t ev_pre = nullptr;        // the replay stream reached this call's replay (PSS_LA_PRE)
+    hipEvent_t ev_pre = nullptr;        // the replay stream reached this call's mapped replay
     hipEvent_t ev_read[kLaBufs] = {};   // per buffer: the last replay that read it
     hipEvent_t ev_done[kLaBufs] = {};   // per buffer: the last lookahead pass that wrote it
     struct Shape {
@@ -855,6 +855,7 @@ int generate_v2_lookahead(pss_sampler *h, const pss::Geometry &g, int32_t rank_l
         return false;
     };
     int buf = -1;
+    bool pre = false;
     for (auto &p : h->pend)
         if (p.valid && p.shape == shape && p.key0 == g.key0 && p.key1 == g.key1) {
             buf = p.buf;
@@ -867,9 +868,13 @@ int generate_v2_lookahead(pss_sampler *h, const pss::Geometry &g, int32_t rank_l
         // (diagnostics: the replay stream's gaps without its wait and/or record; racy)
         PSS_HIP(hipStreamWaitEvent(s, h->ev_done[buf], 0));
 #endif
-#ifdef PSS_LA_PRE
-        PSS_HIP(hipEventRecord(h->ev_pre, s));
-#endif
+        // mapped: this call's passes wait until the replay stream reaches its replay.  The
+        // mapped replay also waits for the epoch's tables (another stream), and the next pass,
+        // released by the previous replay's end, would otherwise take the CUs first: the one
+        // round of replay waves then starts ~25 us late (C2 mapped hand-off 0.260 -> 0.247 ms,
+        // same box; the id replay, ahead of its pass already, loses ~2 % with the extra record)
+        pre = ma != nullptr;
+        if (pre) PSS_HIP(hipEventRecord(h->ev_pre, s));
         PSS_HIP(pss::launch_v2(g, h->d_ranks.p, rank_lo, nr, pos_lo, count, out_dev, V[buf]->p,
                                bwords ? W[buf]->p : nullptr, nullptr, h->d_err.p, s, mk, h->emit_path,
                                pss::V2_STAGE_EMIT, ma, ra));
@@ -912,9 +917,7 @@ int generate_v2_lookahead(pss_sampler *h, const pss::Geometry &g, int32_t rank_l
         pss::Geometry gn = g;
         gn.key0 = k0[d]; gn.key1 = k1[d];
         PSS_HIP(hipStreamWaitEvent(h->side, h->ev_read[nb], 0));   // the replay that read it
-#ifdef PSS_LA_PRE
-        if (buf >= 0) PSS_HIP(hipStreamWaitEvent(h->side, h->ev_pre, 0));
-#endif
+        if (pre) PSS_HIP(hipStreamWaitEvent(h->side, h->ev_pre, 0));
         PSS_HIP(pss::launch_v2(gn, h->d_ranks.p, rank_lo, nr, pos_lo, count, out_dev, V[nb]->p,
                                bwords ? W[nb]->p : nullptr, nullptr, h->d_err.p, h->side, mk, h->emit_path,
                                pss::V2_STAGE_PRE));
