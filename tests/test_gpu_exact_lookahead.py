@@ -143,3 +143,30 @@ def test_leaving_the_exact_order_drops_the_slots_and_coming_back_restarts():
     for e in (4, 5, 6):          # 4: own draws (the slots went), 5 queued by 4 ... 6 from a slot
         check(e)
     eng.close()
+
+
+@pytest.mark.parametrize("B", [1000, 4096])
+def test_v2_exact_odd_num_samples_several_ranks(B):
+    """an odd num_samples puts the chain-mode decode's virtual indices (VV, after
+    the odd-length per-position arrays) at an address that is not 16-byte aligned; the fan-out's
+    16-byte loads must then take their scalar form.  R = 3, ns odd, with and without draw slots,
+    against the exact oracle."""
+    R = 3
+    ns = 2 * B + 2 * (B // 3) + 1                     # odd
+    N = ns * R - 1
+    F = 37
+    lens = np.full(F, N // F, dtype=np.int64)
+    lens[-1] += N - lens.sum()
+    for depth in (0, -1):
+        eng = IndexEngine(lens, N, R, B, 2, device=0, order="exact")
+        eng.set_lookahead(depth, 1 << 30, -1)
+        assert eng.num_samples == ns and ns % 2 == 1
+        for e in range(4):
+            eng.init_iter(e)
+            got = eng.generate(0, R).cpu().numpy()
+            eng.check()
+            old, new = eng.rank_starts()
+            for r in range(R):
+                ref = O.v2_exact_stream_rs(e, int(old[r]), int(new[r]), ns, B, N)
+                assert np.array_equal(got[r], ref), ("epoch", e, "rank", r, "depth", depth)
+        eng.close()
