@@ -582,40 +582,71 @@ __device__ __forceinline__ void v2x_put(const V2xFin &f, const V2xGeo &x, uint32
 // ids of nout ranks from the virtual-index stream VV (position t at VV[t]): v < min(2B, ns) came
 // from the old start, the rest from the new one (V2:135-148), wrapped at N (V2:113-114); each
 // rank's row written coalesced.
-// One-shot: 4 consecutive positions per thread (a 16-byte VV load, two 16-byte stores per rank
-// when the rank rows are 16-byte aligned -- the store shape of torch's fill_).
+// One-shot: 4 consecutive positions per thread, `per_row` ranks per workgroup row (blockIdx.y),
+// 16-byte stores -- the store shape of torch's fill_.  A rank row whose first element sits at an
+// odd element index (an odd `count`: every other row) is written in the 16-byte-aligned pairs
+// (t0 + 1, t0 + 2), (t0 + 3, t0 + 4), the row's first element alone.  (Round 6: the 16-byte path
+// used to need an even count for all rows; C3's 976,563 positions per rank sent all 1024 rows
+// of its exact-order fan-out down the 8-byte path with the rank loop in every thread: 14.8 ms
+// for the 8 GB.)
+// Ranks per workgroup row: 8 for a call of few ranks (one 16-byte VV load serves 8 rows), 1 for
+// many (round 6, same box: exact C3's 1024 ranks 2.31 / 2.17 / 2.07 ms per epoch at 8 / 2 / 1
+// per row, C2's 8 ranks 0.805 / 0.836 / 0.816 ms; profiles/r06/ab_fanout/).
+constexpr int32_t kFanoutRanksFew = 8, kFanoutManyRanks = 64;
 __global__ __launch_bounds__(256) void k_v2x_fanout(Geometry g, const RankDesc *__restrict__ ranks, int32_t rank_lo,
-                                                    int32_t nout, const uint32_t *__restrict__ VV, int64_t pos_lo,
-                                                    int64_t count, int64_t *__restrict__ out, MapArgs ma) {
+                                                    int32_t nout, int32_t per_row, const uint32_t *__restrict__ VV,
+                                                    int64_t pos_lo, int64_t count, int64_t *__restrict__ out, MapArgs ma) {
     const int64_t twoB = 2 * g.B < g.ns ? 2 * g.B : g.ns;
     const int64_t pos_hi = pos_lo + count < g.ns ? pos_lo + count : g.ns;
     const int64_t t0 = pos_lo + ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
     if (t0 >= pos_hi) return;
-    // (the 16-byte VV load needs VV + t0 itself 16-byte aligned, not only t0 % 4 == 0: VV follows
-    // the workspace's other arrays)
-    const bool vec = !ma.fpos && t0 + 4 <= pos_hi && (((uintptr_t)(VV + t0)) & 15u) == 0 &&
-                     ((count | pos_lo) & 1) == 0 && (((uintptr_t)out) & 15u) == 0;
-    if (vec) {
-        const uint4 w = *(const uint4 *)(VV + t0);
-        const int64_t v[4] = {w.x, w.y, w.z, w.w};
-        for (int32_t r = 0; r < nout; r++) {
-            const RankDesc rd = ranks[rank_lo + r];
-            int64_t id[4];
-#pragma unroll
-            for (int k = 0; k < 4; k++) id[k] = wrap_id((v[k] < twoB ? rd.old_start : rd.new_start) + v[k], g.N);
-            longlong2 *o = (longlong2 *)(out + (int64_t)r * count + (t0 - pos_lo));
-            o[0] = make_longlong2(id[0], id[1]);
-            o[1] = make_longlong2(id[2], id[3]);
+    const int32_t r_lo = (int32_t)blockIdx.y * per_row;
+    const int32_t r_hi = nout - r_lo < per_row ? nout : r_lo + per_row;
+    if (ma.fpos) {   // (file, offset) pairs: element by element
+        for (int64_t t = t0; t < t0 + 4 && t < pos_hi; t++) {
+            const int64_t v = VV[t];
+            const bool old_side = v < twoB;
+            for (int32_t r = r_lo; r < r_hi; r++) {
+                const RankDesc rd = ranks[rank_lo + r];
+                put_id_or_pair(out, ma, (int64_t)r * count + (t - pos_lo),
+                               wrap_id((old_side ? rd.old_start : rd.new_start) + v, g.N));
+            }
         }
         return;
     }
-    for (int64_t t = t0; t < t0 + 4 && t < pos_hi; t++) {
-        const int64_t v = VV[t];
-        const bool old_side = v < twoB;
-        for (int32_t r = 0; r < nout; r++) {
-            const RankDesc rd = ranks[rank_lo + r];
-            put_id_or_pair(out, ma, (int64_t)r * count + (t - pos_lo),
-                           wrap_id((old_side ? rd.old_start : rd.new_start) + v, g.N));
+    // the values at t0 .. t0 + 4 (t0 + 4: the odd rows' second pair); the 16-byte VV load needs
+    // VV + t0 itself 16-byte aligned (VV follows the workspace's other arrays)
+    const bool full = t0 + 4 <= pos_hi;
+    uint32_t v[5];
+    if (full && (((uintptr_t)(VV + t0)) & 15u) == 0) {
+        const uint4 w = *(const uint4 *)(VV + t0);
+        v[0] = w.x; v[1] = w.y; v[2] = w.z; v[3] = w.w;
+    } else {
+#pragma unroll
+        for (int k = 0; k < 4; k++) v[k] = t0 + k < pos_hi ? VV[t0 + k] : 0u;
+    }
+    v[4] = t0 + 4 < pos_hi ? VV[t0 + 4] : 0u;
+    const bool out16 = (((uintptr_t)out) & 15u) == 0;
+    for (int32_t r = r_lo; r < r_hi; r++) {
+        const RankDesc rd = ranks[rank_lo + r];
+        int64_t id[5];
+#pragma unroll
+        for (int k = 0; k < 5; k++) id[k] = wrap_id(((int64_t)v[k] < twoB ? rd.old_start : rd.new_start) + (int64_t)v[k], g.N);
+        int64_t *row = out + (int64_t)r * count - pos_lo;   // position t at row[t]
+        const bool even = ((((int64_t)r * count) & 1) == 0);   // row[t0] 16-byte aligned (t0 - pos_lo even)
+        if (out16 && even && full) {
+            *(longlong2 *)(row + t0) = make_longlong2(id[0], id[1]);
+            *(longlong2 *)(row + t0 + 2) = make_longlong2(id[2], id[3]);
+        } else if (out16 && !even) {
+            if (t0 == pos_lo) row[t0] = id[0];
+            if (t0 + 2 < pos_hi) *(longlong2 *)(row + t0 + 1) = make_longlong2(id[1], id[2]);
+            else if (t0 + 1 < pos_hi) row[t0 + 1] = id[1];
+            if (t0 + 4 < pos_hi) *(longlong2 *)(row + t0 + 3) = make_longlong2(id[3], id[4]);
+            else if (t0 + 3 < pos_hi) row[t0 + 3] = id[3];
+        } else {
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+                if (t0 + k < pos_hi) row[t0 + k] = id[k];
         }
     }
 }
@@ -900,9 +931,11 @@ static void v2x_launch_fanout(const Geometry &g, const RankDesc *ranks, int32_t 
                               const MapArgs &ma, hipStream_t s) {
     const int64_t n = pos_hi_of(g, pos_lo, count) - pos_lo;
     const uint32_t blocks = (uint32_t)v2x_cdiv(n, 1024);   // (n < 2^31: v2_exact_supported)
-    if (blocks)
-        hipLaunchKernelGGL(k_v2x_fanout, dim3(blocks), dim3(256), 0, s, g, ranks, rank_lo, nout, VV, pos_lo, count,
-                           out, ma);
+    const int32_t per_row = nout > kFanoutManyRanks ? 1 : kFanoutRanksFew;
+    const uint32_t rows = (uint32_t)v2x_cdiv(nout, per_row);
+    if (blocks && rows)
+        hipLaunchKernelGGL(k_v2x_fanout, dim3(blocks, rows), dim3(256), 0, s, g, ranks, rank_lo, nout, per_row, VV,
+                           pos_lo, count, out, ma);
 }
 
 static V2xGeo v2x_geo(const Geometry &g) {

@@ -1,6 +1,7 @@
-"""Exact order at C3 (100K files, 1B samples, R = 1024, B = 4096): all 1024 ranks per call, a few
-consecutive epochs after two warm-up epochs -- run under rocprofv3 --kernel-trace to see where an
-exact C3 epoch goes.   usage: python tools/prof_exact_c3.py [--epochs 4]"""
+"""Exact order at C3 (100K files, 1B samples, R = 1024, B = 4096; --cfg c2: C2's 8 ranks): all
+ranks per call, a few consecutive epochs after two warm-up epochs -- run under rocprofv3
+--kernel-trace to see where an exact epoch goes.
+usage: python tools/prof_exact_c3.py [--epochs 4] [--cfg c3]"""
 import argparse
 import json
 import os
@@ -17,9 +18,11 @@ from partiallyshuffledistributedsampler_amd.engine import IndexEngine  # noqa: E
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--epochs", type=int, default=4)
+    ap.add_argument("--cfg", default="c3")
+    ap.add_argument("--version", type=int, default=2)
     a = ap.parse_args()
-    lengths, N, R, B, _ = W.shape("c3")
-    eng = IndexEngine(lengths, N, R, B, 2, seed=0, device=0, order="exact")
+    lengths, N, R, B, _ = W.shape(a.cfg)
+    eng = IndexEngine(lengths, N, R, B, a.version, seed=0, device=0, order="exact")
     ns = eng.num_samples
     out = torch.empty((R, ns), dtype=torch.int64, device="cuda")
     for e in range(2):
@@ -34,7 +37,7 @@ def main():
     ms = (time.perf_counter() - t0) / a.epochs * 1e3
     eng.check()
     eng.close()
-    print(json.dumps({"exact_c3_ms_per_epoch": ms, "ids": R * ns}), flush=True)
+    print(json.dumps({"cfg": a.cfg, "version": a.version, "exact_ms_per_epoch": ms, "ids": R * ns}), flush=True)
 
 
 if __name__ == "__main__":
