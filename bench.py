@@ -10,7 +10,8 @@ process per GPU) GPU g owns logical ranks [8g, 8g+8) of an 8N-rank sampler over 
 (count, coverage digest) over RCCL and rank 0 checks exact coverage.
 Other workloads (--workload): c2v1 (V1 on C2's files), c5 (B = 2^20 pools beyond LDS, weak),
 c3 (1B samples / 100K files / R = 1024 sharded over the N GPUs: strong scaling, the total work
-of BASELINE configs[2] is fixed).
+of BASELINE configs[2] is fixed), c4 (configs[3]: Zipf file sizes, 2.59B samples, R = 4096,
+strong).
 
 Prints ONE JSON line (rank 0).  `value` is the whole-job throughput (all GPUs' ids / the
 slowest rank's time), `per_gpu` = value / N is the metric's per-GPU figure.  Also reported:
@@ -48,6 +49,7 @@ WORKLOADS = {
     "c2v1": ("c2", "weak"),
     "c5": ("c5", "weak"),
     "c3": ("c3", "strong"),
+    "c4": ("c4", "strong"),
 }
 
 
