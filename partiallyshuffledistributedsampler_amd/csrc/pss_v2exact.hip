@@ -36,7 +36,14 @@
 //
 // tests/test_gpu_parity.py checks the streams against oracle/pss_oracle.c's exact V2 (pinned
 // by the reference's recorded streams).
+#include <algorithm>
+#include <cmath>
 #include <cstdlib>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <tuple>
+#include <vector>
 
 #include "pss_mt.h"
 
@@ -97,6 +104,8 @@ __device__ __forceinline__ void v2x_tail_block(const V2xGeo &x, int64_t epoch, u
         wave_lds_order();
     }
 }
+
+#include "pss_v2split.h"
 
 // ---- seeding: the windows' MT states (k_mt_seed_streams' blocks), the tail draws alongside ----
 // Both are latency-bound chains on few waves (C2: 191 seeding waves, 64 tail waves), so they share
@@ -1072,6 +1081,57 @@ static void v2x_draws(const V2xGeo &x, int64_t epoch, uint32_t *slot, hipStream_
     }
 }
 
+// The draws of a call that brings no slot, for long windows (pss_v2split.h): the windows' words
+// generated one wave each beside the tail draws, then the segments' pieces, the walk and the
+// emission spread over the chip, phase by phase.  Its scratch is the decode's arrays (free until
+// the tiles run); false (the workgroup form runs instead) when the geometry or the scratch does not
+// suit it.  PSS_V2X_SPLIT=0 / 1 forces the workgroup form / this one (where the scratch fits).
+static bool v2x_draws_split(const V2xGeo &x, int64_t epoch, uint32_t *slot, uint32_t *scratch,
+                            size_t scratch_words, hipStream_t s) {
+    static const int env = [] {
+        const char *e = getenv("PSS_V2X_SPLIT");
+        return e ? atoi(e) : -1;
+    }();
+    if (env == 0 || !x.S) return false;
+    if (env != 1 && !v2x_draws_wg((uint64_t)x.S, x.B)) return false;
+    const uint32_t Wl = x.T - (x.S - 1u) * x.B;
+    const SpPlanHost *hl = sp_plan_get(Wl, x.P);
+    const SpPlanHost *hb = x.S > 1 ? sp_plan_get(x.B, x.P) : hl;
+    if (!hl || !hb) return false;
+    // worth it where most of a full window's words fall in phases
+    if (env != 1 && (double)hb->qend < 0.5 * hb->words) return false;
+    V2xSp a{};
+    a.pl[0] = sp_plan_dev(*hb);
+    a.pl[1] = sp_plan_dev(*hl);
+    a.S = x.S; a.B = x.B; a.P = x.P;
+    a.kb1 = 32u - (uint32_t)__builtin_clz(x.P);
+    const size_t nseg = std::max(hb->seg.size(), hl->seg.size());
+    a.nsegmax = (uint32_t)nseg;
+    const size_t nwp = ((size_t)std::max(hb->nt, hl->nt) * kMtN + 3u) & ~(size_t)3u;
+    a.nwp = (uint32_t)nwp;
+    const size_t w_words = (size_t)x.S * nwp, w_rec = (size_t)x.S * nseg * kSpRec * 2u;
+    const size_t w_ss = (size_t)x.S * nseg * 2u, w_anc = (size_t)x.S * (kSpPh + 1) * 4u;
+    if (w_words + w_rec + w_ss + w_anc > scratch_words || nwp >= ((size_t)1 << 32)) return false;
+    a.words = scratch;
+    a.rec = reinterpret_cast<uint2 *>(scratch + w_words);
+    a.ss = reinterpret_cast<uint2 *>(scratch + w_words + w_rec);
+    a.anc = scratch + w_words + w_rec + w_ss;
+    a.K1 = slot;
+    a.K2 = slot + x.ns;
+    const uint32_t tail_blocks = (x.P + 63u) / 64u;
+    hipLaunchKernelGGL(k_v2x_sp_gen, dim3(x.S + tail_blocks), dim3(64), 0, s, a, x, epoch);
+    const uint32_t nph = std::max(std::max(hb->nph, 1u), std::max(hl->nph, 1u));
+    for (uint32_t p = 0; p < nph; p++) {
+        uint32_t segs = 0;
+        for (const SpPlanHost *h : {hb, hl})
+            if (p < h->nph) segs = std::max(segs, h->ph[p + 1] - h->ph[p]);
+        if (segs) hipLaunchKernelGGL(k_v2x_sp_lvl1, dim3((2u * segs + 3u) / 4u, x.S), dim3(256), 0, s, a, p);
+        hipLaunchKernelGGL(k_v2x_sp_walk, dim3(x.S), dim3(64), 0, s, a, p);
+    }
+    if (nseg) hipLaunchKernelGGL(k_v2x_sp_emit, dim3((uint32_t)((nseg + 3u) / 4u), x.S), dim3(256), 0, s, a);
+    return true;
+}
+
 // epochs drawn ahead: the few long windows of the workgroup form keep ~S CUs busy for
 // milliseconds, so several epochs' draws run side by side (8: C5 V2 exact 10.9 -> 3.4 ms per
 // epoch); the one-wave form already fills the chip, and drawn ahead beside the decode it slowed
@@ -1125,8 +1185,10 @@ static hipError_t v2x_pass(const Geometry &g, const V2xGeo &x, const RankDesc *r
     // chain layout:        V (answers) | Q2 | survivors | chunk maps | chunk starts, then the slot
     const bool chain = v2x_chain(x);
     if (!slot) {
-        slot = ws + v2x_rest_words(x);
-        v2x_draws(x, epoch, slot, s);
+        const size_t rest = v2x_rest_words(x);
+        slot = ws + rest;
+        // the decode's arrays are free until the tiles run: the split draws' scratch
+        if (!v2x_draws_split(x, epoch, slot, ws, rest, s)) v2x_draws(x, epoch, slot, s);
     }
     uint32_t *K1 = slot, *K2 = slot + x.ns;
     uint32_t *V = ws;

@@ -1,0 +1,560 @@
+// pss_v2split.h -- the draws of V2's long pool2 windows spread over the chip (order mode
+// PSS_ORDER_EXACT; included by pss_v2exact.hip, which defines V2xGeo and v2x_tail_block).
+//
+// A window's draws (V2:101-106: k1 = _randbelow(P) and k2 = _randbelow(W - j) alternating) come
+// from ONE freshly seeded MT19937 stream, and which word serves which draw depends on every
+// rejection before it.  mt_draws_pair_wg (pss_mt.h) resolves a window on one CU: ~9.6 ms per
+// 2^20-step window (C5), of which the word generation is a small part and the per-block work of
+// the summaries / combine / emission the rest.  Here the generation stays serial (one wave per
+// window, raw words to HBM) and the rest is split:
+//
+//   plan     (host, per window length) the window's words cut into SEGMENTS; for each, the
+//            interval its start's k2 index can lie in -- the expected count at its word offset
+//            +- K standard deviations of the renewal count, measured from the phase's ANCHOR
+//            (below) -- and a length that keeps the expected number of verdicts that differ over
+//            that interval at about PSS_SPLIT_TARGET.
+//   level 1  (one wave per segment and start role, the whole chip) the segment's transfer as a
+//            function of its start index j over the interval: evaluated exactly at the low end of
+//            a piece (pair_eval), it holds unchanged up to the largest shift of j under which no
+//            k2 verdict changes (an accepted k2 word r at bound n stays accepted while n - d > r,
+//            and no bound crosses a power of two) -- the rest of the piece is evaluated again.  So
+//            a segment's transfer is a short list of pieces [a_p, a_{p+1}) -> (role, j + c_p).
+//   walk     (one wave per window) the segments in order from the exact start: one lookup per
+//            segment (a ballot over its pieces); a segment whose start falls outside its interval
+//            or whose pieces overflowed is run exactly.  The walk ends at the phase's last segment,
+//            which anchors the next phase's intervals (they stay narrow where the bound k2 is small).
+//            After the last phase the walk runs the rest of the window exactly, emitting -- past the
+//            generated words from the stream's saved state.
+//   emit     (one wave per segment) every segment again from its now known start, emitting draws.
+// The pieces are exact, so the draws are the reference's whatever the intervals: a bad estimate
+// only costs an exact run in the walk.
+#pragma once
+// (included inside namespace pss)
+
+namespace {
+constexpr int kSpPh = 4;        // phases (re-anchored intervals) before the exact remainder
+constexpr int kSpPieces = 14;   // pieces kept per (segment, start role)
+constexpr int kSpRec = 32;      // uint2 per segment record: pieces of role 0 | role 1, (lo, hi),
+                                // (count role 0, count role 1), (q, L)
+constexpr int kSpRecLoHi = 28, kSpRecCnt = 29, kSpRecQL = 30;
+constexpr uint32_t kSpOver = 0xFFFFFFFFu;
+#ifndef PSS_SPLIT_K
+#define PSS_SPLIT_K 6.0
+#endif
+#ifndef PSS_SPLIT_TARGET
+#define PSS_SPLIT_TARGET 2.0
+#endif
+
+struct V2xSpPlan {               // one window length
+    const uint4 *seg;            // (q, L, dlo, dhi) per segment, phase after phase
+    uint32_t W, nph, nt, qend;   // k2 draws, phases, twists generated, first word of the remainder
+    uint32_t ph[kSpPh + 1];      // first segment of each phase; ph[nph] = segments
+};
+struct V2xSp {
+    V2xSpPlan pl[2];             // windows 0 .. S-2 (W = B), the last window
+    uint32_t S, B, P, kb1, nsegmax;
+    uint32_t nwp;                // words per window in `words`
+    uint32_t *words;             // raw (untempered) MT words [window][nwp]
+    uint2 *rec;                  // [window][nsegmax][kSpRec]
+    uint2 *ss;                   // [window][nsegmax] start (role, j); role 2: the stream had ended
+    uint32_t *anc;               // [window][kSpPh + 1][4]: (role, j, ended) at each phase's start
+    uint32_t *K1, *K2;           // the slot's draws
+};
+__device__ __forceinline__ const V2xSpPlan &sp_plan(const V2xSp &a, uint32_t s) {
+    return a.pl[s + 1u == a.S ? 1 : 0];
+}
+__device__ __forceinline__ uint32_t sp_phases(const V2xSpPlan &pl) { return pl.nph ? pl.nph : 1u; }
+
+// one MT19937 twist o -> nw (LDS, the two halves of a double buffer) in three dependent
+// 227-word steps, the raw words also stored to dst (HBM)
+__device__ __forceinline__ void mt_twist_store(const uint32_t *o, uint32_t *nw, uint32_t *__restrict__ dst,
+                                               int lane) {
+    constexpr int D = kMtN - kMtM;   // 227
+#pragma unroll
+    for (int p = 0; p < 3; p++) {
+        uint32_t v[4];
+#pragma unroll
+        for (int it = 0; it < 4; it++) {
+            const int tt = lane + 64 * it, k = tt + D * p;
+            v[it] = 0u;
+            if (tt < D && k < kMtN) {
+                if (p == 0) v[it] = mt_twist_word(o[k], o[k + 1], o[k + kMtM]);
+                else if (k < kMtN - 1) v[it] = mt_twist_word(o[k], o[k + 1], nw[k - D]);
+                else v[it] = mt_twist_word(o[kMtN - 1], nw[0], nw[kMtM - 1]);
+            }
+        }
+#pragma unroll
+        for (int it = 0; it < 4; it++) {
+            const int tt = lane + 64 * it, k = tt + D * p;
+            if (tt < D && k < kMtN) {
+                nw[k] = v[it];
+                dst[k] = v[it];
+            }
+        }
+        wave_lds_order();
+    }
+}
+
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t x) {
+#pragma unroll
+    for (int o = 32; o; o >>= 1) {
+        const uint32_t y = (uint32_t)__shfl_xor((int)x, o);
+        x = y < x ? y : x;
+    }
+    return x;
+}
+
+// pair_block's verdicts for one full block at one start (st, i2), without emitting: advances
+// (st, i2) and returns in delta the largest d such that the block makes the same verdicts from
+// (st, i2 + d) -- every k2 lane's index shifts by d: an accepted word r at bound n = W - j stays
+// accepted while d < n - r, a rejected one stays rejected, and the bound keeps its bit length
+// while d <= n - 2^(k-1)
+__device__ __forceinline__ void pair_eval(uint32_t word, uint32_t W, uint32_t P, uint32_t kb1, uint32_t &st,
+                                          uint32_t &i2, uint32_t &delta) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t below = lanemask_lt();
+    const bool a1 = (word >> (32u - kb1)) < P;
+    uint32_t j = 0, role = 0, Fx = 0;
+    bool a2 = false;
+    auto pass = [&](uint32_t n2, uint32_t rr) {
+        a2 = rr < n2;
+        const uint32_t f = ((a1 != a2) ? 2u : 0u) | (a1 ? 1u : 0u);
+        Fx = wave_role_scan(f);
+        const uint32_t Fp = (uint32_t)__shfl((int)Fx, lane > 0 ? lane - 1 : 0);
+        role = lane ? role_apply(Fp, st) : st;
+        const uint64_t m2 = __ballot(role == 1u && a2);
+        j = i2 + (uint32_t)__popcll(m2 & below);
+    };
+    const uint32_t jl = i2 + ((uint32_t)lane + 1u) / 2u;
+    const uint32_t nhi = i2 < W ? W - i2 : 1u, nlo = jl < W ? W - jl : 1u;
+    const uint32_t kbh = 32u - (uint32_t)__builtin_clz(nhi);
+    const uint32_t rh = word >> (32u - kbh);
+    const bool sure = kbh == 32u - (uint32_t)__builtin_clz(nlo) && (rh < nlo || rh >= nhi);
+    if (__ballot(!sure) == 0) {
+        pass(nlo, rh);
+    } else {
+        uint32_t jg = i2 + (uint32_t)lane / 3u;
+        for (;;) {
+            const uint32_t n2 = jg < W ? W - jg : 1u;
+            pass(n2, word >> (32u - (32u - (uint32_t)__builtin_clz(n2))));
+            if (__ballot(j != jg) == 0) break;
+            jg = j;
+        }
+    }
+    uint32_t lim = 0xFFFFFFFFu;
+    if (role == 1u) {
+        const uint32_t n = j < W ? W - j : 1u;
+        const uint32_t kb = 32u - (uint32_t)__builtin_clz(n);
+        const uint32_t r = word >> (32u - kb);
+        lim = n - (1u << (kb - 1u));
+        if (r < n && n - r - 1u < lim) lim = n - r - 1u;
+        if (j >= W) lim = 0u;
+    }
+    delta = wave_min_u32(lim);
+    i2 += (uint32_t)__popcll(__ballot(role == 1u && a2));
+    st = role_apply((uint32_t)__shfl((int)Fx, 63), st);
+}
+}  // namespace
+
+// ---- generation: one wave per window (its raw words), the tail draws on the other blocks ----
+__global__ __launch_bounds__(64) void k_v2x_sp_gen(V2xSp a, V2xGeo x, int64_t epoch) {
+    __shared__ uint32_t mt[2][kMtN];
+    const uint32_t b = blockIdx.x;
+    const int lane = threadIdx.x & 63;
+    if (b >= a.S) {
+        v2x_tail_block(x, epoch, 0u, (b - a.S) * 64u, a.K1, mt[0]);
+        return;
+    }
+    // the generator is a latency chain: it issues first on its SIMD
+    __builtin_amdgcn_s_setprio(3);
+    const uint32_t s = b;
+    const V2xSpPlan &pl = sp_plan(a, s);
+    mt_seed_int(mt[0], s == 0 ? epoch + 2 : epoch + (int64_t)(s - 1) * 10000);
+    uint32_t *dst = a.words + (size_t)s * a.nwp;
+    for (uint32_t t = 0; t < pl.nt; t++) mt_twist_store(mt[t & 1u], mt[(t + 1u) & 1u], dst + (size_t)t * kMtN, lane);
+    if (lane < 4) a.anc[(size_t)s * (kSpPh + 1) * 4 + lane] = 0u;
+}
+
+// ---- level 1: the pieces of one (segment, start role) per wave -------------------------------
+// The branch list lives across the lanes: lane i holds piece i's low end a_i, its role and its
+// count offset c_i (pieces are contiguous: piece i ends at a_{i+1} - 1, the last at hi).
+__global__ __launch_bounds__(256) void k_v2x_sp_lvl1(V2xSp a, uint32_t phase) {
+    const uint32_t s = blockIdx.y;
+    const V2xSpPlan &pl = sp_plan(a, s);
+    if (phase >= pl.nph) return;
+    const int lane = threadIdx.x & 63;
+    const uint32_t item = blockIdx.x * 4u + (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const uint32_t g = pl.ph[phase] + item / 2u, r0 = item & 1u;
+    if (g >= pl.ph[phase + 1]) return;
+    const uint32_t *an = a.anc + ((size_t)s * (kSpPh + 1) + phase) * 4;
+    const uint32_t ai2 = an[1], aend = an[2];
+    const uint4 sg = pl.seg[g];
+    uint2 *rec = a.rec + ((size_t)s * a.nsegmax + g) * kSpRec;
+    const uint32_t lo = ai2 + sg.z, hi = ai2 + sg.w;
+    uint32_t cnt = kSpOver;
+    uint32_t la = lo, lst = r0, lc = 0u;
+    if (!aend) {
+        const uint32_t W = pl.W, P = a.P, kb1 = a.kb1;
+        const uint32_t *wsrc = a.words + (size_t)s * a.nwp + sg.x;
+        uint32_t n = 1u;
+        bool over = false;
+        for (uint32_t bq = 0; bq < sg.y && !over; bq += 64u) {
+            const uint32_t word = mt_temper(wsrc[bq + (uint32_t)lane]);
+            uint32_t na = 0u, nst = 0u, nc = 0u, nn = 0u, lstl = 0u, lcl = 0u;
+            for (uint32_t i = 0; i < n && !over; i++) {
+                uint32_t ba = (uint32_t)__builtin_amdgcn_readlane((int)la, (int)i);
+                const uint32_t bb = i + 1u < n ? (uint32_t)__builtin_amdgcn_readlane((int)la, (int)(i + 1u)) - 1u : hi;
+                const uint32_t bst = (uint32_t)__builtin_amdgcn_readlane((int)lst, (int)i);
+                const uint32_t bc = (uint32_t)__builtin_amdgcn_readlane((int)lc, (int)i);
+                for (;;) {
+                    uint32_t st2 = bst, j2 = ba + bc, d = 0u;
+                    if (j2 + 64u >= W) { over = true; break; }
+                    pair_eval(word, W, P, kb1, st2, j2, d);
+                    const uint32_t e = d >= bb - ba ? bb : ba + d;
+                    const uint32_t c2 = j2 - ba;
+                    if (!(nn && lstl == st2 && lcl == c2)) {   // else: the last piece extends to e
+                        if (nn == 64u) { over = true; break; }
+                        if ((uint32_t)lane == nn) { na = ba; nst = st2; nc = c2; }
+                        nn++;
+                        lstl = st2;
+                        lcl = c2;
+                    }
+                    if (e == bb) break;
+                    ba = e + 1u;
+                }
+            }
+            la = na; lst = nst; lc = nc; n = nn;
+        }
+        if (!over && n <= (uint32_t)kSpPieces) cnt = n;
+    }
+    const uint32_t base = r0 ? (uint32_t)kSpPieces : 0u;
+    if (cnt != kSpOver && (uint32_t)lane < cnt) rec[base + (uint32_t)lane] = make_uint2(la, lst | (lc << 1));
+    if (lane == 0) {
+        reinterpret_cast<uint32_t *>(rec + kSpRecCnt)[r0] = cnt;
+        if (r0 == 0u) {
+            rec[kSpRecLoHi] = make_uint2(lo, hi);
+            rec[kSpRecQL] = make_uint2(sg.x, sg.y);
+        }
+    }
+}
+
+// ---- the walk: one wave per window over one phase's segments ----------------------------------
+__global__ __launch_bounds__(64) void k_v2x_sp_walk(V2xSp a, uint32_t phase) {
+    __shared__ uint32_t mt[kMtN];
+    const uint32_t s = blockIdx.x;
+    const V2xSpPlan &pl = sp_plan(a, s);
+    if (phase >= sp_phases(pl)) return;
+    __builtin_amdgcn_s_setprio(3);
+    const int lane = threadIdx.x & 63;
+    const uint32_t W = pl.W, P = a.P, kb1 = a.kb1;
+    uint32_t *an = a.anc + ((size_t)s * (kSpPh + 1) + phase) * 4;
+    // the state is wave-uniform: in scalar registers (a vector copy would make every use wait on
+    // the outstanding record loads)
+    uint32_t st = (uint32_t)__builtin_amdgcn_readfirstlane((int)an[0]);
+    uint32_t i2 = (uint32_t)__builtin_amdgcn_readfirstlane((int)an[1]);
+    uint32_t ended = (uint32_t)__builtin_amdgcn_readfirstlane((int)an[2]);
+    const uint32_t g0 = pl.ph[phase], g1 = pl.nph ? pl.ph[phase + 1] : 0u;
+    const uint2 *rec = a.rec + (size_t)s * a.nsegmax * kSpRec;
+    uint2 *ss = a.ss + (size_t)s * a.nsegmax;
+    const uint32_t *wsrc = a.words + (size_t)s * a.nwp;
+    auto noemit = [](bool, uint32_t, uint32_t) {};
+    // The records come through LDS in batches of 64 segments (one bulk load of the next batch in
+    // flight while this one is walked), lane k = segment k of the batch, and a batch resolves by
+    // guess and verify: every lane guesses where its segment starts (first the middle of its
+    // interval, then where the last pass put it), takes its pieces' transfer at the guess for
+    // either start role, and one inclusive scan of those transfers (the role maps composed, the
+    // k2 counts added) gives every lane a start.  Lanes up to the first one whose actual start
+    // lies in a piece of another transfer are then exact; that lane's start is exact too, so it
+    // becomes the next pass's first lane with an exact guess (or, outside its interval or with
+    // too many pieces, it runs exactly).  Each pass settles at least one lane, almost always all.
+    // (Walking the segments one by one cost ~550 clocks a segment: a chain of lane reads and
+    // scalar branches; ~900 with the records loaded from HBM per segment.)
+    constexpr uint32_t kBatch = 64, kPad = kSpRec + 1;   // (odd record pitch: lane k's reads spread over the banks)
+    __shared__ uint2 rl[2][kBatch * kPad];
+    uint4 v[16];
+    auto load_batch = [&](uint32_t gb) {
+        const uint4 *src = reinterpret_cast<const uint4 *>(rec + (size_t)gb * kSpRec);
+#pragma unroll
+        for (int i = 0; i < 16; i++) {
+            const uint32_t idx = (uint32_t)lane + 64u * (uint32_t)i;
+            v[i] = gb + (idx >> 4) < g1 ? src[idx] : make_uint4(0u, 0u, 0u, 0u);
+        }
+    };
+    auto store_batch = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < 16; i++) {
+            const uint32_t idx = (uint32_t)lane + 64u * (uint32_t)i;
+            uint2 *d = rl[buf] + (idx >> 4) * kPad + 2u * (idx & 15u);
+            d[0] = make_uint2(v[i].x, v[i].y);
+            d[1] = make_uint2(v[i].z, v[i].w);
+        }
+        wave_lds_order();
+    };
+    // an exact run of segment words [q, q + L) from (st, i2), 8 blocks' words loaded at a time
+    auto run_exact = [&](uint32_t q, uint32_t L) {
+        uint32_t i1 = i2 + st;
+        for (uint32_t bq = 0; bq < L && i2 < W; bq += 512u) {
+            uint32_t w8[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) w8[u] = bq + 64u * u < L ? wsrc[q + bq + 64u * u + (uint32_t)lane] : 0u;
+#pragma unroll
+            for (int u = 0; u < 8; u++)
+                if (bq + 64u * u < L && i2 < W) pair_block(mt_temper(w8[u]), true, W, P, kb1, st, i1, i2, noemit);
+        }
+        if (i2 >= W) ended = 1u;
+    };
+    if (g0 < g1) {
+        load_batch(g0);
+        store_batch(0);
+    }
+    int buf = 0;
+    for (uint32_t gb = g0; gb < g1; gb += kBatch, buf ^= 1) {
+        const bool more = gb + kBatch < g1;
+        if (more) load_batch(gb + kBatch);
+        const uint32_t nb = g1 - gb < kBatch ? g1 - gb : kBatch;
+        const uint32_t ul = (uint32_t)lane;
+        const uint2 *mr = rl[buf] + (ul < nb ? ul : 0u) * kPad;   // this lane's record
+        const uint32_t lo = mr[kSpRecLoHi].x, hi = mr[kSpRecLoHi].y;
+        const uint32_t c0 = mr[kSpRecCnt].x, c1 = mr[kSpRecCnt].y;
+        auto valid = [&](uint32_t r, uint32_t j) { return (r ? c1 : c0) <= (uint32_t)kSpPieces && j >= lo && j <= hi; };
+        auto lookup = [&](uint32_t r, uint32_t j) {   // the transfer (role | c << 1) of the piece holding j
+            const uint32_t base = r ? (uint32_t)kSpPieces : 0u;
+            uint32_t n = r ? c1 : c0;
+            n = n > (uint32_t)kSpPieces ? 1u : n;
+            uint32_t pk = mr[base].y;
+            for (uint32_t q = 1; q < n; q++) {
+                const uint2 e = mr[base + q];
+                if (e.x > j) break;
+                pk = e.y;
+            }
+            return pk;
+        };
+        uint32_t guess = lo + (hi - lo) / 2u;       // where this lane's segment starts, guessed
+        uint32_t sst = 0u, si2 = 0u;                // its start, once settled
+        uint32_t f = 0;                             // lanes below f are settled
+        while (f < nb && !ended) {
+            // transfers at the guesses (identity outside [f, nb))
+            const bool act = ul >= f && ul < nb;
+            const uint32_t p0 = valid(0u, guess) ? lookup(0u, guess) : 0u;
+            const uint32_t p1 = valid(1u, guess) ? lookup(1u, guess) : 2u;
+            const uint32_t r0 = p0 & 1u, r1 = p1 & 1u;
+            uint32_t tF = act ? (r0 == r1 ? 2u | r0 : r0) : 0u;
+            uint32_t t0 = act ? p0 >> 1 : 0u, t1 = act ? p1 >> 1 : 0u;
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {   // inclusive scan: (earlier) then (this)
+                const uint32_t pF = (uint32_t)__shfl_up((int)tF, d), q0c = (uint32_t)__shfl_up((int)t0, d);
+                const uint32_t q1c = (uint32_t)__shfl_up((int)t1, d);
+                if (lane >= d) {
+                    const uint32_t a0 = role_apply(pF, 0u), a1 = role_apply(pF, 1u);
+                    const uint32_t n0 = q0c + (a0 ? t1 : t0), n1 = q1c + (a1 ? t1 : t0);
+                    tF = role_compose(tF, pF);
+                    t0 = n0;
+                    t1 = n1;
+                }
+            }
+            const uint32_t eF = (uint32_t)__shfl_up((int)tF, 1), e0 = (uint32_t)__shfl_up((int)t0, 1);
+            const uint32_t e1 = (uint32_t)__shfl_up((int)t1, 1);
+            const uint32_t bst = ul == f ? st : role_apply(eF, st);
+            const uint32_t bi2 = i2 + (ul == f ? 0u : (st ? e1 : e0));
+            const bool vstart = valid(bst, bi2);
+            const bool ok = vstart && valid(bst, guess) && lookup(bst, bi2) == lookup(bst, guess);
+            const uint64_t bad = __ballot(act && !ok);
+            const uint32_t g = bad ? (uint32_t)__ffsll((long long)bad) - 1u : nb;
+            if (ul >= f && ul < g) { sst = bst; si2 = bi2; }
+            if (g >= nb) {   // all settled: the state after the batch
+                const uint32_t lF = (uint32_t)__builtin_amdgcn_readlane((int)tF, (int)(nb - 1u));
+                const uint32_t l0 = (uint32_t)__builtin_amdgcn_readlane((int)t0, (int)(nb - 1u));
+                const uint32_t l1 = (uint32_t)__builtin_amdgcn_readlane((int)t1, (int)(nb - 1u));
+                i2 += st ? l1 : l0;
+                st = role_apply(lF, st);
+                f = nb;
+                break;
+            }
+            // lane g starts exactly there
+            st = (uint32_t)__builtin_amdgcn_readlane((int)bst, (int)g);
+            i2 = (uint32_t)__builtin_amdgcn_readlane((int)bi2, (int)g);
+            if (!__builtin_amdgcn_readlane((int)vstart, (int)g)) {   // outside its interval: run it
+                if (ul == g) { sst = st; si2 = i2; }
+                run_exact((uint32_t)__builtin_amdgcn_readlane((int)mr[kSpRecQL].x, (int)g),
+                          (uint32_t)__builtin_amdgcn_readlane((int)mr[kSpRecQL].y, (int)g));
+                st = (uint32_t)__builtin_amdgcn_readfirstlane((int)st);
+                i2 = (uint32_t)__builtin_amdgcn_readfirstlane((int)i2);
+                f = g + 1u;
+            } else {
+                f = g;
+            }
+            if (ul >= f) guess = bi2;
+        }
+        if (ended)   // the stream ended inside a segment: every later one is marked
+            if (ul >= f) { sst = 2u; si2 = i2; }
+        if (ul < nb) ss[gb + ul] = make_uint2(sst, si2);
+        if (more) store_batch(buf ^ 1);
+    }
+    if (lane == 0) { an[4] = st; an[5] = i2; an[6] = ended; }
+    if (phase + 1u != sp_phases(pl)) return;
+    // the rest of the window, exactly, emitting
+    const size_t t0 = (size_t)s * a.B;
+    uint32_t *k1 = a.K1 + t0, *k2 = a.K2 + t0;
+    auto emit = [&](bool second, uint32_t i, uint32_t r) {
+        if (second) k2[i] = r;
+        else k1[i] = r;
+    };
+    if (!ended) {
+        uint32_t i1 = i2 + st, q = pl.qend;
+        const uint32_t nw = pl.nt * (uint32_t)kMtN;
+        while (i2 < W && q < nw) {   // 8 blocks' words loaded at a time
+            uint32_t w8[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                const uint32_t qu = q + 64u * u + (uint32_t)lane;
+                w8[u] = qu < nw ? wsrc[qu] : 0u;
+            }
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                if (i2 >= W || q >= nw) break;
+                const uint32_t nval = nw - q < 64u ? nw - q : 64u;
+                const bool valid = (uint32_t)lane < nval;
+                pair_block(valid ? mt_temper(w8[u]) : 0u, valid, W, P, kb1, st, i1, i2, emit);
+                q += nval;
+            }
+        }
+        if (i2 < W) {   // past the generated words: the stream continues from its state (the last twist)
+            for (int i = lane; i < kMtN; i += 64) mt[i] = wsrc[nw - (uint32_t)kMtN + (uint32_t)i];
+            wave_lds_order();
+            while (i2 < W) {
+                mt_twist(mt);
+                for (int q0 = 0; q0 < kMtN && i2 < W; q0 += 64) {
+                    const int nval = kMtN - q0 < 64 ? kMtN - q0 : 64;
+                    const bool valid = lane < nval;
+                    pair_block(valid ? mt_temper(mt[q0 + lane]) : 0u, valid, W, P, kb1, st, i1, i2, emit);
+                }
+            }
+        }
+    }
+    for (uint32_t u = W + (uint32_t)lane; u < a.B; u += 64u) k2[u] = 0u;   // padding steps
+}
+
+// ---- emission: one wave per segment from its start ---------------------------------------------
+__global__ __launch_bounds__(256) void k_v2x_sp_emit(V2xSp a) {
+    const uint32_t s = blockIdx.y;
+    const V2xSpPlan &pl = sp_plan(a, s);
+    const uint32_t g = blockIdx.x * 4u + (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    if (g >= pl.ph[pl.nph]) return;
+    const uint2 st0 = a.ss[(size_t)s * a.nsegmax + g];
+    if (st0.x > 1u) return;
+    const int lane = threadIdx.x & 63;
+    const uint4 sg = pl.seg[g];
+    const uint32_t W = pl.W, P = a.P, kb1 = a.kb1;
+    const uint32_t *wsrc = a.words + (size_t)s * a.nwp + sg.x;
+    const size_t t0 = (size_t)s * a.B;
+    uint32_t *k1 = a.K1 + t0, *k2 = a.K2 + t0;
+    auto emit = [&](bool second, uint32_t i, uint32_t r) {
+        if (second) k2[i] = r;
+        else k1[i] = r;
+    };
+    uint32_t st = st0.x, i2 = st0.y, i1 = i2 + st;
+    for (uint32_t bq = 0; bq < sg.y && i2 < W; bq += 64u)
+        pair_block(mt_temper(wsrc[bq + (uint32_t)lane]), true, W, P, kb1, st, i1, i2, emit);
+}
+
+namespace {
+// ---- host: the plan of one window length (cached per device, W and P) -----------------------
+struct SpPlanHost {
+    std::vector<uint4> seg;
+    uint32_t W = 0, nph = 0, nt = 0, qend = 0;
+    uint32_t ph[kSpPh + 1] = {};
+    double words = 0;            // expected words of the window
+    uint4 *dseg = nullptr;
+};
+
+static uint32_t sp_bitlen(uint64_t n) { return n ? 64u - (uint32_t)__builtin_clzll(n) : 0u; }
+
+static void sp_plan_build(uint32_t W, uint32_t P, SpPlanHost &h) {
+    h.W = W;
+    const uint32_t kb1 = sp_bitlen(P);
+    const double a1 = (double)P / (double)(1ull << kb1);
+    // words per step j (a k1 then a k2 draw at bound W - j) and their variance; running sums
+    std::vector<double> M(W + 1), V(W + 1), E(W ? W : 1);
+    M[0] = V[0] = 0.0;
+    for (uint32_t j = 0; j < W; j++) {
+        const uint32_t n = W - j;
+        const double a2 = (double)n / (double)(1ull << sp_bitlen(n));
+        E[j] = 1.0 / a1 + 1.0 / a2;
+        M[j + 1] = M[j] + E[j];
+        V[j + 1] = V[j] + (1.0 - a1) / (a1 * a1) + (1.0 - a2) / (a2 * a2);
+    }
+    h.words = W ? M[W] : 0.0;
+    auto jat = [&](double q) {   // the step whose expected word offset reaches q
+        const size_t i = (size_t)(std::lower_bound(M.begin(), M.end(), q) - M.begin());
+        return i < W ? i : (size_t)(W ? W - 1 : 0);
+    };
+    uint32_t q = 0;
+    for (int p = 0; p < kSpPh && W; p++) {
+        const uint32_t qa = q;
+        const size_t ja = jat(qa), n0 = h.seg.size();
+        for (;;) {
+            const size_t je = jat(q);
+            const double sd = std::sqrt(V[je] - V[ja] + 1.0) / E[je];
+            const double m = PSS_SPLIT_K * sd + 16.0, width = 2.0 * m + 1.0;
+            const double nmin = (double)W - (double)je - m - 64.0;
+            if (nmin <= 4.0 * width) break;
+            const uint32_t kk = sp_bitlen((uint64_t)nmin);
+            const double f2 = ((double)(1ull << kk) / nmin) / E[je];   // k2 share of the words (upper bound)
+            auto splits = [&](uint32_t L) { return L * f2 * width / (double)(1ull << (kk - 1)); };
+            uint32_t L = 4096;
+            while (L > 64 && splits(L) > PSS_SPLIT_TARGET) L >>= 1;
+            if (splits(L) > 2.0 * PSS_SPLIT_TARGET || (double)je + m + L >= (double)W - 64.0) break;
+            const double rel = (double)je - (double)ja;
+            const double cap = (double)((q - qa) / 2u + 1u);   // at most one k2 per two words
+            double dlo = std::floor(rel - m), dhi = std::ceil(rel + m) + 1.0;
+            if (dlo < 0.0) dlo = 0.0;
+            if (dhi > cap) dhi = cap;
+            if (dlo > dhi) dlo = dhi;
+            h.seg.push_back(make_uint4(q, L, (uint32_t)dlo, (uint32_t)dhi));
+            q += L;
+        }
+        if (h.seg.size() == n0) break;
+        h.nph++;
+        h.ph[h.nph] = (uint32_t)h.seg.size();
+    }
+    for (int p = (int)h.nph + 1; p <= kSpPh; p++) h.ph[p] = (uint32_t)h.seg.size();
+    h.qend = q;
+    double nw = h.words + 12.0 * std::sqrt(W ? V[W] : 0.0) + 2.0 * kMtN;
+    if (nw < (double)q + 64.0) nw = (double)q + 64.0;
+    h.nt = (uint32_t)std::ceil(nw / (double)kMtN);
+}
+
+static const SpPlanHost *sp_plan_get(uint32_t W, uint32_t P) {
+    static std::mutex mu;
+    static std::map<std::tuple<int, uint32_t, uint32_t>, std::unique_ptr<SpPlanHost>> cache;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    std::lock_guard<std::mutex> lk(mu);
+    auto &slot = cache[std::make_tuple(dev, W, P)];
+    if (!slot) {
+        auto h = std::make_unique<SpPlanHost>();
+        sp_plan_build(W, P, *h);
+        if (!h->seg.empty()) {
+            if (hipMalloc((void **)&h->dseg, h->seg.size() * sizeof(uint4)) != hipSuccess) {
+                (void)hipGetLastError();
+                return nullptr;   // (not cached: retried on the next call)
+            }
+            if (hipMemcpy(h->dseg, h->seg.data(), h->seg.size() * sizeof(uint4), hipMemcpyHostToDevice) != hipSuccess) {
+                (void)hipGetLastError();
+                (void)hipFree(h->dseg);
+                return nullptr;
+            }
+        }
+        slot = std::move(h);
+    }
+    return slot.get();
+}
+
+static V2xSpPlan sp_plan_dev(const SpPlanHost &h) {
+    V2xSpPlan p{};
+    p.seg = h.dseg;
+    p.W = h.W; p.nph = h.nph; p.nt = h.nt; p.qend = h.qend;
+    for (int i = 0; i <= kSpPh; i++) p.ph[i] = h.ph[i];
+    return p;
+}
+}  // namespace

@@ -1,0 +1,18 @@
+#!/bin/bash
+# Split exact V2 draws (pss_v2split.h): parity subset, cold C5 exact split vs workgroup form, and a
+# kernel trace of the cold split epochs.
+#   usage: tools/gpu_split.sh <outdir> [tests] [timing] [prof]
+cd "$GRAFT_REPO_ROOT"; O=gpurun_out/$1; shift; mkdir -p $O; export TMPDIR=/tmp
+for what in "$@"; do
+  case $what in
+  tests) timeout -k 10 500 python -u -m pytest tests/test_gpu_configs.py -x -v --timeout 240 --timeout-method thread \
+           -k "big_pool_exact_order or c5_pool_exact or (bench_shape and c5)" > $O/tests.txt 2>&1 || { echo "tests rc=$?"; tail -30 $O/tests.txt; exit 1; } ;;
+  timing) for i in 1 2; do
+      timeout -k 10 200 env PSS_EXACT_LOOKAHEAD=0 python tools/bench_configs.py c5x > $O/cold_split_$i.json 2> $O/cold_split_$i.err || exit 1
+      timeout -k 10 200 env PSS_EXACT_LOOKAHEAD=0 PSS_V2X_SPLIT=0 python tools/bench_configs.py c5x > $O/cold_wg_$i.json 2> $O/cold_wg_$i.err || exit 1
+    done ;;
+  prof) PSS_EXACT_LOOKAHEAD=0 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- \
+          python3 tools/bench_configs.py c5x > $O/prof.log 2>&1 || { echo "prof rc=$?"; tail -20 $O/prof.log; exit 1; } ;;
+  esac
+done
+echo done
