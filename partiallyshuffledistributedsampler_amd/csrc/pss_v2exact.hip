@@ -1119,7 +1119,12 @@ static bool v2x_draws_split(const V2xGeo &x, int64_t epoch, uint32_t *slot, uint
     a.K1 = slot;
     a.K2 = slot + x.ns;
     const uint32_t tail_blocks = (x.P + 63u) / 64u;
-    hipLaunchKernelGGL(k_v2x_sp_gen, dim3(x.S + tail_blocks), dim3(64), 0, s, a, x, epoch);
+#ifdef PSS_DIAG_SP_TAIL_APART   // timing build: the tail draws in a launch of their own after the generators
+    hipLaunchKernelGGL(k_v2x_sp_gen, dim3(x.S), dim3(kSpGenThreads), 0, s, a, x, epoch);
+    hipLaunchKernelGGL(k_v2x_tail_draws, dim3(tail_blocks), dim3(64), 0, s, x, epoch, tail_blocks, (uint64_t)0, slot);
+#else
+    hipLaunchKernelGGL(k_v2x_sp_gen, dim3(x.S + (tail_blocks + 3u) / 4u), dim3(kSpGenThreads), 0, s, a, x, epoch);
+#endif
     const uint32_t nph = std::max(std::max(hb->nph, 1u), std::max(hl->nph, 1u));
     for (uint32_t p = 0; p < nph; p++) {
         uint32_t segs = 0;

@@ -46,7 +46,8 @@ constexpr uint32_t kSpOver = 0xFFFFFFFFu;
 #endif
 
 struct V2xSpPlan {               // one window length
-    const uint4 *seg;            // (q, L, dlo, dhi) per segment, phase after phase
+    const uint4 *seg;            // (q, L, -, -) per segment, phase after phase
+    const float2 *mv;            // (expected words, their variance) to reach step 64 i, i <= W / 64 + 1
     uint32_t W, nph, nt, qend;   // k2 draws, phases, twists generated, first word of the remainder
     uint32_t ph[kSpPh + 1];      // first segment of each phase; ph[nph] = segments
 };
@@ -64,36 +65,6 @@ __device__ __forceinline__ const V2xSpPlan &sp_plan(const V2xSp &a, uint32_t s) 
     return a.pl[s + 1u == a.S ? 1 : 0];
 }
 __device__ __forceinline__ uint32_t sp_phases(const V2xSpPlan &pl) { return pl.nph ? pl.nph : 1u; }
-
-// one MT19937 twist o -> nw (LDS, the two halves of a double buffer) in three dependent
-// 227-word steps, the raw words also stored to dst (HBM)
-__device__ __forceinline__ void mt_twist_store(const uint32_t *o, uint32_t *nw, uint32_t *__restrict__ dst,
-                                               int lane) {
-    constexpr int D = kMtN - kMtM;   // 227
-#pragma unroll
-    for (int p = 0; p < 3; p++) {
-        uint32_t v[4];
-#pragma unroll
-        for (int it = 0; it < 4; it++) {
-            const int tt = lane + 64 * it, k = tt + D * p;
-            v[it] = 0u;
-            if (tt < D && k < kMtN) {
-                if (p == 0) v[it] = mt_twist_word(o[k], o[k + 1], o[k + kMtM]);
-                else if (k < kMtN - 1) v[it] = mt_twist_word(o[k], o[k + 1], nw[k - D]);
-                else v[it] = mt_twist_word(o[kMtN - 1], nw[0], nw[kMtM - 1]);
-            }
-        }
-#pragma unroll
-        for (int it = 0; it < 4; it++) {
-            const int tt = lane + 64 * it, k = tt + D * p;
-            if (tt < D && k < kMtN) {
-                nw[k] = v[it];
-                dst[k] = v[it];
-            }
-        }
-        wave_lds_order();
-    }
-}
 
 __device__ __forceinline__ uint32_t wave_min_u32(uint32_t x) {
 #pragma unroll
@@ -156,23 +127,101 @@ __device__ __forceinline__ void pair_eval(uint32_t word, uint32_t W, uint32_t P,
 }
 }  // namespace
 
-// ---- generation: one wave per window (its raw words), the tail draws on the other blocks ----
-__global__ __launch_bounds__(64) void k_v2x_sp_gen(V2xSp a, V2xGeo x, int64_t epoch) {
-    __shared__ uint32_t mt[2][kMtN];
+// ---- generation: a workgroup per window (its raw words), the tail draws on the other blocks ----
+// Thread t (< 227) owns words t, t + 227 and t + 454 of every twist: new[k] needs old[k],
+// old[k + 1] and either old[k + 397] (k < 227) or new[k - 227] -- the same thread's previous
+// word -- so a twist's three dependent steps run in the thread's registers, and only the previous
+// twist's words cross threads: the state goes through LDS once per twist (double-buffered, one
+// barrier).  new[623] also needs new[0]: its thread computes new[0] again from the old state.
+// (One wave over the whole state ran ~1200 clocks a twist, four waves stepping 227 words at a
+// time with a barrier per step ~900: 2.9 / 2.2 ms for C5's 5.7K twists a window.)
+constexpr int kSpGenThreads = 256;
+__global__ __launch_bounds__(kSpGenThreads) void k_v2x_sp_gen(V2xSp a, V2xGeo x, int64_t epoch) {
+    __shared__ uint32_t sm[4 * kMtN];   // a window's double-buffered state, or four tail waves' MT
     const uint32_t b = blockIdx.x;
-    const int lane = threadIdx.x & 63;
-    if (b >= a.S) {
-        v2x_tail_block(x, epoch, 0u, (b - a.S) * 64u, a.K1, mt[0]);
+    const int tid = threadIdx.x;
+    const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane(tid >> 6);
+    if (b >= a.S) {   // the tail: a wave per 64 tail steps
+        const uint32_t j0 = ((b - a.S) * 4u + wv) * 64u;
+        if (j0 < x.P) v2x_tail_block(x, epoch, 0u, j0, a.K1, sm + kMtN * wv);
         return;
     }
-    // the generator is a latency chain: it issues first on its SIMD
+    // the generator is a latency chain: it issues first on its SIMDs
     __builtin_amdgcn_s_setprio(3);
     const uint32_t s = b;
     const V2xSpPlan &pl = sp_plan(a, s);
-    mt_seed_int(mt[0], s == 0 ? epoch + 2 : epoch + (int64_t)(s - 1) * 10000);
-    uint32_t *dst = a.words + (size_t)s * a.nwp;
-    for (uint32_t t = 0; t < pl.nt; t++) mt_twist_store(mt[t & 1u], mt[(t + 1u) & 1u], dst + (size_t)t * kMtN, lane);
-    if (lane < 4) a.anc[(size_t)s * (kSpPh + 1) * 4 + lane] = 0u;
+    if (wv == 0) mt_seed_int(sm, s == 0 ? epoch + 2 : epoch + (int64_t)(s - 1) * 10000);
+    __syncthreads();
+    constexpr int D = kMtN - kMtM;   // 227
+    const bool own = tid < D, own2 = tid < kMtN - 2 * D;   // words t, t + 227 (all), t + 454 (t < 170)
+    const bool last = tid == kMtN - 1 - 2 * D;            // t = 169: word 623
+    uint32_t o0 = 0u, o1 = 0u, o2 = 0u;
+    if (own) { o0 = sm[tid]; o1 = sm[tid + D]; }
+    if (own2) o2 = sm[tid + 2 * D];
+    uint32_t *dst = a.words + (size_t)s * a.nwp + (uint32_t)tid;
+    for (uint32_t t = 0; t < pl.nt; t++) {
+        const uint32_t *st = sm + (t & 1u) * kMtN;        // the previous twist's words
+        uint32_t *sn = sm + ((t + 1u) & 1u) * kMtN;
+        if (own) {
+            const uint32_t b0 = st[tid + 1], c0 = st[tid + kMtM], b1 = st[tid + D + 1];
+            const uint32_t b2 = own2 && !last ? st[tid + 2 * D + 1] : 0u;
+            uint32_t z0 = 0u, z1 = 0u, z397 = 0u;
+            if (last) { z0 = st[0]; z1 = st[1]; z397 = st[kMtM]; }
+            const uint32_t n0 = mt_twist_word(o0, b0, c0);
+            const uint32_t n1 = mt_twist_word(o1, b1, n0);
+            uint32_t n2 = 0u;
+            if (own2) n2 = last ? mt_twist_word(o2, mt_twist_word(z0, z1, z397), n1) : mt_twist_word(o2, b2, n1);
+            uint32_t *dt = dst + (size_t)t * kMtN;
+            dt[0] = n0;
+            dt[D] = n1;
+            if (own2) dt[2 * D] = n2;
+            sn[tid] = n0;
+            sn[tid + D] = n1;
+            if (own2) sn[tid + 2 * D] = n2;
+            o0 = n0; o1 = n1; o2 = n2;
+        }
+        __syncthreads();
+    }
+    if (tid < 4) a.anc[(size_t)s * (kSpPh + 1) * 4 + tid] = 0u;
+}
+
+// the interval of a segment's start: the expected k2 index after (q - qa) words from the
+// phase's anchor A (the plan's table of expected words per step, linearly interpolated) +-
+// PSS_SPLIT_K standard deviations of the renewal count, + 16
+__device__ __forceinline__ void sp_interval(const V2xSpPlan &pl, uint32_t A, uint32_t dq, uint32_t &lo,
+                                            uint32_t &hi) {
+    const uint32_t nt = pl.W / 64u + 1u;   // table entries - 1
+    auto at = [&](float j, float &m, float &v, float &e) {
+        float fi = j * (1.0f / 64.0f);
+        if (fi > (float)nt - 1.0f) fi = (float)nt - 1.0f;
+        const uint32_t i = (uint32_t)fi;
+        const float fr = fi - (float)i;
+        const float2 x0 = pl.mv[i], x1 = pl.mv[i + 1];
+        m = x0.x + fr * (x1.x - x0.x);
+        v = x0.y + fr * (x1.y - x0.y);
+        e = (x1.x - x0.x) * (1.0f / 64.0f);
+    };
+    float mA, vA, eA;
+    at((float)A, mA, vA, eA);
+    const float target = mA + (float)dq;
+    uint32_t l = 0, h = nt;   // the last entry whose expected words stay below the target
+    while (h - l > 1u) {
+        const uint32_t md = (l + h) / 2u;
+        if (pl.mv[md].x <= target) l = md;
+        else h = md;
+    }
+    const float x0 = pl.mv[l].x, x1 = pl.mv[l + 1].x;
+    float je = 64.0f * ((float)l + (x1 > x0 ? (target - x0) / (x1 - x0) : 0.0f));
+    if (je < (float)A) je = (float)A;
+    float mj, vj, ej;
+    at(je, mj, vj, ej);
+    const float var = vj - vA > 0.0f ? vj - vA : 0.0f;
+    const float m = (float)PSS_SPLIT_K * __builtin_sqrtf(var + 1.0f) / (ej > 1.0f ? ej : 1.0f) + 16.0f;
+    const float flo = je - m, fhi = je + m + 1.0f;
+    lo = flo > (float)A ? (uint32_t)flo : A;
+    const uint32_t cap = A + dq / 2u + 1u;   // at most one k2 per two words
+    hi = fhi < (float)cap ? (uint32_t)fhi : cap;
+    if (lo > hi) lo = hi;
 }
 
 // ---- level 1: the pieces of one (segment, start role) per wave -------------------------------
@@ -190,7 +239,8 @@ __global__ __launch_bounds__(256) void k_v2x_sp_lvl1(V2xSp a, uint32_t phase) {
     const uint32_t ai2 = an[1], aend = an[2];
     const uint4 sg = pl.seg[g];
     uint2 *rec = a.rec + ((size_t)s * a.nsegmax + g) * kSpRec;
-    const uint32_t lo = ai2 + sg.z, hi = ai2 + sg.w;
+    uint32_t lo, hi;
+    sp_interval(pl, ai2, sg.x - pl.seg[pl.ph[phase]].x, lo, hi);
     uint32_t cnt = kSpOver;
     uint32_t la = lo, lst = r0, lc = 0u;
     if (!aend) {
@@ -303,6 +353,10 @@ __global__ __launch_bounds__(64) void k_v2x_sp_walk(V2xSp a, uint32_t phase) {
         }
         if (i2 >= W) ended = 1u;
     };
+#ifdef PSS_DIAG_SP_PRINT   // timing / diagnostic build: passes and exact runs per walk
+    uint32_t dg_pass = 0, dg_exact = 0;
+    const uint64_t dg_t0 = __builtin_amdgcn_s_memtime();
+#endif
     if (g0 < g1) {
         load_batch(g0);
         store_batch(0);
@@ -317,22 +371,34 @@ __global__ __launch_bounds__(64) void k_v2x_sp_walk(V2xSp a, uint32_t phase) {
         const uint32_t lo = mr[kSpRecLoHi].x, hi = mr[kSpRecLoHi].y;
         const uint32_t c0 = mr[kSpRecCnt].x, c1 = mr[kSpRecCnt].y;
         auto valid = [&](uint32_t r, uint32_t j) { return (r ? c1 : c0) <= (uint32_t)kSpPieces && j >= lo && j <= hi; };
-        auto lookup = [&](uint32_t r, uint32_t j) {   // the transfer (role | c << 1) of the piece holding j
-            const uint32_t base = r ? (uint32_t)kSpPieces : 0u;
-            uint32_t n = r ? c1 : c0;
-            n = n > (uint32_t)kSpPieces ? 1u : n;
-            uint32_t pk = mr[base].y;
-            for (uint32_t q = 1; q < n; q++) {
-                const uint2 e = mr[base + q];
-                if (e.x > j) break;
-                pk = e.y;
+        // this lane's pieces in registers (low ends past the count: ~0), read once per batch
+        uint32_t pa[2][kSpPieces], pk[2][kSpPieces];
+#pragma unroll
+        for (int r = 0; r < 2; r++) {
+            const uint32_t n = r ? c1 : c0;
+#pragma unroll
+            for (int q = 0; q < kSpPieces; q++) {
+                const uint2 e = mr[r * kSpPieces + q];
+                pa[r][q] = (uint32_t)q < n ? e.x : 0xFFFFFFFFu;
+                pk[r][q] = e.y;
             }
-            return pk;
+        }
+        auto lookup = [&](uint32_t r, uint32_t j) {   // the transfer (role | c << 1) of the piece holding j
+            uint32_t t = r ? pk[1][0] : pk[0][0];
+#pragma unroll
+            for (int q = 1; q < kSpPieces; q++) {
+                const uint32_t aq = r ? pa[1][q] : pa[0][q];
+                t = aq <= j ? (r ? pk[1][q] : pk[0][q]) : t;
+            }
+            return t;
         };
         uint32_t guess = lo + (hi - lo) / 2u;       // where this lane's segment starts, guessed
         uint32_t sst = 0u, si2 = 0u;                // its start, once settled
         uint32_t f = 0;                             // lanes below f are settled
         while (f < nb && !ended) {
+#ifdef PSS_DIAG_SP_PRINT
+            dg_pass++;
+#endif
             // transfers at the guesses (identity outside [f, nb))
             const bool act = ul >= f && ul < nb;
             const uint32_t p0 = valid(0u, guess) ? lookup(0u, guess) : 0u;
@@ -374,6 +440,9 @@ __global__ __launch_bounds__(64) void k_v2x_sp_walk(V2xSp a, uint32_t phase) {
             st = (uint32_t)__builtin_amdgcn_readlane((int)bst, (int)g);
             i2 = (uint32_t)__builtin_amdgcn_readlane((int)bi2, (int)g);
             if (!__builtin_amdgcn_readlane((int)vstart, (int)g)) {   // outside its interval: run it
+#ifdef PSS_DIAG_SP_PRINT
+                dg_exact++;
+#endif
                 if (ul == g) { sst = st; si2 = i2; }
                 run_exact((uint32_t)__builtin_amdgcn_readlane((int)mr[kSpRecQL].x, (int)g),
                           (uint32_t)__builtin_amdgcn_readlane((int)mr[kSpRecQL].y, (int)g));
@@ -391,6 +460,11 @@ __global__ __launch_bounds__(64) void k_v2x_sp_walk(V2xSp a, uint32_t phase) {
         if (more) store_batch(buf ^ 1);
     }
     if (lane == 0) { an[4] = st; an[5] = i2; an[6] = ended; }
+#ifdef PSS_DIAG_SP_PRINT
+    if (lane == 0 && s == 0)
+        printf("sp_walk phase %u segs %u passes %u exact %u clocks %lu i2 %u W %u\n", phase, g1 - g0, dg_pass, dg_exact,
+               (unsigned long)(__builtin_amdgcn_s_memtime() - dg_t0), i2, W);
+#endif
     if (phase + 1u != sp_phases(pl)) return;
     // the rest of the window, exactly, emitting
     const size_t t0 = (size_t)s * a.B;
@@ -464,7 +538,9 @@ struct SpPlanHost {
     uint32_t W = 0, nph = 0, nt = 0, qend = 0;
     uint32_t ph[kSpPh + 1] = {};
     double words = 0;            // expected words of the window
+    std::vector<float2> mv;      // expected words / variance to reach step 64 i
     uint4 *dseg = nullptr;
+    float2 *dmv = nullptr;
 };
 
 static uint32_t sp_bitlen(uint64_t n) { return n ? 64u - (uint32_t)__builtin_clzll(n) : 0u; }
@@ -484,6 +560,10 @@ static void sp_plan_build(uint32_t W, uint32_t P, SpPlanHost &h) {
         V[j + 1] = V[j] + (1.0 - a1) / (a1 * a1) + (1.0 - a2) / (a2 * a2);
     }
     h.words = W ? M[W] : 0.0;
+    for (uint32_t i = 0; i <= W / 64u + 1u; i++) {
+        const uint32_t j = 64u * i < W ? 64u * i : W;
+        h.mv.push_back(make_float2((float)M[j], (float)V[j]));
+    }
     auto jat = [&](double q) {   // the step whose expected word offset reaches q
         const size_t i = (size_t)(std::lower_bound(M.begin(), M.end(), q) - M.begin());
         return i < W ? i : (size_t)(W ? W - 1 : 0);
@@ -504,13 +584,7 @@ static void sp_plan_build(uint32_t W, uint32_t P, SpPlanHost &h) {
             uint32_t L = 4096;
             while (L > 64 && splits(L) > PSS_SPLIT_TARGET) L >>= 1;
             if (splits(L) > 2.0 * PSS_SPLIT_TARGET || (double)je + m + L >= (double)W - 64.0) break;
-            const double rel = (double)je - (double)ja;
-            const double cap = (double)((q - qa) / 2u + 1u);   // at most one k2 per two words
-            double dlo = std::floor(rel - m), dhi = std::ceil(rel + m) + 1.0;
-            if (dlo < 0.0) dlo = 0.0;
-            if (dhi > cap) dhi = cap;
-            if (dlo > dhi) dlo = dhi;
-            h.seg.push_back(make_uint4(q, L, (uint32_t)dlo, (uint32_t)dhi));
+            h.seg.push_back(make_uint4(q, L, 0u, 0u));   // (the interval comes from the actual anchor: sp_interval)
             q += L;
         }
         if (h.seg.size() == n0) break;
@@ -535,15 +609,20 @@ static const SpPlanHost *sp_plan_get(uint32_t W, uint32_t P) {
         auto h = std::make_unique<SpPlanHost>();
         sp_plan_build(W, P, *h);
         if (!h->seg.empty()) {
-            if (hipMalloc((void **)&h->dseg, h->seg.size() * sizeof(uint4)) != hipSuccess) {
+            const size_t sb = h->seg.size() * sizeof(uint4), mb = h->mv.size() * sizeof(float2);
+            char *d = nullptr;
+            if (hipMalloc((void **)&d, sb + mb) != hipSuccess) {
                 (void)hipGetLastError();
                 return nullptr;   // (not cached: retried on the next call)
             }
-            if (hipMemcpy(h->dseg, h->seg.data(), h->seg.size() * sizeof(uint4), hipMemcpyHostToDevice) != hipSuccess) {
+            if (hipMemcpy(d, h->seg.data(), sb, hipMemcpyHostToDevice) != hipSuccess ||
+                hipMemcpy(d + sb, h->mv.data(), mb, hipMemcpyHostToDevice) != hipSuccess) {
                 (void)hipGetLastError();
-                (void)hipFree(h->dseg);
+                (void)hipFree(d);
                 return nullptr;
             }
+            h->dseg = reinterpret_cast<uint4 *>(d);
+            h->dmv = reinterpret_cast<float2 *>(d + sb);
         }
         slot = std::move(h);
     }
@@ -553,6 +632,7 @@ static const SpPlanHost *sp_plan_get(uint32_t W, uint32_t P) {
 static V2xSpPlan sp_plan_dev(const SpPlanHost &h) {
     V2xSpPlan p{};
     p.seg = h.dseg;
+    p.mv = h.dmv;
     p.W = h.W; p.nph = h.nph; p.nt = h.nt; p.qend = h.qend;
     for (int i = 0; i <= kSpPh; i++) p.ph[i] = h.ph[i];
     return p;

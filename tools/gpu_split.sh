@@ -13,6 +13,10 @@ for what in "$@"; do
     done ;;
   prof) PSS_EXACT_LOOKAHEAD=0 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- \
           python3 tools/bench_configs.py c5x > $O/prof.log 2>&1 || { echo "prof rc=$?"; tail -20 $O/prof.log; exit 1; } ;;
+  proflib:*) n=${what#proflib:}; PSS_LIB=build/ab/$n/libpss.so PSS_EXACT_LOOKAHEAD=0 timeout -k 10 300 rocprofv3 --kernel-trace --stats \
+          --output-format csv -d $O/prof_$n -o run -- python3 tools/bench_configs.py c5x > $O/prof_$n.log 2>&1 || { echo "prof rc=$?"; exit 1; } ;;
+  runlib:*) n=${what#runlib:}; PSS_LIB=build/ab/$n/libpss.so PSS_EXACT_LOOKAHEAD=0 timeout -k 10 200 \
+          python3 tools/bench_configs.py c5x > $O/run_$n.log 2>&1 || { echo "run rc=$?"; exit 1; } ;;
   esac
 done
 echo done
