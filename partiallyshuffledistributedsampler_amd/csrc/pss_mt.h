@@ -216,6 +216,10 @@ __device__ __forceinline__ uint32_t dpp_role(uint32_t x) {
     if constexpr (ROWMASK == 0xF) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xF, 0xF, true);
     else return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, ROWMASK, 0xF, false);
 }
+// lane l - 1's value (lane 0: 0) by a DPP wave shift, where a shuffle takes an LDS round trip
+__device__ __forceinline__ uint32_t wave_prev_lane(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x138, 0xF, 0xF, true);   // wave_shr:1
+}
 __device__ __forceinline__ uint32_t wave_role_scan(uint32_t x) {
     x = role_compose(x, dpp_role<0x111, 0xF>(x));
     x = role_compose(x, dpp_role<0x112, 0xF>(x));
@@ -247,7 +251,7 @@ __device__ __forceinline__ void pair_block(uint32_t word, bool valid, uint32_t W
         // offered k1: accepted -> k2 next, else k1; offered k2: accepted -> k1, else k2
         const uint32_t f = ((a1 != a2) ? 2u : 0u) | (a1 ? 1u : 0u);
         Fx = wave_role_scan(f);
-        const uint32_t Fp = (uint32_t)__shfl((int)Fx, lane > 0 ? lane - 1 : 0);
+        const uint32_t Fp = wave_prev_lane(Fx);
         role = lane ? role_apply(Fp, st) : st;
         const uint64_t m2 = __ballot(valid && role == 1u && a2);
         j = i2 + (uint32_t)__popcll(m2 & below);
@@ -284,7 +288,7 @@ __device__ __forceinline__ void pair_block(uint32_t word, bool valid, uint32_t W
     }
     i1 += (uint32_t)__popcll(m1);
     i2 += (uint32_t)__popcll(m2);
-    st = role_apply((uint32_t)__shfl((int)Fx, 63), st);
+    st = role_apply((uint32_t)__builtin_amdgcn_readlane((int)Fx, 63), st);
 }
 
 template <class Emit>
@@ -477,7 +481,7 @@ __device__ void mt_draws_pair_wg(MtWgShared &sh, int cur, uint32_t W, uint32_t P
                 if (settled) {
                     const bool a2 = valid && rh < nlo;
                     const uint32_t Fx = wave_role_scan(((a1 != a2) ? 2u : 0u) | (a1 ? 1u : 0u));
-                    const uint32_t Fp = (uint32_t)__shfl((int)Fx, lane > 0 ? lane - 1 : 0);
+                    const uint32_t Fp = wave_prev_lane(Fx);
                     uint32_t c[4];
 #pragma unroll
                     for (uint32_t s0 = 0; s0 < 2; s0++) {

@@ -32,12 +32,13 @@
 // (included inside namespace pss)
 
 namespace {
-constexpr int kSpPh = 4;        // phases (re-anchored intervals) before the exact remainder
+constexpr int kSpPh = 10;       // phases (re-anchored intervals) before the exact remainder
 constexpr int kSpPieces = 14;   // pieces kept per (segment, start role)
 constexpr int kSpRec = 32;      // uint2 per segment record: pieces of role 0 | role 1, (lo, hi),
                                 // (count role 0, count role 1), (q, L)
 constexpr int kSpRecLoHi = 28, kSpRecCnt = 29, kSpRecQL = 30;
 constexpr uint32_t kSpOver = 0xFFFFFFFFu;
+constexpr double kSpCrossMargin = 300.0;   // a phase ends ahead of a crossing its intervals are wider than
 #ifndef PSS_SPLIT_K
 #define PSS_SPLIT_K 6.0
 #endif
@@ -66,13 +67,21 @@ __device__ __forceinline__ const V2xSpPlan &sp_plan(const V2xSp &a, uint32_t s) 
 }
 __device__ __forceinline__ uint32_t sp_phases(const V2xSpPlan &pl) { return pl.nph ? pl.nph : 1u; }
 
+// the wave's minimum, uniform: DPP row shifts and row broadcasts (lanes without a source keep
+// ~0), then lane 63 -- no LDS round trip (a shuffle per step cost ~100 clocks each)
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ uint32_t dpp_min_step(uint32_t x) {
+    const uint32_t y = (uint32_t)__builtin_amdgcn_update_dpp((int)0xFFFFFFFF, (int)x, CTRL, ROWMASK, 0xF, false);
+    return y < x ? y : x;
+}
 __device__ __forceinline__ uint32_t wave_min_u32(uint32_t x) {
-#pragma unroll
-    for (int o = 32; o; o >>= 1) {
-        const uint32_t y = (uint32_t)__shfl_xor((int)x, o);
-        x = y < x ? y : x;
-    }
-    return x;
+    x = dpp_min_step<0x111, 0xF>(x);
+    x = dpp_min_step<0x112, 0xF>(x);
+    x = dpp_min_step<0x114, 0xF>(x);
+    x = dpp_min_step<0x118, 0xF>(x);
+    x = dpp_min_step<0x142, 0xA>(x);
+    x = dpp_min_step<0x143, 0xC>(x);
+    return (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
 }
 
 // pair_block's verdicts for one full block at one start (st, i2), without emitting: advances
@@ -91,7 +100,7 @@ __device__ __forceinline__ void pair_eval(uint32_t word, uint32_t W, uint32_t P,
         a2 = rr < n2;
         const uint32_t f = ((a1 != a2) ? 2u : 0u) | (a1 ? 1u : 0u);
         Fx = wave_role_scan(f);
-        const uint32_t Fp = (uint32_t)__shfl((int)Fx, lane > 0 ? lane - 1 : 0);
+        const uint32_t Fp = wave_prev_lane(Fx);
         role = lane ? role_apply(Fp, st) : st;
         const uint64_t m2 = __ballot(role == 1u && a2);
         j = i2 + (uint32_t)__popcll(m2 & below);
@@ -123,7 +132,7 @@ __device__ __forceinline__ void pair_eval(uint32_t word, uint32_t W, uint32_t P,
     }
     delta = wave_min_u32(lim);
     i2 += (uint32_t)__popcll(__ballot(role == 1u && a2));
-    st = role_apply((uint32_t)__shfl((int)Fx, 63), st);
+    st = role_apply((uint32_t)__builtin_amdgcn_readlane((int)Fx, 63), st);
 }
 }  // namespace
 
@@ -248,8 +257,17 @@ __global__ __launch_bounds__(256) void k_v2x_sp_lvl1(V2xSp a, uint32_t phase) {
         const uint32_t *wsrc = a.words + (size_t)s * a.nwp + sg.x;
         uint32_t n = 1u;
         bool over = false;
+        uint32_t w8[8];   // the next 8 blocks' words, loaded together
         for (uint32_t bq = 0; bq < sg.y && !over; bq += 64u) {
-            const uint32_t word = mt_temper(wsrc[bq + (uint32_t)lane]);
+            const uint32_t u8 = (bq >> 6) & 7u;
+            if (u8 == 0u) {
+#pragma unroll
+                for (int u = 0; u < 8; u++) w8[u] = bq + 64u * u < sg.y ? wsrc[bq + 64u * u + (uint32_t)lane] : 0u;
+            }
+            uint32_t wr = w8[0];
+#pragma unroll
+            for (int u = 1; u < 8; u++) wr = u8 == (uint32_t)u ? w8[u] : wr;
+            const uint32_t word = mt_temper(wr);
             uint32_t na = 0u, nst = 0u, nc = 0u, nn = 0u, lstl = 0u, lcl = 0u;
             for (uint32_t i = 0; i < n && !over; i++) {
                 uint32_t ba = (uint32_t)__builtin_amdgcn_readlane((int)la, (int)i);
@@ -263,7 +281,9 @@ __global__ __launch_bounds__(256) void k_v2x_sp_lvl1(V2xSp a, uint32_t phase) {
                     const uint32_t e = d >= bb - ba ? bb : ba + d;
                     const uint32_t c2 = j2 - ba;
                     if (!(nn && lstl == st2 && lcl == c2)) {   // else: the last piece extends to e
-                        if (nn == 64u) { over = true; break; }
+                        // (far more pieces than a record keeps -- a bound crossing a power of two
+                        // inside the segment makes one per k2 word -- : the walk runs it exactly)
+                        if (nn == (uint32_t)kSpPieces + 8u) { over = true; break; }
                         if ((uint32_t)lane == nn) { na = ba; nst = st2; nc = c2; }
                         nn++;
                         lstl = st2;
@@ -383,10 +403,23 @@ __global__ __launch_bounds__(64) void k_v2x_sp_walk(V2xSp a, uint32_t phase) {
                 pk[r][q] = e.y;
             }
         }
+        // the batch's largest piece count bounds the lookups (uniform)
+        uint32_t nmax = 1u;
+        {
+            const uint32_t m0 = ul < nb && c0 <= (uint32_t)kSpPieces ? c0 : 1u, m1 = ul < nb && c1 <= (uint32_t)kSpPieces ? c1 : 1u;
+            uint32_t mm = m0 > m1 ? m0 : m1;
+#pragma unroll
+            for (int o = 32; o; o >>= 1) {
+                const uint32_t y = (uint32_t)__shfl_xor((int)mm, o);
+                mm = y > mm ? y : mm;
+            }
+            nmax = (uint32_t)__builtin_amdgcn_readfirstlane((int)mm);
+        }
         auto lookup = [&](uint32_t r, uint32_t j) {   // the transfer (role | c << 1) of the piece holding j
             uint32_t t = r ? pk[1][0] : pk[0][0];
 #pragma unroll
             for (int q = 1; q < kSpPieces; q++) {
+                if ((uint32_t)q >= nmax) break;
                 const uint32_t aq = r ? pa[1][q] : pa[0][q];
                 t = aq <= j ? (r ? pk[1][q] : pk[0][q]) : t;
             }
@@ -406,18 +439,21 @@ __global__ __launch_bounds__(64) void k_v2x_sp_walk(V2xSp a, uint32_t phase) {
             const uint32_t r0 = p0 & 1u, r1 = p1 & 1u;
             uint32_t tF = act ? (r0 == r1 ? 2u | r0 : r0) : 0u;
             uint32_t t0 = act ? p0 >> 1 : 0u, t1 = act ? p1 >> 1 : 0u;
-#pragma unroll
-            for (int d = 1; d < 64; d <<= 1) {   // inclusive scan: (earlier) then (this)
-                const uint32_t pF = (uint32_t)__shfl_up((int)tF, d), q0c = (uint32_t)__shfl_up((int)t0, d);
-                const uint32_t q1c = (uint32_t)__shfl_up((int)t1, d);
-                if (lane >= d) {
-                    const uint32_t a0 = role_apply(pF, 0u), a1 = role_apply(pF, 1u);
-                    const uint32_t n0 = q0c + (a0 ? t1 : t0), n1 = q1c + (a1 ? t1 : t0);
-                    tF = role_compose(tF, pF);
-                    t0 = n0;
-                    t1 = n1;
-                }
-            }
+            // inclusive scan, (earlier) then (this), on DPP row shifts and row broadcasts (lanes
+            // without a source read the identity, 0): no LDS round trip per step
+            auto step = [&](uint32_t pF, uint32_t q0c, uint32_t q1c) {
+                const uint32_t a0 = role_apply(pF, 0u), a1 = role_apply(pF, 1u);
+                const uint32_t n0 = q0c + (a0 ? t1 : t0), n1 = q1c + (a1 ? t1 : t0);
+                tF = role_compose(tF, pF);
+                t0 = n0;
+                t1 = n1;
+            };
+            step(dpp_role<0x111, 0xF>(tF), dpp_role<0x111, 0xF>(t0), dpp_role<0x111, 0xF>(t1));
+            step(dpp_role<0x112, 0xF>(tF), dpp_role<0x112, 0xF>(t0), dpp_role<0x112, 0xF>(t1));
+            step(dpp_role<0x114, 0xF>(tF), dpp_role<0x114, 0xF>(t0), dpp_role<0x114, 0xF>(t1));
+            step(dpp_role<0x118, 0xF>(tF), dpp_role<0x118, 0xF>(t0), dpp_role<0x118, 0xF>(t1));
+            step(dpp_role<0x142, 0xA>(tF), dpp_role<0x142, 0xA>(t0), dpp_role<0x142, 0xA>(t1));
+            step(dpp_role<0x143, 0xC>(tF), dpp_role<0x143, 0xC>(t0), dpp_role<0x143, 0xC>(t1));
             const uint32_t eF = (uint32_t)__shfl_up((int)tF, 1), e0 = (uint32_t)__shfl_up((int)t0, 1);
             const uint32_t e1 = (uint32_t)__shfl_up((int)t1, 1);
             const uint32_t bst = ul == f ? st : role_apply(eF, st);
@@ -527,8 +563,14 @@ __global__ __launch_bounds__(256) void k_v2x_sp_emit(V2xSp a) {
         else k1[i] = r;
     };
     uint32_t st = st0.x, i2 = st0.y, i1 = i2 + st;
-    for (uint32_t bq = 0; bq < sg.y && i2 < W; bq += 64u)
-        pair_block(mt_temper(wsrc[bq + (uint32_t)lane]), true, W, P, kb1, st, i1, i2, emit);
+    for (uint32_t bq = 0; bq < sg.y && i2 < W; bq += 512u) {   // 8 blocks' words loaded together
+        uint32_t w8[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) w8[u] = bq + 64u * u < sg.y ? wsrc[bq + 64u * u + (uint32_t)lane] : 0u;
+#pragma unroll
+        for (int u = 0; u < 8; u++)
+            if (bq + 64u * u < sg.y && i2 < W) pair_block(mt_temper(w8[u]), true, W, P, kb1, st, i1, i2, emit);
+    }
 }
 
 namespace {
@@ -584,6 +626,16 @@ static void sp_plan_build(uint32_t W, uint32_t P, SpPlanHost &h) {
             uint32_t L = 4096;
             while (L > 64 && splits(L) > PSS_SPLIT_TARGET) L >>= 1;
             if (splits(L) > 2.0 * PSS_SPLIT_TARGET || (double)je + m + L >= (double)W - 64.0) break;
+            // The bound W - j crossing a power of two inside a segment changes the bit length of
+            // every later k2 word, at a point that moves with the start: about one piece per k2
+            // word, far more than a record keeps.  So a phase ends ahead of each crossing (the next
+            // one re-anchors there, its intervals narrow again) and the segments whose intervals
+            // still straddle a crossing are one block long (their exact runs in the walk are short).
+            const double jlo = (double)je - m > 0.0 ? (double)je - m : 0.0, jhi = (double)je + m + L / 2.0 + 1.0;
+            if (sp_bitlen((uint64_t)((double)W - jlo)) != sp_bitlen((uint64_t)std::max(1.0, (double)W - jhi))) {
+                if (m > kSpCrossMargin && h.seg.size() > n0) break;
+                L = 64;
+            }
             h.seg.push_back(make_uint4(q, L, 0u, 0u));   // (the interval comes from the actual anchor: sp_interval)
             q += L;
         }
