@@ -1118,18 +1118,44 @@ static bool v2x_draws_split(const V2xGeo &x, int64_t epoch, uint32_t *slot, uint
     a.anc = scratch + w_words + w_rec + w_ss;
     a.K1 = slot;
     a.K2 = slot + x.ns;
-    const uint32_t tail_blocks = (x.P + 63u) / 64u;
-#ifdef PSS_DIAG_SP_TAIL_APART   // timing build: the tail draws in a launch of their own after the generators
-    hipLaunchKernelGGL(k_v2x_sp_gen, dim3(x.S), dim3(kSpGenThreads), 0, s, a, x, epoch);
-    hipLaunchKernelGGL(k_v2x_tail_draws, dim3(tail_blocks), dim3(64), 0, s, x, epoch, tail_blocks, (uint64_t)0, slot);
-#else
-    hipLaunchKernelGGL(k_v2x_sp_gen, dim3(x.S + (tail_blocks + 3u) / 4u), dim3(kSpGenThreads), 0, s, a, x, epoch);
-#endif
+    const uint32_t tail_blocks = (x.P + 63u) / 64u, tail_wg = (tail_blocks + 3u) / 4u;
     const uint32_t nph = std::max(std::max(hb->nph, 1u), std::max(hl->nph, 1u));
+    // the twists phase p needs: up to its last segment's end, all of them for a window's last
+    // phase (its walk runs the remainder)
+    uint32_t need[kSpPh] = {};
+    for (uint32_t p = 0; p < nph; p++)
+        for (const SpPlanHost *h : {hb, hl}) {
+            uint32_t n = h->nt;
+            if (p + 1u < std::max(h->nph, 1u)) {
+                const uint4 sg = h->seg[h->ph[p + 1] - 1u];
+                n = std::min(h->nt, (sg.x + sg.y + (uint32_t)kMtN - 1u) / (uint32_t)kMtN);
+            }
+            need[p] = std::max(need[p], n);
+        }
+    for (uint32_t p = 1; p < nph; p++) need[p] = std::max(need[p], need[p - 1]);
+    SpSide *side = sp_side();
+    std::unique_lock<std::mutex> lk;
+    if (side) {   // generator chunks on the side stream, each phase waits for the words it reads
+        lk = std::unique_lock<std::mutex>(side->mu);
+        (void)hipEventRecord(side->start, s);   // (the scratch is the previous call's decode arrays)
+        (void)hipStreamWaitEvent(side->g, side->start, 0);
+        uint32_t t = 0;
+        for (uint32_t p = 0; p < nph; p++) {
+            if (need[p] > t || p == 0) {
+                hipLaunchKernelGGL(k_v2x_sp_gen, dim3(x.S + (t == 0 ? tail_wg : 0u)), dim3(kSpGenThreads), 0, side->g,
+                                   a, x, epoch, t, need[p]);
+                t = need[p];
+            }
+            (void)hipEventRecord(side->ev[p], side->g);
+        }
+    } else {
+        hipLaunchKernelGGL(k_v2x_sp_gen, dim3(x.S + tail_wg), dim3(kSpGenThreads), 0, s, a, x, epoch, 0u, need[nph - 1]);
+    }
     for (uint32_t p = 0; p < nph; p++) {
         uint32_t segs = 0;
         for (const SpPlanHost *h : {hb, hl})
             if (p < h->nph) segs = std::max(segs, h->ph[p + 1] - h->ph[p]);
+        if (side) (void)hipStreamWaitEvent(s, side->ev[p], 0);
         if (segs) hipLaunchKernelGGL(k_v2x_sp_lvl1, dim3((2u * segs + 3u) / 4u, x.S), dim3(256), 0, s, a, p);
         hipLaunchKernelGGL(k_v2x_sp_walk, dim3(x.S), dim3(64), 0, s, a, p);
     }

@@ -145,7 +145,11 @@ __device__ __forceinline__ void pair_eval(uint32_t word, uint32_t W, uint32_t P,
 // (One wave over the whole state ran ~1200 clocks a twist, four waves stepping 227 words at a
 // time with a barrier per step ~900: 2.9 / 2.2 ms for C5's 5.7K twists a window.)
 constexpr int kSpGenThreads = 256;
-__global__ __launch_bounds__(kSpGenThreads) void k_v2x_sp_gen(V2xSp a, V2xGeo x, int64_t epoch) {
+// Twists [t0, t1) of every window (a chunk: the phases that need only the words before t1 run
+// while later chunks are generated); the first chunk seeds and carries the tail draws, a later one
+// resumes from the last twist's words (the state).
+__global__ __launch_bounds__(kSpGenThreads) void k_v2x_sp_gen(V2xSp a, V2xGeo x, int64_t epoch, uint32_t t0,
+                                                              uint32_t t1) {
     __shared__ uint32_t sm[4 * kMtN];   // a window's double-buffered state, or four tail waves' MT
     const uint32_t b = blockIdx.x;
     const int tid = threadIdx.x;
@@ -155,20 +159,29 @@ __global__ __launch_bounds__(kSpGenThreads) void k_v2x_sp_gen(V2xSp a, V2xGeo x,
         if (j0 < x.P) v2x_tail_block(x, epoch, 0u, j0, a.K1, sm + kMtN * wv);
         return;
     }
-    // the generator is a latency chain: it issues first on its SIMDs
-    __builtin_amdgcn_s_setprio(3);
     const uint32_t s = b;
     const V2xSpPlan &pl = sp_plan(a, s);
-    if (wv == 0) mt_seed_int(sm, s == 0 ? epoch + 2 : epoch + (int64_t)(s - 1) * 10000);
+    if (t0 == 0 && tid < 4) a.anc[(size_t)s * (kSpPh + 1) * 4 + tid] = 0u;   // phase 0 starts at (k1, 0)
+    if (t1 > pl.nt) t1 = pl.nt;
+    if (t0 >= t1) return;
+    // the generator is a latency chain: it issues first on its SIMDs
+    __builtin_amdgcn_s_setprio(3);
+    uint32_t *wbase = a.words + (size_t)s * a.nwp;
+    uint32_t *sm0 = sm + (t0 & 1u) * kMtN;   // the state the first twist reads
+    if (t0 == 0) {
+        if (wv == 0) mt_seed_int(sm0, s == 0 ? epoch + 2 : epoch + (int64_t)(s - 1) * 10000);
+    } else {
+        for (int i = tid; i < kMtN; i += kSpGenThreads) sm0[i] = wbase[(size_t)(t0 - 1u) * kMtN + (uint32_t)i];
+    }
     __syncthreads();
     constexpr int D = kMtN - kMtM;   // 227
     const bool own = tid < D, own2 = tid < kMtN - 2 * D;   // words t, t + 227 (all), t + 454 (t < 170)
     const bool last = tid == kMtN - 1 - 2 * D;            // t = 169: word 623
     uint32_t o0 = 0u, o1 = 0u, o2 = 0u;
-    if (own) { o0 = sm[tid]; o1 = sm[tid + D]; }
-    if (own2) o2 = sm[tid + 2 * D];
-    uint32_t *dst = a.words + (size_t)s * a.nwp + (uint32_t)tid;
-    for (uint32_t t = 0; t < pl.nt; t++) {
+    if (own) { o0 = sm0[tid]; o1 = sm0[tid + D]; }
+    if (own2) o2 = sm0[tid + 2 * D];
+    uint32_t *dst = wbase + (uint32_t)tid;
+    for (uint32_t t = t0; t < t1; t++) {
         const uint32_t *st = sm + (t & 1u) * kMtN;        // the previous twist's words
         uint32_t *sn = sm + ((t + 1u) & 1u) * kMtN;
         if (own) {
@@ -191,7 +204,6 @@ __global__ __launch_bounds__(kSpGenThreads) void k_v2x_sp_gen(V2xSp a, V2xGeo x,
         }
         __syncthreads();
     }
-    if (tid < 4) a.anc[(size_t)s * (kSpPh + 1) * 4 + tid] = 0u;
 }
 
 // the interval of a segment's start: the expected k2 index after (q - qa) words from the
@@ -252,6 +264,10 @@ __global__ __launch_bounds__(256) void k_v2x_sp_lvl1(V2xSp a, uint32_t phase) {
     sp_interval(pl, ai2, sg.x - pl.seg[pl.ph[phase]].x, lo, hi);
     uint32_t cnt = kSpOver;
     uint32_t la = lo, lst = r0, lc = 0u;
+#ifdef PSS_DIAG_SP_PRINT
+    const uint64_t dg_t0 = __builtin_amdgcn_s_memtime();
+    uint32_t dg_evals = 0, dg_maxn = 0;
+#endif
     if (!aend) {
         const uint32_t W = pl.W, P = a.P, kb1 = a.kb1;
         const uint32_t *wsrc = a.words + (size_t)s * a.nwp + sg.x;
@@ -278,12 +294,15 @@ __global__ __launch_bounds__(256) void k_v2x_sp_lvl1(V2xSp a, uint32_t phase) {
                     uint32_t st2 = bst, j2 = ba + bc, d = 0u;
                     if (j2 + 64u >= W) { over = true; break; }
                     pair_eval(word, W, P, kb1, st2, j2, d);
+#ifdef PSS_DIAG_SP_PRINT
+                    dg_evals++;
+#endif
                     const uint32_t e = d >= bb - ba ? bb : ba + d;
                     const uint32_t c2 = j2 - ba;
                     if (!(nn && lstl == st2 && lcl == c2)) {   // else: the last piece extends to e
                         // (far more pieces than a record keeps -- a bound crossing a power of two
                         // inside the segment makes one per k2 word -- : the walk runs it exactly)
-                        if (nn == (uint32_t)kSpPieces + 8u) { over = true; break; }
+                        if (nn == (uint32_t)kSpPieces) { over = true; break; }
                         if ((uint32_t)lane == nn) { na = ba; nst = st2; nc = c2; }
                         nn++;
                         lstl = st2;
@@ -294,9 +313,20 @@ __global__ __launch_bounds__(256) void k_v2x_sp_lvl1(V2xSp a, uint32_t phase) {
                 }
             }
             la = na; lst = nst; lc = nc; n = nn;
+#ifdef PSS_DIAG_SP_PRINT
+            dg_maxn = n > dg_maxn ? n : dg_maxn;
+#endif
         }
         if (!over && n <= (uint32_t)kSpPieces) cnt = n;
     }
+#ifdef PSS_DIAG_SP_PRINT
+    {
+        const uint64_t dg = __builtin_amdgcn_s_memtime() - dg_t0;
+        if (lane == 0 && s == 0 && (dg > 200000u || (g & 255u) == 0u))
+            printf("sp_lvl1 phase %u g %u r0 %u L %u hi-lo %u evals %u maxn %u cnt %u clocks %lu\n", phase, g, r0, sg.y,
+                   hi - lo, dg_evals, dg_maxn, cnt, (unsigned long)dg);
+    }
+#endif
     const uint32_t base = r0 ? (uint32_t)kSpPieces : 0u;
     if (cnt != kSpOver && (uint32_t)lane < cnt) rec[base + (uint32_t)lane] = make_uint2(la, lst | (lc << 1));
     if (lane == 0) {
@@ -631,7 +661,8 @@ static void sp_plan_build(uint32_t W, uint32_t P, SpPlanHost &h) {
             // word, far more than a record keeps.  So a phase ends ahead of each crossing (the next
             // one re-anchors there, its intervals narrow again) and the segments whose intervals
             // still straddle a crossing are one block long (their exact runs in the walk are short).
-            const double jlo = (double)je - m > 0.0 ? (double)je - m : 0.0, jhi = (double)je + m + L / 2.0 + 1.0;
+            const double jlo = (double)je - 2.0 * m > 0.0 ? (double)je - 2.0 * m : 0.0;
+            const double jhi = (double)je + 2.0 * m + L / 2.0 + 1.0;
             if (sp_bitlen((uint64_t)((double)W - jlo)) != sp_bitlen((uint64_t)std::max(1.0, (double)W - jhi))) {
                 if (m > kSpCrossMargin && h.seg.size() > n0) break;
                 L = 64;
@@ -679,6 +710,34 @@ static const SpPlanHost *sp_plan_get(uint32_t W, uint32_t P) {
         slot = std::move(h);
     }
     return slot.get();
+}
+
+// per device: a stream for the generator chunks and their events (the phases on the caller's
+// stream wait on them); the mutex keeps one call's record / wait pairs together
+struct SpSide {
+    std::mutex mu;
+    hipStream_t g = nullptr;
+    hipEvent_t start = nullptr, ev[kSpPh + 1] = {};
+    bool ok = false;
+};
+static SpSide *sp_side() {
+    static std::mutex mu;
+    static std::map<int, std::unique_ptr<SpSide>> per;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    std::lock_guard<std::mutex> lk(mu);
+    auto &p = per[dev];
+    if (!p) {
+        p = std::make_unique<SpSide>();
+        int lo = 0, hi = 0;
+        bool ok = hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess &&
+                  hipStreamCreateWithPriority(&p->g, hipStreamNonBlocking, hi) == hipSuccess &&
+                  hipEventCreateWithFlags(&p->start, hipEventDisableTiming) == hipSuccess;
+        for (hipEvent_t &e : p->ev) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
+        if (!ok) (void)hipGetLastError();
+        p->ok = ok;
+    }
+    return p->ok ? p.get() : nullptr;
 }
 
 static V2xSpPlan sp_plan_dev(const SpPlanHost &h) {
