@@ -1133,7 +1133,15 @@ static bool v2x_draws_split(const V2xGeo &x, int64_t epoch, uint32_t *slot, uint
             need[p] = std::max(need[p], n);
         }
     for (uint32_t p = 1; p < nph; p++) need[p] = std::max(need[p], need[p - 1]);
+#ifdef PSS_DIAG_SP_TAIL_APART   // timing build: the generator alone on the caller's stream, then the tail
+    SpSide *side = nullptr;
+    hipLaunchKernelGGL(k_v2x_sp_gen, dim3(x.S), dim3(kSpGenThreads), 0, s, a, x, epoch, 0u, need[nph - 1]);
+    hipLaunchKernelGGL(k_v2x_tail_draws, dim3(tail_blocks), dim3(64), 0, s, x, epoch, tail_blocks, (uint64_t)0, slot);
+    const bool gen_done = true;
+#else
     SpSide *side = sp_side();
+    const bool gen_done = false;
+#endif
     std::unique_lock<std::mutex> lk;
     if (side) {   // generator chunks on the side stream, each phase waits for the words it reads
         lk = std::unique_lock<std::mutex>(side->mu);
@@ -1148,7 +1156,7 @@ static bool v2x_draws_split(const V2xGeo &x, int64_t epoch, uint32_t *slot, uint
             }
             (void)hipEventRecord(side->ev[p], side->g);
         }
-    } else {
+    } else if (!gen_done) {
         hipLaunchKernelGGL(k_v2x_sp_gen, dim3(x.S + tail_wg), dim3(kSpGenThreads), 0, s, a, x, epoch, 0u, need[nph - 1]);
     }
     for (uint32_t p = 0; p < nph; p++) {

@@ -235,6 +235,31 @@ def test_big_pool_exact_order_matches_rank_select_oracle(B):
     gpu.close()
 
 
+@pytest.mark.parametrize("B,ns_mult", [(300_007, 2.6), ((1 << 17) + 3, 4.3)])
+def test_split_draws_odd_pools_match_rank_select_oracle(B, ns_mult):
+    """The split draws of long pool2 windows (pss_v2split.h, DESIGN 4.4: per-segment piecewise
+    transfers, the guess-and-verify walk, phases re-anchored ahead of the power-of-two crossings
+    of the k2 bound) at pools that are not powers of two -- the k1 bound's acceptance is not 1/2,
+    so the plan's rates and the crossings differ from C5's -- with a last window of another
+    length (a second plan), over two consecutive epochs and an epoch jump (cold calls: the
+    split form; a prepared next epoch: the workgroup form).  == the exact oracle (V2:96-116)."""
+    R = 2
+    ns = int(ns_mult * B)
+    N, F = ns * R - 1, 53             # one pad id: the last rank's block wraps at N
+    lengths = np.full(F, N // F)
+    lengths[-1] += N - lengths.sum()
+    gpu = pss.IndexEngine(lengths, N, R, B, 2, device=0, shuffle=True, seed=11, order="exact")
+    assert gpu.num_samples == ns
+    for epoch in (3, 4, 9):
+        gpu.init_iter(epoch)
+        old, new = gpu.rank_starts()
+        a = _gen(gpu, 0, R).cpu().numpy()
+        for r in range(R):
+            ref = O.v2_exact_stream_rs(epoch, int(old[r]), int(new[r]), ns, B, N)
+            assert np.array_equal(a[r], ref), (B, epoch, r, int(np.argmax(a[r] != ref)))
+    gpu.close()
+
+
 def test_c5_pool_exact_order_equals_cpu_mode():
     """The same C5 pool (B = 2^20) through the product's CPU mode (Fenwick trees,
     pss_cpu.cpp): GPU == CPU mode bit for bit (both are checked against the rank-select oracle
