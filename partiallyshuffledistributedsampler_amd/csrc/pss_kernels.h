@@ -159,6 +159,11 @@ size_t v2_exact_ws_bytes(const Geometry &g, int32_t nr);
 size_t v2_exact_slot_bytes(const Geometry &g);
 int v2_exact_lookahead_depth(const Geometry &g);   // epochs drawn ahead (0: none)
 hipError_t launch_v2_exact_draws(const Geometry &g, int64_t epoch, uint32_t *slot, hipStream_t s);
+// V1's long windows drawn in the split form (pss_v2split.h; pss_v2exact.hip): false when the
+// workgroup form should run instead (scratch null: draws made ahead into a slot)
+bool v1x_draws_split(int64_t w_lo, uint32_t nj, uint32_t n_full, uint32_t n_last, uint32_t B, uint32_t nbk,
+                     int64_t epoch, uint32_t *J, uint32_t *BCNT, uint32_t *scratch, size_t scratch_words,
+                     bool wg_form, hipStream_t s);
 hipError_t launch_v2_exact(const Geometry &g, const RankDesc *ranks, int32_t rank_lo, int32_t nr,
                            int64_t pos_lo, int64_t count, int64_t epoch, int64_t *out, uint32_t *ws,
                            hipStream_t s, const MapArgs *mapped = nullptr, uint32_t *slot = nullptr);

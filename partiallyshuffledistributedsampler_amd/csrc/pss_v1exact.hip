@@ -216,7 +216,7 @@ __device__ __forceinline__ bool v1x_block(const V1xBig &b, uint32_t &slot, uint3
     return slot < b.nj;
 }
 
-__device__ __forceinline__ int v1x_len(const Geometry &g, int64_t w) {
+__host__ __device__ __forceinline__ int v1x_len(const Geometry &g, int64_t w) {
     const int64_t wb = w * g.B;
     return (int)(g.ns - wb < g.B ? g.ns - wb : g.B);
 }
@@ -683,6 +683,13 @@ static hipError_t v1x_big_draws(const Geometry &g, const V1xBig &b, int64_t epoc
         return e ? atoi(e) : -1;
     }();
     const bool wg = wg_env == 0 || wg_env == 1 ? wg_env == 1 : b.nj < 1024;
+    // a call's own single pass of few long windows: split over the chip (pss_v2split.h), the
+    // scratch being the pass's S, H and PART (free until the partition runs; a slot drawn ahead
+    // has none: b.S null)
+    if (b.S && b.j0 == 0 && (uint64_t)b.nj == (uint64_t)b.nw &&
+        v1x_draws_split(b.w_lo, b.nj, (uint32_t)v1x_len(g, b.w_lo), (uint32_t)v1x_len(g, b.w_lo + b.nw - 1), b.B,
+                        b.nbk, epoch, b.J, b.BCNT, b.S, (size_t)3 * b.nj * b.B, wg, s))
+        return hipGetLastError();
     if (wg) hipLaunchKernelGGL(k_v1x_draws32_wg, dim3(b.nj), dim3(kMtWgThreads), 0, s, g, b, epoch);
     else hipLaunchKernelGGL(k_v1x_draws32, dim3(b.nj), dim3(64), 0, s, g, b, epoch);
     return hipGetLastError();

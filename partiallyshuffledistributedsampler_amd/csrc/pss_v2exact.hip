@@ -1081,44 +1081,38 @@ static void v2x_draws(const V2xGeo &x, int64_t epoch, uint32_t *slot, hipStream_
     }
 }
 
-// The draws of a call that brings no slot, for long windows (pss_v2split.h): the windows' words
-// generated one wave each beside the tail draws, then the segments' pieces, the walk and the
-// emission spread over the chip, phase by phase.  Its scratch is the decode's arrays (free until
-// the tiles run); false (the workgroup form runs instead) when the geometry or the scratch does not
-// suit it.  PSS_V2X_SPLIT=0 / 1 forces the workgroup form / this one (where the scratch fits).
-static bool v2x_draws_split(const V2xGeo &x, int64_t epoch, uint32_t *slot, uint32_t *scratch,
-                            size_t scratch_words, hipStream_t s) {
+// PSS_EXACT_SPLIT=0 / 1: the exact orders' long-window draws in the workgroup form / in the split
+// form (pss_v2split.h) for any window length the scratch holds; by default the split form where
+// the workgroup form would run (few long windows) and the plan covers most of a window
+static int sp_env() {
     static const int env = [] {
-        const char *e = getenv("PSS_V2X_SPLIT");
+        const char *e = getenv("PSS_EXACT_SPLIT");
         return e ? atoi(e) : -1;
     }();
-    if (env == 0 || !x.S) return false;
-    if (env != 1 && !v2x_draws_wg((uint64_t)x.S, x.B)) return false;
-    const uint32_t Wl = x.T - (x.S - 1u) * x.B;
-    const SpPlanHost *hl = sp_plan_get(Wl, x.P);
-    const SpPlanHost *hb = x.S > 1 ? sp_plan_get(x.B, x.P) : hl;
-    if (!hl || !hb) return false;
-    // worth it where most of a full window's words fall in phases
-    if (env != 1 && (double)hb->qend < 0.5 * hb->words) return false;
-    V2xSp a{};
+    return env;
+}
+
+// Scratch layout and the launches of the split draws for a.S streams (windows): hb the plan of
+// windows 0 .. S-2, hl of the last one; x carries the V2 tail (V1: none).  false when the scratch
+// cannot hold it.
+template <bool kV1>
+static bool sp_launch(V2xSp a, const SpPlanHost *hb, const SpPlanHost *hl, const V2xGeo &x, int64_t epoch,
+                      uint32_t *scratch, size_t scratch_words, hipStream_t s) {
+    if (!scratch) return false;
     a.pl[0] = sp_plan_dev(*hb);
     a.pl[1] = sp_plan_dev(*hl);
-    a.S = x.S; a.B = x.B; a.P = x.P;
-    a.kb1 = 32u - (uint32_t)__builtin_clz(x.P);
     const size_t nseg = std::max(hb->seg.size(), hl->seg.size());
     a.nsegmax = (uint32_t)nseg;
     const size_t nwp = ((size_t)std::max(hb->nt, hl->nt) * kMtN + 3u) & ~(size_t)3u;
     a.nwp = (uint32_t)nwp;
-    const size_t w_words = (size_t)x.S * nwp, w_rec = (size_t)x.S * nseg * kSpRec * 2u;
-    const size_t w_ss = (size_t)x.S * nseg * 2u, w_anc = (size_t)x.S * (kSpPh + 1) * 4u;
+    const size_t w_words = (size_t)a.S * nwp, w_rec = (size_t)a.S * nseg * kSpRec * 2u;
+    const size_t w_ss = (size_t)a.S * nseg * 2u, w_anc = (size_t)a.S * (kSpPh + 1) * 4u;
     if (w_words + w_rec + w_ss + w_anc > scratch_words || nwp >= ((size_t)1 << 32)) return false;
     a.words = scratch;
     a.rec = reinterpret_cast<uint2 *>(scratch + w_words);
     a.ss = reinterpret_cast<uint2 *>(scratch + w_words + w_rec);
     a.anc = scratch + w_words + w_rec + w_ss;
-    a.K1 = slot;
-    a.K2 = slot + x.ns;
-    const uint32_t tail_blocks = (x.P + 63u) / 64u, tail_wg = (tail_blocks + 3u) / 4u;
+    const uint32_t tail_blocks = kV1 ? 0u : (x.P + 63u) / 64u, tail_wg = (tail_blocks + 3u) / 4u;
     const uint32_t nph = std::max(std::max(hb->nph, 1u), std::max(hl->nph, 1u));
     // the twists phase p needs: up to its last segment's end, all of them for a window's last
     // phase (its walk runs the remainder)
@@ -1135,8 +1129,9 @@ static bool v2x_draws_split(const V2xGeo &x, int64_t epoch, uint32_t *slot, uint
     for (uint32_t p = 1; p < nph; p++) need[p] = std::max(need[p], need[p - 1]);
 #ifdef PSS_DIAG_SP_TAIL_APART   // timing build: the generator alone on the caller's stream, then the tail
     SpSide *side = nullptr;
-    hipLaunchKernelGGL(k_v2x_sp_gen, dim3(x.S), dim3(kSpGenThreads), 0, s, a, x, epoch, 0u, need[nph - 1]);
-    hipLaunchKernelGGL(k_v2x_tail_draws, dim3(tail_blocks), dim3(64), 0, s, x, epoch, tail_blocks, (uint64_t)0, slot);
+    hipLaunchKernelGGL(k_v2x_sp_gen<kV1>, dim3(a.S), dim3(kSpGenThreads), 0, s, a, x, epoch, 0u, need[nph - 1]);
+    if (tail_blocks)
+        hipLaunchKernelGGL(k_v2x_tail_draws, dim3(tail_blocks), dim3(64), 0, s, x, epoch, tail_blocks, (uint64_t)0, a.K1);
     const bool gen_done = true;
 #else
     SpSide *side = sp_side();
@@ -1150,25 +1145,77 @@ static bool v2x_draws_split(const V2xGeo &x, int64_t epoch, uint32_t *slot, uint
         uint32_t t = 0;
         for (uint32_t p = 0; p < nph; p++) {
             if (need[p] > t || p == 0) {
-                hipLaunchKernelGGL(k_v2x_sp_gen, dim3(x.S + (t == 0 ? tail_wg : 0u)), dim3(kSpGenThreads), 0, side->g,
-                                   a, x, epoch, t, need[p]);
+                hipLaunchKernelGGL(k_v2x_sp_gen<kV1>, dim3(a.S + (t == 0 ? tail_wg : 0u)), dim3(kSpGenThreads), 0,
+                                   side->g, a, x, epoch, t, need[p]);
                 t = need[p];
             }
             (void)hipEventRecord(side->ev[p], side->g);
         }
     } else if (!gen_done) {
-        hipLaunchKernelGGL(k_v2x_sp_gen, dim3(x.S + tail_wg), dim3(kSpGenThreads), 0, s, a, x, epoch, 0u, need[nph - 1]);
+        hipLaunchKernelGGL(k_v2x_sp_gen<kV1>, dim3(a.S + tail_wg), dim3(kSpGenThreads), 0, s, a, x, epoch, 0u,
+                           need[nph - 1]);
     }
     for (uint32_t p = 0; p < nph; p++) {
         uint32_t segs = 0;
         for (const SpPlanHost *h : {hb, hl})
             if (p < h->nph) segs = std::max(segs, h->ph[p + 1] - h->ph[p]);
         if (side) (void)hipStreamWaitEvent(s, side->ev[p], 0);
-        if (segs) hipLaunchKernelGGL(k_v2x_sp_lvl1, dim3((2u * segs + 3u) / 4u, x.S), dim3(256), 0, s, a, p);
-        hipLaunchKernelGGL(k_v2x_sp_walk, dim3(x.S), dim3(64), 0, s, a, p);
+        const uint32_t items = kV1 ? segs : 2u * segs;   // (V1: one role)
+        if (segs) hipLaunchKernelGGL(k_v2x_sp_lvl1<kV1>, dim3((items + 3u) / 4u, a.S), dim3(256), 0, s, a, p);
+        hipLaunchKernelGGL(k_v2x_sp_walk<kV1>, dim3(a.S), dim3(64), 0, s, a, p);
     }
-    if (nseg) hipLaunchKernelGGL(k_v2x_sp_emit, dim3((uint32_t)((nseg + 3u) / 4u), x.S), dim3(256), 0, s, a);
+    if (nseg) hipLaunchKernelGGL(k_v2x_sp_emit<kV1>, dim3((uint32_t)((nseg + 3u) / 4u), a.S), dim3(256), 0, s, a);
+    if (kV1)
+        hipLaunchKernelGGL(k_v1x_sp_count, dim3((uint32_t)((std::max(hb->W, hl->W) + kSpCountPer - 1u) / kSpCountPer), a.S),
+                           dim3(256), 0, s, a);
     return true;
+}
+
+// The draws of a call that brings no slot, for long windows (pss_v2split.h): the windows' words
+// generated beside the tail draws, then the segments' pieces, the walk and the emission spread
+// over the chip, phase by phase.  Its scratch is the decode's arrays (free until the tiles run);
+// false (the workgroup form runs instead) when the geometry or the scratch does not suit it.
+static bool v2x_draws_split(const V2xGeo &x, int64_t epoch, uint32_t *slot, uint32_t *scratch,
+                            size_t scratch_words, hipStream_t s) {
+    const int env = sp_env();
+    if (env == 0 || !x.S) return false;
+    if (env != 1 && !v2x_draws_wg((uint64_t)x.S, x.B)) return false;
+    const uint32_t Wl = x.T - (x.S - 1u) * x.B;
+    const SpPlanHost *hl = sp_plan_get(Wl, x.P, false);
+    const SpPlanHost *hb = x.S > 1 ? sp_plan_get(x.B, x.P, false) : hl;
+    if (!hl || !hb) return false;
+    // worth it where most of a full window's words fall in phases
+    if (env != 1 && (double)hb->qend < 0.5 * hb->words) return false;
+    V2xSp a{};
+    a.S = x.S; a.B = x.B; a.P = x.P;
+    a.kb1 = 32u - (uint32_t)__builtin_clz(x.P);
+    a.K1 = slot;
+    a.K2 = slot + x.ns;
+    return sp_launch<false>(a, hb, hl, x, epoch, scratch, scratch_words, s);
+}
+
+// V1 (pss_v1exact.hip v1x_big_draws): the draws of nj windows from w_lo (full ones of n_full
+// entries, the last of n_last) into J[job][B] and the bucket counts BCNT[job][nbk] (zeroed by the
+// caller), with the scratch given (null: none -- the draws made ahead into a slot); false: the
+// workgroup form runs instead
+bool v1x_draws_split(int64_t w_lo, uint32_t nj, uint32_t n_full, uint32_t n_last, uint32_t B, uint32_t nbk,
+                     int64_t epoch, uint32_t *J, uint32_t *BCNT, uint32_t *scratch, size_t scratch_words,
+                     bool wg_form, hipStream_t s) {
+    const int env = sp_env();
+    if (env == 0 || !nj || !scratch || n_full < 2) return false;
+    if (env != 1 && !wg_form) return false;
+    const SpPlanHost *hl = sp_plan_get(n_last, 0u, true);
+    const SpPlanHost *hb = nj > 1 ? sp_plan_get(n_full, 0u, true) : hl;
+    if (!hl || !hb) return false;
+    if (env != 1 && (double)hb->qend < 0.5 * hb->words) return false;
+    V2xSp a{};
+    a.S = nj; a.B = B; a.P = 0u; a.kb1 = 1u;
+    a.K1 = J;
+    a.K2 = BCNT;
+    a.w0 = w_lo;
+    a.nbk = nbk;
+    const V2xGeo x{};   // (no tail)
+    return sp_launch<true>(a, hb, hl, x, epoch, scratch, scratch_words, s);
 }
 
 // epochs drawn ahead: the few long windows of the workgroup form keep ~S CUs busy for

@@ -28,6 +28,9 @@
 //   emit     (one wave per segment) every segment again from its now known start, emitting draws.
 // The pieces are exact, so the draws are the reference's whatever the intervals: a bad estimate
 // only costs an exact run in the walk.
+// V1's long windows (kV1: pss_v1exact.hip's Fisher-Yates draws j = _randbelow(n - d), V1:165-171)
+// are the single-role case of the same machinery: every word serves a draw of bound n - d, the
+// stream ends after n - 1 draws, and the emission writes J[n - 1 - d] and the draw's bucket count.
 #pragma once
 // (included inside namespace pss)
 
@@ -60,8 +63,26 @@ struct V2xSp {
     uint2 *rec;                  // [window][nsegmax][kSpRec]
     uint2 *ss;                   // [window][nsegmax] start (role, j); role 2: the stream had ended
     uint32_t *anc;               // [window][kSpPh + 1][4]: (role, j, ended) at each phase's start
-    uint32_t *K1, *K2;           // the slot's draws
+    uint32_t *K1, *K2;           // the slot's draws (V1: J [window][B] and the bucket counts [window][nbk])
+    int64_t w0;                  // V1: the window of job 0
+    uint32_t nbk;                // V1: buckets per window
 };
+template <bool kV1>
+__device__ __forceinline__ uint32_t sp_nd(uint32_t W) { return kV1 ? (W ? W - 1u : 0u) : W; }   // draws of a stream
+
+// one block of a stream exactly, emitting (the lanes below nval hold words): V2's pair_block, or
+// V1's draw_block at draw i2 (bound W - d)
+template <bool kV1, class Emit>
+__device__ __forceinline__ void sp_block(uint32_t word, uint32_t nval, uint32_t W, uint32_t P, uint32_t kb1,
+                                         uint32_t &st, uint32_t &i1, uint32_t &i2, Emit &emit) {
+    if constexpr (kV1) {
+        auto bound = [&](uint32_t d) { return W - d; };
+        auto em = [&](uint32_t d, uint32_t r) { emit(true, d, r); };
+        i2 += draw_block(word, (int)nval, i2, sp_nd<true>(W), bound, em);
+    } else {
+        pair_block(word, (uint32_t)(threadIdx.x & 63) < nval, W, P, kb1, st, i1, i2, emit);
+    }
+}
 __device__ __forceinline__ const V2xSpPlan &sp_plan(const V2xSp &a, uint32_t s) {
     return a.pl[s + 1u == a.S ? 1 : 0];
 }
@@ -134,6 +155,41 @@ __device__ __forceinline__ void pair_eval(uint32_t word, uint32_t W, uint32_t P,
     i2 += (uint32_t)__popcll(__ballot(role == 1u && a2));
     st = role_apply((uint32_t)__builtin_amdgcn_readlane((int)Fx, 63), st);
 }
+// V1: one block's draws at draw index i2 (bound W - d, a single role), without emitting: advances
+// i2 and returns the largest shift under which every verdict stays (as pair_eval's k2 lanes)
+__device__ __forceinline__ void draw_eval(uint32_t word, uint32_t W, uint32_t &i2, uint32_t &delta) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t below = lanemask_lt();
+    uint32_t j = 0;
+    bool acc = false;
+    // lane l's draw index lies in [i2, i2 + l]: where every verdict is the same over its range, one pass
+    const uint32_t jl = i2 + (uint32_t)lane;
+    const uint32_t nhi = i2 < W ? W - i2 : 1u, nlo = jl < W ? W - jl : 1u;
+    const uint32_t kbh = 32u - (uint32_t)__builtin_clz(nhi);
+    const uint32_t rh = word >> (32u - kbh);
+    const bool sure = kbh == 32u - (uint32_t)__builtin_clz(nlo) && (rh < nlo || rh >= nhi);
+    if (__ballot(!sure) == 0) {
+        acc = rh < nlo;
+        j = i2 + (uint32_t)__popcll(__ballot(acc) & below);
+    } else {
+        uint32_t jg = i2 + (uint32_t)lane / 2u;
+        for (;;) {
+            const uint32_t n2 = jg < W ? W - jg : 1u;
+            acc = (word >> (32u - (32u - (uint32_t)__builtin_clz(n2)))) < n2;
+            j = i2 + (uint32_t)__popcll(__ballot(acc) & below);
+            if (__ballot(j != jg) == 0) break;
+            jg = j;
+        }
+    }
+    const uint32_t n = j < W ? W - j : 1u;
+    const uint32_t kb = 32u - (uint32_t)__builtin_clz(n);
+    const uint32_t r = word >> (32u - kb);
+    uint32_t lim = n - (1u << (kb - 1u));
+    if (r < n && n - r - 1u < lim) lim = n - r - 1u;
+    if (j >= W) lim = 0u;
+    delta = wave_min_u32(lim);
+    i2 += (uint32_t)__popcll(__ballot(acc));
+}
 }  // namespace
 
 // ---- generation: a workgroup per window (its raw words), the tail draws on the other blocks ----
@@ -148,6 +204,7 @@ constexpr int kSpGenThreads = 256;
 // Twists [t0, t1) of every window (a chunk: the phases that need only the words before t1 run
 // while later chunks are generated); the first chunk seeds and carries the tail draws, a later one
 // resumes from the last twist's words (the state).
+template <bool kV1>
 __global__ __launch_bounds__(kSpGenThreads) void k_v2x_sp_gen(V2xSp a, V2xGeo x, int64_t epoch, uint32_t t0,
                                                               uint32_t t1) {
     __shared__ uint32_t sm[4 * kMtN];   // a window's double-buffered state, or four tail waves' MT
@@ -161,7 +218,8 @@ __global__ __launch_bounds__(kSpGenThreads) void k_v2x_sp_gen(V2xSp a, V2xGeo x,
     }
     const uint32_t s = b;
     const V2xSpPlan &pl = sp_plan(a, s);
-    if (t0 == 0 && tid < 4) a.anc[(size_t)s * (kSpPh + 1) * 4 + tid] = 0u;   // phase 0 starts at (k1, 0)
+    if (t0 == 0 && tid < 4)   // phase 0 starts at (k1, 0) -- V1: its one role, (1, 0)
+        a.anc[(size_t)s * (kSpPh + 1) * 4 + tid] = kV1 && tid == 0 ? 1u : 0u;
     if (t1 > pl.nt) t1 = pl.nt;
     if (t0 >= t1) return;
     // the generator is a latency chain: it issues first on its SIMDs
@@ -169,7 +227,16 @@ __global__ __launch_bounds__(kSpGenThreads) void k_v2x_sp_gen(V2xSp a, V2xGeo x,
     uint32_t *wbase = a.words + (size_t)s * a.nwp;
     uint32_t *sm0 = sm + (t0 & 1u) * kMtN;   // the state the first twist reads
     if (t0 == 0) {
-        if (wv == 0) mt_seed_int(sm0, s == 0 ? epoch + 2 : epoch + (int64_t)(s - 1) * 10000);
+        if (wv == 0) {
+            int64_t seed;
+            if constexpr (kV1) {   // V1:102,165-171: window w seeds epoch + w * 10000
+                const int64_t w = a.w0 + (int64_t)s;
+                seed = w == 0 ? epoch : epoch + w * 10000;
+            } else {               // V2:107-109,147
+                seed = s == 0 ? epoch + 2 : epoch + (int64_t)(s - 1) * 10000;
+            }
+            mt_seed_int(sm0, seed);
+        }
     } else {
         for (int i = tid; i < kMtN; i += kSpGenThreads) sm0[i] = wbase[(size_t)(t0 - 1u) * kMtN + (uint32_t)i];
     }
@@ -209,7 +276,7 @@ __global__ __launch_bounds__(kSpGenThreads) void k_v2x_sp_gen(V2xSp a, V2xGeo x,
 // the interval of a segment's start: the expected k2 index after (q - qa) words from the
 // phase's anchor A (the plan's table of expected words per step, linearly interpolated) +-
 // PSS_SPLIT_K standard deviations of the renewal count, + 16
-__device__ __forceinline__ void sp_interval(const V2xSpPlan &pl, uint32_t A, uint32_t dq, uint32_t &lo,
+__device__ __forceinline__ void sp_interval(const V2xSpPlan &pl, uint32_t A, uint32_t dq, bool v1, uint32_t &lo,
                                             uint32_t &hi) {
     const uint32_t nt = pl.W / 64u + 1u;   // table entries - 1
     auto at = [&](float j, float &m, float &v, float &e) {
@@ -240,7 +307,7 @@ __device__ __forceinline__ void sp_interval(const V2xSpPlan &pl, uint32_t A, uin
     const float m = (float)PSS_SPLIT_K * __builtin_sqrtf(var + 1.0f) / (ej > 1.0f ? ej : 1.0f) + 16.0f;
     const float flo = je - m, fhi = je + m + 1.0f;
     lo = flo > (float)A ? (uint32_t)flo : A;
-    const uint32_t cap = A + dq / 2u + 1u;   // at most one k2 per two words
+    const uint32_t cap = A + (v1 ? dq : dq / 2u) + 1u;   // at most one k2 per two words (V1: a draw a word)
     hi = fhi < (float)cap ? (uint32_t)fhi : cap;
     if (lo > hi) lo = hi;
 }
@@ -248,20 +315,22 @@ __device__ __forceinline__ void sp_interval(const V2xSpPlan &pl, uint32_t A, uin
 // ---- level 1: the pieces of one (segment, start role) per wave -------------------------------
 // The branch list lives across the lanes: lane i holds piece i's low end a_i, its role and its
 // count offset c_i (pieces are contiguous: piece i ends at a_{i+1} - 1, the last at hi).
+template <bool kV1>
 __global__ __launch_bounds__(256) void k_v2x_sp_lvl1(V2xSp a, uint32_t phase) {
     const uint32_t s = blockIdx.y;
     const V2xSpPlan &pl = sp_plan(a, s);
     if (phase >= pl.nph) return;
     const int lane = threadIdx.x & 63;
     const uint32_t item = blockIdx.x * 4u + (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const uint32_t g = pl.ph[phase] + item / 2u, r0 = item & 1u;
+    // (V1: one role -- the record's role-0 half stays empty)
+    const uint32_t g = pl.ph[phase] + (kV1 ? item : item / 2u), r0 = kV1 ? 1u : item & 1u;
     if (g >= pl.ph[phase + 1]) return;
     const uint32_t *an = a.anc + ((size_t)s * (kSpPh + 1) + phase) * 4;
     const uint32_t ai2 = an[1], aend = an[2];
     const uint4 sg = pl.seg[g];
     uint2 *rec = a.rec + ((size_t)s * a.nsegmax + g) * kSpRec;
     uint32_t lo, hi;
-    sp_interval(pl, ai2, sg.x - pl.seg[pl.ph[phase]].x, lo, hi);
+    sp_interval(pl, ai2, sg.x - pl.seg[pl.ph[phase]].x, kV1, lo, hi);
     uint32_t cnt = kSpOver;
     uint32_t la = lo, lst = r0, lc = 0u;
 #ifdef PSS_DIAG_SP_PRINT
@@ -292,8 +361,9 @@ __global__ __launch_bounds__(256) void k_v2x_sp_lvl1(V2xSp a, uint32_t phase) {
                 const uint32_t bc = (uint32_t)__builtin_amdgcn_readlane((int)lc, (int)i);
                 for (;;) {
                     uint32_t st2 = bst, j2 = ba + bc, d = 0u;
-                    if (j2 + 64u >= W) { over = true; break; }
-                    pair_eval(word, W, P, kb1, st2, j2, d);
+                    if (j2 + 64u >= sp_nd<kV1>(W)) { over = true; break; }
+                    if constexpr (kV1) draw_eval(word, W, j2, d);
+                    else pair_eval(word, W, P, kb1, st2, j2, d);
 #ifdef PSS_DIAG_SP_PRINT
                     dg_evals++;
 #endif
@@ -331,7 +401,8 @@ __global__ __launch_bounds__(256) void k_v2x_sp_lvl1(V2xSp a, uint32_t phase) {
     if (cnt != kSpOver && (uint32_t)lane < cnt) rec[base + (uint32_t)lane] = make_uint2(la, lst | (lc << 1));
     if (lane == 0) {
         reinterpret_cast<uint32_t *>(rec + kSpRecCnt)[r0] = cnt;
-        if (r0 == 0u) {
+        if (kV1) reinterpret_cast<uint32_t *>(rec + kSpRecCnt)[0] = kSpOver;
+        if (r0 == (kV1 ? 1u : 0u)) {
             rec[kSpRecLoHi] = make_uint2(lo, hi);
             rec[kSpRecQL] = make_uint2(sg.x, sg.y);
         }
@@ -339,6 +410,7 @@ __global__ __launch_bounds__(256) void k_v2x_sp_lvl1(V2xSp a, uint32_t phase) {
 }
 
 // ---- the walk: one wave per window over one phase's segments ----------------------------------
+template <bool kV1>
 __global__ __launch_bounds__(64) void k_v2x_sp_walk(V2xSp a, uint32_t phase) {
     __shared__ uint32_t mt[kMtN];
     const uint32_t s = blockIdx.x;
@@ -391,17 +463,18 @@ __global__ __launch_bounds__(64) void k_v2x_sp_walk(V2xSp a, uint32_t phase) {
         wave_lds_order();
     };
     // an exact run of segment words [q, q + L) from (st, i2), 8 blocks' words loaded at a time
+    const uint32_t nd = sp_nd<kV1>(W);
     auto run_exact = [&](uint32_t q, uint32_t L) {
         uint32_t i1 = i2 + st;
-        for (uint32_t bq = 0; bq < L && i2 < W; bq += 512u) {
+        for (uint32_t bq = 0; bq < L && i2 < nd; bq += 512u) {
             uint32_t w8[8];
 #pragma unroll
             for (int u = 0; u < 8; u++) w8[u] = bq + 64u * u < L ? wsrc[q + bq + 64u * u + (uint32_t)lane] : 0u;
 #pragma unroll
             for (int u = 0; u < 8; u++)
-                if (bq + 64u * u < L && i2 < W) pair_block(mt_temper(w8[u]), true, W, P, kb1, st, i1, i2, noemit);
+                if (bq + 64u * u < L && i2 < nd) sp_block<kV1>(mt_temper(w8[u]), 64u, W, P, kb1, st, i1, i2, noemit);
         }
-        if (i2 >= W) ended = 1u;
+        if (i2 >= nd) ended = 1u;
     };
 #ifdef PSS_DIAG_SP_PRINT   // timing / diagnostic build: passes and exact runs per walk
     uint32_t dg_pass = 0, dg_exact = 0;
@@ -536,13 +609,17 @@ __global__ __launch_bounds__(64) void k_v2x_sp_walk(V2xSp a, uint32_t phase) {
     const size_t t0 = (size_t)s * a.B;
     uint32_t *k1 = a.K1 + t0, *k2 = a.K2 + t0;
     auto emit = [&](bool second, uint32_t i, uint32_t r) {
-        if (second) k2[i] = r;
-        else k1[i] = r;
+        if constexpr (kV1) {   // J[n - 1 - d] (the buckets are counted afterwards: k_v1x_sp_count)
+            k1[W - 1u - i] = r;
+        } else {
+            if (second) k2[i] = r;
+            else k1[i] = r;
+        }
     };
     if (!ended) {
         uint32_t i1 = i2 + st, q = pl.qend;
         const uint32_t nw = pl.nt * (uint32_t)kMtN;
-        while (i2 < W && q < nw) {   // 8 blocks' words loaded at a time
+        while (i2 < nd && q < nw) {   // 8 blocks' words loaded at a time
             uint32_t w8[8];
 #pragma unroll
             for (int u = 0; u < 8; u++) {
@@ -551,30 +628,32 @@ __global__ __launch_bounds__(64) void k_v2x_sp_walk(V2xSp a, uint32_t phase) {
             }
 #pragma unroll
             for (int u = 0; u < 8; u++) {
-                if (i2 >= W || q >= nw) break;
+                if (i2 >= nd || q >= nw) break;
                 const uint32_t nval = nw - q < 64u ? nw - q : 64u;
                 const bool valid = (uint32_t)lane < nval;
-                pair_block(valid ? mt_temper(w8[u]) : 0u, valid, W, P, kb1, st, i1, i2, emit);
+                sp_block<kV1>(valid ? mt_temper(w8[u]) : 0u, nval, W, P, kb1, st, i1, i2, emit);
                 q += nval;
             }
         }
-        if (i2 < W) {   // past the generated words: the stream continues from its state (the last twist)
+        if (i2 < nd) {   // past the generated words: the stream continues from its state (the last twist)
             for (int i = lane; i < kMtN; i += 64) mt[i] = wsrc[nw - (uint32_t)kMtN + (uint32_t)i];
             wave_lds_order();
-            while (i2 < W) {
+            while (i2 < nd) {
                 mt_twist(mt);
-                for (int q0 = 0; q0 < kMtN && i2 < W; q0 += 64) {
+                for (int q0 = 0; q0 < kMtN && i2 < nd; q0 += 64) {
                     const int nval = kMtN - q0 < 64 ? kMtN - q0 : 64;
                     const bool valid = lane < nval;
-                    pair_block(valid ? mt_temper(mt[q0 + lane]) : 0u, valid, W, P, kb1, st, i1, i2, emit);
+                    sp_block<kV1>(valid ? mt_temper(mt[q0 + lane]) : 0u, (uint32_t)nval, W, P, kb1, st, i1, i2, emit);
                 }
             }
         }
     }
-    for (uint32_t u = W + (uint32_t)lane; u < a.B; u += 64u) k2[u] = 0u;   // padding steps
+    if (!kV1)
+        for (uint32_t u = W + (uint32_t)lane; u < a.B; u += 64u) k2[u] = 0u;   // padding steps
 }
 
 // ---- emission: one wave per segment from its start ---------------------------------------------
+template <bool kV1>
 __global__ __launch_bounds__(256) void k_v2x_sp_emit(V2xSp a) {
     const uint32_t s = blockIdx.y;
     const V2xSpPlan &pl = sp_plan(a, s);
@@ -589,17 +668,52 @@ __global__ __launch_bounds__(256) void k_v2x_sp_emit(V2xSp a) {
     const size_t t0 = (size_t)s * a.B;
     uint32_t *k1 = a.K1 + t0, *k2 = a.K2 + t0;
     auto emit = [&](bool second, uint32_t i, uint32_t r) {
-        if (second) k2[i] = r;
-        else k1[i] = r;
+        if constexpr (kV1) {   // J[n - 1 - d]
+            k1[W - 1u - i] = r;
+        } else {
+            if (second) k2[i] = r;
+            else k1[i] = r;
+        }
     };
+    const uint32_t nd = sp_nd<kV1>(W);
     uint32_t st = st0.x, i2 = st0.y, i1 = i2 + st;
-    for (uint32_t bq = 0; bq < sg.y && i2 < W; bq += 512u) {   // 8 blocks' words loaded together
+    for (uint32_t bq = 0; bq < sg.y && i2 < nd; bq += 512u) {   // 8 blocks' words loaded together
         uint32_t w8[8];
 #pragma unroll
         for (int u = 0; u < 8; u++) w8[u] = bq + 64u * u < sg.y ? wsrc[bq + 64u * u + (uint32_t)lane] : 0u;
 #pragma unroll
         for (int u = 0; u < 8; u++)
-            if (bq + 64u * u < sg.y && i2 < W) pair_block(mt_temper(w8[u]), true, W, P, kb1, st, i1, i2, emit);
+            if (bq + 64u * u < sg.y && i2 < nd) sp_block<kV1>(mt_temper(w8[u]), 64u, W, P, kb1, st, i1, i2, emit);
+    }
+}
+
+// V1: the draws' bucket counts (j >> 11 of J[1 .. n), pss_v1exact.hip kV1bShift) once J is
+// written -- per-draw atomics on a window's few hundred counters in the emission took 1.7 ms at C5;
+// here an LDS histogram per 16K entries, then one atomic per (workgroup, bucket)
+constexpr uint32_t kSpCountPer = 16384, kSpCountLds = 8192;
+__global__ __launch_bounds__(256) void k_v1x_sp_count(V2xSp a) {
+    __shared__ uint32_t h[kSpCountLds];
+    const uint32_t s = blockIdx.y;
+    const uint32_t n = sp_plan(a, s).W;
+    const uint32_t i0 = blockIdx.x * kSpCountPer;
+    if (i0 >= n) return;
+    const uint32_t *j = a.K1 + (size_t)s * a.B;
+    uint32_t *bc = a.K2 + (size_t)s * a.nbk;
+    const uint32_t i1 = i0 + kSpCountPer < n ? i0 + kSpCountPer : n;
+    const bool lds = a.nbk <= kSpCountLds;
+    if (lds) {
+        for (uint32_t b = threadIdx.x; b < a.nbk; b += 256u) h[b] = 0u;
+        __syncthreads();
+    }
+    for (uint32_t i = (i0 ? i0 : 1u) + threadIdx.x; i < i1; i += 256u) {
+        const uint32_t b = j[i] >> 11;
+        if (lds) atomicAdd(&h[b], 1u);
+        else atomicAdd(&bc[b], 1u);
+    }
+    if (lds) {
+        __syncthreads();
+        for (uint32_t b = threadIdx.x; b < a.nbk; b += 256u)
+            if (h[b]) atomicAdd(&bc[b], h[b]);
     }
 }
 
@@ -617,17 +731,17 @@ struct SpPlanHost {
 
 static uint32_t sp_bitlen(uint64_t n) { return n ? 64u - (uint32_t)__builtin_clzll(n) : 0u; }
 
-static void sp_plan_build(uint32_t W, uint32_t P, SpPlanHost &h) {
+static void sp_plan_build(uint32_t W, uint32_t P, bool v1, SpPlanHost &h) {
     h.W = W;
     const uint32_t kb1 = sp_bitlen(P);
-    const double a1 = (double)P / (double)(1ull << kb1);
+    const double a1 = v1 ? 1.0 : (double)P / (double)(1ull << kb1);   // (V1: no k1 draws)
     // words per step j (a k1 then a k2 draw at bound W - j) and their variance; running sums
     std::vector<double> M(W + 1), V(W + 1), E(W ? W : 1);
     M[0] = V[0] = 0.0;
     for (uint32_t j = 0; j < W; j++) {
         const uint32_t n = W - j;
         const double a2 = (double)n / (double)(1ull << sp_bitlen(n));
-        E[j] = 1.0 / a1 + 1.0 / a2;
+        E[j] = (v1 ? 0.0 : 1.0 / a1) + 1.0 / a2;
         M[j + 1] = M[j] + E[j];
         V[j + 1] = V[j] + (1.0 - a1) / (a1 * a1) + (1.0 - a2) / (a2 * a2);
     }
@@ -662,7 +776,7 @@ static void sp_plan_build(uint32_t W, uint32_t P, SpPlanHost &h) {
             // one re-anchors there, its intervals narrow again) and the segments whose intervals
             // still straddle a crossing are one block long (their exact runs in the walk are short).
             const double jlo = (double)je - 2.0 * m > 0.0 ? (double)je - 2.0 * m : 0.0;
-            const double jhi = (double)je + 2.0 * m + L / 2.0 + 1.0;
+            const double jhi = (double)je + 2.0 * m + (v1 ? (double)L : L / 2.0) + 1.0;
             if (sp_bitlen((uint64_t)((double)W - jlo)) != sp_bitlen((uint64_t)std::max(1.0, (double)W - jhi))) {
                 if (m > kSpCrossMargin && h.seg.size() > n0) break;
                 L = 64;
@@ -681,16 +795,16 @@ static void sp_plan_build(uint32_t W, uint32_t P, SpPlanHost &h) {
     h.nt = (uint32_t)std::ceil(nw / (double)kMtN);
 }
 
-static const SpPlanHost *sp_plan_get(uint32_t W, uint32_t P) {
+static const SpPlanHost *sp_plan_get(uint32_t W, uint32_t P, bool v1) {
     static std::mutex mu;
-    static std::map<std::tuple<int, uint32_t, uint32_t>, std::unique_ptr<SpPlanHost>> cache;
+    static std::map<std::tuple<int, uint32_t, uint32_t, bool>, std::unique_ptr<SpPlanHost>> cache;
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return nullptr;
     std::lock_guard<std::mutex> lk(mu);
-    auto &slot = cache[std::make_tuple(dev, W, P)];
+    auto &slot = cache[std::make_tuple(dev, W, P, v1)];
     if (!slot) {
         auto h = std::make_unique<SpPlanHost>();
-        sp_plan_build(W, P, *h);
+        sp_plan_build(W, P, v1, *h);
         if (!h->seg.empty()) {
             const size_t sb = h->seg.size() * sizeof(uint4), mb = h->mv.size() * sizeof(float2);
             char *d = nullptr;

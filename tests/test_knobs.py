@@ -11,7 +11,7 @@ tests/knob_worker.py in a child interpreter with the variable set before any GPU
                                        line on the caller's stream
   PSS_EXACT_LOOKAHEAD=0                no exact-order draw lookahead: every exact V2 call makes its
                                        own MT draws
-  PSS_V2X_SPLIT=0 / 1                  the exact V2 draws of a call without a prepared slot: the
+  PSS_EXACT_SPLIT=0 / 1                  the exact V2 draws of a call without a prepared slot: the
                                        workgroup form / the split form (pss_v2split.h) even for
                                        short windows (by default the split form for long windows)
   PSS_CPU_THREADS=1 / 3                host threads of the CPU mode
@@ -33,8 +33,8 @@ GPU_CASES = [
     ("exact", {"PSS_V1X_DRAWS_WG": "1", "PSS_V2X_DRAWS_WG": "1"}),
     ("exact", {"PSS_V1X_GRID2D": "1"}),
     ("exact", {"PSS_EXACT_LOOKAHEAD": "0"}),
-    ("exact", {"PSS_V2X_SPLIT": "0"}),
-    ("exact", {"PSS_V2X_SPLIT": "1", "PSS_EXACT_LOOKAHEAD": "0"}),
+    ("exact", {"PSS_EXACT_SPLIT": "0"}),
+    ("exact", {"PSS_EXACT_SPLIT": "1", "PSS_EXACT_LOOKAHEAD": "0"}),
     ("counter", {"PSS_V2_LOOKAHEAD": "0"}),
 ]
 CPU_CASES = [("cpu", {"PSS_CPU_THREADS": "1"}), ("cpu", {"PSS_CPU_THREADS": "3"})]
