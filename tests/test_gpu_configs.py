@@ -260,6 +260,43 @@ def test_split_draws_odd_pools_match_rank_select_oracle(B, ns_mult):
     gpu.close()
 
 
+def test_split_draws_two_engines_on_threads():
+    """Two engines on two host threads and two streams, each drawing cold exact epochs of long
+    pool2 windows at the same time: the split form (pss_v2split.h) shares one generator side
+    stream and its events per device, one call's record / wait pairs kept together by a mutex.
+    Epochs are not consecutive (no draws made ahead: every call draws for itself).  Each engine's
+    streams == the exact oracle (V2:96-116)."""
+    from concurrent.futures import ThreadPoolExecutor
+    B, R = 1 << 18, 2
+    ns = int(2.5 * B)
+    N, F = ns * R - 1, 31
+    lengths = np.full(F, N // F)
+    lengths[-1] += N - lengths.sum()
+    engs = [pss.IndexEngine(lengths, N, R, B, 2, device=0, shuffle=True, seed=sd, order="exact") for sd in (5, 6)]
+    streams = [torch.cuda.Stream(device=0) for _ in engs]
+
+    def run(k):
+        eng, st, res = engs[k], streams[k], []
+        for epoch in (11, 3, 40):
+            eng.init_iter(epoch)
+            old, new = eng.rank_starts()
+            out = eng.generate(0, R, stream=st)
+            st.synchronize()
+            eng.check(st)
+            res.append((epoch, old, new, out.cpu().numpy()))
+        return res
+
+    with ThreadPoolExecutor(2) as ex:
+        results = list(ex.map(run, range(2)))
+    for res in results:
+        for epoch, old, new, a in res:
+            for r in range(R):
+                ref = O.v2_exact_stream_rs(epoch, int(old[r]), int(new[r]), ns, B, N)
+                assert np.array_equal(a[r], ref), (epoch, r, int(np.argmax(a[r] != ref)))
+    for eng in engs:
+        eng.close()
+
+
 def test_c5_pool_exact_order_equals_cpu_mode():
     """The same C5 pool (B = 2^20) through the product's CPU mode (Fenwick trees,
     pss_cpu.cpp): GPU == CPU mode bit for bit (both are checked against the rank-select oracle
