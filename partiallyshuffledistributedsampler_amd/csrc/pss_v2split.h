@@ -43,7 +43,10 @@ constexpr int kSpRecLoHi = 28, kSpRecCnt = 29, kSpRecQL = 30;
 constexpr uint32_t kSpOver = 0xFFFFFFFFu;
 constexpr double kSpCrossMargin = 300.0;   // a phase ends ahead of a crossing its intervals are wider than
 #ifndef PSS_SPLIT_K
-#define PSS_SPLIT_K 6.0
+#define PSS_SPLIT_K 6.0      // interval margin in standard deviations (V2)
+#endif
+#ifndef PSS_SPLIT_K_V1
+#define PSS_SPLIT_K_V1 4.0   // (V1; same-box sweeps, profiles/r06/exact_split/sweep.txt)
 #endif
 #ifndef PSS_SPLIT_TARGET
 #define PSS_SPLIT_TARGET 2.0
@@ -53,6 +56,7 @@ struct V2xSpPlan {               // one window length
     const uint4 *seg;            // (q, L, -, -) per segment, phase after phase
     const float2 *mv;            // (expected words, their variance) to reach step 64 i, i <= W / 64 + 1
     uint32_t W, nph, nt, qend;   // k2 draws, phases, twists generated, first word of the remainder
+    float K;                     // interval margin, standard deviations
     uint32_t ph[kSpPh + 1];      // first segment of each phase; ph[nph] = segments
 };
 struct V2xSp {
@@ -304,7 +308,7 @@ __device__ __forceinline__ void sp_interval(const V2xSpPlan &pl, uint32_t A, uin
     float mj, vj, ej;
     at(je, mj, vj, ej);
     const float var = vj - vA > 0.0f ? vj - vA : 0.0f;
-    const float m = (float)PSS_SPLIT_K * __builtin_sqrtf(var + 1.0f) / (ej > 1.0f ? ej : 1.0f) + 16.0f;
+    const float m = pl.K * __builtin_sqrtf(var + 1.0f) / (ej > 1.0f ? ej : 1.0f) + 16.0f;
     const float flo = je - m, fhi = je + m + 1.0f;
     lo = flo > (float)A ? (uint32_t)flo : A;
     const uint32_t cap = A + (v1 ? dq : dq / 2u) + 1u;   // at most one k2 per two words (V1: a draw a word)
@@ -722,6 +726,7 @@ namespace {
 struct SpPlanHost {
     std::vector<uint4> seg;
     uint32_t W = 0, nph = 0, nt = 0, qend = 0;
+    double K = PSS_SPLIT_K;
     uint32_t ph[kSpPh + 1] = {};
     double words = 0;            // expected words of the window
     std::vector<float2> mv;      // expected words / variance to reach step 64 i
@@ -733,6 +738,7 @@ static uint32_t sp_bitlen(uint64_t n) { return n ? 64u - (uint32_t)__builtin_clz
 
 static void sp_plan_build(uint32_t W, uint32_t P, bool v1, SpPlanHost &h) {
     h.W = W;
+    h.K = v1 ? PSS_SPLIT_K_V1 : PSS_SPLIT_K;
     const uint32_t kb1 = sp_bitlen(P);
     const double a1 = v1 ? 1.0 : (double)P / (double)(1ull << kb1);   // (V1: no k1 draws)
     // words per step j (a k1 then a k2 draw at bound W - j) and their variance; running sums
@@ -761,7 +767,7 @@ static void sp_plan_build(uint32_t W, uint32_t P, bool v1, SpPlanHost &h) {
         for (;;) {
             const size_t je = jat(q);
             const double sd = std::sqrt(V[je] - V[ja] + 1.0) / E[je];
-            const double m = PSS_SPLIT_K * sd + 16.0, width = 2.0 * m + 1.0;
+            const double m = h.K * sd + 16.0, width = 2.0 * m + 1.0;
             const double nmin = (double)W - (double)je - m - 64.0;
             if (nmin <= 4.0 * width) break;
             const uint32_t kk = sp_bitlen((uint64_t)nmin);
@@ -859,6 +865,7 @@ static V2xSpPlan sp_plan_dev(const SpPlanHost &h) {
     p.seg = h.dseg;
     p.mv = h.dmv;
     p.W = h.W; p.nph = h.nph; p.nt = h.nt; p.qend = h.qend;
+    p.K = (float)h.K;
     for (int i = 0; i <= kSpPh; i++) p.ph[i] = h.ph[i];
     return p;
 }
