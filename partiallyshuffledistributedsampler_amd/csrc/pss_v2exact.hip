@@ -1083,7 +1083,11 @@ static void v2x_draws(const V2xGeo &x, int64_t epoch, uint32_t *slot, hipStream_
 
 // PSS_EXACT_SPLIT=0 / 1: the exact orders' long-window draws in the workgroup form / in the split
 // form (pss_v2split.h) for any window length the scratch holds; by default the split form where
-// the workgroup form would run (few long windows) and the plan covers most of a window
+// the workgroup form would run (few long windows), the windows hold at least kSpMinWindow entries
+// and the plan covers most of a window.  (Cold epochs at C2's files, same box: V2 B = 2^14 / 2^16
+// even, 2^18 3.33 against 5.02 ms; V1 2^14 1.42 / 1.56, 2^16 1.58 / 1.36, 2^18 1.75 / 1.95 --
+// profiles/r06/exact_split/pool_size_probe_*.txt.)
+constexpr uint32_t kSpMinWindow = 1u << 17;
 static int sp_env() {
     static const int env = [] {
         const char *e = getenv("PSS_EXACT_SPLIT");
@@ -1179,7 +1183,7 @@ static bool v2x_draws_split(const V2xGeo &x, int64_t epoch, uint32_t *slot, uint
                             size_t scratch_words, hipStream_t s) {
     const int env = sp_env();
     if (env == 0 || !x.S) return false;
-    if (env != 1 && !v2x_draws_wg((uint64_t)x.S, x.B)) return false;
+    if (env != 1 && (!v2x_draws_wg((uint64_t)x.S, x.B) || x.B < kSpMinWindow)) return false;
     const uint32_t Wl = x.T - (x.S - 1u) * x.B;
     const SpPlanHost *hl = sp_plan_get(Wl, x.P, false);
     const SpPlanHost *hb = x.S > 1 ? sp_plan_get(x.B, x.P, false) : hl;
@@ -1203,7 +1207,7 @@ bool v1x_draws_split(int64_t w_lo, uint32_t nj, uint32_t n_full, uint32_t n_last
                      bool wg_form, hipStream_t s) {
     const int env = sp_env();
     if (env == 0 || !nj || !scratch || n_full < 2) return false;
-    if (env != 1 && !wg_form) return false;
+    if (env != 1 && (!wg_form || n_full < kSpMinWindow)) return false;
     const SpPlanHost *hl = sp_plan_get(n_last, 0u, true);
     const SpPlanHost *hb = nj > 1 ? sp_plan_get(n_full, 0u, true) : hl;
     if (!hl || !hb) return false;
