@@ -5,32 +5,36 @@
 // from ONE freshly seeded MT19937 stream, and which word serves which draw depends on every
 // rejection before it.  mt_draws_pair_wg (pss_mt.h) resolves a window on one CU: ~9.6 ms per
 // 2^20-step window (C5), of which the word generation is a small part and the per-block work of
-// the summaries / combine / emission the rest.  Here the generation stays serial (one wave per
-// window, raw words to HBM) and the rest is split:
+// the summaries / combine / emission the rest.  Here the generation stays serial (a workgroup per
+// window, raw words to HBM, in chunks on a side stream) and the rest is split:
 //
-//   plan     (host, per window length) the window's words cut into SEGMENTS; for each, the
-//            interval its start's k2 index can lie in -- the expected count at its word offset
-//            +- K standard deviations of the renewal count, measured from the phase's ANCHOR
-//            (below) -- and a length that keeps the expected number of verdicts that differ over
-//            that interval at about PSS_SPLIT_TARGET.
+//   plan     (host, per window length) the window's words cut into SEGMENTS in PHASES, each
+//            segment's length keeping the expected number of verdicts that differ over its
+//            interval at about PSS_SPLIT_TARGET; the interval (sp_interval, on the device) is
+//            the expected k2 index at the segment's word offset +- K standard deviations of the
+//            renewal count, counted from the phase's ANCHOR (the exact state the previous phase's
+//            walk ended in).  A phase ends where its intervals grow too wide, and ahead of every
+//            power-of-two crossing of the bound W - j.
 //   level 1  (one wave per segment and start role, the whole chip) the segment's transfer as a
 //            function of its start index j over the interval: evaluated exactly at the low end of
 //            a piece (pair_eval), it holds unchanged up to the largest shift of j under which no
 //            k2 verdict changes (an accepted k2 word r at bound n stays accepted while n - d > r,
 //            and no bound crosses a power of two) -- the rest of the piece is evaluated again.  So
 //            a segment's transfer is a short list of pieces [a_p, a_{p+1}) -> (role, j + c_p).
-//   walk     (one wave per window) the segments in order from the exact start: one lookup per
-//            segment (a ballot over its pieces); a segment whose start falls outside its interval
-//            or whose pieces overflowed is run exactly.  The walk ends at the phase's last segment,
-//            which anchors the next phase's intervals (they stay narrow where the bound k2 is small).
-//            After the last phase the walk runs the rest of the window exactly, emitting -- past the
-//            generated words from the stream's saved state.
+//   walk     (one wave per window and phase) the segments in order from the exact anchor, 64 at
+//            a time by guess and verify (a DPP scan of the pieces' transfers at guessed starts,
+//            settled up to the first lane whose start lies in another piece); a segment whose
+//            start falls outside its interval or whose pieces overflowed is run exactly.  The
+//            walk's end anchors the next phase.  After the last phase the walk runs the rest of the
+//            window exactly, emitting -- past the generated words from the stream's saved state.
 //   emit     (one wave per segment) every segment again from its now known start, emitting draws.
+// Each phase waits only for the generator chunk holding its last word.
 // The pieces are exact, so the draws are the reference's whatever the intervals: a bad estimate
 // only costs an exact run in the walk.
 // V1's long windows (kV1: pss_v1exact.hip's Fisher-Yates draws j = _randbelow(n - d), V1:165-171)
 // are the single-role case of the same machinery: every word serves a draw of bound n - d, the
-// stream ends after n - 1 draws, and the emission writes J[n - 1 - d] and the draw's bucket count.
+// stream ends after n - 1 draws, the emission writes J[n - 1 - d], and k_v1x_sp_count counts the
+// draws' buckets afterwards.
 #pragma once
 // (included inside namespace pss)
 
